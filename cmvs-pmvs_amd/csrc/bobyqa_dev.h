@@ -1,0 +1,1511 @@
+// bobyqa_dev.h -- BOBYQA (Powell, DAMTP 2009/NA06) with the NLopt 2.6.1 LN_BOBYQA driver
+// semantics the reference relies on (reference source/pmvs/optim.cpp:615-647: n = 3,
+// xtol_rel = 1e-7, maxeval = 1000, bounds +-23.99999 on the two angles), written as a
+// REVERSE-COMMUNICATION state machine for the GPU:
+//
+//   BqState st;  bq_begin(st, x0, lb, ub, xtol_rel, maxeval);
+//   while (bq_step(st, f) == BQ_NEED_F) f = objective(st.xeval);   // xeval is unscaled
+//   result: st.rc (NLopt numbering), st.xout[0..2]
+//
+// All of Powell's locals live in BqState so the optimizer can yield at each CALFUN site
+// (PRELIM, the main loop's label 360 and RESCUE) and resume.  One lane owns a BqState while
+// the whole wavefront evaluates the objective (cmvs-pmvs_amd/csrc/pmvs_kernels.hip).  The
+// arithmetic is Powell's, operation for operation; parity against the CPU oracle
+// (oracle/bobyqa_oracle.h) is tested trajectory-for-trajectory in tests/test_bobyqa.py.
+#pragma once
+
+#if defined(__HIPCC__)
+#define BQ_HD __host__ __device__ inline
+#else
+#define BQ_HD inline
+#endif
+
+#include <math.h>
+
+namespace pmvsdev {
+
+enum { BQ_NEED_F = 1, BQ_DONE = 0 };
+enum {
+  BQR_SUCCESS = 1, BQR_XTOL = 4, BQR_MAXEVAL = 5, BQR_INVALID_ARGS = -2, BQR_ROUNDOFF = -4
+};
+
+constexpr int BQN = 3;
+constexpr int BQNPT = 2 * BQN + 1;
+constexpr int BQNP = BQN + 1;
+constexpr int BQNPTM = BQNPT - BQNP;
+constexpr int BQNDIM = BQNPT + BQN;
+constexpr int BQNH = BQN * BQNP / 2;
+
+BQ_HD double bq_min(double a, double b) { return (a <= b) ? a : b; }  // NLopt MIN2
+BQ_HD double bq_max(double a, double b) { return (a >= b) ? a : b; }  // NLopt MAX2
+
+struct BqState {
+  // problem (rescaled space, 1-based)
+  double x[BQN + 1], xl[BQN + 1], xu[BQN + 1], s[BQN];
+  double rhobeg, rhoend;
+  int maxeval, nevals;
+  // BOBYQB arrays
+  double xbase[BQN + 1], xpt[BQNPT + 1][BQN + 1], fval[BQNPT + 1], xopt[BQN + 1], gopt[BQN + 1],
+      hq[BQNH + 1], pq[BQNPT + 1], bmat[BQNDIM + 1][BQN + 1], zmat[BQNPT + 1][BQNPTM + 1],
+      sl[BQN + 1], su[BQN + 1], xnew[BQN + 1], xalt[BQN + 1], d[BQN + 1], vlag[BQNDIM + 1],
+      w[BQNDIM + BQNPT + 1];
+  double gnew[BQN + 1];  // TRSBOX's GNEW (Powell's W(1..N) after TRSBOX)
+  double ptsaux[3][BQN + 1], ptsid[BQNPT + 1];
+  // BOBYQB scalars
+  double f, fbeg, fsave, xoptsq, rho, delta, diffa, diffb, diffc, dnorm, distsq, dsq, crvmin,
+      adelt, alpha, cauchy, beta, denom, fopt, vquad, diff, ratio, stepa, stepb;
+  int nf, kopt, kbase, nresc, ntrits, itest, nfsav, knew;
+  // PRELIM / RESCUE loop state kept across CALFUN
+  int nfm, nfx, kpt, rs_ip, rs_iq;
+  double rs_xp, rs_xq, rs_vq, rs_fbase;
+  int rc;
+  int resume;
+  double xeval[BQN];  // unscaled point whose f is requested
+  double xout[BQN];   // unscaled final point
+  double minf;
+};
+
+// ---------------------------------------------------------------- TRSBOX
+BQ_HD void bq_trsbox(const double (*xpt)[BQN + 1], const double* xopt, const double* gopt,
+                     const double* hq, const double* pq, const double* sl, const double* su,
+                     double delta, double* xnew, double* d, double* gnew, double* dsq_out,
+                     double* crvmin_out) {
+  const double half = 0.5, one = 1.0, onemin = -1.0, zero = 0.0;
+  double xbdi[BQN + 1], s[BQN + 1], hs[BQN + 1], hred[BQN + 1];
+  int iterc = 0, nact = 0, itermax = 0, itcsav = 0, iact = 0, isav = 0, iu = 0;
+  double delsq, qred, crvmin, beta = 0, stepsq = 0, gredsq = 0, resid, ds, shs = 0, temp, blen = 0,
+         stplen = 0, xsum, sdec, ggsav = 0, dredsq = 0, dredg = 0, sredg = 0, angbd = 0, tempa, tempb,
+         ssq, xsav = 0, dhs = 0, dhd = 0, redmax, redsav, angt = 0, sth, rednew, rdprev = 0,
+         rdnext = 0, cth;
+  for (int i = 1; i <= BQN; ++i) {
+    xbdi[i] = zero;
+    if (xopt[i] <= sl[i]) {
+      if (gopt[i] >= zero) xbdi[i] = onemin;
+    } else if (xopt[i] >= su[i]) {
+      if (gopt[i] <= zero) xbdi[i] = one;
+    }
+    if (xbdi[i] != zero) ++nact;
+    d[i] = zero;
+    gnew[i] = gopt[i];
+  }
+  delsq = delta * delta;
+  qred = zero;
+  crvmin = onemin;
+L20:
+  beta = zero;
+L30:
+  stepsq = zero;
+  for (int i = 1; i <= BQN; ++i) {
+    if (xbdi[i] != zero) s[i] = zero;
+    else if (beta == zero) s[i] = -gnew[i];
+    else s[i] = beta * s[i] - gnew[i];
+    stepsq += s[i] * s[i];
+  }
+  if (stepsq == zero) goto L190;
+  if (beta == zero) {
+    gredsq = stepsq;
+    itermax = iterc + BQN - nact;
+  }
+  if (gredsq * delsq <= qred * 1e-4 * qred) goto L190;
+  goto L210;
+L50:
+  resid = delsq;
+  ds = zero;
+  shs = zero;
+  for (int i = 1; i <= BQN; ++i) {
+    if (xbdi[i] == zero) {
+      resid -= d[i] * d[i];
+      ds += s[i] * d[i];
+      shs += s[i] * hs[i];
+    }
+  }
+  if (resid <= zero) goto L90;
+  temp = sqrt(stepsq * resid + ds * ds);
+  if (ds < zero) blen = (temp - ds) / stepsq;
+  else blen = resid / (temp + ds);
+  stplen = blen;
+  if (shs > zero) stplen = bq_min(blen, gredsq / shs);
+  iact = 0;
+  for (int i = 1; i <= BQN; ++i) {
+    if (s[i] != zero) {
+      xsum = xopt[i] + d[i];
+      if (s[i] > zero) temp = (su[i] - xsum) / s[i];
+      else temp = (sl[i] - xsum) / s[i];
+      if (temp < stplen) {
+        stplen = temp;
+        iact = i;
+      }
+    }
+  }
+  sdec = zero;
+  if (stplen > zero) {
+    ++iterc;
+    temp = shs / stepsq;
+    if (iact == 0 && temp > zero) {
+      crvmin = bq_min(crvmin, temp);
+      if (crvmin == onemin) crvmin = temp;
+    }
+    ggsav = gredsq;
+    gredsq = zero;
+    for (int i = 1; i <= BQN; ++i) {
+      gnew[i] += stplen * hs[i];
+      if (xbdi[i] == zero) gredsq += gnew[i] * gnew[i];
+      d[i] += stplen * s[i];
+    }
+    sdec = bq_max(stplen * (ggsav - half * stplen * shs), zero);
+    qred += sdec;
+  }
+  if (iact > 0) {
+    ++nact;
+    xbdi[iact] = one;
+    if (s[iact] < zero) xbdi[iact] = onemin;
+    delsq -= d[iact] * d[iact];
+    if (delsq <= zero) goto L90;
+    goto L20;
+  }
+  if (stplen < blen) {
+    if (iterc == itermax) goto L190;
+    if (sdec <= qred * .01) goto L190;
+    beta = gredsq / ggsav;
+    goto L30;
+  }
+L90:
+  crvmin = zero;
+L100:
+  if (nact >= BQN - 1) goto L190;
+  dredsq = zero;
+  dredg = zero;
+  gredsq = zero;
+  for (int i = 1; i <= BQN; ++i) {
+    if (xbdi[i] == zero) {
+      dredsq += d[i] * d[i];
+      dredg += d[i] * gnew[i];
+      gredsq += gnew[i] * gnew[i];
+      s[i] = d[i];
+    } else {
+      s[i] = zero;
+    }
+  }
+  itcsav = iterc;
+  goto L210;
+L120:
+  ++iterc;
+  temp = gredsq * dredsq - dredg * dredg;
+  if (temp <= qred * 1e-4 * qred) goto L190;
+  temp = sqrt(temp);
+  for (int i = 1; i <= BQN; ++i) {
+    if (xbdi[i] == zero) s[i] = (dredg * d[i] - dredsq * gnew[i]) / temp;
+    else s[i] = zero;
+  }
+  sredg = -temp;
+  angbd = one;
+  iact = 0;
+  for (int i = 1; i <= BQN; ++i) {
+    if (xbdi[i] == zero) {
+      tempa = xopt[i] + d[i] - sl[i];
+      tempb = su[i] - xopt[i] - d[i];
+      if (tempa <= zero) {
+        ++nact;
+        xbdi[i] = onemin;
+        goto L100;
+      } else if (tempb <= zero) {
+        ++nact;
+        xbdi[i] = one;
+        goto L100;
+      }
+      ssq = d[i] * d[i] + s[i] * s[i];
+      temp = xopt[i] - sl[i];
+      temp = ssq - temp * temp;
+      if (temp > zero) {
+        temp = sqrt(temp) - s[i];
+        if (angbd * temp > tempa) {
+          angbd = tempa / temp;
+          iact = i;
+          xsav = onemin;
+        }
+      }
+      temp = su[i] - xopt[i];
+      temp = ssq - temp * temp;
+      if (temp > zero) {
+        temp = sqrt(temp) + s[i];
+        if (angbd * temp > tempb) {
+          angbd = tempb / temp;
+          iact = i;
+          xsav = one;
+        }
+      }
+    }
+  }
+  goto L210;
+L150:
+  shs = zero;
+  dhs = zero;
+  dhd = zero;
+  for (int i = 1; i <= BQN; ++i) {
+    if (xbdi[i] == zero) {
+      shs += s[i] * hs[i];
+      dhs += d[i] * hs[i];
+      dhd += d[i] * hred[i];
+    }
+  }
+  redmax = zero;
+  isav = 0;
+  redsav = zero;
+  iu = (int)(angbd * 17. + 3.1);
+  for (int i = 1; i <= iu; ++i) {
+    angt = angbd * (double)i / (double)iu;
+    sth = (angt + angt) / (one + angt * angt);
+    temp = shs + angt * (angt * dhd - dhs - dhs);
+    rednew = sth * (angt * dredg - sredg - half * sth * temp);
+    if (rednew > redmax) {
+      redmax = rednew;
+      isav = i;
+      rdprev = redsav;
+    } else if (i == isav + 1) {
+      rdnext = rednew;
+    }
+    redsav = rednew;
+  }
+  if (isav == 0) goto L190;
+  if (isav < iu) {
+    temp = (rdnext - rdprev) / (redmax + redmax - rdprev - rdnext);
+    angt = angbd * ((double)isav + half * temp) / (double)iu;
+  }
+  cth = (one - angt * angt) / (one + angt * angt);
+  sth = (angt + angt) / (one + angt * angt);
+  temp = shs + angt * (angt * dhd - dhs - dhs);
+  sdec = sth * (angt * dredg - sredg - half * sth * temp);
+  if (sdec <= zero) goto L190;
+  dredg = zero;
+  gredsq = zero;
+  for (int i = 1; i <= BQN; ++i) {
+    gnew[i] = gnew[i] + (cth - one) * hred[i] + sth * hs[i];
+    if (xbdi[i] == zero) {
+      d[i] = cth * d[i] + sth * s[i];
+      dredg += d[i] * gnew[i];
+      gredsq += gnew[i] * gnew[i];
+    }
+    hred[i] = cth * hred[i] + sth * hs[i];
+  }
+  qred += sdec;
+  if (iact > 0 && isav == iu) {
+    ++nact;
+    xbdi[iact] = xsav;
+    goto L100;
+  }
+  if (sdec > qred * .01) goto L120;
+L190:
+  *dsq_out = zero;
+  for (int i = 1; i <= BQN; ++i) {
+    xnew[i] = bq_max(bq_min(xopt[i] + d[i], su[i]), sl[i]);
+    if (xbdi[i] == onemin) xnew[i] = sl[i];
+    if (xbdi[i] == one) xnew[i] = su[i];
+    d[i] = xnew[i] - xopt[i];
+    *dsq_out += d[i] * d[i];
+  }
+  *crvmin_out = crvmin;
+  return;
+L210: {
+    int ih = 0;
+    for (int j = 1; j <= BQN; ++j) {
+      hs[j] = zero;
+      for (int i = 1; i <= j; ++i) {
+        ++ih;
+        if (i < j) hs[j] += hq[ih] * s[i];
+        hs[i] += hq[ih] * s[j];
+      }
+    }
+    for (int k = 1; k <= BQNPT; ++k) {
+      if (pq[k] != zero) {
+        temp = zero;
+        for (int j = 1; j <= BQN; ++j) temp += xpt[k][j] * s[j];
+        temp *= pq[k];
+        for (int i = 1; i <= BQN; ++i) hs[i] += temp * xpt[k][i];
+      }
+    }
+    if (crvmin != zero) goto L50;
+    if (iterc > itcsav) goto L150;
+    for (int i = 1; i <= BQN; ++i) hred[i] = hs[i];
+    goto L120;
+  }
+}
+
+// ---------------------------------------------------------------- ALTMOV
+BQ_HD void bq_altmov(const double (*xpt)[BQN + 1], const double* xopt, const double (*bmat)[BQN + 1],
+                     const double (*zmat)[BQNPTM + 1], const double* sl, const double* su, int kopt,
+                     int knew, double adelt, double* xnew, double* xalt, double* alpha,
+                     double* cauchy) {
+  const double half = 0.5, one = 1.0, zero = 0.0;
+  const double cnst = one + sqrt(2.0);
+  double glag[BQN + 1], hcol[BQNPT + 1], w[2 * BQN + 1];
+  double ha, temp, presav, dderiv, distsq, subd, slbd, sumin, diff, step = 0, vlag, tempd, tempa,
+      tempb, predsq, stpsav = 0, bigstp, wfixsq, ggfree, wsqsav, gw, curv, scale, csave = 0;
+  int ilbd, iubd, isbd, ksav = 0, ibdsav = 0, iflag;
+  for (int k = 1; k <= BQNPT; ++k) hcol[k] = zero;
+  for (int j = 1; j <= BQNPTM; ++j) {
+    temp = zmat[knew][j];
+    for (int k = 1; k <= BQNPT; ++k) hcol[k] += temp * zmat[k][j];
+  }
+  *alpha = hcol[knew];
+  ha = half * *alpha;
+  for (int i = 1; i <= BQN; ++i) glag[i] = bmat[knew][i];
+  for (int k = 1; k <= BQNPT; ++k) {
+    temp = zero;
+    for (int j = 1; j <= BQN; ++j) temp += xpt[k][j] * xopt[j];
+    temp = hcol[k] * temp;
+    for (int i = 1; i <= BQN; ++i) glag[i] += temp * xpt[k][i];
+  }
+  presav = zero;
+  for (int k = 1; k <= BQNPT; ++k) {
+    if (k == kopt) continue;
+    dderiv = zero;
+    distsq = zero;
+    for (int i = 1; i <= BQN; ++i) {
+      temp = xpt[k][i] - xopt[i];
+      dderiv += glag[i] * temp;
+      distsq += temp * temp;
+    }
+    subd = adelt / sqrt(distsq);
+    slbd = -subd;
+    ilbd = 0;
+    iubd = 0;
+    sumin = bq_min(one, subd);
+    for (int i = 1; i <= BQN; ++i) {
+      temp = xpt[k][i] - xopt[i];
+      if (temp > zero) {
+        if (slbd * temp < sl[i] - xopt[i]) {
+          slbd = (sl[i] - xopt[i]) / temp;
+          ilbd = -i;
+        }
+        if (subd * temp > su[i] - xopt[i]) {
+          subd = bq_max(sumin, (su[i] - xopt[i]) / temp);
+          iubd = i;
+        }
+      } else if (temp < zero) {
+        if (slbd * temp > su[i] - xopt[i]) {
+          slbd = (su[i] - xopt[i]) / temp;
+          ilbd = i;
+        }
+        if (subd * temp < sl[i] - xopt[i]) {
+          subd = bq_max(sumin, (sl[i] - xopt[i]) / temp);
+          iubd = -i;
+        }
+      }
+    }
+    if (k == knew) {
+      diff = dderiv - one;
+      step = slbd;
+      vlag = slbd * (dderiv - slbd * diff);
+      isbd = ilbd;
+      temp = subd * (dderiv - subd * diff);
+      if (fabs(temp) > fabs(vlag)) {
+        step = subd;
+        vlag = temp;
+        isbd = iubd;
+      }
+      tempd = half * dderiv;
+      tempa = tempd - diff * slbd;
+      tempb = tempd - diff * subd;
+      if (tempa * tempb < zero) {
+        temp = tempd * tempd / diff;
+        if (fabs(temp) > fabs(vlag)) {
+          step = tempd / diff;
+          vlag = temp;
+          isbd = 0;
+        }
+      }
+    } else {
+      step = slbd;
+      vlag = slbd * (one - slbd);
+      isbd = ilbd;
+      temp = subd * (one - subd);
+      if (fabs(temp) > fabs(vlag)) {
+        step = subd;
+        vlag = temp;
+        isbd = iubd;
+      }
+      if (subd > half) {
+        if (fabs(vlag) < .25) {
+          step = half;
+          vlag = .25;
+          isbd = 0;
+        }
+      }
+      vlag *= dderiv;
+    }
+    temp = step * (one - step) * distsq;
+    predsq = vlag * vlag * (vlag * vlag + ha * temp * temp);
+    if (predsq > presav) {
+      presav = predsq;
+      ksav = k;
+      stpsav = step;
+      ibdsav = isbd;
+    }
+  }
+  for (int i = 1; i <= BQN; ++i) {
+    temp = xopt[i] + stpsav * (xpt[ksav][i] - xopt[i]);
+    xnew[i] = bq_max(sl[i], bq_min(su[i], temp));
+  }
+  if (ibdsav < 0) xnew[-ibdsav] = sl[-ibdsav];
+  if (ibdsav > 0) xnew[ibdsav] = su[ibdsav];
+  bigstp = adelt + adelt;
+  iflag = 0;
+L100:
+  wfixsq = zero;
+  ggfree = zero;
+  for (int i = 1; i <= BQN; ++i) {
+    w[i] = zero;
+    tempa = bq_min(xopt[i] - sl[i], glag[i]);
+    tempb = bq_max(xopt[i] - su[i], glag[i]);
+    if (tempa > zero || tempb < zero) {
+      w[i] = bigstp;
+      ggfree += glag[i] * glag[i];
+    }
+  }
+  if (ggfree == zero) {
+    *cauchy = zero;
+    return;
+  }
+L120:
+  temp = adelt * adelt - wfixsq;
+  if (temp > zero) {
+    wsqsav = wfixsq;
+    step = sqrt(temp / ggfree);
+    ggfree = zero;
+    for (int i = 1; i <= BQN; ++i) {
+      if (w[i] == bigstp) {
+        temp = xopt[i] - step * glag[i];
+        if (temp <= sl[i]) {
+          w[i] = sl[i] - xopt[i];
+          wfixsq += w[i] * w[i];
+        } else if (temp >= su[i]) {
+          w[i] = su[i] - xopt[i];
+          wfixsq += w[i] * w[i];
+        } else {
+          ggfree += glag[i] * glag[i];
+        }
+      }
+    }
+    if (wfixsq > wsqsav && ggfree > zero) goto L120;
+  }
+  gw = zero;
+  for (int i = 1; i <= BQN; ++i) {
+    if (w[i] == bigstp) {
+      w[i] = -step * glag[i];
+      xalt[i] = bq_max(sl[i], bq_min(su[i], xopt[i] + w[i]));
+    } else if (w[i] == zero) {
+      xalt[i] = xopt[i];
+    } else if (glag[i] > zero) {
+      xalt[i] = sl[i];
+    } else {
+      xalt[i] = su[i];
+    }
+    gw += glag[i] * w[i];
+  }
+  curv = zero;
+  for (int k = 1; k <= BQNPT; ++k) {
+    temp = zero;
+    for (int j = 1; j <= BQN; ++j) temp += xpt[k][j] * w[j];
+    curv += hcol[k] * temp * temp;
+  }
+  if (iflag == 1) curv = -curv;
+  if (curv > -gw && curv < -cnst * gw) {
+    scale = -gw / curv;
+    for (int i = 1; i <= BQN; ++i) {
+      temp = xopt[i] + scale * w[i];
+      xalt[i] = bq_max(sl[i], bq_min(su[i], temp));
+    }
+    temp = half * gw * scale;
+    *cauchy = temp * temp;
+  } else {
+    temp = gw + half * curv;
+    *cauchy = temp * temp;
+  }
+  if (iflag == 0) {
+    for (int i = 1; i <= BQN; ++i) {
+      glag[i] = -glag[i];
+      w[BQN + i] = xalt[i];
+    }
+    csave = *cauchy;
+    iflag = 1;
+    goto L100;
+  }
+  if (csave > *cauchy) {
+    for (int i = 1; i <= BQN; ++i) xalt[i] = w[BQN + i];
+    *cauchy = csave;
+  }
+}
+
+// ---------------------------------------------------------------- UPDATE
+BQ_HD void bq_update(double (*bmat)[BQN + 1], double (*zmat)[BQNPTM + 1], double* vlag, double beta,
+                     double denom, int knew, double* w) {
+  const double one = 1.0, zero = 0.0;
+  double ztest = zero, temp, tempa, tempb, alpha, tau;
+  for (int k = 1; k <= BQNPT; ++k)
+    for (int j = 1; j <= BQNPTM; ++j) ztest = bq_max(ztest, fabs(zmat[k][j]));
+  ztest *= 1e-20;
+  for (int j = 2; j <= BQNPTM; ++j) {
+    if (fabs(zmat[knew][j]) > ztest) {
+      const double d1 = zmat[knew][1], d2 = zmat[knew][j];
+      temp = sqrt(d1 * d1 + d2 * d2);
+      tempa = zmat[knew][1] / temp;
+      tempb = zmat[knew][j] / temp;
+      for (int i = 1; i <= BQNPT; ++i) {
+        temp = tempa * zmat[i][1] + tempb * zmat[i][j];
+        zmat[i][j] = tempa * zmat[i][j] - tempb * zmat[i][1];
+        zmat[i][1] = temp;
+      }
+    }
+    zmat[knew][j] = zero;
+  }
+  for (int i = 1; i <= BQNPT; ++i) w[i] = zmat[knew][1] * zmat[i][1];
+  alpha = w[knew];
+  tau = vlag[knew];
+  vlag[knew] -= one;
+  temp = sqrt(denom);
+  tempb = zmat[knew][1] / temp;
+  tempa = tau / temp;
+  for (int i = 1; i <= BQNPT; ++i) zmat[i][1] = tempa * zmat[i][1] - tempb * vlag[i];
+  for (int j = 1; j <= BQN; ++j) {
+    const int jp = BQNPT + j;
+    w[jp] = bmat[knew][j];
+    tempa = (alpha * vlag[jp] - tau * w[jp]) / denom;
+    tempb = (-beta * w[jp] - tau * vlag[jp]) / denom;
+    for (int i = 1; i <= jp; ++i) {
+      bmat[i][j] = bmat[i][j] + tempa * vlag[i] + tempb * w[i];
+      if (i > BQNPT) bmat[jp][i - BQNPT] = bmat[i][j];
+    }
+  }
+}
+
+// NLopt 2.6.1 nlopt_set_default_initial_step for one coordinate.
+BQ_HD double bq_default_step(double x, double lb, double ub) {
+  double step = HUGE_VAL;
+  if (!isinf(ub) && !isinf(lb) && (ub - lb) * 0.25 < step && ub > lb) step = (ub - lb) * 0.25;
+  if (!isinf(ub) && ub - x < step && ub > x) step = (ub - x) * 0.75;
+  if (!isinf(lb) && x - lb < step && x > lb) step = (x - lb) * 0.75;
+  if (isinf(step)) {
+    if (!isinf(ub) && fabs(ub - x) < fabs(step)) step = (ub - x) * 1.1;
+    if (!isinf(lb) && fabs(x - lb) < fabs(step)) step = (x - lb) * 1.1;
+  }
+  if (isinf(step) || step == 0.0 || fabs(step) < 2.2250738585072014e-308) step = x;
+  if (isinf(step) || step == 0.0) step = 1;
+  return step;
+}
+
+// Initialise: the nlopt_optimize -> bobyqa() wrapper up to the call of BOBYQB.
+// Returns 0 (then call bq_step with any f) or a negative NLopt error code.
+BQ_HD int bq_begin(BqState& st, const double* x0, const double* lb, const double* ub,
+                   double xtol_rel, int maxeval) {
+  double dxs[BQN];
+  for (int i = 0; i < BQN; ++i) dxs[i] = bq_default_step(x0[i], lb[i], ub[i]);
+  for (int i = 0; i < BQN; ++i) st.s[i] = 1.0;
+  {
+    int i = 1;
+    for (; i < BQN && dxs[i] == dxs[i - 1]; ++i) {
+    }
+    if (i < BQN)
+      for (i = 1; i < BQN; ++i) st.s[i] = dxs[i] / dxs[0];
+  }
+  for (int i = 0; i < BQN; ++i) {
+    st.x[i + 1] = x0[i] / st.s[i];
+    st.xl[i + 1] = lb[i] / st.s[i];
+    st.xu[i + 1] = ub[i] / st.s[i];
+  }
+  st.rhobeg = fabs(dxs[0] / st.s[0]);
+  st.rhoend = xtol_rel * st.rhobeg;
+  st.maxeval = maxeval;
+  st.nevals = 0;
+  st.rc = BQR_SUCCESS;
+  st.resume = 0;
+  st.minf = 0;
+  for (int j = 1; j <= BQN; ++j) {
+    const double temp = st.xu[j] - st.xl[j];
+    if (temp < st.rhobeg + st.rhobeg) {
+      st.rc = BQR_INVALID_ARGS;
+      for (int i = 0; i < BQN; ++i) st.xout[i] = x0[i];
+      st.resume = -1;
+      return BQR_INVALID_ARGS;
+    }
+    st.sl[j] = st.xl[j] - st.x[j];
+    st.su[j] = st.xu[j] - st.x[j];
+    if (st.sl[j] >= -st.rhobeg) {
+      if (st.sl[j] >= 0.0) {
+        st.x[j] = st.xl[j];
+        st.sl[j] = 0.0;
+        st.su[j] = temp;
+      } else {
+        st.x[j] = st.xl[j] + st.rhobeg;
+        st.sl[j] = -st.rhobeg;
+        st.su[j] = bq_max(st.xu[j] - st.x[j], st.rhobeg);
+      }
+    } else if (st.su[j] <= st.rhobeg) {
+      if (st.su[j] <= 0.0) {
+        st.x[j] = st.xu[j];
+        st.sl[j] = -temp;
+        st.su[j] = 0.0;
+      } else {
+        st.x[j] = st.xu[j] - st.rhobeg;
+        st.sl[j] = bq_min(st.xl[j] - st.x[j], -st.rhobeg);
+        st.su[j] = st.rhobeg;
+      }
+    }
+  }
+  return 0;
+}
+
+// Request an evaluation at the rescaled point p (1-based): nlopt's rescale_fun unscales it.
+#define BQ_CALFUN(P, LABEL_ID)                                             \
+  do {                                                                     \
+    for (int i_ = 0; i_ < BQN; ++i_) st.xeval[i_] = (P)[i_ + 1] * st.s[i_]; \
+    st.nevals++;                                                           \
+    st.resume = LABEL_ID;                                                  \
+    return BQ_NEED_F;                                                      \
+  } while (0)
+
+// Advance the optimizer.  fin is the objective value requested by the previous call (ignored
+// on the first call).  Returns BQ_NEED_F with st.xeval set, or BQ_DONE with st.rc/st.xout.
+BQ_HD int bq_step(BqState& st, double fin) {
+  const double half = 0.5, one = 1.0, ten = 10.0, tenth = 0.1, two = 2.0, zero = 0.0;
+  double temp, sum, suma, sumb, bsum, dx, delsq, scaden, biglsq, hdiag, den, errbig, frhosq,
+      bdtol, bdtest, curv, fracsq, sumpq, sumz, sumw, densav, pqold, gqsq, gisq, dist;
+  int ih, ksav;
+  switch (st.resume) {
+    case 0: goto PSTART;
+    case 1: goto PRESUME;
+    case 2: goto L360R;
+    case 3: goto R260R;
+    default: return BQ_DONE;
+  }
+PSTART: {
+    for (int j = 1; j <= BQN; ++j) {
+      st.xbase[j] = st.x[j];
+      for (int k = 1; k <= BQNPT; ++k) st.xpt[k][j] = zero;
+      for (int i = 1; i <= BQNDIM; ++i) st.bmat[i][j] = zero;
+    }
+    for (int i = 1; i <= BQNH; ++i) st.hq[i] = zero;
+    for (int k = 1; k <= BQNPT; ++k) {
+      st.pq[k] = zero;
+      for (int j = 1; j <= BQNPTM; ++j) st.zmat[k][j] = zero;
+    }
+    st.nf = 0;
+    st.kopt = 1;
+  PLOOP:
+    st.nfm = st.nf;
+    st.nfx = st.nf - BQN;
+    ++st.nf;
+    if (st.nfm <= 2 * BQN) {
+      if (st.nfm >= 1 && st.nfm <= BQN) {
+        st.stepa = st.rhobeg;
+        if (st.su[st.nfm] == zero) st.stepa = -st.stepa;
+        st.xpt[st.nf][st.nfm] = st.stepa;
+      } else if (st.nfm > BQN) {
+        st.stepa = st.xpt[st.nf - BQN][st.nfx];
+        st.stepb = -st.rhobeg;
+        if (st.sl[st.nfx] == zero) st.stepb = bq_min(two * st.rhobeg, st.su[st.nfx]);
+        if (st.su[st.nfx] == zero) st.stepb = bq_max(-two * st.rhobeg, st.sl[st.nfx]);
+        st.xpt[st.nf][st.nfx] = st.stepb;
+      }
+    }
+    for (int j = 1; j <= BQN; ++j) {
+      st.x[j] = bq_min(bq_max(st.xl[j], st.xbase[j] + st.xpt[st.nf][j]), st.xu[j]);
+      if (st.xpt[st.nf][j] == st.sl[j]) st.x[j] = st.xl[j];
+      if (st.xpt[st.nf][j] == st.su[j]) st.x[j] = st.xu[j];
+    }
+    BQ_CALFUN(st.x, 1);
+  }
+PRESUME: {
+    const double rhosq = st.rhobeg * st.rhobeg;
+    const int nf = st.nf, nfm = st.nfm, nfx = st.nfx;
+    st.f = fin;
+    st.fval[nf] = st.f;
+    if (nf == 1) {
+      st.fbeg = st.f;
+      st.kopt = 1;
+    } else if (st.f < st.fval[st.kopt]) {
+      st.kopt = nf;
+    }
+    if (nf <= 2 * BQN + 1) {
+      if (nf >= 2 && nf <= BQN + 1) {
+        st.gopt[nfm] = (st.f - st.fbeg) / st.stepa;
+        if (BQNPT < nf + BQN) {
+          st.bmat[1][nfm] = -one / st.stepa;
+          st.bmat[nf][nfm] = one / st.stepa;
+          st.bmat[BQNPT + nfm][nfm] = -half * rhosq;
+        }
+      } else if (nf >= BQN + 2) {
+        ih = nfx * (nfx + 1) / 2;
+        temp = (st.f - st.fbeg) / st.stepb;
+        st.diff = st.stepb - st.stepa;
+        st.hq[ih] = two * (temp - st.gopt[nfx]) / st.diff;
+        st.gopt[nfx] = (st.gopt[nfx] * st.stepb - temp * st.stepa) / st.diff;
+        if (st.stepa * st.stepb < zero) {
+          if (st.f < st.fval[nf - BQN]) {
+            st.fval[nf] = st.fval[nf - BQN];
+            st.fval[nf - BQN] = st.f;
+            if (st.kopt == nf) st.kopt = nf - BQN;
+            st.xpt[nf - BQN][nfx] = st.stepb;
+            st.xpt[nf][nfx] = st.stepa;
+          }
+        }
+        st.bmat[1][nfx] = -(st.stepa + st.stepb) / (st.stepa * st.stepb);
+        st.bmat[nf][nfx] = -half / st.xpt[nf - BQN][nfx];
+        st.bmat[nf - BQN][nfx] = -st.bmat[1][nfx] - st.bmat[nf][nfx];
+        st.zmat[1][nfx] = sqrt(two) / (st.stepa * st.stepb);
+        st.zmat[nf][nfx] = sqrt(half) / rhosq;
+        st.zmat[nf - BQN][nfx] = -st.zmat[1][nfx] - st.zmat[nf][nfx];
+      }
+    }
+    if (st.maxeval > 0 && st.nevals >= st.maxeval) {
+      st.rc = BQR_MAXEVAL;
+    } else if (st.nf < BQNPT) {
+      goto PLOOP;
+    }
+  }
+  st.xoptsq = zero;
+  for (int i = 1; i <= BQN; ++i) {
+    st.xopt[i] = st.xpt[st.kopt][i];
+    st.xoptsq += st.xopt[i] * st.xopt[i];
+  }
+  st.fsave = st.fval[1];
+  if (st.rc != BQR_SUCCESS) goto L720;
+  st.kbase = 1;
+  st.rho = st.rhobeg;
+  st.delta = st.rho;
+  st.nresc = st.nf;
+  st.ntrits = 0;
+  st.diffa = zero;
+  st.diffb = zero;
+  st.diffc = zero;
+  st.ratio = zero;
+  st.itest = 0;
+  st.nfsav = st.nf;
+  st.knew = 0;
+L20:
+  if (st.kopt != st.kbase) {
+    ih = 0;
+    for (int j = 1; j <= BQN; ++j) {
+      for (int i = 1; i <= j; ++i) {
+        ++ih;
+        if (i < j) st.gopt[j] += st.hq[ih] * st.xopt[i];
+        st.gopt[i] += st.hq[ih] * st.xopt[j];
+      }
+    }
+    if (st.nf > BQNPT) {
+      for (int k = 1; k <= BQNPT; ++k) {
+        temp = zero;
+        for (int j = 1; j <= BQN; ++j) temp += st.xpt[k][j] * st.xopt[j];
+        temp = st.pq[k] * temp;
+        for (int i = 1; i <= BQN; ++i) st.gopt[i] += temp * st.xpt[k][i];
+      }
+    }
+  }
+L60:
+  bq_trsbox(st.xpt, st.xopt, st.gopt, st.hq, st.pq, st.sl, st.su, st.delta, st.xnew, st.d, st.gnew,
+            &st.dsq, &st.crvmin);
+  st.dnorm = bq_min(st.delta, sqrt(st.dsq));
+  if (st.dnorm < half * st.rho) {
+    st.ntrits = -1;
+    temp = ten * st.rho;
+    st.distsq = temp * temp;
+    if (st.nf <= st.nfsav + 2) goto L650;
+    errbig = bq_max(bq_max(st.diffa, st.diffb), st.diffc);
+    frhosq = st.rho * .125 * st.rho;
+    if (st.crvmin > zero && errbig > frhosq * st.crvmin) goto L650;
+    bdtol = errbig / st.rho;
+    for (int j = 1; j <= BQN; ++j) {
+      bdtest = bdtol;
+      if (st.xnew[j] == st.sl[j]) bdtest = st.gnew[j];
+      if (st.xnew[j] == st.su[j]) bdtest = -st.gnew[j];
+      if (bdtest < bdtol) {
+        curv = st.hq[(j + j * j) / 2];
+        for (int k = 1; k <= BQNPT; ++k) curv += st.pq[k] * (st.xpt[k][j] * st.xpt[k][j]);
+        bdtest += half * curv * st.rho;
+        if (bdtest < bdtol) goto L650;
+      }
+    }
+    goto L680;
+  }
+  ++st.ntrits;
+L90:
+  if (st.dsq <= st.xoptsq * .001) {
+    fracsq = st.xoptsq * .25;
+    sumpq = zero;
+    for (int k = 1; k <= BQNPT; ++k) {
+      sumpq += st.pq[k];
+      sum = -half * st.xoptsq;
+      for (int i = 1; i <= BQN; ++i) sum += st.xpt[k][i] * st.xopt[i];
+      st.w[BQNPT + k] = sum;
+      temp = fracsq - half * sum;
+      for (int i = 1; i <= BQN; ++i) {
+        st.w[i] = st.bmat[k][i];
+        st.vlag[i] = sum * st.xpt[k][i] + temp * st.xopt[i];
+        const int ip = BQNPT + i;
+        for (int j = 1; j <= i; ++j)
+          st.bmat[ip][j] = st.bmat[ip][j] + st.w[i] * st.vlag[j] + st.vlag[i] * st.w[j];
+      }
+    }
+    for (int jj = 1; jj <= BQNPTM; ++jj) {
+      sumz = zero;
+      sumw = zero;
+      for (int k = 1; k <= BQNPT; ++k) {
+        sumz += st.zmat[k][jj];
+        st.vlag[k] = st.w[BQNPT + k] * st.zmat[k][jj];
+        sumw += st.vlag[k];
+      }
+      for (int j = 1; j <= BQN; ++j) {
+        sum = (fracsq * sumz - half * sumw) * st.xopt[j];
+        for (int k = 1; k <= BQNPT; ++k) sum += st.vlag[k] * st.xpt[k][j];
+        st.w[j] = sum;
+        for (int k = 1; k <= BQNPT; ++k) st.bmat[k][j] += sum * st.zmat[k][jj];
+      }
+      for (int i = 1; i <= BQN; ++i) {
+        const int ip = i + BQNPT;
+        temp = st.w[i];
+        for (int j = 1; j <= i; ++j) st.bmat[ip][j] += temp * st.w[j];
+      }
+    }
+    ih = 0;
+    for (int j = 1; j <= BQN; ++j) {
+      st.w[j] = -half * sumpq * st.xopt[j];
+      for (int k = 1; k <= BQNPT; ++k) {
+        st.w[j] += st.pq[k] * st.xpt[k][j];
+        st.xpt[k][j] -= st.xopt[j];
+      }
+      for (int i = 1; i <= j; ++i) {
+        ++ih;
+        st.hq[ih] = st.hq[ih] + st.w[i] * st.xopt[j] + st.xopt[i] * st.w[j];
+        st.bmat[BQNPT + i][j] = st.bmat[BQNPT + j][i];
+      }
+    }
+    for (int i = 1; i <= BQN; ++i) {
+      st.xbase[i] += st.xopt[i];
+      st.xnew[i] -= st.xopt[i];
+      st.sl[i] -= st.xopt[i];
+      st.su[i] -= st.xopt[i];
+      st.xopt[i] = zero;
+    }
+    st.xoptsq = zero;
+  }
+  if (st.ntrits == 0) goto L210;
+  goto L230;
+
+L190:  // ---- RESCUE
+  st.nfsav = st.nf;
+  st.kbase = st.kopt;
+  {
+    const double sfrac = half / (double)BQNP;
+    double winc = zero, bet2 = 0, den2 = 0, dsqmin, vlmxsq;
+    int nrem, kold, kn, ip, iq, iw;
+    sumpq = zero;
+    for (int k = 1; k <= BQNPT; ++k) {
+      st.distsq = zero;
+      for (int j = 1; j <= BQN; ++j) {
+        st.xpt[k][j] -= st.xopt[j];
+        st.distsq += st.xpt[k][j] * st.xpt[k][j];
+      }
+      sumpq += st.pq[k];
+      st.w[BQNDIM + k] = st.distsq;
+      winc = bq_max(winc, st.distsq);
+      for (int j = 1; j <= BQNPTM; ++j) st.zmat[k][j] = zero;
+    }
+    ih = 0;
+    for (int j = 1; j <= BQN; ++j) {
+      st.w[j] = half * sumpq * st.xopt[j];
+      for (int k = 1; k <= BQNPT; ++k) st.w[j] += st.pq[k] * st.xpt[k][j];
+      for (int i = 1; i <= j; ++i) {
+        ++ih;
+        st.hq[ih] = st.hq[ih] + st.w[i] * st.xopt[j] + st.w[j] * st.xopt[i];
+      }
+    }
+    for (int j = 1; j <= BQN; ++j) {
+      st.xbase[j] += st.xopt[j];
+      st.sl[j] -= st.xopt[j];
+      st.su[j] -= st.xopt[j];
+      st.xopt[j] = zero;
+      st.ptsaux[1][j] = bq_min(st.delta, st.su[j]);
+      st.ptsaux[2][j] = bq_max(-st.delta, st.sl[j]);
+      if (st.ptsaux[1][j] + st.ptsaux[2][j] < zero) {
+        temp = st.ptsaux[1][j];
+        st.ptsaux[1][j] = st.ptsaux[2][j];
+        st.ptsaux[2][j] = temp;
+      }
+      if (fabs(st.ptsaux[2][j]) < half * fabs(st.ptsaux[1][j])) st.ptsaux[2][j] = half * st.ptsaux[1][j];
+      for (int i = 1; i <= BQNDIM; ++i) st.bmat[i][j] = zero;
+    }
+    st.rs_fbase = st.fval[st.kopt];
+    st.ptsid[1] = sfrac;
+    for (int j = 1; j <= BQN; ++j) {
+      const int jp = j + 1, jpn = jp + BQN;
+      st.ptsid[jp] = (double)j + sfrac;
+      if (jpn <= BQNPT) {
+        st.ptsid[jpn] = (double)j / (double)BQNP + sfrac;
+        temp = one / (st.ptsaux[1][j] - st.ptsaux[2][j]);
+        st.bmat[jp][j] = -temp + one / st.ptsaux[1][j];
+        st.bmat[jpn][j] = temp + one / st.ptsaux[2][j];
+        st.bmat[1][j] = -st.bmat[jp][j] - st.bmat[jpn][j];
+        st.zmat[1][j] = sqrt(2.) / fabs(st.ptsaux[1][j] * st.ptsaux[2][j]);
+        st.zmat[jp][j] = st.zmat[1][j] * st.ptsaux[2][j] * temp;
+        st.zmat[jpn][j] = -st.zmat[1][j] * st.ptsaux[1][j] * temp;
+      } else {
+        st.bmat[1][j] = -one / st.ptsaux[1][j];
+        st.bmat[jp][j] = one / st.ptsaux[1][j];
+        st.bmat[j + BQNPT][j] = -half * (st.ptsaux[1][j] * st.ptsaux[1][j]);
+      }
+    }
+    nrem = BQNPT;
+    kold = 1;
+    kn = st.kopt;
+  R80:
+    for (int j = 1; j <= BQN; ++j) {
+      temp = st.bmat[kold][j];
+      st.bmat[kold][j] = st.bmat[kn][j];
+      st.bmat[kn][j] = temp;
+    }
+    for (int j = 1; j <= BQNPTM; ++j) {
+      temp = st.zmat[kold][j];
+      st.zmat[kold][j] = st.zmat[kn][j];
+      st.zmat[kn][j] = temp;
+    }
+    st.ptsid[kold] = st.ptsid[kn];
+    st.ptsid[kn] = zero;
+    st.w[BQNDIM + kn] = zero;
+    --nrem;
+    if (kn != st.kopt) {
+      temp = st.vlag[kold];
+      st.vlag[kold] = st.vlag[kn];
+      st.vlag[kn] = temp;
+      bq_update(st.bmat, st.zmat, st.vlag, bet2, den2, kn, st.w);
+      if (nrem == 0) goto R350;
+      for (int k = 1; k <= BQNPT; ++k) st.w[BQNDIM + k] = fabs(st.w[BQNDIM + k]);
+    }
+  R120:
+    dsqmin = zero;
+    for (int k = 1; k <= BQNPT; ++k) {
+      if (st.w[BQNDIM + k] > zero) {
+        if (dsqmin == zero || st.w[BQNDIM + k] < dsqmin) {
+          kn = k;
+          dsqmin = st.w[BQNDIM + k];
+        }
+      }
+    }
+    if (dsqmin == zero) goto R260;
+    for (int j = 1; j <= BQN; ++j) st.w[BQNPT + j] = st.xpt[kn][j];
+    for (int k = 1; k <= BQNPT; ++k) {
+      sum = zero;
+      if (k == st.kopt) {
+      } else if (st.ptsid[k] == zero) {
+        for (int j = 1; j <= BQN; ++j) sum += st.w[BQNPT + j] * st.xpt[k][j];
+      } else {
+        ip = (int)st.ptsid[k];
+        if (ip > 0) sum = st.w[BQNPT + ip] * st.ptsaux[1][ip];
+        iq = (int)((double)BQNP * st.ptsid[k] - (double)(ip * BQNP));
+        if (iq > 0) {
+          iw = 1;
+          if (ip == 0) iw = 2;
+          sum += st.w[BQNPT + iq] * st.ptsaux[iw][iq];
+        }
+      }
+      st.w[k] = half * sum * sum;
+    }
+    for (int k = 1; k <= BQNPT; ++k) {
+      sum = zero;
+      for (int j = 1; j <= BQN; ++j) sum += st.bmat[k][j] * st.w[BQNPT + j];
+      st.vlag[k] = sum;
+    }
+    bet2 = zero;
+    for (int j = 1; j <= BQNPTM; ++j) {
+      sum = zero;
+      for (int k = 1; k <= BQNPT; ++k) sum += st.zmat[k][j] * st.w[k];
+      bet2 -= sum * sum;
+      for (int k = 1; k <= BQNPT; ++k) st.vlag[k] += sum * st.zmat[k][j];
+    }
+    bsum = zero;
+    st.distsq = zero;
+    for (int j = 1; j <= BQN; ++j) {
+      sum = zero;
+      for (int k = 1; k <= BQNPT; ++k) sum += st.bmat[k][j] * st.w[k];
+      const int jp = j + BQNPT;
+      bsum += sum * st.w[jp];
+      for (int ipp = BQNPT + 1; ipp <= BQNDIM; ++ipp) sum += st.bmat[ipp][j] * st.w[ipp];
+      bsum += sum * st.w[jp];
+      st.vlag[jp] = sum;
+      st.distsq += st.xpt[kn][j] * st.xpt[kn][j];
+    }
+    bet2 = half * st.distsq * st.distsq + bet2 - bsum;
+    st.vlag[st.kopt] += one;
+    den2 = zero;
+    vlmxsq = zero;
+    for (int k = 1; k <= BQNPT; ++k) {
+      if (st.ptsid[k] != zero) {
+        hdiag = zero;
+        for (int j = 1; j <= BQNPTM; ++j) hdiag += st.zmat[k][j] * st.zmat[k][j];
+        den = bet2 * hdiag + st.vlag[k] * st.vlag[k];
+        if (den > den2) {
+          kold = k;
+          den2 = den;
+        }
+      }
+      vlmxsq = bq_max(vlmxsq, st.vlag[k] * st.vlag[k]);
+    }
+    if (den2 <= vlmxsq * .01) {
+      st.w[BQNDIM + kn] = -st.w[BQNDIM + kn] - winc;
+      goto R120;
+    }
+    goto R80;
+  }
+R260:
+  st.kpt = 1;
+R260LOOP:
+  if (st.kpt > BQNPT) goto R350;
+  if (st.ptsid[st.kpt] == zero) {
+    ++st.kpt;
+    goto R260LOOP;
+  }
+  if (st.maxeval > 0 && st.nevals >= st.maxeval) {
+    st.nf = -1;
+    goto R350;
+  }
+  {
+    const int kpt = st.kpt;
+    ih = 0;
+    for (int j = 1; j <= BQN; ++j) {
+      st.w[j] = st.xpt[kpt][j];
+      st.xpt[kpt][j] = zero;
+      temp = st.pq[kpt] * st.w[j];
+      for (int i = 1; i <= j; ++i) {
+        ++ih;
+        st.hq[ih] += temp * st.w[i];
+      }
+    }
+    st.pq[kpt] = zero;
+    st.rs_ip = (int)st.ptsid[kpt];
+    st.rs_iq = (int)((double)BQNP * st.ptsid[kpt] - (double)(st.rs_ip * BQNP));
+    const int ip = st.rs_ip, iq = st.rs_iq;
+    int ihp = 0, ihq;
+    if (ip > 0) {
+      st.rs_xp = st.ptsaux[1][ip];
+      st.xpt[kpt][ip] = st.rs_xp;
+    }
+    if (iq > 0) {
+      st.rs_xq = st.ptsaux[1][iq];
+      if (ip == 0) st.rs_xq = st.ptsaux[2][iq];
+      st.xpt[kpt][iq] = st.rs_xq;
+    }
+    st.rs_vq = st.rs_fbase;
+    if (ip > 0) {
+      ihp = (ip + ip * ip) / 2;
+      st.rs_vq += st.rs_xp * (st.gopt[ip] + half * st.rs_xp * st.hq[ihp]);
+    }
+    if (iq > 0) {
+      ihq = (iq + iq * iq) / 2;
+      st.rs_vq += st.rs_xq * (st.gopt[iq] + half * st.rs_xq * st.hq[ihq]);
+      if (ip > 0) {
+        const int iw = (ihp > ihq ? ihp : ihq) - (ip > iq ? ip - iq : iq - ip);
+        st.rs_vq += st.rs_xp * st.rs_xq * st.hq[iw];
+      }
+    }
+    for (int k = 1; k <= BQNPT; ++k) {
+      temp = zero;
+      if (ip > 0) temp += st.rs_xp * st.xpt[k][ip];
+      if (iq > 0) temp += st.rs_xq * st.xpt[k][iq];
+      st.rs_vq += half * st.pq[k] * temp * temp;
+    }
+    for (int i = 1; i <= BQN; ++i) {
+      st.w[i] = bq_min(bq_max(st.xl[i], st.xbase[i] + st.xpt[kpt][i]), st.xu[i]);
+      if (st.xpt[kpt][i] == st.sl[i]) st.w[i] = st.xl[i];
+      if (st.xpt[kpt][i] == st.su[i]) st.w[i] = st.xu[i];
+    }
+    ++st.nf;
+    BQ_CALFUN(st.w, 3);
+  }
+R260R: {
+    const int kpt = st.kpt, ip0 = st.rs_ip, iq0 = st.rs_iq;
+    (void)ip0; (void)iq0;
+    st.f = fin;
+    st.fval[kpt] = st.f;
+    if (st.f < st.fval[st.kopt]) st.kopt = kpt;
+    st.diff = st.f - st.rs_vq;
+    for (int i = 1; i <= BQN; ++i) st.gopt[i] += st.diff * st.bmat[kpt][i];
+    for (int k = 1; k <= BQNPT; ++k) {
+      sum = zero;
+      for (int j = 1; j <= BQNPTM; ++j) sum += st.zmat[k][j] * st.zmat[kpt][j];
+      temp = st.diff * sum;
+      if (st.ptsid[k] == zero) {
+        st.pq[k] += temp;
+      } else {
+        const int ip = (int)st.ptsid[k];
+        const int iq = (int)((double)BQNP * st.ptsid[k] - (double)(ip * BQNP));
+        const int ihq = (iq * iq + iq) / 2;
+        if (ip == 0) {
+          st.hq[ihq] += temp * (st.ptsaux[2][iq] * st.ptsaux[2][iq]);
+        } else {
+          const int ihp = (ip * ip + ip) / 2;
+          st.hq[ihp] += temp * (st.ptsaux[1][ip] * st.ptsaux[1][ip]);
+          if (iq > 0) {
+            st.hq[ihq] += temp * (st.ptsaux[1][iq] * st.ptsaux[1][iq]);
+            const int iw = (ihp > ihq ? ihp : ihq) - (iq > ip ? iq - ip : ip - iq);
+            st.hq[iw] += temp * st.ptsaux[1][ip] * st.ptsaux[1][iq];
+          }
+        }
+      }
+    }
+    st.ptsid[kpt] = zero;
+    ++st.kpt;
+    goto R260LOOP;
+  }
+R350:
+  st.xoptsq = zero;
+  if (st.kopt != st.kbase) {
+    for (int i = 1; i <= BQN; ++i) {
+      st.xopt[i] = st.xpt[st.kopt][i];
+      st.xoptsq += st.xopt[i] * st.xopt[i];
+    }
+  }
+  if (st.nf < 0) {
+    st.nf = st.maxeval;
+    st.rc = BQR_MAXEVAL;
+    goto L720;
+  }
+  st.nresc = st.nf;
+  if (st.nfsav < st.nf) {
+    st.nfsav = st.nf;
+    goto L20;
+  }
+  if (st.ntrits > 0) goto L60;
+L210:
+  bq_altmov(st.xpt, st.xopt, st.bmat, st.zmat, st.sl, st.su, st.kopt, st.knew, st.adelt, st.xnew,
+            st.xalt, &st.alpha, &st.cauchy);
+  for (int i = 1; i <= BQN; ++i) st.d[i] = st.xnew[i] - st.xopt[i];
+L230:
+  for (int k = 1; k <= BQNPT; ++k) {
+    suma = zero;
+    sumb = zero;
+    sum = zero;
+    for (int j = 1; j <= BQN; ++j) {
+      suma += st.xpt[k][j] * st.d[j];
+      sumb += st.xpt[k][j] * st.xopt[j];
+      sum += st.bmat[k][j] * st.d[j];
+    }
+    st.w[k] = suma * (half * suma + sumb);
+    st.vlag[k] = sum;
+    st.w[BQNPT + k] = suma;
+  }
+  st.beta = zero;
+  for (int jj = 1; jj <= BQNPTM; ++jj) {
+    sum = zero;
+    for (int k = 1; k <= BQNPT; ++k) sum += st.zmat[k][jj] * st.w[k];
+    st.beta -= sum * sum;
+    for (int k = 1; k <= BQNPT; ++k) st.vlag[k] += sum * st.zmat[k][jj];
+  }
+  st.dsq = zero;
+  bsum = zero;
+  dx = zero;
+  for (int j = 1; j <= BQN; ++j) {
+    st.dsq += st.d[j] * st.d[j];
+    sum = zero;
+    for (int k = 1; k <= BQNPT; ++k) sum += st.w[k] * st.bmat[k][j];
+    bsum += sum * st.d[j];
+    const int jp = BQNPT + j;
+    for (int i = 1; i <= BQN; ++i) sum += st.bmat[jp][i] * st.d[i];
+    st.vlag[jp] = sum;
+    bsum += sum * st.d[j];
+    dx += st.d[j] * st.xopt[j];
+  }
+  st.beta = dx * dx + st.dsq * (st.xoptsq + dx + dx + half * st.dsq) + st.beta - bsum;
+  st.vlag[st.kopt] += one;
+  if (st.ntrits == 0) {
+    st.denom = st.vlag[st.knew] * st.vlag[st.knew] + st.alpha * st.beta;
+    if (st.denom < st.cauchy && st.cauchy > zero) {
+      for (int i = 1; i <= BQN; ++i) {
+        st.xnew[i] = st.xalt[i];
+        st.d[i] = st.xnew[i] - st.xopt[i];
+      }
+      st.cauchy = zero;
+      goto L230;
+    }
+    if (st.denom <= half * (st.vlag[st.knew] * st.vlag[st.knew])) {
+      if (st.nf > st.nresc) goto L190;
+      st.rc = BQR_ROUNDOFF;
+      goto L720;
+    }
+  } else {
+    delsq = st.delta * st.delta;
+    scaden = zero;
+    biglsq = zero;
+    st.knew = 0;
+    for (int k = 1; k <= BQNPT; ++k) {
+      if (k == st.kopt) continue;
+      hdiag = zero;
+      for (int jj = 1; jj <= BQNPTM; ++jj) hdiag += st.zmat[k][jj] * st.zmat[k][jj];
+      den = st.beta * hdiag + st.vlag[k] * st.vlag[k];
+      st.distsq = zero;
+      for (int j = 1; j <= BQN; ++j) {
+        temp = st.xpt[k][j] - st.xopt[j];
+        st.distsq += temp * temp;
+      }
+      temp = st.distsq / delsq;
+      temp = bq_max(one, temp * temp);
+      if (temp * den > scaden) {
+        scaden = temp * den;
+        st.knew = k;
+        st.denom = den;
+      }
+      biglsq = bq_max(biglsq, temp * (st.vlag[k] * st.vlag[k]));
+    }
+    if (scaden <= half * biglsq) {
+      if (st.nf > st.nresc) goto L190;
+      st.rc = BQR_ROUNDOFF;
+      goto L720;
+    }
+  }
+L360:
+  for (int i = 1; i <= BQN; ++i) {
+    st.x[i] = bq_min(bq_max(st.xl[i], st.xbase[i] + st.xnew[i]), st.xu[i]);
+    if (st.xnew[i] == st.sl[i]) st.x[i] = st.xl[i];
+    if (st.xnew[i] == st.su[i]) st.x[i] = st.xu[i];
+  }
+  if (st.maxeval > 0 && st.nevals >= st.maxeval) {
+    st.rc = BQR_MAXEVAL;
+    goto L720;
+  }
+  ++st.nf;
+  BQ_CALFUN(st.x, 2);
+L360R:
+  st.f = fin;
+  if (st.ntrits == -1) {
+    st.fsave = st.f;
+    st.rc = BQR_XTOL;
+    if (st.fsave < st.fval[st.kopt]) {
+      st.minf = st.f;
+      for (int i = 0; i < BQN; ++i) st.xout[i] = st.x[i + 1] * st.s[i];
+      st.resume = -1;
+      return BQ_DONE;
+    }
+    goto L720;
+  }
+  st.fopt = st.fval[st.kopt];
+  st.vquad = zero;
+  ih = 0;
+  for (int j = 1; j <= BQN; ++j) {
+    st.vquad += st.d[j] * st.gopt[j];
+    for (int i = 1; i <= j; ++i) {
+      ++ih;
+      temp = st.d[i] * st.d[j];
+      if (i == j) temp = half * temp;
+      st.vquad += st.hq[ih] * temp;
+    }
+  }
+  for (int k = 1; k <= BQNPT; ++k) {
+    temp = st.w[BQNPT + k];
+    st.vquad += half * st.pq[k] * (temp * temp);
+  }
+  st.diff = st.f - st.fopt - st.vquad;
+  st.diffc = st.diffb;
+  st.diffb = st.diffa;
+  st.diffa = fabs(st.diff);
+  if (st.dnorm > st.rho) st.nfsav = st.nf;
+  if (st.ntrits > 0) {
+    if (st.vquad >= zero) {
+      st.rc = BQR_ROUNDOFF;
+      goto L720;
+    }
+    st.ratio = (st.f - st.fopt) / st.vquad;
+    if (st.ratio <= tenth) st.delta = bq_min(half * st.delta, st.dnorm);
+    else if (st.ratio <= .7) st.delta = bq_max(half * st.delta, st.dnorm);
+    else st.delta = bq_max(half * st.delta, st.dnorm + st.dnorm);
+    if (st.delta <= st.rho * 1.5) st.delta = st.rho;
+    if (st.f < st.fopt) {
+      ksav = st.knew;
+      densav = st.denom;
+      delsq = st.delta * st.delta;
+      scaden = zero;
+      biglsq = zero;
+      st.knew = 0;
+      for (int k = 1; k <= BQNPT; ++k) {
+        hdiag = zero;
+        for (int jj = 1; jj <= BQNPTM; ++jj) hdiag += st.zmat[k][jj] * st.zmat[k][jj];
+        den = st.beta * hdiag + st.vlag[k] * st.vlag[k];
+        st.distsq = zero;
+        for (int j = 1; j <= BQN; ++j) {
+          temp = st.xpt[k][j] - st.xnew[j];
+          st.distsq += temp * temp;
+        }
+        temp = st.distsq / delsq;
+        temp = bq_max(one, temp * temp);
+        if (temp * den > scaden) {
+          scaden = temp * den;
+          st.knew = k;
+          st.denom = den;
+        }
+        biglsq = bq_max(biglsq, temp * (st.vlag[k] * st.vlag[k]));
+      }
+      if (scaden <= half * biglsq) {
+        st.knew = ksav;
+        st.denom = densav;
+      }
+    }
+  }
+  bq_update(st.bmat, st.zmat, st.vlag, st.beta, st.denom, st.knew, st.w);
+  ih = 0;
+  pqold = st.pq[st.knew];
+  st.pq[st.knew] = zero;
+  for (int i = 1; i <= BQN; ++i) {
+    temp = pqold * st.xpt[st.knew][i];
+    for (int j = 1; j <= i; ++j) {
+      ++ih;
+      st.hq[ih] += temp * st.xpt[st.knew][j];
+    }
+  }
+  for (int jj = 1; jj <= BQNPTM; ++jj) {
+    temp = st.diff * st.zmat[st.knew][jj];
+    for (int k = 1; k <= BQNPT; ++k) st.pq[k] += temp * st.zmat[k][jj];
+  }
+  st.fval[st.knew] = st.f;
+  for (int i = 1; i <= BQN; ++i) {
+    st.xpt[st.knew][i] = st.xnew[i];
+    st.w[i] = st.bmat[st.knew][i];
+  }
+  for (int k = 1; k <= BQNPT; ++k) {
+    suma = zero;
+    for (int jj = 1; jj <= BQNPTM; ++jj) suma += st.zmat[st.knew][jj] * st.zmat[k][jj];
+    sumb = zero;
+    for (int j = 1; j <= BQN; ++j) sumb += st.xpt[k][j] * st.xopt[j];
+    temp = suma * sumb;
+    for (int i = 1; i <= BQN; ++i) st.w[i] += temp * st.xpt[k][i];
+  }
+  for (int i = 1; i <= BQN; ++i) st.gopt[i] += st.diff * st.w[i];
+  if (st.f < st.fopt) {
+    st.kopt = st.knew;
+    st.xoptsq = zero;
+    ih = 0;
+    for (int j = 1; j <= BQN; ++j) {
+      st.xopt[j] = st.xnew[j];
+      st.xoptsq += st.xopt[j] * st.xopt[j];
+      for (int i = 1; i <= j; ++i) {
+        ++ih;
+        if (i < j) st.gopt[j] += st.hq[ih] * st.d[i];
+        st.gopt[i] += st.hq[ih] * st.d[j];
+      }
+    }
+    for (int k = 1; k <= BQNPT; ++k) {
+      temp = zero;
+      for (int j = 1; j <= BQN; ++j) temp += st.xpt[k][j] * st.d[j];
+      temp = st.pq[k] * temp;
+      for (int i = 1; i <= BQN; ++i) st.gopt[i] += temp * st.xpt[k][i];
+    }
+  }
+  if (st.ntrits > 0) {
+    for (int k = 1; k <= BQNPT; ++k) {
+      st.vlag[k] = st.fval[k] - st.fval[st.kopt];
+      st.w[k] = zero;
+    }
+    for (int j = 1; j <= BQNPTM; ++j) {
+      sum = zero;
+      for (int k = 1; k <= BQNPT; ++k) sum += st.zmat[k][j] * st.vlag[k];
+      for (int k = 1; k <= BQNPT; ++k) st.w[k] += sum * st.zmat[k][j];
+    }
+    for (int k = 1; k <= BQNPT; ++k) {
+      sum = zero;
+      for (int j = 1; j <= BQN; ++j) sum += st.xpt[k][j] * st.xopt[j];
+      st.w[k + BQNPT] = st.w[k];
+      st.w[k] = sum * st.w[k];
+    }
+    gqsq = zero;
+    gisq = zero;
+    for (int i = 1; i <= BQN; ++i) {
+      sum = zero;
+      for (int k = 1; k <= BQNPT; ++k) sum = sum + st.bmat[k][i] * st.vlag[k] + st.xpt[k][i] * st.w[k];
+      if (st.xopt[i] == st.sl[i]) {
+        temp = bq_min(zero, st.gopt[i]);
+        gqsq += temp * temp;
+        temp = bq_min(zero, sum);
+        gisq += temp * temp;
+      } else if (st.xopt[i] == st.su[i]) {
+        temp = bq_max(zero, st.gopt[i]);
+        gqsq += temp * temp;
+        temp = bq_max(zero, sum);
+        gisq += temp * temp;
+      } else {
+        gqsq += st.gopt[i] * st.gopt[i];
+        gisq += sum * sum;
+      }
+      st.vlag[BQNPT + i] = sum;
+    }
+    ++st.itest;
+    if (gqsq < ten * gisq) st.itest = 0;
+    if (st.itest >= 3) {
+      const int imax = BQNPT > BQNH ? BQNPT : BQNH;
+      for (int i = 1; i <= imax; ++i) {
+        if (i <= BQN) st.gopt[i] = st.vlag[BQNPT + i];
+        if (i <= BQNPT) st.pq[i] = st.w[BQNPT + i];
+        if (i <= BQNH) st.hq[i] = zero;
+        st.itest = 0;
+      }
+    }
+  }
+  if (st.ntrits == 0) goto L60;
+  if (st.f <= st.fopt + tenth * st.vquad) goto L60;
+  {
+    const double t1 = two * st.delta, t2 = ten * st.rho;
+    st.distsq = bq_max(t1 * t1, t2 * t2);
+  }
+L650:
+  st.knew = 0;
+  for (int k = 1; k <= BQNPT; ++k) {
+    sum = zero;
+    for (int j = 1; j <= BQN; ++j) {
+      temp = st.xpt[k][j] - st.xopt[j];
+      sum += temp * temp;
+    }
+    if (sum > st.distsq) {
+      st.knew = k;
+      st.distsq = sum;
+    }
+  }
+  if (st.knew > 0) {
+    dist = sqrt(st.distsq);
+    if (st.ntrits == -1) {
+      st.delta = bq_min(tenth * st.delta, half * dist);
+      if (st.delta <= st.rho * 1.5) st.delta = st.rho;
+    }
+    st.ntrits = 0;
+    st.adelt = bq_max(bq_min(tenth * dist, st.delta), st.rho);
+    st.dsq = st.adelt * st.adelt;
+    goto L90;
+  }
+  if (st.ntrits == -1) goto L680;
+  if (st.ratio > zero) goto L60;
+  if (bq_max(st.delta, st.dnorm) > st.rho) goto L60;
+L680:
+  if (st.rho > st.rhoend) {
+    st.delta = half * st.rho;
+    st.ratio = st.rho / st.rhoend;
+    if (st.ratio <= 16.) st.rho = st.rhoend;
+    else if (st.ratio <= 250.) st.rho = sqrt(st.ratio) * st.rhoend;
+    else st.rho = tenth * st.rho;
+    st.delta = bq_max(st.delta, st.rho);
+    st.ntrits = 0;
+    st.nfsav = st.nf;
+    goto L60;
+  }
+  if (st.ntrits == -1) goto L360;
+  st.rc = BQR_XTOL;
+L720:
+  if (st.fval[st.kopt] <= st.fsave) {
+    for (int i = 1; i <= BQN; ++i) {
+      st.x[i] = bq_min(bq_max(st.xl[i], st.xbase[i] + st.xopt[i]), st.xu[i]);
+      if (st.xopt[i] == st.sl[i]) st.x[i] = st.xl[i];
+      if (st.xopt[i] == st.su[i]) st.x[i] = st.xu[i];
+    }
+    st.f = st.fval[st.kopt];
+  }
+  st.minf = st.f;
+  for (int i = 0; i < BQN; ++i) st.xout[i] = st.x[i + 1] * st.s[i];
+  st.resume = -1;
+  return BQ_DONE;
+}
+
+#undef BQ_CALFUN
+
+}  // namespace pmvsdev

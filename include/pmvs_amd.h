@@ -1,0 +1,185 @@
+/*
+ * pmvs_amd.h -- C-ABI of the MI355X-native PMVS2 dense-matching core.
+ *
+ * The reference (robjermy/CMVS-PMVS) has no plugin/FFI surface for its hot path: the stages
+ * share one CFindMatch& (reference include/pmvs/findMatch.hpp:150-163).  This ABI is the
+ * boundary SURVEY.md §8(b) defines; each entry point names the reference interface it
+ * replaces.  Plain pointers and sizes only; no exceptions cross it; errors are status codes
+ * with a message from pmvs_last_error().  Never calls exit().
+ *
+ * Index convention: every image number below is an *index* into the scene's view list
+ * (targets first, then other images), exactly like the reference's internal _images
+ * (CPatchOrganizerS::image2index / index2image, patchOrganizerS.cpp:16-52).
+ *
+ * Ownership: all input/output arrays belong to the caller (host memory); a scene owns its
+ * device memory.  Threading: calls on one scene are serialised on that scene's HIP stream;
+ * different scenes (one per GPU) may be driven from different host threads.
+ */
+#ifndef PMVS_AMD_H
+#define PMVS_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PMVS_MAX_IMAGES 64 /* capacity of one patch's image list (reference: unbounded vector) */
+#define PMVS_MAX_TAU 16    /* max textures in the objective: tau = min(2*minImageNum, num) */
+#define PMVS_MAX_LEVEL 4   /* reference MyPow2 table limits level to <= 4 (optim.cpp:808-811) */
+
+typedef enum pmvs_status {
+  PMVS_OK = 0,
+  PMVS_EINVAL = 1,      /* invalid argument */
+  PMVS_EDEVICE = 2,     /* HIP runtime error */
+  PMVS_ENOMEM = 3,      /* allocation failure */
+  PMVS_EUNSUPPORTED = 4 /* configuration outside the supported envelope */
+} pmvs_status;
+
+/* Outcome of one candidate in pmvs_refine_batch (CSeed::initialMatchSub seed.cpp:387-414,
+ * CExpand::expandSub expand.cpp:225-237: preProcess -> refinePatch -> postProcess). */
+typedef enum pmvs_candidate_status {
+  PMVS_ACCEPTED = 0,      /* postProcess returned 0 */
+  PMVS_FAIL_PRE = 1,      /* COptim::preProcess returned 1 */
+  PMVS_FAIL_POST = 2,     /* COptim::postProcess returned 1 */
+  PMVS_FAIL_OVERFLOW = 3  /* image list exceeded PMVS_MAX_IMAGES (not a reference outcome) */
+} pmvs_candidate_status;
+
+/* One view: CPhoto = CImage (pyramid) + CCamera (projection), reference include/image/photo.hpp. */
+typedef struct pmvs_view_desc {
+  int32_t width, height;    /* level-0 size */
+  const uint8_t* rgb;       /* width*height*3 interleaved RGB8, row-major (CImage::_images[0]) */
+  const uint8_t* mask;      /* optional width*height, 0 = outside; NULL = no mask */
+  const uint8_t* edge;      /* optional width*height; NULL = no edge map */
+  float projection[12];     /* level-0 3x4 projection, row-major (txt/%08d.txt, CCamera::init) */
+} pmvs_view_desc;
+
+/* Scene: SOption (option.cpp:10-28,30-158) + CFindMatch::init (findMatch.cpp:30-107). */
+typedef struct pmvs_scene_desc {
+  int32_t num_views;          /* _num = |timages| + |oimages| */
+  int32_t num_targets;        /* _tnum = |timages| */
+  int32_t level;              /* option level (0..PMVS_MAX_LEVEL) */
+  int32_t csize;              /* option csize */
+  int32_t wsize;              /* option wsize (odd) */
+  int32_t min_image_num;      /* option minImageNum */
+  float threshold;            /* option threshold (initial _nccThreshold) */
+  float max_angle;            /* SOption::_maxAngleThreshold in radians (maxAngle * M_PI/180) */
+  float quad_threshold;       /* option quad */
+  int32_t sequence;           /* option sequence (-1 = off) */
+  const int32_t* visdata2_offsets; /* CSR row starts, num_views+1 entries (SOption::_visdata2) */
+  const int32_t* visdata2;         /* CSR column indexes */
+  int32_t num_bindexes;            /* SOption::_bindexes (useBound) */
+  const int32_t* bindexes;
+  const pmvs_view_desc* views;     /* num_views entries */
+} pmvs_scene_desc;
+
+/* A patch candidate before preProcess (Patch::CPatch, reference include/pmvs/patch.hpp:10-77). */
+typedef struct pmvs_candidate {
+  float coord[4];  /* _coord, w = 1 */
+  float normal[4]; /* _normal, w = 0 */
+  float dscale;    /* initial _dscale (0 for a freshly constructed CPatch) */
+  int32_t num_images;
+  int32_t images[PMVS_MAX_IMAGES]; /* _images (indexes); [0] is the reference image */
+} pmvs_candidate;
+
+/* A candidate after preProcess -> refinePatch -> postProcess. */
+typedef struct pmvs_refined {
+  int32_t status;      /* pmvs_candidate_status */
+  int32_t refine_code; /* optimizer result, NLopt numbering (4 = XTOL_REACHED, 5 = MAXEVAL, -4 = ROUNDOFF) */
+  int32_t evals;       /* objective evaluations (COptim::my_f calls) in refinePatch */
+  int32_t num_images;
+  float coord[4];
+  float normal[4];
+  float ncc;           /* _ncc (stays -1 if refinement failed, as in the reference) */
+  float dscale;
+  float ascale;
+  float tmp;           /* _tmp = score2(nccThreshold) */
+  int32_t timages;
+  int32_t reserved;
+  int32_t images[PMVS_MAX_IMAGES];
+  int32_t grids[PMVS_MAX_IMAGES][2]; /* _grids (cell x, cell y) per image */
+} pmvs_refined;
+
+/* Objective query: the refine state of refinePatchBFGS (optim.cpp:580-599) for a patch, and
+ * an optimizer point x at which COptim::my_f (optim.cpp:507-578) is evaluated. */
+typedef struct pmvs_eval_query {
+  float coord[4];
+  float normal[4];
+  float dscale;
+  int32_t num_images;
+  int32_t images[PMVS_MAX_TAU]; /* first min(tau, num_images) are used */
+  double x[3];
+} pmvs_eval_query;
+
+/* One texture grab: COptim::grabTex (optim.cpp:815-863) followed by COptim::normalize
+ * (optim.cpp:1031-1067) when valid. */
+typedef struct pmvs_tex_query {
+  float coord[4];
+  float pxaxis[4];
+  float pyaxis[4];
+  float normal[4];
+  int32_t view;
+  int32_t normalize; /* 1 = apply normalize() to a valid texture */
+} pmvs_tex_query;
+
+typedef struct pmvs_stats {
+  int64_t candidates;
+  int64_t accepted;
+  int64_t fail_pre;
+  int64_t fail_post;
+  int64_t refine_failed;  /* optimizer result not in {SUCCESS, STOPVAL, FTOL, XTOL} */
+  int64_t evals;          /* my_f evaluations inside refinePatch */
+  int64_t tex_valid;      /* sum over those evaluations of valid textures (algorithmic bytes = 588*this for wsize 7) */
+  int64_t tex_grabs;      /* every grabTex executed (incl. pre/post-processing) */
+  double kernel_ms;       /* device time of the last call's kernels (HIP events on the scene stream) */
+} pmvs_stats;
+
+typedef struct pmvs_scene pmvs_scene;
+
+/* Last error message of the calling thread (never NULL). */
+const char* pmvs_last_error(void);
+
+/* Number of visible HIP devices (0 if none). */
+int32_t pmvs_device_count(void);
+
+/* Replaces CFindMatch::init's image/camera setup (findMatch.cpp:30-107): CPhotoSetS::init
+ * (photoSetS.cpp:12-80) + CImage::buildImage pyramids (image.cpp:228-325, built ON DEVICE),
+ * CCamera::updateCamera (camera.cpp:109-138), COptim::setAxesScales (optim.cpp:43-64) and the
+ * threshold defaults (findMatch.cpp:92-106).  Copies everything to device `device`. */
+pmvs_status pmvs_scene_create(const pmvs_scene_desc* desc, int32_t device, pmvs_scene** out);
+
+void pmvs_scene_destroy(pmvs_scene* scene);
+
+/* CFindMatch::updateThreshold semantics (findMatch.cpp:23-28) made explicit, plus _depth. */
+pmvs_status pmvs_set_thresholds(pmvs_scene* scene, float ncc, float ncc_before, int32_t depth);
+
+/* Read back one pyramid level of one view (parity of CImage::buildImage). */
+pmvs_status pmvs_scene_get_level(pmvs_scene* scene, int32_t view, int32_t level, uint8_t* out,
+                                 int32_t* width, int32_t* height);
+
+/* Batched COptim::grabTex + normalize: out_tex is n * 3*wsize*wsize floats, out_valid n ints
+ * (1 = texture grabbed, 0 = grabTex returned 1 / empty texture). */
+pmvs_status pmvs_grab_tex(pmvs_scene* scene, const pmvs_tex_query* q, int32_t n, float* out_tex,
+                          int32_t* out_valid);
+
+/* Batched COptim::my_f: out_f[i] = my_f(q[i].x) after the refinePatchBFGS setup of q[i]. */
+pmvs_status pmvs_incc_eval(pmvs_scene* scene, const pmvs_eval_query* q, int32_t n, double* out_f,
+                           pmvs_stats* stats);
+
+/* Batched preProcess -> refinePatch -> postProcess (optim.cpp:95-190, 496-658) for n candidates
+ * at the scene's current thresholds and depth (depth must be 0 in this release: the
+ * depth >= 1 organizer steps setVImagesVGrids/check are not part of this call). */
+pmvs_status pmvs_refine_batch(pmvs_scene* scene, const pmvs_candidate* in, int32_t n,
+                              pmvs_refined* out, pmvs_stats* stats);
+
+/* Device-resident variant for benchmarking: candidates/results already on the device
+ * (pointers from hipMalloc / torch).  Launches on the scene stream, does not synchronise;
+ * call pmvs_scene_sync() and read stats afterwards. */
+pmvs_status pmvs_refine_batch_device(pmvs_scene* scene, const pmvs_candidate* d_in, int32_t n,
+                                     pmvs_refined* d_out);
+pmvs_status pmvs_scene_sync(pmvs_scene* scene, pmvs_stats* stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PMVS_AMD_H */

@@ -1,0 +1,148 @@
+// oracle/ref_driver.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// A thin extern "C" driver around the reference's own, unmodified translation units that
+// compile in this image without any stand-in headers (see oracle/Makefile):
+//   /root/reference/source/image/camera.cpp  (CCamera: CONTOUR parsing, per-level projections,
+//                                             optical centre/axis, camera axes)
+//   /root/reference/source/pmvs/option.cpp   (SOption: pmvs2 option-file parsing, vis.dat)
+//   /root/reference/source/pmvs/patch.cpp    (CPatch text serialisation, operator<< / >>)
+// plus the header-only numeric library (include/numeric/*.hpp) and the inline
+// CCamera::project (include/image/camera.hpp:89-108).  The resulting oracle/_ref/libpmvs_ref.so
+// pins the oracle restatement and the product's host plumbing bit-for-bit on those pieces.
+// It is built only in the build container (where /root/reference exists) and is never
+// linked into the product.
+#include <cstring>
+#include <fstream>
+#include <iomanip>
+#include <limits>
+#include <sstream>
+#include <string>
+
+#include "image/camera.hpp"
+#include "pmvs/option.hpp"
+#include "pmvs/patch.hpp"
+
+namespace {
+// Exposes the protected camera axes computed by CCamera::updateCamera (camera.cpp:117-121),
+// which are the same formulas COptim::setAxesScales uses (optim.cpp:48-52).
+struct CamProbe : public Image::CCamera {
+  void axes(float* out) const {
+    for (int i = 0; i < 3; ++i) {
+      out[i] = _xaxis[i];
+      out[3 + i] = _yaxis[i];
+      out[6 + i] = _zaxis[i];
+    }
+  }
+};
+}  // namespace
+
+extern "C" {
+
+// out: [0..3] center, [4..7] oaxis, [8..16] x/y/z axes, [17..28] P at `level`.
+int ref_camera(const char* txt, int max_level, int level, float* out) {
+  CamProbe cam;
+  cam.init(txt, max_level);
+  const Vec4f c = cam.OpticalCenter(), a = cam.OpticalAxis();
+  for (int i = 0; i < 4; ++i) {
+    out[i] = c[i];
+    out[4 + i] = a[i];
+  }
+  cam.axes(out + 8);
+  const auto P = cam.ProjectionMatrix();
+  for (int y = 0; y < 3; ++y)
+    for (int x = 0; x < 4; ++x) out[17 + 4 * y + x] = P[level][y][x];
+  return 0;
+}
+
+int ref_project(const char* txt, int max_level, int level, const float* coords4, int n, float* out3) {
+  Image::CCamera cam;
+  cam.init(txt, max_level);
+  for (int i = 0; i < n; ++i) {
+    const Vec4f c(coords4[4 * i], coords4[4 * i + 1], coords4[4 * i + 2], coords4[4 * i + 3]);
+    const Vec3f r = cam.project(c, level);
+    out3[3 * i] = r[0];
+    out3[3 * i + 1] = r[1];
+    out3[3 * i + 2] = r[2];
+  }
+  return 0;
+}
+
+// SOption::init(prefix, option).  Scalars: [level, csize, wsize, minImageNum, CPU, useBound,
+// useVisData, sequence, tflag, oflag] in iout[0..9]; [threshold, setEdge, maxAngle, quad] in
+// fout[0..3].  timages/oimages/bindexes and visdata2 (CSR) written to the arrays given
+// (capacity cap each); counts in iout[10..13] = ntimages, noimages, nbindexes, nvis.
+int ref_option(const char* prefix, const char* option, int* iout, float* fout, int* timages, int* oimages,
+               int* bindexes, int* vis_off, int* vis, int cap) {
+  PMVS3::SOption o;
+  o.init(prefix, option);
+  iout[0] = o._level; iout[1] = o._csize; iout[2] = o._wsize; iout[3] = o._minImageNum; iout[4] = o._CPU;
+  iout[5] = o._useBound; iout[6] = o._useVisData; iout[7] = o._sequence; iout[8] = o._tflag; iout[9] = o._oflag;
+  fout[0] = o._threshold; fout[1] = o._setEdge; fout[2] = o._maxAngleThreshold; fout[3] = o._quadThreshold;
+  iout[10] = (int)o._timages.size();
+  iout[11] = (int)o._oimages.size();
+  iout[12] = (int)o._bindexes.size();
+  for (int i = 0; i < (int)o._timages.size() && i < cap; ++i) timages[i] = o._timages[i];
+  for (int i = 0; i < (int)o._oimages.size() && i < cap; ++i) oimages[i] = o._oimages[i];
+  for (int i = 0; i < (int)o._bindexes.size() && i < cap; ++i) bindexes[i] = o._bindexes[i];
+  int k = 0;
+  vis_off[0] = 0;
+  for (int r = 0; r < (int)o._visdata2.size(); ++r) {
+    for (int v : o._visdata2[r])
+      if (k < cap) vis[k++] = v;
+    vis_off[r + 1] = k;
+  }
+  iout[13] = k;
+  return 0;
+}
+
+// CPatch serialisation exactly as CPatchOrganizerS::writePatches2 emits it
+// (patchOrganizerS.cpp:98-116: setprecision(max_digits10), "PATCHES\n<n>\n", patch << "\n").
+// Each patch: coord[4], normal[4], ncc, dscale, ascale (11 floats at fin[11*p]); image ids in
+// ids (nimg[p] each) and vimage ids in vids (nvimg[p] each).  Returns bytes written to out.
+int ref_write_patches(int n, const float* fin, const int* nimg, const int* ids, const int* nvimg,
+                      const int* vids, char* out, int cap) {
+  std::ostringstream ofstr;
+  ofstr << std::setprecision(std::numeric_limits<double>::max_digits10);
+  ofstr << "PATCHES" << std::endl << n << std::endl;
+  int ki = 0, kv = 0;
+  for (int p = 0; p < n; ++p) {
+    Patch::CPatch patch;
+    const float* f = fin + 11 * p;
+    patch._coord = Vec4f(f[0], f[1], f[2], f[3]);
+    patch._normal = Vec4f(f[4], f[5], f[6], f[7]);
+    patch._ncc = f[8];
+    patch._dscale = f[9];
+    patch._ascale = f[10];
+    for (int i = 0; i < nimg[p]; ++i) patch._images.push_back(ids[ki++]);
+    for (int i = 0; i < nvimg[p]; ++i) patch._vimages.push_back(vids[kv++]);
+    ofstr << patch << "\n";
+  }
+  const std::string s = ofstr.str();
+  const int len = (int)s.size();
+  if (len < cap) std::memcpy(out, s.data(), len + 1);
+  return len;
+}
+
+// .pset lines (patchOrganizerS.cpp:118-131): default stream precision.
+int ref_write_pset(int n, const float* fin, char* out, int cap) {
+  std::ostringstream ofstr;
+  for (int p = 0; p < n; ++p) {
+    const float* f = fin + 11 * p;
+    ofstr << f[0] << ' ' << f[1] << ' ' << f[2] << ' ' << f[4] << ' ' << f[5] << ' ' << f[6] << "\n";
+  }
+  const std::string s = ofstr.str();
+  const int len = (int)s.size();
+  if (len < cap) std::memcpy(out, s.data(), len + 1);
+  return len;
+}
+
+// Header-only numeric library: ortho (vec4.hpp:303-322) used by CExpand::findEmptyBlocks.
+void ref_ortho(const float* z, float* out) {
+  Vec4f zz(z[0], z[1], z[2], z[3]), x, y;
+  ortho(zz, x, y);
+  for (int i = 0; i < 4; ++i) {
+    out[i] = x[i];
+    out[4 + i] = y[i];
+  }
+}
+}
