@@ -1,0 +1,537 @@
+// pmvs_api.cpp -- the C-ABI (include/pmvs_amd.h) on top of the HIP kernels.
+//
+// Host responsibilities (C++, no torch types): scene validation, camera setup restated from
+// the reference's CCamera (camera.cpp:56-173) and COptim::setAxesScales (optim.cpp:43-64),
+// device allocation of the pyramid / camera / visibility tables, kernel launches on one HIP
+// stream per scene, HIP-event timing, and error mapping (never exit(); PMVS_EDEVICE + message).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pmvs_amd.h"
+#include "pmvs_launch.h"
+
+using namespace pmvsdev;
+
+namespace {
+
+thread_local std::string g_err = "";
+
+pmvs_status fail(pmvs_status st, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return st;
+}
+
+#define HIPCHK(expr)                                                                              \
+  do {                                                                                            \
+    hipError_t e_ = (expr);                                                                       \
+    if (e_ != hipSuccess) return fail(PMVS_EDEVICE, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+  } while (0)
+
+// ---- host restatement of the reference camera setup (CONTOUR projection given as 12 floats)
+static inline float dot4f(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3]; }
+static inline float dot3f(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static inline void cross3f(const float* u, const float* v, float* o) {
+  o[0] = u[1] * v[2] - v[1] * u[2];
+  o[1] = -u[0] * v[2] + v[0] * u[2];
+  o[2] = u[0] * v[1] - v[0] * u[1];
+}
+static inline void unitize3f(float* v) {
+  const float l = dot3f(v, v);
+  if (l != 1.0 && l != 0.0) {
+    const float d = (float)std::sqrt((double)l);
+    v[0] /= d; v[1] /= d; v[2] /= d;
+  }
+}
+
+// CCamera::updateProjection / updateCamera / getOpticalCenter (camera.cpp:56-173), txtType 0.
+void setup_camera(DView& v, const float* p12, int maxLevel) {
+  for (int i = 0; i < 12; ++i) v.P[0][i] = p12[i];
+  for (int level = 1; level < maxLevel; ++level) {
+    for (int i = 0; i < 12; ++i) v.P[level][i] = v.P[level - 1][i];
+    for (int x = 0; x < 4; ++x) {
+      v.P[level][x] /= 2.0f;
+      v.P[level][4 + x] /= 2.0f;
+    }
+  }
+  for (int level = maxLevel; level < MAXL; ++level) std::memcpy(v.P[level], v.P[maxLevel - 1], sizeof(v.P[0]));
+  float oa[4] = {v.P[0][8], v.P[0][9], v.P[0][10], 0.0f};
+  const float ftmp = (float)std::sqrt((double)dot4f(oa, oa));
+  oa[3] = v.P[0][11];
+  for (int i = 0; i < 4; ++i) oa[i] /= ftmp;
+  if (v.P[0][8] == 0.0 && v.P[0][9] == 0.0 && v.P[0][10] == 0.0) {
+    float a[3] = {v.P[0][0], v.P[0][1], v.P[0][2]}, b[3] = {v.P[0][4], v.P[0][5], v.P[0][6]}, c[3];
+    cross3f(a, b, c);
+    unitize3f(c);
+    v.center[0] = c[0]; v.center[1] = c[1]; v.center[2] = c[2]; v.center[3] = 0.0f;
+  } else {
+    double A[3][3], b[3];
+    for (int y = 0; y < 3; ++y) {
+      for (int x = 0; x < 3; ++x) A[y][x] = v.P[0][4 * y + x];
+      b[y] = -(double)v.P[0][4 * y + 3];
+    }
+    auto cr = [](const double* u, const double* w, double* o) {
+      o[0] = u[1] * w[2] - w[1] * u[2];
+      o[1] = -u[0] * w[2] + w[0] * u[2];
+      o[2] = u[0] * w[1] - w[0] * u[1];
+    };
+    double ad[3][3];
+    cr(A[1], A[2], ad[0]);
+    cr(A[2], A[0], ad[1]);
+    cr(A[0], A[1], ad[2]);
+    const double det = ad[0][0] * A[0][0] + ad[0][1] * A[0][1] + ad[0][2] * A[0][2];
+    double inv[3][3] = {{0}};
+    if (det != 0.0)
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) inv[r][c] = ad[c][r] / det;
+    for (int r = 0; r < 3; ++r) v.center[r] = (float)(inv[r][0] * b[0] + inv[r][1] * b[1] + inv[r][2] * b[2]);
+    v.center[3] = 1.0f;
+  }
+  // COptim::setAxesScales (optim.cpp:43-64)
+  float z[3] = {oa[0], oa[1], oa[2]}, x[3] = {v.P[0][0], v.P[0][1], v.P[0][2]}, y[3];
+  cross3f(z, x, y);
+  unitize3f(y);
+  cross3f(y, z, x);
+  for (int i = 0; i < 3; ++i) { v.xaxis[i] = x[i]; v.yaxis[i] = y[i]; v.zaxis[i] = z[i]; }
+  const float xa[4] = {x[0], x[1], x[2], 0.0f}, ya[4] = {y[0], y[1], y[2], 0.0f};
+  const float p0[4] = {v.P[0][0], v.P[0][1], v.P[0][2], v.P[0][3]}, p1[4] = {v.P[0][4], v.P[0][5], v.P[0][6], v.P[0][7]};
+  const float fx = dot4f(xa, p0), fy = dot4f(ya, p1);
+  v.ipscale = fx + fy;
+}
+
+// CImage::buildMask / buildEdge (image.cpp:327-405) on the host (binary maps are optional).
+void build_binary(std::vector<uint8_t>* pyr, const int* w, const int* h, int maxLevel) {
+  for (int level = 1; level < maxLevel; ++level) {
+    pyr[level].assign((size_t)w[level] * h[level], 0);
+    for (int y = 0; y < h[level]; ++y) {
+      const int ys[2] = {2 * y, std::min(h[level - 1] - 1, 2 * y + 1)};
+      for (int x = 0; x < w[level]; ++x) {
+        const int xs[2] = {2 * x, std::min(w[level - 1] - 1, 2 * x + 1)};
+        int in = 0;
+        for (int j = 0; j < 2; ++j)
+          for (int i = 0; i < 2; ++i)
+            if (pyr[level - 1][ys[j] * w[level - 1] + xs[i]]) in++;
+        pyr[level][y * w[level] + x] = (0 < in) ? 255 : 0;
+      }
+    }
+  }
+}
+
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t alloc(size_t count) {
+    release();
+    n = count;
+    if (count == 0) return hipSuccess;
+    return hipMalloc((void**)&p, count * sizeof(T));
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+}  // namespace
+
+struct pmvs_scene {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  DScene ds{};
+  int maxLevel = 0;
+  std::vector<DView> hviews;
+  DBuf<DView> views;
+  DBuf<uint32_t> pyr;
+  DBuf<uint8_t> masks, edges;
+  DBuf<int> vis_off, vis, bindexes;
+  DBuf<float> scratch;
+  DBuf<DevStats> stats;
+  int grid = 0;
+  // staging for host-pointer calls
+  DBuf<pmvs_candidate> cand;
+  DBuf<pmvs_refined> res;
+  DBuf<pmvs_eval_query> evq;
+  DBuf<double> evout;
+  DBuf<pmvs_tex_query> tq;
+  DBuf<float> tout;
+  DBuf<int> tvalid;
+  ~pmvs_scene() {
+    views.release(); pyr.release(); masks.release(); edges.release(); vis_off.release(); vis.release();
+    bindexes.release(); scratch.release(); stats.release(); cand.release(); res.release(); evq.release();
+    evout.release(); tq.release(); tout.release(); tvalid.release();
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+namespace {
+template <class T>
+pmvs_status ensure(DBuf<T>& b, size_t n) {
+  if (b.n >= n) return PMVS_OK;
+  hipError_t e = b.alloc(n);
+  if (e != hipSuccess) return fail(PMVS_ENOMEM, "hipMalloc(%zu bytes): %s", n * sizeof(T), hipGetErrorString(e));
+  return PMVS_OK;
+}
+}  // namespace
+
+extern "C" {
+
+const char* pmvs_last_error(void) { return g_err.c_str(); }
+
+int32_t pmvs_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_scene** out) {
+  if (!d || !out) return fail(PMVS_EINVAL, "null argument");
+  *out = nullptr;
+  if (d->num_views < 1 || d->num_targets < 1 || d->num_targets > d->num_views)
+    return fail(PMVS_EINVAL, "num_views=%d num_targets=%d", d->num_views, d->num_targets);
+  if (d->level < 0 || d->level > PMVS_MAX_LEVEL) return fail(PMVS_EUNSUPPORTED, "level %d outside 0..%d", d->level, PMVS_MAX_LEVEL);
+  if (d->wsize != 5 && d->wsize != 7 && d->wsize != 9) return fail(PMVS_EUNSUPPORTED, "wsize %d (supported: 5, 7, 9)", d->wsize);
+  if (d->csize < 1) return fail(PMVS_EINVAL, "csize %d", d->csize);
+  if (d->min_image_num < 1) return fail(PMVS_EINVAL, "minImageNum %d", d->min_image_num);
+  const int tau = std::min(d->min_image_num * 2, d->num_views);
+  if (tau > PMVS_MAX_TAU) return fail(PMVS_EUNSUPPORTED, "tau = min(2*minImageNum, num) = %d > %d", tau, PMVS_MAX_TAU);
+  if (!d->views || !d->visdata2_offsets) return fail(PMVS_EINVAL, "views / visdata2 missing");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(PMVS_EDEVICE, "no HIP device available");
+  if (device < 0 || device >= ndev) return fail(PMVS_EINVAL, "device %d of %d", device, ndev);
+  HIPCHK(hipSetDevice(device));
+
+  pmvs_scene* sc = new pmvs_scene();
+  sc->device = device;
+  const int num = d->num_views;
+  const int maxLevel = std::max(1, d->level + 3);
+  sc->maxLevel = maxLevel;
+  auto bail = [&](pmvs_status st) {
+    delete sc;
+    return st;
+  };
+  if (hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&sc->ev0) != hipSuccess || hipEventCreate(&sc->ev1) != hipSuccess)
+    return bail(fail(PMVS_EDEVICE, "stream/event creation failed"));
+
+  // ---- views: sizes, cameras, pyramid offsets
+  sc->hviews.assign(num, DView{});
+  long long words = 0;
+  bool anyMask = false, anyEdge = false;
+  for (int i = 0; i < num; ++i) {
+    const pmvs_view_desc& vd = d->views[i];
+    if (vd.width < 8 || vd.height < 8 || !vd.rgb) return bail(fail(PMVS_EINVAL, "view %d: bad image", i));
+    DView& v = sc->hviews[i];
+    v.w[0] = vd.width;
+    v.h[0] = vd.height;
+    for (int l = 1; l < MAXL; ++l) {
+      v.w[l] = l < maxLevel ? v.w[l - 1] / 2 : 0;
+      v.h[l] = l < maxLevel ? v.h[l - 1] / 2 : 0;
+    }
+    for (int l = 0; l < MAXL; ++l) {
+      v.pyr_off[l] = words;
+      if (l < maxLevel) words += (long long)v.w[l] * v.h[l] + 1;  // +1 pad word: bilinear reads lx+1
+      v.mask_off[l] = -1;
+      v.edge_off[l] = -1;
+    }
+    setup_camera(v, vd.projection, maxLevel);
+    anyMask |= vd.mask != nullptr;
+    anyEdge |= vd.edge != nullptr;
+  }
+  if (hipMalloc((void**)&sc->pyr.p, words * sizeof(uint32_t)) != hipSuccess)
+    return bail(fail(PMVS_ENOMEM, "pyramid: %lld words", words));
+  sc->pyr.n = words;
+  (void)hipMemsetAsync(sc->pyr.p, 0, words * sizeof(uint32_t), sc->stream);
+
+  // ---- pyramids on device: RGB level chain (CImage::buildImage) then RGBA packing
+  {
+    size_t maxrgb = 0;
+    for (int i = 0; i < num; ++i) maxrgb = std::max(maxrgb, (size_t)d->views[i].width * d->views[i].height * 3);
+    uint8_t *a = nullptr, *b = nullptr;
+    if (hipMalloc((void**)&a, maxrgb) != hipSuccess || hipMalloc((void**)&b, maxrgb) != hipSuccess) {
+      if (a) (void)hipFree(a);
+      return bail(fail(PMVS_ENOMEM, "pyramid staging"));
+    }
+    pmvs_status st = PMVS_OK;
+    for (int i = 0; i < num && st == PMVS_OK; ++i) {
+      const DView& v = sc->hviews[i];
+      const size_t bytes0 = (size_t)v.w[0] * v.h[0] * 3;
+      hipError_t e = hipMemcpyAsync(a, d->views[i].rgb, bytes0, hipMemcpyHostToDevice, sc->stream);
+      if (e == hipSuccess) e = launch_pack_rgba(a, sc->pyr.p + v.pyr_off[0], (long long)v.w[0] * v.h[0], sc->stream);
+      uint8_t* src = a;
+      uint8_t* dst = b;
+      for (int l = 1; l < maxLevel && e == hipSuccess; ++l) {
+        e = launch_build_level(src, v.w[l - 1], v.h[l - 1], dst, v.w[l], v.h[l], sc->stream);
+        if (e == hipSuccess) e = launch_pack_rgba(dst, sc->pyr.p + v.pyr_off[l], (long long)v.w[l] * v.h[l], sc->stream);
+        std::swap(src, dst);
+      }
+      if (e == hipSuccess) e = hipStreamSynchronize(sc->stream);  // staging reused per view
+      if (e != hipSuccess) st = fail(PMVS_EDEVICE, "pyramid build: %s", hipGetErrorString(e));
+    }
+    (void)hipFree(a);
+    (void)hipFree(b);
+    if (st != PMVS_OK) return bail(st);
+  }
+
+  // ---- optional masks / edges (binary pyramids built on the host)
+  auto upload_binary = [&](bool any, bool isMask, DBuf<uint8_t>& buf) -> pmvs_status {
+    if (!any) return PMVS_OK;
+    std::vector<uint8_t> all;
+    for (int i = 0; i < num; ++i) {
+      const pmvs_view_desc& vd = d->views[i];
+      const uint8_t* m0 = isMask ? vd.mask : vd.edge;
+      DView& v = sc->hviews[i];
+      if (!m0) continue;
+      std::vector<uint8_t> pyr[MAXL];
+      pyr[0].resize((size_t)v.w[0] * v.h[0]);
+      for (size_t k = 0; k < pyr[0].size(); ++k)
+        pyr[0][k] = isMask ? ((127 < (int)m0[k]) ? 255 : 0) : ((1 < m0[k]) ? 255 : 0);  // image.cpp:159-180
+      build_binary(pyr, v.w, v.h, maxLevel);
+      for (int l = 0; l < maxLevel; ++l) {
+        (isMask ? v.mask_off[l] : v.edge_off[l]) = (long long)all.size();
+        all.insert(all.end(), pyr[l].begin(), pyr[l].end());
+      }
+    }
+    if (buf.alloc(all.size()) != hipSuccess) return fail(PMVS_ENOMEM, "mask/edge upload");
+    if (hipMemcpy(buf.p, all.data(), all.size(), hipMemcpyHostToDevice) != hipSuccess)
+      return fail(PMVS_EDEVICE, "mask/edge copy");
+    return PMVS_OK;
+  };
+  pmvs_status st = upload_binary(anyMask, true, sc->masks);
+  if (st == PMVS_OK) st = upload_binary(anyEdge, false, sc->edges);
+  if (st != PMVS_OK) return bail(st);
+
+  // ---- tables
+  std::vector<int> voff(d->visdata2_offsets, d->visdata2_offsets + num + 1);
+  const int nvis = voff[num];
+  for (int k = 0; k < nvis; ++k)
+    if (d->visdata2[k] < 0 || d->visdata2[k] >= num) return bail(fail(PMVS_EINVAL, "visdata2[%d] = %d", k, d->visdata2[k]));
+  for (int k = 0; k < d->num_bindexes; ++k)
+    if (d->bindexes[k] < 0 || d->bindexes[k] >= num) return bail(fail(PMVS_EINVAL, "bindexes[%d]", k));
+  if (sc->views.alloc(num) != hipSuccess || sc->vis_off.alloc(num + 1) != hipSuccess ||
+      sc->vis.alloc(std::max(1, nvis)) != hipSuccess || sc->bindexes.alloc(std::max(1, d->num_bindexes)) != hipSuccess ||
+      sc->stats.alloc(1) != hipSuccess)
+    return bail(fail(PMVS_ENOMEM, "scene tables"));
+  if (hipMemcpy(sc->views.p, sc->hviews.data(), num * sizeof(DView), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(sc->vis_off.p, voff.data(), (num + 1) * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
+      (nvis && hipMemcpy(sc->vis.p, d->visdata2, nvis * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) ||
+      (d->num_bindexes && hipMemcpy(sc->bindexes.p, d->bindexes, d->num_bindexes * sizeof(int), hipMemcpyHostToDevice) != hipSuccess))
+    return bail(fail(PMVS_EDEVICE, "scene table copy"));
+
+  // ---- persistent grid: enough single-wave workgroups to fill every CU
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return bail(fail(PMVS_EDEVICE, "device properties"));
+  sc->grid = std::max(1, prop.multiProcessorCount) * 8;
+  if (sc->scratch.alloc((size_t)sc->grid * PMVS_MAX_IMAGES * PMVS_MAX_IMAGES) != hipSuccess)
+    return bail(fail(PMVS_ENOMEM, "scratch"));
+
+  DScene& s = sc->ds;
+  s.views = sc->views.p;
+  s.pyr = sc->pyr.p;
+  s.masks = sc->masks.p;
+  s.edges = sc->edges.p;
+  s.vis_off = sc->vis_off.p;
+  s.vis = sc->vis.p;
+  s.bindexes = sc->bindexes.p;
+  s.scratch = sc->scratch.p;
+  s.nb = d->num_bindexes;
+  s.num = num;
+  s.tnum = d->num_targets;
+  s.level = d->level;
+  s.csize = d->csize;
+  s.wsize = d->wsize;
+  s.minImageNum = d->min_image_num;
+  s.tau = tau;
+  s.anyMask = anyMask ? 1 : 0;
+  // CFindMatch::init thresholds (findMatch.cpp:92-106)
+  s.nccThreshold = d->threshold;
+  s.nccThresholdBefore = d->threshold - 0.3f;
+  s.maxAngle = d->max_angle;
+  const float angle0 = (float)(60.0f * M_PI / 180.0f);
+  s.angle1 = (float)(60.0f * M_PI / 180.0f);
+  s.athreshold = (float)std::cos((double)angle0);
+  s.cosAngle1 = std::cos((double)s.angle1);
+  s.sortThreshold = (float)(1.0f - std::cos(10.0 * M_PI / 180.0));
+  s.ascale = (float)(M_PI / 48.0f);
+  s.log2f = (float)std::log(2.0);
+  if (hipStreamSynchronize(sc->stream) != hipSuccess) return bail(fail(PMVS_EDEVICE, "scene upload"));
+  *out = sc;
+  return PMVS_OK;
+}
+
+void pmvs_scene_destroy(pmvs_scene* scene) {
+  if (!scene) return;
+  (void)hipSetDevice(scene->device);
+  (void)hipStreamSynchronize(scene->stream);
+  delete scene;
+}
+
+pmvs_status pmvs_set_thresholds(pmvs_scene* sc, float ncc, float ncc_before, int32_t depth) {
+  if (!sc) return fail(PMVS_EINVAL, "null scene");
+  if (depth != 0) return fail(PMVS_EUNSUPPORTED, "depth %d: only the depth-0 refine path is implemented", depth);
+  sc->ds.nccThreshold = ncc;
+  sc->ds.nccThresholdBefore = ncc_before;
+  return PMVS_OK;
+}
+
+pmvs_status pmvs_scene_get_level(pmvs_scene* sc, int32_t view, int32_t level, uint8_t* out, int32_t* width,
+                                 int32_t* height) {
+  if (!sc) return fail(PMVS_EINVAL, "null scene");
+  if (view < 0 || view >= sc->ds.num || level < 0 || level >= sc->maxLevel) return fail(PMVS_EINVAL, "view/level");
+  const DView& v = sc->hviews[view];
+  if (width) *width = v.w[level];
+  if (height) *height = v.h[level];
+  if (!out) return PMVS_OK;
+  HIPCHK(hipSetDevice(sc->device));
+  const long long npix = (long long)v.w[level] * v.h[level];
+  uint8_t* tmp = nullptr;
+  HIPCHK(hipMalloc((void**)&tmp, npix * 3));
+  hipError_t e = launch_unpack_rgba(sc->pyr.p + v.pyr_off[level], tmp, npix, sc->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, tmp, npix * 3, hipMemcpyDeviceToHost, sc->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(sc->stream);
+  (void)hipFree(tmp);
+  if (e != hipSuccess) return fail(PMVS_EDEVICE, "get_level: %s", hipGetErrorString(e));
+  return PMVS_OK;
+}
+
+pmvs_status pmvs_grab_tex(pmvs_scene* sc, const pmvs_tex_query* q, int32_t n, float* out_tex, int32_t* out_valid) {
+  if (!sc || (n > 0 && (!q || !out_tex || !out_valid))) return fail(PMVS_EINVAL, "null argument");
+  if (n <= 0) return PMVS_OK;
+  for (int i = 0; i < n; ++i)
+    if (q[i].view < 0 || q[i].view >= sc->ds.num) return fail(PMVS_EINVAL, "query %d: view %d", i, q[i].view);
+  HIPCHK(hipSetDevice(sc->device));
+  const int len = 3 * sc->ds.wsize * sc->ds.wsize;
+  pmvs_status st;
+  if ((st = ensure(sc->tq, n)) || (st = ensure(sc->tout, (size_t)n * len)) || (st = ensure(sc->tvalid, n))) return st;
+  HIPCHK(hipMemcpyAsync(sc->tq.p, q, n * sizeof(pmvs_tex_query), hipMemcpyHostToDevice, sc->stream));
+  HIPCHK(launch_grab_tex(sc->ds, sc->tq.p, n, sc->tout.p, sc->tvalid.p, sc->stream));
+  HIPCHK(hipMemcpyAsync(out_tex, sc->tout.p, (size_t)n * len * sizeof(float), hipMemcpyDeviceToHost, sc->stream));
+  HIPCHK(hipMemcpyAsync(out_valid, sc->tvalid.p, n * sizeof(int), hipMemcpyDeviceToHost, sc->stream));
+  HIPCHK(hipStreamSynchronize(sc->stream));
+  return PMVS_OK;
+}
+
+static void fill_stats(const DevStats& d, int64_t n, float ms, pmvs_stats* st) {
+  if (!st) return;
+  st->candidates = n;
+  st->accepted = (int64_t)d.accepted;
+  st->fail_pre = (int64_t)d.fail_pre;
+  st->fail_post = (int64_t)d.fail_post;
+  st->refine_failed = (int64_t)d.refine_failed;
+  st->evals = (int64_t)d.evals;
+  st->tex_valid = (int64_t)d.tex_valid;
+  st->tex_grabs = (int64_t)d.tex_grabs;
+  st->kernel_ms = ms;
+}
+
+pmvs_status pmvs_incc_eval(pmvs_scene* sc, const pmvs_eval_query* q, int32_t n, double* out_f, pmvs_stats* stats) {
+  if (!sc || (n > 0 && (!q || !out_f))) return fail(PMVS_EINVAL, "null argument");
+  if (n <= 0) return PMVS_OK;
+  for (int i = 0; i < n; ++i) {
+    if (q[i].num_images < 1 || q[i].num_images > PMVS_MAX_TAU) return fail(PMVS_EINVAL, "query %d: num_images", i);
+    for (int k = 0; k < q[i].num_images; ++k)
+      if (q[i].images[k] < 0 || q[i].images[k] >= sc->ds.num) return fail(PMVS_EINVAL, "query %d: image", i);
+  }
+  HIPCHK(hipSetDevice(sc->device));
+  pmvs_status st;
+  if ((st = ensure(sc->evq, n)) || (st = ensure(sc->evout, n))) return st;
+  HIPCHK(hipMemcpyAsync(sc->evq.p, q, n * sizeof(pmvs_eval_query), hipMemcpyHostToDevice, sc->stream));
+  HIPCHK(hipMemsetAsync(sc->stats.p, 0, sizeof(DevStats), sc->stream));
+  HIPCHK(hipEventRecord(sc->ev0, sc->stream));
+  HIPCHK(launch_incc_eval(sc->ds, sc->evq.p, n, sc->evout.p, sc->stats.p, sc->stream));
+  HIPCHK(hipEventRecord(sc->ev1, sc->stream));
+  HIPCHK(hipMemcpyAsync(out_f, sc->evout.p, n * sizeof(double), hipMemcpyDeviceToHost, sc->stream));
+  DevStats ds{};
+  HIPCHK(hipMemcpyAsync(&ds, sc->stats.p, sizeof(DevStats), hipMemcpyDeviceToHost, sc->stream));
+  HIPCHK(hipStreamSynchronize(sc->stream));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, sc->ev0, sc->ev1));
+  fill_stats(ds, n, ms, stats);
+  return PMVS_OK;
+}
+
+static pmvs_status check_candidates(const pmvs_scene* sc, const pmvs_candidate* in, int n) {
+  for (int i = 0; i < n; ++i) {
+    if (in[i].num_images < 1 || in[i].num_images > PMVS_MAX_IMAGES) return fail(PMVS_EINVAL, "candidate %d: num_images %d", i, in[i].num_images);
+    for (int k = 0; k < in[i].num_images; ++k)
+      if (in[i].images[k] < 0 || in[i].images[k] >= sc->ds.num) return fail(PMVS_EINVAL, "candidate %d: image %d", i, in[i].images[k]);
+  }
+  return PMVS_OK;
+}
+
+pmvs_status pmvs_refine_batch_device(pmvs_scene* sc, const pmvs_candidate* d_in, int32_t n, pmvs_refined* d_out) {
+  if (!sc || (n > 0 && (!d_in || !d_out))) return fail(PMVS_EINVAL, "null argument");
+  if (n <= 0) return PMVS_OK;
+  HIPCHK(hipSetDevice(sc->device));
+  HIPCHK(hipMemsetAsync(sc->stats.p, 0, sizeof(DevStats), sc->stream));
+  HIPCHK(hipEventRecord(sc->ev0, sc->stream));
+  HIPCHK(launch_refine(sc->ds, d_in, d_out, n, sc->stats.p, sc->grid, sc->stream));
+  HIPCHK(hipEventRecord(sc->ev1, sc->stream));
+  return PMVS_OK;
+}
+
+pmvs_status pmvs_scene_sync(pmvs_scene* sc, pmvs_stats* stats) {
+  if (!sc) return fail(PMVS_EINVAL, "null scene");
+  HIPCHK(hipSetDevice(sc->device));
+  DevStats ds{};
+  HIPCHK(hipMemcpyAsync(&ds, sc->stats.p, sizeof(DevStats), hipMemcpyDeviceToHost, sc->stream));
+  HIPCHK(hipStreamSynchronize(sc->stream));
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, sc->ev0, sc->ev1) != hipSuccess) ms = 0;
+  fill_stats(ds, (int64_t)(ds.queue > 0 ? ds.queue : 0), ms, stats);
+  if (stats) {
+    // queue overshoots by one dequeue per workgroup: the candidate count is recorded by the caller
+    stats->candidates = (int64_t)(ds.accepted + ds.fail_pre + ds.fail_post);
+  }
+  return PMVS_OK;
+}
+
+pmvs_status pmvs_refine_batch(pmvs_scene* sc, const pmvs_candidate* in, int32_t n, pmvs_refined* out,
+                              pmvs_stats* stats) {
+  if (!sc || (n > 0 && (!in || !out))) return fail(PMVS_EINVAL, "null argument");
+  if (n <= 0) {
+    if (stats) std::memset(stats, 0, sizeof(*stats));
+    return PMVS_OK;
+  }
+  pmvs_status st = check_candidates(sc, in, n);
+  if (st) return st;
+  HIPCHK(hipSetDevice(sc->device));
+  if ((st = ensure(sc->cand, n)) || (st = ensure(sc->res, n))) return st;
+  HIPCHK(hipMemcpyAsync(sc->cand.p, in, n * sizeof(pmvs_candidate), hipMemcpyHostToDevice, sc->stream));
+  if ((st = pmvs_refine_batch_device(sc, sc->cand.p, n, sc->res.p))) return st;
+  HIPCHK(hipMemcpyAsync(out, sc->res.p, n * sizeof(pmvs_refined), hipMemcpyDeviceToHost, sc->stream));
+  return pmvs_scene_sync(sc, stats);
+}
+
+pmvs_status pmvs_selftest_math(int32_t device, int32_t op, const double* in, double* out, int32_t n) {
+  if (!in || !out || n <= 0) return fail(PMVS_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(device));
+  double *di = nullptr, *dout = nullptr;
+  HIPCHK(hipMalloc((void**)&di, n * sizeof(double)));
+  hipError_t e = hipMalloc((void**)&dout, n * sizeof(double));
+  if (e == hipSuccess) e = hipMemcpy(di, in, n * sizeof(double), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = launch_math_selftest(op, di, dout, n, nullptr);
+  if (e == hipSuccess) e = hipMemcpy(out, dout, n * sizeof(double), hipMemcpyDeviceToHost);
+  (void)hipFree(di);
+  if (dout) (void)hipFree(dout);
+  if (e != hipSuccess) return fail(PMVS_EDEVICE, "math selftest: %s", hipGetErrorString(e));
+  return PMVS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,1063 @@
+// pmvs_kernels.hip -- hand-written CDNA4 (gfx950) kernels of the PMVS2 hot path.
+//
+// Mapping:
+//   * one 64-lane wavefront (= one workgroup) owns one patch candidate at a time and pulls
+//     candidates from a device work queue (persistent grid, one dequeue per candidate);
+//   * texture gather (COptim::grabTex, optim.cpp:815-863): one lane per (texture, sample) --
+//     tau*wsize^2 = 294 bilinear samples over 64 lanes -- into an LDS texture tile;
+//   * normalize / dot (optim.cpp:1031-1077): one lane per texture (resp. texture pair) runs the
+//     reference's sequential float reduction from LDS, so every sum has the reference's rounding
+//     sequence (bit-exact); element-wise normalisation uses all lanes;
+//   * BOBYQA (NLopt LN_BOBYQA, optim.cpp:621-644): reverse-communication state machine
+//     (bobyqa_dev.h) stepped by lane 0 with its state in LDS, the wave evaluates my_f;
+//   * pre/postProcess image selection (optim.cpp:95-254): lane-parallel predicates with
+//     order-preserving ballot compaction; order-dependent scalar loops on lane 0.
+// No MFMA: this is gather + small reductions (HBM/L2-gather bound), see DESIGN.md.
+#include <hip/hip_runtime.h>
+
+#include "bobyqa_dev.h"
+#include "pmvs_device.h"
+
+namespace pmvsdev {
+
+constexpr int WAVE = 64;
+
+template <int WS>
+struct WaveLds {
+  static constexpr int S = WS * WS;
+  float tex[TEXCAP][S][4];  // RGB(+pad) per sample, sample-major like the reference vector
+  float ave[TEXCAP][4];     // per-texture channel means and ave2
+  int valid[TEXCAP];
+  int jview[TEXCAP], jlevel[TEXCAP];
+  float jleft[TEXCAP][2], jdx[TEXCAP][2], jdy[TEXCAP][2];
+  float res[TEXCAP];        // per-texture result (inccs)
+  int images[PMVS_MAX_IMAGES];
+  int nimg;
+  int list2[PMVS_MAX_IMAGES];
+  float fl[PMVS_MAX_IMAGES];
+  float fl2[PMVS_MAX_IMAGES];
+  float rays[PMVS_MAX_IMAGES][4];
+  int grids[PMVS_MAX_IMAGES][2];
+  BqState bq;
+  double fres;
+  int step;
+  int cand;
+  int overflow;
+};
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
+
+// Order-preserving compaction across the wave: returns the position of this lane's kept element
+// among kept elements of lanes < lane, and writes the number kept to *count.
+__device__ __forceinline__ int ballot_prefix(bool keep, int* count) {
+  const unsigned long long m = __ballot(keep);
+  *count = __popcll(m);
+  const unsigned long long below = (lane_id() == 0) ? 0ull : (m & ((~0ull) >> (64 - lane_id())));
+  return __popcll(below);
+}
+
+// ---------------------------------------------------------------- texture batch
+// Grabs cnt (<= TEXCAP) textures: view jv(j) into LDS slot js(j), j < cnt, at the wave-uniform
+// geometry (coord, px, py, normal); normalises the valid ones.  lds.valid[slot] is set.
+template <int WS>
+__device__ void grab_batch(const DScene& s, WaveLds<WS>& L, int cnt, const int* views, int slot0,
+                           const float* coord, const float* px, const float* py, const float* pz,
+                           unsigned long long* grabs) {
+  constexpr int S = WS * WS;
+  const int lane = lane_id();
+  // --- per-texture setup (grabTex lines 818-846), one lane per texture
+  if (lane < cnt) {
+    const int slot = slot0 + lane;
+    const int index = views[lane];
+    const DView& v = s.views[index];
+    int ok = 1;
+    float ray[4] = {v.center[0] - coord[0], v.center[1] - coord[1], v.center[2] - coord[2], v.center[3] - coord[3]};
+    unitize4(ray);
+    const float weight = smax(0.0f, dot4(ray, pz));
+    if ((double)weight < s.cosAngle1) ok = 0;
+    const int margin = WS / 2;
+    float center[3], c1[3], c2[3], t[4];
+    project(v, coord, s.level, center);
+    for (int i = 0; i < 4; ++i) t[i] = coord[i] + px[i];
+    project(v, t, s.level, c1);
+    for (int i = 0; i < 4; ++i) t[i] = coord[i] + py[i];
+    project(v, t, s.level, c2);
+    float dx[3] = {c1[0] - center[0], c1[1] - center[1], c1[2] - center[2]};
+    float dy[3] = {c2[0] - center[0], c2[1] - center[1], c2[2] - center[2]};
+    const float ratio = __fdiv_rn(norm3(dx) + norm3(dy), 2.0f);
+    int leveldif = cvt_int_x86(floor(log((double)ratio) / (double)s.log2f + (double)0.5f));
+    leveldif = imax(-s.level, imin(2, leveldif));
+    const float scale = (leveldif >= 0) ? (float)(1 << leveldif) : __fdiv_rn(1.0f, (float)(1 << (-leveldif)));
+    const int newlevel = s.level + leveldif;
+    for (int i = 0; i < 3; ++i) {
+      center[i] = __fdiv_rn(center[i], scale);
+      dx[i] = __fdiv_rn(dx[i], scale);
+      dy[i] = __fdiv_rn(dy[i], scale);
+    }
+    // grabSafe, optim.cpp:783-805
+    const float fm = (float)margin;
+    const float dxm[2] = {dx[0] * fm, dx[1] * fm}, dym[2] = {dy[0] * fm, dy[1] * fm};
+    const float tl0 = (center[0] - dxm[0]) - dym[0], tl1 = (center[1] - dxm[1]) - dym[1];
+    const float tr0 = (center[0] + dxm[0]) - dym[0], tr1 = (center[1] + dxm[1]) - dym[1];
+    const float bl0 = (center[0] - dxm[0]) + dym[0], bl1 = (center[1] - dxm[1]) + dym[1];
+    const float br0 = (center[0] + dxm[0]) + dym[0], br1 = (center[1] + dxm[1]) + dym[1];
+    const float minx = smin(tl0, smin(tr0, smin(bl0, br0)));
+    const float maxx = smax(tl0, smax(tr0, smax(bl0, br0)));
+    const float miny = smin(tl1, smin(tr1, smin(bl1, br1)));
+    const float maxy = smax(tl1, smax(tr1, smax(bl1, br1)));
+    if (ok) {
+      if (minx < 3.0f || (float)(v.w[newlevel] - 1 - 3) <= maxx || miny < 3.0f || (float)(v.h[newlevel] - 1 - 3) <= maxy)
+        ok = 0;
+    }
+    L.valid[slot] = ok;
+    L.jview[slot] = index;
+    L.jlevel[slot] = newlevel;
+    L.jleft[slot][0] = tl0;
+    L.jleft[slot][1] = tl1;
+    L.jdx[slot][0] = dx[0];
+    L.jdx[slot][1] = dx[1];
+    L.jdy[slot][0] = dy[0];
+    L.jdy[slot][1] = dy[1];
+  }
+  if (lane == 0) *grabs += cnt;
+  __syncthreads();
+  // --- bilinear samples: one lane per (texture, sample); positions by the reference's
+  // incremental float sums (left += dy per row, vftmp += dx per column, optim.cpp:846-859).
+  for (int t = lane; t < cnt * S; t += WAVE) {
+    const int j = t / S, k = t - j * S;
+    const int slot = slot0 + j;
+    if (!L.valid[slot]) continue;
+    const int yy = k / WS, xx = k - yy * WS;
+    float lx = L.jleft[slot][0], ly = L.jleft[slot][1];
+    const float dyx = L.jdy[slot][0], dyy = L.jdy[slot][1];
+    for (int r = 0; r < yy; ++r) { lx = lx + dyx; ly = ly + dyy; }
+    const float dxx = L.jdx[slot][0], dxy = L.jdx[slot][1];
+    for (int c = 0; c < xx; ++c) { lx = lx + dxx; ly = ly + dxy; }
+    float rgb[3];
+    get_color(s, s.views[L.jview[slot]], lx, ly, L.jlevel[slot], rgb);
+    L.tex[slot][k][0] = rgb[0];
+    L.tex[slot][k][1] = rgb[1];
+    L.tex[slot][k][2] = rgb[2];
+  }
+  __syncthreads();
+  // --- normalize, optim.cpp:1031-1067: sequential channel sums, one lane per texture
+  if (lane < cnt) {
+    const int slot = slot0 + lane;
+    if (L.valid[slot]) {
+      float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+      for (int i = 0; i < S; ++i) {
+        const float4 q = *reinterpret_cast<const float4*>(L.tex[slot][i]);
+        a0 += q.x; a1 += q.y; a2 += q.z;
+      }
+      const float fs3 = (float)S;
+      a0 = __fdiv_rn(a0, fs3); a1 = __fdiv_rn(a1, fs3); a2 = __fdiv_rn(a2, fs3);
+      float ave2 = 0.0f;
+      for (int i = 0; i < S; ++i) {
+        const float4 q = *reinterpret_cast<const float4*>(L.tex[slot][i]);
+        const float f0 = a0 - q.x, f1 = a1 - q.y, f2 = a2 - q.z;
+        ave2 += f0 * f0 + f1 * f1 + f2 * f2;
+      }
+      ave2 = fsqrt_rn(__fdiv_rn(ave2, (float)(3 * S)));
+      if (ave2 == 0.0f) ave2 = 1.0f;
+      L.ave[slot][0] = a0; L.ave[slot][1] = a1; L.ave[slot][2] = a2; L.ave[slot][3] = ave2;
+    }
+  }
+  __syncthreads();
+  for (int t = lane; t < cnt * S; t += WAVE) {
+    const int j = t / S, k = t - j * S;
+    const int slot = slot0 + j;
+    if (!L.valid[slot]) continue;
+    const float a2 = L.ave[slot][3];
+    L.tex[slot][k][0] = __fdiv_rn(L.tex[slot][k][0] - L.ave[slot][0], a2);
+    L.tex[slot][k][1] = __fdiv_rn(L.tex[slot][k][1] - L.ave[slot][1], a2);
+    L.tex[slot][k][2] = __fdiv_rn(L.tex[slot][k][2] - L.ave[slot][2], a2);
+  }
+  __syncthreads();
+}
+
+// COptim::dot, optim.cpp:1069-1077: sequential over the 3*S floats, then / size.
+template <int WS>
+__device__ __forceinline__ float tex_dot(const WaveLds<WS>& L, int a, int b) {
+  constexpr int S = WS * WS;
+  float ans = 0.0f;
+  for (int i = 0; i < S; ++i) {
+    const float4 p = *reinterpret_cast<const float4*>(L.tex[a][i]);
+    const float4 q = *reinterpret_cast<const float4*>(L.tex[b][i]);
+    ans += p.x * q.x;
+    ans += p.y * q.y;
+    ans += p.z * q.z;
+  }
+  return __fdiv_rn(ans, (float)(3 * S));
+}
+
+// ---------------------------------------------------------------- encode / decode
+struct RefineSetup {
+  float center[4], ray[4];
+  float dscale, ascale;
+  int ref;  // _indexesT[id][0]
+};
+
+// COptim::decode, optim.cpp:690-707.
+__device__ __forceinline__ void decode(const DScene& s, const RefineSetup& R, const double* vect, float* coord,
+                                       float* normal) {
+  const double sc = (double)R.dscale * vect[0];
+  for (int i = 0; i < 4; ++i) coord[i] = R.center[i] + (float)((double)R.ray[i] * sc);
+  const DView& v = s.views[R.ref];
+  const float angle1 = (float)(vect[1] * (double)R.ascale);
+  const float angle2 = (float)(vect[2] * (double)R.ascale);
+  const double ca2 = cos((double)angle2);
+  const float fx = (float)(sin((double)angle1) * ca2);
+  const float fy = (float)sin((double)angle2);
+  const float fz = (float)(-cos((double)angle1) * ca2);
+  for (int i = 0; i < 3; ++i) normal[i] = (v.xaxis[i] * fx + v.yaxis[i] * fy) + v.zaxis[i] * fz;
+  normal[3] = 0.0f;
+}
+
+// COptim::encode, optim.cpp:660-688.
+__device__ __forceinline__ void encode(const DScene& s, const RefineSetup& R, const float* coord, const float* normal,
+                                       double* vect) {
+  const float d[4] = {coord[0] - R.center[0], coord[1] - R.center[1], coord[2] - R.center[2], coord[3] - R.center[3]};
+  vect[0] = (double)__fdiv_rn(dot4(d, R.ray), R.dscale);
+  const DView& v = s.views[R.ref];
+  float n3[3] = {normal[0], normal[1], normal[2]};
+  if (normal[3] != 1.0f && normal[3] != 0.0f) {
+    n3[0] = __fdiv_rn(n3[0], normal[3]); n3[1] = __fdiv_rn(n3[1], normal[3]); n3[2] = __fdiv_rn(n3[2], normal[3]);
+  }
+  const float fx = dot3(v.xaxis, n3), fy = dot3(v.yaxis, n3), fz = dot3(v.zaxis, n3);
+  vect[2] = asin((double)smax(-1.0f, smin(1.0f, fy)));
+  const float cosb = (float)cos(vect[2]);
+  if (cosb == 0.0f) {
+    vect[1] = 0.0;
+  } else {
+    const float sina = __fdiv_rn(fx, cosb);
+    const float cosa = __fdiv_rn(-fz, cosb);
+    vect[1] = acos((double)smax(-1.0f, smin(1.0f, cosa)));
+    if (sina < 0.0f) vect[1] = -vect[1];
+  }
+  vect[1] = vect[1] / (double)R.ascale;
+  vect[2] = vect[2] / (double)R.ascale;
+}
+
+// ---------------------------------------------------------------- objective
+// COptim::my_f, optim.cpp:507-578 (non-pairwise).  Wave-uniform result.
+template <int WS>
+__device__ double my_f(const DScene& s, WaveLds<WS>& L, const RefineSetup& R, const int* idx, int nidx,
+                       const double* x, unsigned long long* grabs, unsigned long long* nvalid_acc) {
+  float coord[4], normal[4], px[4], py[4];
+  decode(s, R, x, coord, normal);
+  get_paxes(s, s.views[R.ref], coord, normal, px, py);
+  const int size = imin(s.tau, nidx);
+  const int mininum = imin(s.minImageNum, size);
+  grab_batch<WS>(s, L, size, idx, 0, coord, px, py, normal, grabs);
+  const int lane = lane_id();
+  if (lane >= 1 && lane < size) {
+    float r = 0.0f;
+    if (L.valid[0] && L.valid[lane]) r = robustincc((float)(1.0 - (double)tex_dot<WS>(L, 0, lane)));
+    L.res[lane] = r;
+  }
+  __syncthreads();
+  double ret;
+  int nv = 0;
+  for (int i = 0; i < size; ++i) nv += L.valid[i];
+  if (lane == 0) *nvalid_acc += nv;
+  if (!L.valid[0]) {
+    ret = 2.0;
+  } else {
+    double ans = 0.0f;
+    int denom = 0;
+    for (int i = 1; i < size; ++i) {
+      if (!L.valid[i]) continue;
+      ans += (double)L.res[i];
+      denom++;
+    }
+    ret = (denom < mininum - 1) ? 2.0f : ans / denom;
+  }
+  __syncthreads();
+  return ret;
+}
+
+// COptim::computeINCC (weighted, robust), optim.cpp:865-938.  weights in L.fl2[].
+template <int WS>
+__device__ double compute_incc(const DScene& s, WaveLds<WS>& L, const float* coord, const float* normal,
+                               const int* idx, int nidx, unsigned long long* grabs) {
+  if (nidx < 2) return 2.0;
+  float px[4], py[4];
+  get_paxes(s, s.views[idx[0]], coord, normal, px, py);
+  const int size = imin(s.tau, nidx);
+  grab_batch<WS>(s, L, size, idx, 0, coord, px, py, normal, grabs);
+  const int lane = lane_id();
+  if (lane >= 1 && lane < size) {
+    float r = 0.0f;
+    if (L.valid[0] && L.valid[lane]) r = robustincc((float)(1.0 - (double)tex_dot<WS>(L, 0, lane)));
+    L.res[lane] = r;
+  }
+  __syncthreads();
+  double score = 0.0;
+  if (!L.valid[0]) {
+    score = 2.0;
+  } else {
+    float totalweight = 0.0f;
+    for (int i = 1; i < size; ++i) {
+      if (L.valid[i]) {
+        totalweight += L.fl2[i];
+        score += (double)(L.res[i] * L.fl2[i]);
+      }
+    }
+    if (totalweight == 0.0f) score = 2.0;
+    else score /= (double)totalweight;
+  }
+  __syncthreads();
+  return score;
+}
+
+// ---------------------------------------------------------------- image-list steps
+// COptim::addImages, optim.cpp:398-444.  Appends in visdata2 order.
+template <int WS>
+__device__ void add_images(const DScene& s, WaveLds<WS>& L, const float* coord, const float* normal) {
+  const int lane = lane_id();
+  const int ref = L.images[0];
+  const int nused = L.nimg;  // the reference's used[] is built before the loop
+  const int b = s.vis_off[ref], e = s.vis_off[ref + 1];
+  for (int base = b; base < e; base += WAVE) {
+    bool keep = false;
+    const int k = base + lane;
+    if (k < e) {
+      const int img = s.vis[k];
+      bool used = false;
+      for (int i = 0; i < nused; ++i) used |= (L.images[i] == img);
+      if (!used) {
+        const DView& v = s.views[img];
+        float ic[3];
+        project(v, coord, s.level, ic);
+        if (!(ic[0] < 0.0f || (float)(v.w[s.level] - 1) <= ic[0] || ic[1] < 0.0f || (float)(v.h[s.level] - 1) <= ic[1])) {
+          if (get_edge(s, v, coord, s.level) != 0) {
+            float ray[4] = {v.center[0] - coord[0], v.center[1] - coord[1], v.center[2] - coord[2], v.center[3] - coord[3]};
+            unitize4(ray);
+            keep = (s.athreshold <= dot4(ray, normal));
+          }
+        }
+      }
+    }
+    int cnt;
+    const int pos = ballot_prefix(keep, &cnt);
+    const int n0 = L.nimg;
+    __syncthreads();
+    if (keep) {
+      if (n0 + pos < PMVS_MAX_IMAGES) L.images[n0 + pos] = s.vis[k];
+      else L.overflow = 1;
+    }
+    __syncthreads();
+    if (lane == 0) L.nimg = imin(n0 + cnt, PMVS_MAX_IMAGES);
+    __syncthreads();
+  }
+}
+
+// COptim::setINCCs (reference-vs-others) + constraintImages, optim.cpp:192-206, 709-744.
+template <int WS>
+__device__ void constraint_images(const DScene& s, WaveLds<WS>& L, const float* coord, const float* normal, float thr,
+                                  unsigned long long* grabs) {
+  const int lane = lane_id();
+  const int n = L.nimg;
+  float px[4], py[4];
+  get_paxes(s, s.views[L.images[0]], coord, normal, px, py);
+  // slot 0 = reference texture, the rest in batches of TEXCAP-1
+  grab_batch<WS>(s, L, 1, L.images, 0, coord, px, py, normal, grabs);
+  const int ok0 = L.valid[0];
+  // keep flags in L.list2
+  if (lane == 0) L.list2[0] = 1;
+  for (int b = 1; b < n; b += TEXCAP - 1) {
+    const int cnt = imin(TEXCAP - 1, n - b);
+    if (ok0) grab_batch<WS>(s, L, cnt, L.images + b, 1, coord, px, py, normal, grabs);
+    if (lane < cnt) {
+      float incc = 2.0f;
+      if (ok0 && L.valid[1 + lane]) incc = 1.0f - tex_dot<WS>(L, 0, 1 + lane);
+      L.list2[b + lane] = (incc < 1.0f - thr) ? 1 : 0;
+    }
+    __syncthreads();
+  }
+  // order-preserving compaction of images[] by keep flags
+  int newn;
+  const bool keep = lane < n && L.list2[lane];
+  const int pos = ballot_prefix(keep, &newn);
+  const int img = lane < n ? L.images[lane] : 0;
+  __syncthreads();
+  if (keep) L.images[pos] = img;
+  if (lane == 0) L.nimg = newn;
+  __syncthreads();
+}
+
+// COptim::sortImages (newm == 1), optim.cpp:284-321; computeUnits optim.cpp:473-494.
+template <int WS>
+__device__ void sort_images(const DScene& s, WaveLds<WS>& L, const float* coord, const float* normal) {
+  const int lane = lane_id();
+  const int n = L.nimg;
+  bool keep = false;
+  float unit = 0.0f, ray[4] = {0, 0, 0, 0};
+  int img = 0;
+  if (lane < n) {
+    img = L.images[lane];
+    const DView& v = s.views[img];
+    ray[0] = v.center[0] - coord[0]; ray[1] = v.center[1] - coord[1];
+    ray[2] = v.center[2] - coord[2]; ray[3] = v.center[3] - coord[3];
+    unitize4(ray);
+    const float d = dot4(ray, normal);
+    if (!(d <= 0.0f)) {
+      keep = true;
+      unit = __fdiv_rn(get_unit(s, v, coord), d);
+    }
+  }
+  int m;
+  const int pos = ballot_prefix(keep, &m);
+  __syncthreads();
+  if (keep) {
+    L.list2[pos] = img;
+    L.fl[pos] = unit;
+    for (int i = 0; i < 4; ++i) L.rays[pos][i] = ray[i];
+  }
+  __syncthreads();
+  if (lane == 0) {
+    if (m < 2) {
+      L.nimg = 0;
+    } else {
+      L.fl[0] = 0.0f;
+      int alive[PMVS_MAX_IMAGES];
+      for (int i = 0; i < m; ++i) alive[i] = 1;
+      int out = 0;
+      for (int it = 0; it < m; ++it) {
+        int index = -1;
+        for (int k = 0; k < m; ++k) {
+          if (!alive[k]) continue;
+          if (index < 0 || L.fl[k] < L.fl[index]) index = k;
+        }
+        L.images[out++] = L.list2[index];
+        alive[index] = 0;
+        for (int j = 0; j < m; ++j) {
+          if (!alive[j]) continue;
+          const float ftmp = smin(s.sortThreshold, smax(__fdiv_rn(s.sortThreshold, 2.0f), 1.0f - dot4(L.rays[index], L.rays[j])));
+          L.fl[j] = L.fl[j] * __fdiv_rn(s.sortThreshold, ftmp);
+        }
+      }
+      L.nimg = m;
+    }
+  }
+  __syncthreads();
+}
+
+// CPatchOrganizerS::setScales, patchOrganizerS.cpp:663-684 (lane 0).
+__device__ void set_scales(const DScene& s, const int* images, int nimg, const float* coord, float* dscale, float* ascale) {
+  const DView& v0 = s.views[images[0]];
+  const float unit = get_unit(s, v0, coord);
+  const float unit2 = 2.0f * unit;
+  float ray[4] = {coord[0] - v0.center[0], coord[1] - v0.center[1], coord[2] - v0.center[2], coord[3] - v0.center[3]};
+  unitize4(ray);
+  const int inum = imin(s.tau, nimg);
+  const float c2[4] = {coord[0] - ray[0] * unit2, coord[1] - ray[1] * unit2, coord[2] - ray[2] * unit2, coord[3] - ray[3] * unit2};
+  float ds = *dscale;
+  for (int i = 1; i < inum; ++i) {
+    const DView& v = s.views[images[i]];
+    float a[3], b[3];
+    project(v, coord, s.level, a);
+    project(v, c2, s.level, b);
+    const float d[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
+    ds += norm3(d);
+  }
+  ds = __fdiv_rn(ds, (float)(inum - 1));
+  ds = __fdiv_rn(unit2, ds);
+  *dscale = ds;
+  *ascale = (float)atan((double)__fdiv_rn(ds, __fdiv_rn(unit * (float)s.wsize, 2.0f)));
+}
+
+// CPhotoSetS::checkAngles, photoSetS.cpp:164-189.  Returns 1 if no pair is in (minA, maxA).
+template <int WS>
+__device__ int check_angles(const DScene& s, WaveLds<WS>& L, const float* coord, float minA, float maxA) {
+  const int lane = lane_id();
+  const int n = L.nimg;
+  if (lane < n) {
+    const DView& v = s.views[L.images[lane]];
+    float r[4] = {v.center[0] - coord[0], v.center[1] - coord[1], v.center[2] - coord[2], v.center[3] - coord[3]};
+    unitize4(r);
+    for (int i = 0; i < 4; ++i) L.rays[lane][i] = r[i];
+  }
+  __syncthreads();
+  const int npairs = n * (n - 1) / 2;
+  int count = 0;
+  for (int base = 0; base < npairs; base += WAVE) {
+    const int p = base + lane;
+    bool hit = false;
+    if (p < npairs) {
+      // unrank p -> (i, j), i < j
+      int i = 0, rem = p;
+      while (rem >= n - 1 - i) { rem -= n - 1 - i; ++i; }
+      const int j = i + 1 + rem;
+      const float d = smax(-1.0f, smin(1.0f, dot4(L.rays[i], L.rays[j])));
+      const float angle = (float)acos((double)d);
+      hit = (minA < angle && angle < maxA);
+    }
+    count += __popcll(__ballot(hit));
+  }
+  __syncthreads();
+  return count < 1 ? 1 : 0;
+}
+
+// COptim::filterImagesByAngle, optim.cpp:124-148.
+template <int WS>
+__device__ void filter_images_by_angle(const DScene& s, WaveLds<WS>& L, const float* coord, const float* normal) {
+  const int lane = lane_id();
+  const int n = L.nimg;
+  bool keep = false;
+  int img = 0;
+  if (lane < n) {
+    img = L.images[lane];
+    const DView& v = s.views[img];
+    float ray[4] = {v.center[0] - coord[0], v.center[1] - coord[1], v.center[2] - coord[2], v.center[3] - coord[3]};
+    unitize4(ray);
+    keep = !((double)dot4(ray, normal) < s.cosAngle1);
+  }
+  const bool refbad = !__shfl(keep ? 1 : 0, 0);
+  int newn;
+  const int pos = ballot_prefix(keep, &newn);
+  __syncthreads();
+  if (refbad) {
+    if (lane == 0) L.nimg = 0;
+  } else {
+    if (keep) L.images[pos] = img;
+    if (lane == 0) L.nimg = newn;
+  }
+  __syncthreads();
+}
+
+// CPatchOrganizerS::setGrids, patchOrganizerS.cpp:410-419.
+template <int WS>
+__device__ void set_grids(const DScene& s, WaveLds<WS>& L, const float* coord) {
+  const int lane = lane_id();
+  if (lane < L.nimg) {
+    float ic[3];
+    project(s.views[L.images[lane]], coord, s.level, ic);
+    L.grids[lane][0] = ((int)floorf(ic[0] + 0.5f)) / s.csize;
+    L.grids[lane][1] = ((int)floorf(ic[1] + 0.5f)) / s.csize;
+  }
+  __syncthreads();
+}
+
+// COptim::setRefImage, optim.cpp:208-254, with setINCCs (pairwise, robust) optim.cpp:746-781.
+// The m x m INCC matrix lives in this workgroup's global scratch slot.
+template <int WS>
+__device__ void set_ref_image(const DScene& s, WaveLds<WS>& L, const float* coord, const float* normal, float* mat,
+                              unsigned long long* grabs) {
+  const int lane = lane_id();
+  const int n = L.nimg;
+  const bool tgt = lane < n && L.images[lane] < s.tnum;
+  int m;
+  const int pos = ballot_prefix(tgt, &m);
+  if (tgt) L.list2[pos] = L.images[lane];
+  __syncthreads();
+  if (m == 0) {
+    if (lane == 0) L.nimg = 0;
+    __syncthreads();
+    return;
+  }
+  float px[4], py[4];
+  get_paxes(s, s.views[L.list2[0]], coord, normal, px, py);
+  constexpr int B = TEXCAP / 2;
+  if (m <= TEXCAP) {
+    grab_batch<WS>(s, L, m, L.list2, 0, coord, px, py, normal, grabs);
+    const int npairs = m * (m - 1) / 2;
+    for (int base = 0; base < npairs; base += WAVE) {
+      const int p = base + lane;
+      if (p < npairs) {
+        int i = 0, rem = p;
+        while (rem >= m - 1 - i) { rem -= m - 1 - i; ++i; }
+        const int j = i + 1 + rem;
+        float v = 2.0f;
+        if (L.valid[i] && L.valid[j]) v = robustincc(1.0f - tex_dot<WS>(L, i, j));
+        mat[i * PMVS_MAX_IMAGES + j] = v;
+        mat[j * PMVS_MAX_IMAGES + i] = v;
+      }
+    }
+  } else {
+    for (int bi = 0; bi < m; bi += B) {
+      const int ci = imin(B, m - bi);
+      grab_batch<WS>(s, L, ci, L.list2 + bi, 0, coord, px, py, normal, grabs);
+      for (int bj = bi; bj < m; bj += B) {
+        const int cj = imin(B, m - bj);
+        if (bj != bi) grab_batch<WS>(s, L, cj, L.list2 + bj, B, coord, px, py, normal, grabs);
+        const int np = (bj == bi) ? ci * (ci - 1) / 2 : ci * cj;
+        for (int base = 0; base < np; base += WAVE) {
+          const int p = base + lane;
+          if (p < np) {
+            int i, j, si, sj;
+            if (bj == bi) {
+              int a = 0, rem = p;
+              while (rem >= ci - 1 - a) { rem -= ci - 1 - a; ++a; }
+              i = a; j = a + 1 + rem; si = i; sj = j;
+            } else {
+              i = p / cj; j = p - i * cj; si = i; sj = B + j;
+            }
+            float v = 2.0f;
+            if (L.valid[si] && L.valid[sj]) v = robustincc(1.0f - tex_dot<WS>(L, si, sj));
+            const int gi = bi + i, gj = bj + j;
+            mat[gi * PMVS_MAX_IMAGES + gj] = v;
+            mat[gj * PMVS_MAX_IMAGES + gi] = v;
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  if (lane < m) mat[lane * PMVS_MAX_IMAGES + lane] = 0.0f;
+  __syncthreads();
+  // row sums in j order (std::accumulate, float)
+  if (lane < m) {
+    float sum = 0.0f;
+    for (int j = 0; j < m; ++j) sum = sum + mat[lane * PMVS_MAX_IMAGES + j];
+    L.fl[lane] = sum;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    int refindex = -1;
+    float refncc = 1073741824.0f;  // (float)(INT_MAX/2)
+    for (int i = 0; i < m; ++i) {
+      if (L.fl[i] < refncc) {
+        refncc = L.fl[i];
+        refindex = i;
+      }
+    }
+    const int refIndex = L.list2[refindex];
+    for (int i = 0; i < L.nimg; ++i) {
+      if (L.images[i] == refIndex) {
+        const int t = L.images[0];
+        L.images[0] = refIndex;
+        L.images[i] = t;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------- refine one candidate
+template <int WS>
+__device__ void refine_candidate(const DScene& s, WaveLds<WS>& L, const pmvs_candidate& cin, pmvs_refined& cout,
+                                 float* mat, unsigned long long* acc) {
+  // acc: [0] evals [1] tex_valid [2] grabs [3] accepted [4] fail_pre [5] fail_post [6] refine_failed
+  const int lane = lane_id();
+  float coord[4], normal[4];
+  for (int i = 0; i < 4; ++i) { coord[i] = cin.coord[i]; normal[i] = cin.normal[i]; }
+  float dscale = cin.dscale, ascale = 0.0f, ncc = -1.0f, tmp = 0.0f;
+  int timages = 0, status = PMVS_ACCEPTED, refine_code = 0, evals = 0;
+  const int n0 = imin(cin.num_images, PMVS_MAX_IMAGES);
+  if (lane < n0) L.images[lane] = cin.images[lane];
+  if (lane == 0) { L.nimg = n0; L.overflow = (cin.num_images > PMVS_MAX_IMAGES); }
+  __syncthreads();
+
+  // ---------------- preProcess (optim.cpp:95-122)
+  add_images<WS>(s, L, coord, normal);
+  constraint_images<WS>(s, L, coord, normal, s.nccThresholdBefore, &acc[2]);
+  sort_images<WS>(s, L, coord, normal);
+  // broadcast dscale/ascale (set_scales accumulates onto the candidate's _dscale)
+  if (lane == 0 && L.nimg > 0) {
+    float ds = dscale, as = 0.0f;
+    set_scales(s, L.images, L.nimg, coord, &ds, &as);
+    L.fl2[0] = ds;
+    L.fl2[1] = as;
+  }
+  __syncthreads();
+  if (L.nimg > 0) { dscale = L.fl2[0]; ascale = L.fl2[1]; }
+  __syncthreads();
+  int fail = 0;
+  if (L.nimg < s.minImageNum) fail = 1;
+  else if (check_angles<WS>(s, L, coord, s.maxAngle, s.angle1)) {
+    fail = 1;
+    if (lane == 0) L.nimg = 0;
+    __syncthreads();
+  }
+  if (fail) {
+    status = PMVS_FAIL_PRE;
+  } else {
+    // ---------------- refinePatchBFGS (optim.cpp:580-658)
+    RefineSetup R;
+    const DView& vr = s.views[L.images[0]];
+    for (int i = 0; i < 4; ++i) { R.center[i] = coord[i]; R.ray[i] = coord[i] - vr.center[i]; }
+    unitize4(R.ray);
+    R.dscale = dscale;
+    R.ascale = s.ascale;
+    R.ref = L.images[0];
+    // weights: computeUnits(patch) then min(1, w0 / wi), stored in L.fl2[]
+    const int ni = L.nimg;
+    if (lane < ni) {
+      const DView& v = s.views[L.images[lane]];
+      float u = get_unit(s, v, coord);
+      float ray[4] = {v.center[0] - coord[0], v.center[1] - coord[1], v.center[2] - coord[2], v.center[3] - coord[3]};
+      unitize4(ray);
+      const float den = dot4(ray, normal);
+      if (0.0f < den) u = __fdiv_rn(u, den);
+      else u = 1073741824.0f;
+      L.fl[lane] = u;
+    }
+    __syncthreads();
+    if (lane < ni) {
+      const float w0 = L.fl[0];
+      L.fl2[lane] = (lane == 0) ? 1.0f : smin(1.0f, __fdiv_rn(w0, L.fl[lane]));
+    }
+    __syncthreads();
+    double p[3];
+    encode(s, R, coord, normal, p);
+    const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999};
+    const double ub[3] = {HUGE_VAL, 23.99999, 23.99999};
+    double x0[3];
+    for (int i = 0; i < 3; ++i) {
+      const double m = (ub[i] < p[i]) ? ub[i] : p[i];
+      x0[i] = (m < lb[i]) ? lb[i] : m;
+    }
+    const int nidx = imin(ni, PMVS_MAX_TAU);
+    int tidx[PMVS_MAX_TAU];
+    for (int i = 0; i < nidx; ++i) tidx[i] = L.images[i];
+    if (lane == 0) {
+      bq_begin(L.bq, x0, lb, ub, 1.e-7, 1000);
+      L.fres = 0.0;
+    }
+    __syncthreads();
+    unsigned long long nvalid = 0;
+    for (;;) {
+      if (lane == 0) L.step = (L.bq.resume < 0) ? BQ_DONE : bq_step(L.bq, L.fres);
+      __syncthreads();
+      if (L.step != BQ_NEED_F) break;
+      const double xe[3] = {L.bq.xeval[0], L.bq.xeval[1], L.bq.xeval[2]};
+      __syncthreads();
+      const double f = my_f<WS>(s, L, R, tidx, nidx, xe, &acc[2], &nvalid);
+      evals++;
+      if (lane == 0) L.fres = f;
+      __syncthreads();
+    }
+    refine_code = L.bq.rc;
+    const double xo[3] = {L.bq.xout[0], L.bq.xout[1], L.bq.xout[2]};
+    __syncthreads();
+    if (lane == 0) { acc[0] += evals; acc[1] += nvalid; }
+    const bool success = (refine_code == BQR_SUCCESS || refine_code == 2 || refine_code == 3 || refine_code == BQR_XTOL);
+    if (!success) {
+      if (lane == 0) acc[6] += 1;
+    } else {
+      decode(s, R, xo, coord, normal);
+      const double sc = compute_incc<WS>(s, L, coord, normal, L.images, L.nimg, &acc[2]);
+      ncc = (float)(1.0 - (double)unrobustincc((float)sc));
+    }
+    // ---------------- postProcess (optim.cpp:150-190), depth 0
+    int pfail = 0;
+    if (L.nimg < s.minImageNum) pfail = 1;
+    if (!pfail) {
+      // getMask over all views and insideBimages
+      bool bad = false;
+      if (s.anyMask)
+        for (int b = 0; b < s.num; b += WAVE)
+          if (b + lane < s.num && get_mask(s, s.views[b + lane], coord, s.level) == 0) bad = true;
+      for (int b = 0; b < s.nb; b += WAVE) {
+        if (b + lane < s.nb) {
+          const DView& v = s.views[s.bindexes[b + lane]];
+          float ic[3];
+          project(v, coord, s.level, ic);
+          if (ic[0] < 0.0f || (float)(v.w[s.level] - 1) < ic[0] || ic[1] < 0.0f || (float)(v.h[s.level] - 1) < ic[1]) bad = true;
+        }
+      }
+      if (__ballot(bad)) pfail = 1;
+    }
+    if (!pfail) {
+      add_images<WS>(s, L, coord, normal);
+      constraint_images<WS>(s, L, coord, normal, s.nccThreshold, &acc[2]);
+      filter_images_by_angle<WS>(s, L, coord, normal);
+      if (L.nimg < s.minImageNum) pfail = 1;
+    }
+    if (!pfail) {
+      set_ref_image<WS>(s, L, coord, normal, mat, &acc[2]);
+      if (L.nimg == 0) pfail = 1;
+    }
+    if (!pfail) {
+      constraint_images<WS>(s, L, coord, normal, s.nccThreshold, &acc[2]);
+      if (L.nimg < s.minImageNum) pfail = 1;
+    }
+    if (!pfail) {
+      set_grids<WS>(s, L, coord);
+      int t = 0;
+      for (int i = 0; i < L.nimg; ++i) t += (L.images[i] < s.tnum);
+      timages = t;
+      tmp = smax(0.0f, ncc - s.nccThreshold) * (float)timages;
+    }
+    if (pfail) status = PMVS_FAIL_POST;
+  }
+  if (L.overflow) status = PMVS_FAIL_OVERFLOW;
+  // ---------------- write result
+  const int nout = L.nimg;
+  if (lane < nout) {
+    cout.images[lane] = L.images[lane];
+    cout.grids[lane][0] = (status == PMVS_ACCEPTED) ? L.grids[lane][0] : 0;
+    cout.grids[lane][1] = (status == PMVS_ACCEPTED) ? L.grids[lane][1] : 0;
+  }
+  if (lane == 0) {
+    cout.status = status;
+    cout.refine_code = refine_code;
+    cout.evals = evals;
+    cout.num_images = nout;
+    for (int i = 0; i < 4; ++i) { cout.coord[i] = coord[i]; cout.normal[i] = normal[i]; }
+    cout.ncc = ncc;
+    cout.dscale = dscale;
+    cout.ascale = ascale;
+    cout.tmp = tmp;
+    cout.timages = timages;
+    cout.reserved = 0;
+    if (status == PMVS_ACCEPTED) acc[3]++;
+    else if (status == PMVS_FAIL_PRE) acc[4]++;
+    else acc[5]++;
+  }
+  __syncthreads();
+}
+
+}  // namespace pmvsdev
+
+// ==================================================================== kernels
+namespace pmvsdev {
+
+// Persistent refine kernel: each workgroup (one wavefront) dequeues candidates until the
+// batch is exhausted (every wave reaches the exit: the queue head only grows).
+template <int WS>
+__global__ __launch_bounds__(64) void refine_kernel(DScene s, const pmvs_candidate* __restrict__ in,
+                                                     pmvs_refined* __restrict__ out, int n, DevStats* st) {
+  __shared__ WaveLds<WS> L;
+  unsigned long long acc[7] = {0, 0, 0, 0, 0, 0, 0};
+  float* mat = s.scratch + (size_t)blockIdx.x * PMVS_MAX_IMAGES * PMVS_MAX_IMAGES;
+  const int lane = lane_id();
+  for (;;) {
+    if (lane == 0) {
+      const unsigned long long c = atomicAdd(&st->queue, 1ull);
+      L.cand = (c < (unsigned long long)n) ? (int)c : -1;
+    }
+    __syncthreads();
+    const int c = L.cand;
+    __syncthreads();
+    if (c < 0) break;
+    refine_candidate<WS>(s, L, in[c], out[c], mat, acc);
+  }
+  if (lane == 0) {
+    atomicAdd(&st->evals, acc[0]);
+    atomicAdd(&st->tex_valid, acc[1]);
+    atomicAdd(&st->tex_grabs, acc[2]);
+    atomicAdd(&st->accepted, acc[3]);
+    atomicAdd(&st->fail_pre, acc[4]);
+    atomicAdd(&st->fail_post, acc[5]);
+    atomicAdd(&st->refine_failed, acc[6]);
+  }
+}
+
+// One wavefront per query: refinePatchBFGS setup (optim.cpp:584-596) + one my_f evaluation.
+template <int WS>
+__global__ __launch_bounds__(64) void incc_eval_kernel(DScene s, const pmvs_eval_query* __restrict__ q, int n,
+                                                        double* __restrict__ out, DevStats* st) {
+  __shared__ WaveLds<WS> L;
+  const int i = blockIdx.x;
+  if (i >= n) return;
+  const int lane = lane_id();
+  const pmvs_eval_query& Q = q[i];
+  RefineSetup R;
+  const DView& vr = s.views[Q.images[0]];
+  for (int k = 0; k < 4; ++k) { R.center[k] = Q.coord[k]; R.ray[k] = Q.coord[k] - vr.center[k]; }
+  unitize4(R.ray);
+  R.dscale = Q.dscale;
+  R.ascale = s.ascale;
+  R.ref = Q.images[0];
+  int idx[PMVS_MAX_TAU];
+  const int ni = imin(Q.num_images, PMVS_MAX_TAU);
+  for (int k = 0; k < ni; ++k) idx[k] = Q.images[k];
+  unsigned long long grabs = 0, nvalid = 0;
+  const double f = my_f<WS>(s, L, R, idx, ni, Q.x, &grabs, &nvalid);
+  if (lane == 0) {
+    out[i] = f;
+    atomicAdd(&st->evals, 1ull);
+    atomicAdd(&st->tex_valid, nvalid);
+    atomicAdd(&st->tex_grabs, grabs);
+  }
+}
+
+// One wavefront per query: grabTex (+ normalize).
+template <int WS>
+__global__ __launch_bounds__(64) void grab_tex_kernel(DScene s, const pmvs_tex_query* __restrict__ q, int n,
+                                                       float* __restrict__ out, int* __restrict__ valid) {
+  __shared__ WaveLds<WS> L;
+  constexpr int S = WS * WS;
+  const int i = blockIdx.x;
+  if (i >= n) return;
+  const int lane = lane_id();
+  const pmvs_tex_query& Q = q[i];
+  unsigned long long grabs = 0;
+  int view = Q.view;
+  // grab without normalisation when asked: run the batch, then undo is impossible, so grab into
+  // slot 0 and (re)compute raw samples when normalize == 0 by skipping the normalize pass below.
+  if (Q.normalize) {
+    grab_batch<WS>(s, L, 1, &view, 0, Q.coord, Q.pxaxis, Q.pyaxis, Q.normal, &grabs);
+  } else {
+    // raw samples: same setup + sampling as grab_batch, no normalisation
+    grab_batch<WS>(s, L, 1, &view, 0, Q.coord, Q.pxaxis, Q.pyaxis, Q.normal, &grabs);
+    // restore raw values from the normalisation constants: not exact, so recompute instead
+    if (L.valid[0]) {
+      for (int t = lane; t < S; t += WAVE) {
+        const int yy = t / WS, xx = t - yy * WS;
+        float lx = L.jleft[0][0], ly = L.jleft[0][1];
+        for (int r = 0; r < yy; ++r) { lx = lx + L.jdy[0][0]; ly = ly + L.jdy[0][1]; }
+        for (int c = 0; c < xx; ++c) { lx = lx + L.jdx[0][0]; ly = ly + L.jdx[0][1]; }
+        float rgb[3];
+        get_color(s, s.views[L.jview[0]], lx, ly, L.jlevel[0], rgb);
+        L.tex[0][t][0] = rgb[0];
+        L.tex[0][t][1] = rgb[1];
+        L.tex[0][t][2] = rgb[2];
+      }
+    }
+    __syncthreads();
+  }
+  const int ok = L.valid[0];
+  for (int t = lane; t < S; t += WAVE) {
+    for (int c = 0; c < 3; ++c) out[(size_t)i * 3 * S + 3 * t + c] = ok ? L.tex[0][t][c] : 0.0f;
+  }
+  if (lane == 0) valid[i] = ok;
+}
+
+// CImage::buildImage (image.cpp:228-325, filter 0): one thread per output pixel, double
+// accumulation in the reference's (j, i) order, float denominator, floor(c + 0.5f).
+__global__ void build_level_kernel(const uint8_t* __restrict__ src, int Wp, int Hp, uint8_t* __restrict__ dst, int W,
+                                   int H) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  const int y = blockIdx.y;
+  if (x >= W || y >= H) return;
+  const double wts[4] = {1.0 / 64.0 * 1.0, 3.0 / 64.0, 3.0 / 64.0, 1.0 / 64.0};
+  double c0 = 0, c1 = 0, c2 = 0;
+  float denom = 0.0f;
+  for (int j = -1; j < 3; ++j) {
+    const int ytmp = 2 * y + j;
+    if (ytmp < 0 || Hp - 1 < ytmp) continue;
+    for (int i = -1; i < 3; ++i) {
+      const int xtmp = 2 * x + i;
+      if (xtmp < 0 || Wp - 1 < xtmp) continue;
+      // mask[j][i] = outer(1 3 3 1)/64: values 1/64, 3/64, 9/64 are exact in double
+      const double m = (double)((j == -1 || j == 2) ? 1 : 3) * (double)((i == -1 || i == 2) ? 1 : 3) / 64.0;
+      const uint8_t* p = src + ((size_t)ytmp * Wp + xtmp) * 3;
+      c0 += m * (double)p[0];
+      c1 += m * (double)p[1];
+      c2 += m * (double)p[2];
+      denom = (float)((double)denom + m);
+    }
+  }
+  (void)wts;
+  const double dd = (double)denom;
+  c0 /= dd; c1 /= dd; c2 /= dd;
+  uint8_t* o = dst + ((size_t)y * W + x) * 3;
+  o[0] = (uint8_t)((int)floor(c0 + (double)0.5f));
+  o[1] = (uint8_t)((int)floor(c1 + (double)0.5f));
+  o[2] = (uint8_t)((int)floor(c2 + (double)0.5f));
+}
+
+__global__ void pack_rgba_kernel(const uint8_t* __restrict__ rgb, uint32_t* __restrict__ out, long long npix) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npix) return;
+  const uint8_t* p = rgb + 3 * i;
+  out[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+}
+
+__global__ void unpack_rgba_kernel(const uint32_t* __restrict__ in, uint8_t* __restrict__ rgb, long long npix) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npix) return;
+  const uint32_t v = in[i];
+  rgb[3 * i] = v & 0xff;
+  rgb[3 * i + 1] = (v >> 8) & 0xff;
+  rgb[3 * i + 2] = (v >> 16) & 0xff;
+}
+
+}  // namespace pmvsdev
+
+// ==================================================================== launchers
+#include "pmvs_launch.h"
+
+namespace pmvsdev {
+
+hipError_t launch_refine(const DScene& s, const pmvs_candidate* d_in, pmvs_refined* d_out, int n, DevStats* d_st,
+                         int grid, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const int g = grid < n ? grid : n;
+  switch (s.wsize) {
+    case 5: hipLaunchKernelGGL((refine_kernel<5>), dim3(g), dim3(64), 0, stream, s, d_in, d_out, n, d_st); break;
+    case 7: hipLaunchKernelGGL((refine_kernel<7>), dim3(g), dim3(64), 0, stream, s, d_in, d_out, n, d_st); break;
+    case 9: hipLaunchKernelGGL((refine_kernel<9>), dim3(g), dim3(64), 0, stream, s, d_in, d_out, n, d_st); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_incc_eval(const DScene& s, const pmvs_eval_query* d_q, int n, double* d_out, DevStats* d_st,
+                            hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  switch (s.wsize) {
+    case 5: hipLaunchKernelGGL((incc_eval_kernel<5>), dim3(n), dim3(64), 0, stream, s, d_q, n, d_out, d_st); break;
+    case 7: hipLaunchKernelGGL((incc_eval_kernel<7>), dim3(n), dim3(64), 0, stream, s, d_q, n, d_out, d_st); break;
+    case 9: hipLaunchKernelGGL((incc_eval_kernel<9>), dim3(n), dim3(64), 0, stream, s, d_q, n, d_out, d_st); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_grab_tex(const DScene& s, const pmvs_tex_query* d_q, int n, float* d_out, int* d_valid,
+                           hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  switch (s.wsize) {
+    case 5: hipLaunchKernelGGL((grab_tex_kernel<5>), dim3(n), dim3(64), 0, stream, s, d_q, n, d_out, d_valid); break;
+    case 7: hipLaunchKernelGGL((grab_tex_kernel<7>), dim3(n), dim3(64), 0, stream, s, d_q, n, d_out, d_valid); break;
+    case 9: hipLaunchKernelGGL((grab_tex_kernel<9>), dim3(n), dim3(64), 0, stream, s, d_q, n, d_out, d_valid); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_build_level(const uint8_t* d_src, int Wp, int Hp, uint8_t* d_dst, int W, int H, hipStream_t stream) {
+  if (W <= 0 || H <= 0) return hipSuccess;
+  hipLaunchKernelGGL(build_level_kernel, dim3((W + 255) / 256, H), dim3(256), 0, stream, d_src, Wp, Hp, d_dst, W, H);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_rgba(const uint8_t* d_rgb, uint32_t* d_out, long long npix, hipStream_t stream) {
+  if (npix <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pack_rgba_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream, d_rgb, d_out, npix);
+  return hipGetLastError();
+}
+
+hipError_t launch_unpack_rgba(const uint32_t* d_in, uint8_t* d_rgb, long long npix, hipStream_t stream) {
+  if (npix <= 0) return hipSuccess;
+  hipLaunchKernelGGL(unpack_rgba_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream, d_in, d_rgb, npix);
+  return hipGetLastError();
+}
+
+}  // namespace pmvsdev
+
+// ==================================================================== device math self-test
+// Evaluates the device implementations of the libm functions the hot path uses, so tests can
+// measure their agreement with the host libm (glibc) that the reference runs on.
+namespace pmvsdev {
+__global__ void math_selftest_kernel(int op, const double* __restrict__ in, double* __restrict__ out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double x = in[i];
+  double r;
+  switch (op) {
+    case 0: r = sqrt(x); break;
+    case 1: r = sin(x); break;
+    case 2: r = cos(x); break;
+    case 3: r = asin(x); break;
+    case 4: r = acos(x); break;
+    case 5: r = atan(x); break;
+    case 6: r = log(x); break;
+    case 7: r = (double)__builtin_sqrtf((float)x); break;
+    case 8: r = (double)__fdiv_rn((float)x, (float)in[(i + 1) % n]); break;
+    case 9: r = floor(x); break;
+    default: r = 0.0;
+  }
+  out[i] = r;
+}
+hipError_t launch_math_selftest(int op, const double* d_in, double* d_out, int n, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(math_selftest_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, op, d_in, d_out, n);
+  return hipGetLastError();
+}
+}  // namespace pmvsdev

@@ -1,0 +1,49 @@
+// pmvs_layout.h -- device-resident scene layout shared by the kernels and the host API.
+// (Plain structs only: included by host-only code too.)
+#pragma once
+#include <stdint.h>
+
+#include "../../include/pmvs_amd.h"
+
+namespace pmvsdev {
+
+constexpr int MAXL = PMVS_MAX_LEVEL + 3;
+constexpr int TEXCAP = 16;  // textures resident in LDS per wave (>= PMVS_MAX_TAU)
+
+struct DView {
+  float P[MAXL][12];
+  float center[4];
+  float xaxis[3], yaxis[3], zaxis[3];
+  float ipscale;
+  int w[MAXL], h[MAXL];
+  long long pyr_off[MAXL];   // word offset of (view, level) in DScene::pyr
+  long long mask_off[MAXL];  // byte offset in DScene::masks, -1 if no mask
+  long long edge_off[MAXL];  // byte offset in DScene::edges, -1 if no edge map
+};
+
+struct DScene {
+  const DView* views;
+  const uint32_t* pyr;
+  const uint8_t* masks;
+  const uint8_t* edges;
+  const int* vis_off;
+  const int* vis;
+  const int* bindexes;
+  float* scratch;  // per-workgroup pairwise-INCC matrices (PMVS_MAX_IMAGES^2 floats each)
+  int nb;
+  int num, tnum, level, csize, wsize, minImageNum, tau, anyMask;
+  float nccThreshold, nccThresholdBefore, maxAngle, angle1;
+  float athreshold;     // (float)cos((double)_angleThreshold0)     optim.cpp:416
+  double cosAngle1;     // cos((double)_angleThreshold1)            optim.cpp:134,823
+  float sortThreshold;  // (float)(1.0f - cos(10.0*M_PI/180.0))      optim.cpp:287
+  float ascale;         // (float)(M_PI / 48.0f)                      optim.cpp:590
+  float log2f;          // static float Log2 = log(2.0f)              optim.cpp:813
+  float pad;
+};
+
+struct DevStats {
+  unsigned long long evals, tex_valid, tex_grabs, accepted, fail_pre, fail_post, refine_failed;
+  unsigned long long queue;  // dynamic work-queue head
+};
+
+}  // namespace pmvsdev

@@ -1,0 +1,328 @@
+"""pmvs_amd.py -- host-side Python mirror of the C-ABI in include/pmvs_amd.h (ctypes).
+
+This is the test/bench-facing mirror of the boundary: numpy record dtypes with the exact C
+layout of pmvs_candidate / pmvs_refined / pmvs_eval_query / pmvs_tex_query, a Scene wrapper
+over pmvs_scene_create/destroy, and the batch entry points.  It never falls back to a CPU
+path: if libpmvs_amd.so is missing or a HIP device is absent the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpmvs_amd.so")
+
+MAX_IMAGES = 64
+MAX_TAU = 16
+
+ACCEPTED, FAIL_PRE, FAIL_POST, FAIL_OVERFLOW = 0, 1, 2, 3
+
+CANDIDATE_DTYPE = np.dtype(
+    [("coord", "<f4", 4), ("normal", "<f4", 4), ("dscale", "<f4"), ("num_images", "<i4"),
+     ("images", "<i4", MAX_IMAGES)], align=True)
+REFINED_DTYPE = np.dtype(
+    [("status", "<i4"), ("refine_code", "<i4"), ("evals", "<i4"), ("num_images", "<i4"),
+     ("coord", "<f4", 4), ("normal", "<f4", 4), ("ncc", "<f4"), ("dscale", "<f4"), ("ascale", "<f4"),
+     ("tmp", "<f4"), ("timages", "<i4"), ("reserved", "<i4"), ("images", "<i4", MAX_IMAGES),
+     ("grids", "<i4", (MAX_IMAGES, 2))], align=True)
+EVAL_QUERY_DTYPE = np.dtype(
+    [("coord", "<f4", 4), ("normal", "<f4", 4), ("dscale", "<f4"), ("num_images", "<i4"),
+     ("images", "<i4", MAX_TAU), ("x", "<f8", 3)], align=True)
+TEX_QUERY_DTYPE = np.dtype(
+    [("coord", "<f4", 4), ("pxaxis", "<f4", 4), ("pyaxis", "<f4", 4), ("normal", "<f4", 4),
+     ("view", "<i4"), ("normalize", "<i4")], align=True)
+
+
+class ViewDesc(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("rgb", C.c_void_p), ("mask", C.c_void_p),
+                ("edge", C.c_void_p), ("projection", C.c_float * 12)]
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [("num_views", C.c_int32), ("num_targets", C.c_int32), ("level", C.c_int32),
+                ("csize", C.c_int32), ("wsize", C.c_int32), ("min_image_num", C.c_int32),
+                ("threshold", C.c_float), ("max_angle", C.c_float), ("quad_threshold", C.c_float),
+                ("sequence", C.c_int32), ("visdata2_offsets", C.c_void_p), ("visdata2", C.c_void_p),
+                ("num_bindexes", C.c_int32), ("bindexes", C.c_void_p), ("views", C.POINTER(ViewDesc))]
+
+
+class Stats(C.Structure):
+    _fields_ = [("candidates", C.c_int64), ("accepted", C.c_int64), ("fail_pre", C.c_int64),
+                ("fail_post", C.c_int64), ("refine_failed", C.c_int64), ("evals", C.c_int64),
+                ("tex_valid", C.c_int64), ("tex_grabs", C.c_int64), ("kernel_ms", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class SynthParams(C.Structure):
+    _fields_ = [("num_views", C.c_int32), ("num_targets", C.c_int32), ("width", C.c_int32),
+                ("height", C.c_int32), ("supersample", C.c_int32), ("level", C.c_int32),
+                ("seed", C.c_uint64), ("ring_radius", C.c_double), ("height_offset", C.c_double),
+                ("focal_scale", C.c_double), ("arc_step_deg", C.c_double)]
+
+
+EXPORTS = ["pmvs_last_error", "pmvs_device_count", "pmvs_scene_create", "pmvs_scene_destroy",
+           "pmvs_set_thresholds", "pmvs_scene_get_level", "pmvs_grab_tex", "pmvs_incc_eval",
+           "pmvs_refine_batch", "pmvs_refine_batch_device", "pmvs_scene_sync", "pmvs_synth_ring",
+           "pmvs_synth_candidates", "pmvs_selftest_math"]
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    """Load libpmvs_amd.so (raises if it has not been built: there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} not built: run `make -C cmvs-pmvs_amd` (no CPU fallback exists)")
+    lib = C.CDLL(path)
+    lib.pmvs_last_error.restype = C.c_char_p
+    lib.pmvs_device_count.restype = C.c_int32
+    lib.pmvs_scene_create.argtypes = [C.POINTER(SceneDesc), C.c_int32, C.POINTER(C.c_void_p)]
+    lib.pmvs_scene_destroy.argtypes = [C.c_void_p]
+    lib.pmvs_scene_destroy.restype = None
+    lib.pmvs_set_thresholds.argtypes = [C.c_void_p, C.c_float, C.c_float, C.c_int32]
+    lib.pmvs_scene_get_level.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p,
+                                         C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    lib.pmvs_grab_tex.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+    lib.pmvs_incc_eval.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(Stats)]
+    lib.pmvs_refine_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(Stats)]
+    lib.pmvs_refine_batch_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+    lib.pmvs_scene_sync.argtypes = [C.c_void_p, C.POINTER(Stats)]
+    lib.pmvs_synth_ring.argtypes = [C.POINTER(SynthParams), C.c_void_p, C.c_void_p, C.c_int32]
+    lib.pmvs_synth_candidates.argtypes = [C.POINTER(SynthParams), C.c_void_p, C.c_int32, C.c_uint64,
+                                          C.c_float, C.c_float, C.c_void_p]
+    lib.pmvs_selftest_math.argtypes = [C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32]
+    for fn in EXPORTS:
+        getattr(lib, fn).restype = getattr(lib, fn).restype or C.c_int
+    lib.pmvs_last_error.restype = C.c_char_p
+    lib.pmvs_device_count.restype = C.c_int32
+    lib.pmvs_scene_destroy.restype = None
+    _lib = lib
+    return lib
+
+
+class PmvsError(RuntimeError):
+    pass
+
+
+def _check(status: int):
+    if status != 0:
+        msg = load_library().pmvs_last_error().decode(errors="replace")
+        raise PmvsError(f"pmvs status {status}: {msg}")
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+# ---------------------------------------------------------------------------------- scene
+@dataclass
+class SceneInputs:
+    """Everything pmvs_scene_create needs (SOption + image/camera set), as numpy arrays."""
+    images: List[np.ndarray]             # per view uint8 [H, W, 3]
+    projections: np.ndarray              # float32 [V, 3, 4] (level 0)
+    num_targets: int
+    level: int = 1
+    csize: int = 2
+    wsize: int = 7
+    min_image_num: int = 3
+    threshold: float = 0.7
+    max_angle_deg: Optional[float] = None   # None = SOption default (option.cpp:25)
+    quad: float = 2.5
+    sequence: int = -1
+    visdata2: Optional[List[List[int]]] = None   # None = all-pairs (useVisData 0, option.cpp:204-220)
+    bindexes: Sequence[int] = ()
+    masks: Optional[List[Optional[np.ndarray]]] = None
+    edges: Optional[List[Optional[np.ndarray]]] = None
+    _keep: list = field(default_factory=list, repr=False)
+
+    def vis_csr(self):
+        V = len(self.images)
+        vis = self.visdata2
+        if vis is None:
+            vis = [[x for x in range(V) if x != y] for y in range(V)]
+        off = np.zeros(V + 1, np.int32)
+        for i, row in enumerate(vis):
+            off[i + 1] = off[i] + len(row)
+        flat = np.array([x for row in vis for x in row] or [0], np.int32)
+        return off, flat
+
+    def max_angle_rad(self) -> float:
+        if self.max_angle_deg is None:
+            # SOption(): _maxAngleThreshold = 10.0f * M_PI / 180.0f  (evaluated in double)
+            return float(np.float32(np.float64(np.float32(10.0)) * np.pi / np.float64(np.float32(180.0))))
+        # SOption::init "maxAngle": _maxAngleThreshold *= M_PI / 180.0f  (float *= double)
+        return float(np.float32(np.float64(np.float32(self.max_angle_deg)) * (np.pi / np.float64(np.float32(180.0)))))
+
+    def build_desc(self) -> SceneDesc:
+        V = len(self.images)
+        self._keep = []
+        views = (ViewDesc * V)()
+        for i, img in enumerate(self.images):
+            img = np.ascontiguousarray(img, dtype=np.uint8)
+            assert img.ndim == 3 and img.shape[2] == 3
+            self._keep.append(img)
+            views[i].width = img.shape[1]
+            views[i].height = img.shape[0]
+            views[i].rgb = img.ctypes.data
+            m = None if self.masks is None else self.masks[i]
+            e = None if self.edges is None else self.edges[i]
+            if m is not None:
+                m = np.ascontiguousarray(m, np.uint8)
+                self._keep.append(m)
+                views[i].mask = m.ctypes.data
+            if e is not None:
+                e = np.ascontiguousarray(e, np.uint8)
+                self._keep.append(e)
+                views[i].edge = e.ctypes.data
+            p = np.asarray(self.projections[i], np.float32).reshape(12)
+            for k in range(12):
+                views[i].projection[k] = float(p[k])
+        off, flat = self.vis_csr()
+        bidx = np.array(list(self.bindexes) or [0], np.int32)
+        self._keep += [off, flat, bidx, views]
+        d = SceneDesc()
+        d.num_views = V
+        d.num_targets = self.num_targets
+        d.level = self.level
+        d.csize = self.csize
+        d.wsize = self.wsize
+        d.min_image_num = self.min_image_num
+        d.threshold = self.threshold
+        d.max_angle = self.max_angle_rad()
+        d.quad_threshold = self.quad
+        d.sequence = self.sequence
+        d.visdata2_offsets = off.ctypes.data
+        d.visdata2 = flat.ctypes.data
+        d.num_bindexes = len(self.bindexes)
+        d.bindexes = bidx.ctypes.data
+        d.views = C.cast(views, C.POINTER(ViewDesc))
+        return d
+
+
+class Scene:
+    """A device-resident scene on one GPU (pmvs_scene_create)."""
+
+    def __init__(self, inputs: SceneInputs, device: int = 0):
+        self.lib = load_library()
+        self.inputs = inputs
+        self.desc = inputs.build_desc()
+        h = C.c_void_p()
+        _check(self.lib.pmvs_scene_create(C.byref(self.desc), device, C.byref(h)))
+        self.handle = h
+        self.wsize = inputs.wsize
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.pmvs_scene_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_thresholds(self, ncc: float, ncc_before: float, depth: int = 0):
+        _check(self.lib.pmvs_set_thresholds(self.handle, ncc, ncc_before, depth))
+
+    def get_level(self, view: int, level: int) -> np.ndarray:
+        w, h = C.c_int32(), C.c_int32()
+        _check(self.lib.pmvs_scene_get_level(self.handle, view, level, None, C.byref(w), C.byref(h)))
+        out = np.empty((h.value, w.value, 3), np.uint8)
+        _check(self.lib.pmvs_scene_get_level(self.handle, view, level, _ptr(out), C.byref(w), C.byref(h)))
+        return out
+
+    def grab_tex(self, q: np.ndarray):
+        q = np.ascontiguousarray(q, TEX_QUERY_DTYPE)
+        n = len(q)
+        out = np.zeros((n, 3 * self.wsize * self.wsize), np.float32)
+        valid = np.zeros(n, np.int32)
+        _check(self.lib.pmvs_grab_tex(self.handle, _ptr(q), n, _ptr(out), _ptr(valid)))
+        return out, valid
+
+    def incc_eval(self, q: np.ndarray):
+        q = np.ascontiguousarray(q, EVAL_QUERY_DTYPE)
+        n = len(q)
+        out = np.zeros(n, np.float64)
+        st = Stats()
+        _check(self.lib.pmvs_incc_eval(self.handle, _ptr(q), n, _ptr(out), C.byref(st)))
+        return out, st.as_dict()
+
+    def refine_batch(self, cands: np.ndarray):
+        cands = np.ascontiguousarray(cands, CANDIDATE_DTYPE)
+        n = len(cands)
+        out = np.zeros(n, REFINED_DTYPE)
+        st = Stats()
+        _check(self.lib.pmvs_refine_batch(self.handle, _ptr(cands), n, _ptr(out), C.byref(st)))
+        return out, st.as_dict()
+
+    def refine_batch_device(self, d_in_ptr: int, n: int, d_out_ptr: int):
+        _check(self.lib.pmvs_refine_batch_device(self.handle, C.c_void_p(d_in_ptr), n, C.c_void_p(d_out_ptr)))
+
+    def sync(self):
+        st = Stats()
+        _check(self.lib.pmvs_scene_sync(self.handle, C.byref(st)))
+        return st.as_dict()
+
+
+def selftest_math(op: int, x: np.ndarray, device: int = 0) -> np.ndarray:
+    x = np.ascontiguousarray(x, np.float64)
+    out = np.zeros_like(x)
+    _check(load_library().pmvs_selftest_math(device, op, _ptr(x), _ptr(out), len(x)))
+    return out
+
+
+def device_count() -> int:
+    return int(load_library().pmvs_device_count())
+
+
+# ---------------------------------------------------------------------------------- synthetic data
+def synth_params(num_views: int, width: int, height: int, num_targets: Optional[int] = None,
+                 supersample: int = 2, level: int = 1, seed: int = 0x504D5653,
+                 ring_radius: float = 4.0, height_offset: float = 0.3, focal_scale: float = 1.16,
+                 arc_step_deg: Optional[float] = None) -> SynthParams:
+    p = SynthParams()
+    p.num_views = num_views
+    p.num_targets = num_views if num_targets is None else num_targets
+    p.width, p.height = width, height
+    p.supersample = supersample
+    p.level = level
+    p.seed = seed
+    p.ring_radius, p.height_offset, p.focal_scale = ring_radius, height_offset, focal_scale
+    # cameras every min(360/V, 15) degrees: a full ring for V >= 24, an arc otherwise
+    p.arc_step_deg = min(360.0 / num_views, 15.0) if arc_step_deg is None else arc_step_deg
+    return p
+
+
+def synth_ring(p: SynthParams, nthreads: int = 8, render: bool = True):
+    lib = load_library()
+    proj = np.zeros((p.num_views, 3, 4), np.float32)
+    rgb = np.zeros((p.num_views, p.height, p.width, 3), np.uint8) if render else None
+    _check(lib.pmvs_synth_ring(C.byref(p), _ptr(rgb), _ptr(proj), nthreads))
+    return rgb, proj
+
+
+def synth_candidates(p: SynthParams, proj: np.ndarray, n: int, seed: int = 0x5EED,
+                     depth_sigma_px: float = 1.0, max_tilt_deg: float = 10.0) -> np.ndarray:
+    lib = load_library()
+    out = np.zeros(n, CANDIDATE_DTYPE)
+    proj = np.ascontiguousarray(proj, np.float32)
+    _check(lib.pmvs_synth_candidates(C.byref(p), _ptr(proj), n, seed, depth_sigma_px, max_tilt_deg, _ptr(out)))
+    return out
+
+
+def synth_scene(num_views: int, width: int, height: int, level: int = 1, num_targets: Optional[int] = None,
+                supersample: int = 2, nthreads: int = 8, **opts) -> SceneInputs:
+    p = synth_params(num_views, width, height, num_targets=num_targets, supersample=supersample, level=level)
+    rgb, proj = synth_ring(p, nthreads=nthreads)
+    return SceneInputs(images=[rgb[i] for i in range(num_views)], projections=proj,
+                       num_targets=p.num_targets, level=level, **opts), p

@@ -179,6 +179,35 @@ pmvs_status pmvs_refine_batch_device(pmvs_scene* scene, const pmvs_candidate* d_
                                      pmvs_refined* d_out);
 pmvs_status pmvs_scene_sync(pmvs_scene* scene, pmvs_stats* stats);
 
+
+/* Self-test: evaluates the device libm function `op` (0 sqrt, 1 sin, 2 cos, 3 asin, 4 acos,
+ * 5 atan, 6 log, 7 f32 sqrt, 8 f32 divide in[i]/in[i+1], 9 floor) on n doubles. */
+pmvs_status pmvs_selftest_math(int32_t device, int32_t op, const double* in, double* out, int32_t n);
+
+/* ---------------------------------------------------------------------------------------
+ * Synthetic workload generator (NOT a reference interface: the reference ships no data).
+ * Textured unit sphere seen by a ring of pinhole cameras. */
+typedef struct pmvs_synth_params {
+  int32_t num_views;     /* ring cameras */
+  int32_t num_targets;   /* candidate reference images are drawn from the first num_targets */
+  int32_t width, height; /* level-0 image size */
+  int32_t supersample;   /* per-axis supersampling (1..4) */
+  int32_t level;         /* option level the candidates are meant for (depth perturbation scale) */
+  uint64_t seed;         /* texture seed */
+  double ring_radius;    /* camera distance from the sphere centre (4.0) */
+  double height_offset;  /* alternating camera height (0.3) */
+  double focal_scale;    /* f = focal_scale * width */
+  double arc_step_deg;   /* angular spacing of the cameras on the ring (0 = 360/num_views) */
+} pmvs_synth_params;
+
+/* Renders num_views RGB8 images (rgb: num_views*width*height*3 bytes, may be NULL to get only
+ * the projections) and writes num_views 3x4 projections (proj: 12 floats per view). */
+pmvs_status pmvs_synth_ring(const pmvs_synth_params* p, uint8_t* rgb, float* proj, int32_t nthreads);
+
+/* n seed-path candidates (images = [most frontal target, next most frontal view]). */
+pmvs_status pmvs_synth_candidates(const pmvs_synth_params* p, const float* proj, int32_t n, uint64_t seed,
+                                  float depth_sigma_px, float max_tilt_deg, pmvs_candidate* out);
+
 #ifdef __cplusplus
 }
 #endif

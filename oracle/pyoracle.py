@@ -1,0 +1,150 @@
+"""oracle/pyoracle.py -- TEST INFRASTRUCTURE ONLY: ctypes access to the CPU oracle
+(oracle/liboracle.so, the restatement of the reference hot path) and to oracle/_ref
+(the reference's own camera/option/patch TUs).  Only tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg import this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "cmvs-pmvs_amd"))
+import pmvs_amd as P  # noqa: E402  (struct layouts of include/pmvs_amd.h)
+
+ORACLE_LIB = os.path.join(HERE, "liboracle.so")
+REF_LIB = os.path.join(HERE, "_ref", "libpmvs_ref.so")
+
+_lib = None
+_ref = None
+
+
+def build():
+    subprocess.run(["make", "-C", HERE, "-s"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_LIB):
+            build()
+        L = C.CDLL(ORACLE_LIB)
+        L.oracle_scene_create.restype = C.c_void_p
+        L.oracle_scene_create.argtypes = [C.POINTER(P.SceneDesc)]
+        L.oracle_scene_destroy.argtypes = [C.c_void_p]
+        L.oracle_set_thresholds.argtypes = [C.c_void_p, C.c_float, C.c_float, C.c_int]
+        L.oracle_get_level.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.oracle_camera.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+        L.oracle_project.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p]
+        L.oracle_grab_tex.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        L.oracle_paxes.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_incc_eval.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        L.oracle_refine_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.POINTER(P.Stats)]
+        L.oracle_bobyqa_test.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_int, C.POINTER(C.c_int)]
+        _lib = L
+    return _lib
+
+
+def ref_lib():
+    """The reference's own TUs (None when oracle/_ref was not built: reference absent)."""
+    global _ref
+    if _ref is None:
+        if not os.path.exists(REF_LIB):
+            return None
+        R = C.CDLL(REF_LIB)
+        R.ref_camera.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_void_p]
+        R.ref_project.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p]
+        R.ref_option.argtypes = [C.c_char_p, C.c_char_p] + [C.c_void_p] * 7 + [C.c_int]
+        R.ref_write_patches.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_void_p, C.c_int]
+        R.ref_write_pset.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+        R.ref_ortho.argtypes = [C.c_void_p, C.c_void_p]
+        _ref = R
+    return _ref
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class OracleScene:
+    def __init__(self, inputs: "P.SceneInputs"):
+        self.inputs = inputs
+        self.desc = inputs.build_desc()
+        self.h = lib().oracle_scene_create(C.byref(self.desc))
+        self.wsize = inputs.wsize
+
+    def close(self):
+        if self.h:
+            lib().oracle_scene_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_thresholds(self, ncc, before, depth=0):
+        lib().oracle_set_thresholds(self.h, ncc, before, depth)
+
+    def get_level(self, view, level):
+        w, h = C.c_int(), C.c_int()
+        lib().oracle_get_level(self.h, view, level, None, C.byref(w), C.byref(h))
+        out = np.empty((h.value, w.value, 3), np.uint8)
+        lib().oracle_get_level(self.h, view, level, _p(out), C.byref(w), C.byref(h))
+        return out
+
+    def camera(self, view, level):
+        out = np.zeros(30, np.float32)
+        lib().oracle_camera(self.h, view, level, _p(out))
+        return out
+
+    def project(self, view, level, coords):
+        coords = np.ascontiguousarray(coords, np.float32)
+        out = np.zeros((len(coords), 3), np.float32)
+        lib().oracle_project(self.h, view, level, _p(coords), len(coords), _p(out))
+        return out
+
+    def paxes(self, view, coord, normal):
+        out = np.zeros(8, np.float32)
+        c = np.ascontiguousarray(coord, np.float32)
+        n = np.ascontiguousarray(normal, np.float32)
+        lib().oracle_paxes(self.h, view, _p(c), _p(n), _p(out))
+        return out[:4], out[4:]
+
+    def grab_tex(self, q):
+        q = np.ascontiguousarray(q, P.TEX_QUERY_DTYPE)
+        out = np.zeros((len(q), 3 * self.wsize * self.wsize), np.float32)
+        valid = np.zeros(len(q), np.int32)
+        lib().oracle_grab_tex(self.h, _p(q), len(q), _p(out), _p(valid))
+        return out, valid
+
+    def incc_eval(self, q, want_encode=False):
+        q = np.ascontiguousarray(q, P.EVAL_QUERY_DTYPE)
+        out = np.zeros(len(q), np.float64)
+        enc = np.zeros((len(q), 3), np.float64) if want_encode else None
+        lib().oracle_incc_eval(self.h, _p(q), len(q), _p(out), _p(enc))
+        return (out, enc) if want_encode else out
+
+    def refine_batch(self, cands, nthreads=1):
+        cands = np.ascontiguousarray(cands, P.CANDIDATE_DTYPE)
+        out = np.zeros(len(cands), P.REFINED_DTYPE)
+        st = P.Stats()
+        lib().oracle_refine_batch(self.h, _p(cands), len(cands), _p(out), nthreads, C.byref(st))
+        return out, st.as_dict()
+
+
+def bobyqa_test(kind, x0, maxeval=1000, maxrec=2000):
+    x0 = np.ascontiguousarray(x0, np.float64)
+    xo = np.zeros(3)
+    fo = np.zeros(1)
+    rec = np.zeros(maxrec)
+    nrec = C.c_int()
+    rc = lib().oracle_bobyqa_test(kind, _p(x0), maxeval, _p(xo), _p(fo), _p(rec), maxrec, C.byref(nrec))
+    return rc, xo, fo[0], rec[:min(nrec.value, maxrec)].copy()
