@@ -161,7 +161,8 @@ struct pmvs_scene {
   DBuf<int> vis_off, vis, bindexes;
   DBuf<float> scratch;
   DBuf<DevStats> stats;
-  int grid = 0;
+  DBuf<RefineJob> jobs;
+  int grid = 0, refine_grid = 0;
   // staging for host-pointer calls
   DBuf<pmvs_candidate> cand;
   DBuf<pmvs_refined> res;
@@ -172,7 +173,7 @@ struct pmvs_scene {
   DBuf<int> tvalid;
   ~pmvs_scene() {
     views.release(); pyr.release(); masks.release(); edges.release(); vis_off.release(); vis.release();
-    bindexes.release(); scratch.release(); stats.release(); cand.release(); res.release(); evq.release();
+    bindexes.release(); scratch.release(); stats.release(); jobs.release(); cand.release(); res.release(); evq.release();
     evout.release(); tq.release(); tout.release(); tvalid.release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -338,6 +339,7 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return bail(fail(PMVS_EDEVICE, "device properties"));
   sc->grid = std::max(1, prop.multiProcessorCount) * 8;
+  sc->refine_grid = std::max(1, prop.multiProcessorCount) * 4;
   if (sc->scratch.alloc((size_t)sc->grid * PMVS_MAX_IMAGES * PMVS_MAX_IMAGES) != hipSuccess)
     return bail(fail(PMVS_ENOMEM, "scratch"));
 
@@ -479,9 +481,11 @@ pmvs_status pmvs_refine_batch_device(pmvs_scene* sc, const pmvs_candidate* d_in,
   if (!sc || (n > 0 && (!d_in || !d_out))) return fail(PMVS_EINVAL, "null argument");
   if (n <= 0) return PMVS_OK;
   HIPCHK(hipSetDevice(sc->device));
+  pmvs_status st;
+  if ((st = ensure(sc->jobs, n))) return st;
   HIPCHK(hipMemsetAsync(sc->stats.p, 0, sizeof(DevStats), sc->stream));
   HIPCHK(hipEventRecord(sc->ev0, sc->stream));
-  HIPCHK(launch_refine(sc->ds, d_in, d_out, n, sc->stats.p, sc->grid, sc->stream));
+  HIPCHK(launch_refine(sc->ds, d_in, sc->jobs.p, d_out, n, sc->stats.p, sc->grid, sc->refine_grid, sc->stream));
   HIPCHK(hipEventRecord(sc->ev1, sc->stream));
   return PMVS_OK;
 }
@@ -531,6 +535,32 @@ pmvs_status pmvs_selftest_math(int32_t device, int32_t op, const double* in, dou
   (void)hipFree(di);
   if (dout) (void)hipFree(dout);
   if (e != hipSuccess) return fail(PMVS_EDEVICE, "math selftest: %s", hipGetErrorString(e));
+  return PMVS_OK;
+}
+
+pmvs_status pmvs_selftest_bobyqa(int32_t device, int32_t mode, int32_t kind, const double* x0, int32_t n,
+                                 int32_t maxeval, double* out, double* ms) {
+  if (!x0 || !out || n <= 0) return fail(PMVS_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(device));
+  double *dx = nullptr, *dout = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  HIPCHK(hipMalloc((void**)&dx, 3 * n * sizeof(double)));
+  hipError_t e = hipMalloc((void**)&dout, 6 * n * sizeof(double));
+  if (e == hipSuccess) e = hipEventCreate(&e0);
+  if (e == hipSuccess) e = hipEventCreate(&e1);
+  if (e == hipSuccess) e = hipMemcpy(dx, x0, 3 * n * sizeof(double), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipEventRecord(e0, nullptr);
+  if (e == hipSuccess) e = launch_bobyqa_selftest(mode, kind, dx, n, maxeval, dout, nullptr);
+  if (e == hipSuccess) e = hipEventRecord(e1, nullptr);
+  if (e == hipSuccess) e = hipMemcpy(out, dout, 6 * n * sizeof(double), hipMemcpyDeviceToHost);
+  float t = 0;
+  if (e == hipSuccess) e = hipEventElapsedTime(&t, e0, e1);
+  if (ms) *ms = t;
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  (void)hipFree(dx);
+  if (dout) (void)hipFree(dout);
+  if (e != hipSuccess) return fail(PMVS_EDEVICE, "bobyqa selftest: %s", hipGetErrorString(e));
   return PMVS_OK;
 }
 

@@ -21,6 +21,9 @@
 namespace pmvsdev {
 
 constexpr int WAVE = 64;
+#ifndef REFINE_TSLOTS
+#define REFINE_TSLOTS 48
+#endif
 
 template <int WS>
 struct WaveLds {
@@ -635,55 +638,55 @@ __device__ void set_ref_image(const DScene& s, WaveLds<WS>& L, const float* coor
   __syncthreads();
 }
 
-// ---------------------------------------------------------------- refine one candidate
+// ---------------------------------------------------------------- preProcess (kernel 1)
+// COptim::preProcess (optim.cpp:95-122) + the refinePatchBFGS setup (optim.cpp:584-599,629-634)
+// for one candidate; writes a RefineJob.  acc: [2] grabs.
 template <int WS>
-__device__ void refine_candidate(const DScene& s, WaveLds<WS>& L, const pmvs_candidate& cin, pmvs_refined& cout,
-                                 float* mat, unsigned long long* acc) {
-  // acc: [0] evals [1] tex_valid [2] grabs [3] accepted [4] fail_pre [5] fail_post [6] refine_failed
+__device__ void pre_candidate(const DScene& s, WaveLds<WS>& L, const pmvs_candidate& cin, RefineJob& job,
+                              unsigned long long* acc) {
   const int lane = lane_id();
   float coord[4], normal[4];
   for (int i = 0; i < 4; ++i) { coord[i] = cin.coord[i]; normal[i] = cin.normal[i]; }
-  float dscale = cin.dscale, ascale = 0.0f, ncc = -1.0f, tmp = 0.0f;
-  int timages = 0, status = PMVS_ACCEPTED, refine_code = 0, evals = 0;
+  float dscale = cin.dscale, ascale = 0.0f;
   const int n0 = imin(cin.num_images, PMVS_MAX_IMAGES);
-  if (lane < n0) L.images[lane] = cin.images[lane];
-  if (lane == 0) { L.nimg = n0; L.overflow = (cin.num_images > PMVS_MAX_IMAGES); }
-  __syncthreads();
-
-  // ---------------- preProcess (optim.cpp:95-122)
-  add_images<WS>(s, L, coord, normal);
-  constraint_images<WS>(s, L, coord, normal, s.nccThresholdBefore, &acc[2]);
-  sort_images<WS>(s, L, coord, normal);
-  // broadcast dscale/ascale (set_scales accumulates onto the candidate's _dscale)
-  if (lane == 0 && L.nimg > 0) {
-    float ds = dscale, as = 0.0f;
-    set_scales(s, L.images, L.nimg, coord, &ds, &as);
-    L.fl2[0] = ds;
-    L.fl2[1] = as;
+  bool badidx = false;
+  if (lane < n0) {
+    const int img = cin.images[lane];
+    badidx = (img < 0 || img >= s.num);
+    L.images[lane] = badidx ? 0 : img;
   }
+  badidx = __ballot(badidx) != 0;
+  if (lane == 0) { L.nimg = n0; L.overflow = (cin.num_images > PMVS_MAX_IMAGES || n0 < 1 || badidx); }
   __syncthreads();
-  if (L.nimg > 0) { dscale = L.fl2[0]; ascale = L.fl2[1]; }
-  __syncthreads();
-  int fail = 0;
-  if (L.nimg < s.minImageNum) fail = 1;
-  else if (check_angles<WS>(s, L, coord, s.maxAngle, s.angle1)) {
-    fail = 1;
-    if (lane == 0) L.nimg = 0;
-    __syncthreads();
-  }
-  if (fail) {
-    status = PMVS_FAIL_PRE;
+  int status = PMVS_ACCEPTED;
+  if (L.overflow) {
+    status = PMVS_FAIL_OVERFLOW;
   } else {
-    // ---------------- refinePatchBFGS (optim.cpp:580-658)
-    RefineSetup R;
-    const DView& vr = s.views[L.images[0]];
-    for (int i = 0; i < 4; ++i) { R.center[i] = coord[i]; R.ray[i] = coord[i] - vr.center[i]; }
-    unitize4(R.ray);
-    R.dscale = dscale;
-    R.ascale = s.ascale;
-    R.ref = L.images[0];
-    // weights: computeUnits(patch) then min(1, w0 / wi), stored in L.fl2[]
-    const int ni = L.nimg;
+    add_images<WS>(s, L, coord, normal);
+    constraint_images<WS>(s, L, coord, normal, s.nccThresholdBefore, &acc[2]);
+    sort_images<WS>(s, L, coord, normal);
+    // setScales accumulates onto the candidate's _dscale (patchOrganizerS.cpp:672)
+    if (lane == 0 && L.nimg > 0) {
+      float ds = dscale, as = 0.0f;
+      set_scales(s, L.images, L.nimg, coord, &ds, &as);
+      L.fl2[0] = ds;
+      L.fl2[1] = as;
+    }
+    __syncthreads();
+    if (L.nimg > 0) { dscale = L.fl2[0]; ascale = L.fl2[1]; }
+    __syncthreads();
+    if (L.nimg < s.minImageNum) {
+      status = PMVS_FAIL_PRE;
+    } else if (check_angles<WS>(s, L, coord, s.maxAngle, s.angle1)) {
+      status = PMVS_FAIL_PRE;
+      if (lane == 0) L.nimg = 0;
+      __syncthreads();
+    }
+    if (L.overflow) status = PMVS_FAIL_OVERFLOW;
+  }
+  const int ni = L.nimg;
+  if (status == PMVS_ACCEPTED) {
+    // weights: computeUnits(patch) (optim.cpp:446-471) then min(1, w0 / wi)
     if (lane < ni) {
       const DView& v = s.views[L.images[lane]];
       float u = get_unit(s, v, coord);
@@ -691,62 +694,74 @@ __device__ void refine_candidate(const DScene& s, WaveLds<WS>& L, const pmvs_can
       unitize4(ray);
       const float den = dot4(ray, normal);
       if (0.0f < den) u = __fdiv_rn(u, den);
-      else u = 1073741824.0f;
+      else u = 1073741824.0f;  // (float)(INT_MAX/2)
       L.fl[lane] = u;
     }
     __syncthreads();
-    if (lane < ni) {
+    if (lane < ni && lane < PMVS_MAX_TAU) {
       const float w0 = L.fl[0];
-      L.fl2[lane] = (lane == 0) ? 1.0f : smin(1.0f, __fdiv_rn(w0, L.fl[lane]));
+      job.weights[lane] = (lane == 0) ? 1.0f : smin(1.0f, __fdiv_rn(w0, L.fl[lane]));
     }
-    __syncthreads();
-    double p[3];
-    encode(s, R, coord, normal, p);
-    const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999};
-    const double ub[3] = {HUGE_VAL, 23.99999, 23.99999};
-    double x0[3];
-    for (int i = 0; i < 3; ++i) {
-      const double m = (ub[i] < p[i]) ? ub[i] : p[i];
-      x0[i] = (m < lb[i]) ? lb[i] : m;
-    }
-    const int nidx = imin(ni, PMVS_MAX_TAU);
-    int tidx[PMVS_MAX_TAU];
-    for (int i = 0; i < nidx; ++i) tidx[i] = L.images[i];
     if (lane == 0) {
-      bq_begin(L.bq, x0, lb, ub, 1.e-7, 1000);
-      L.fres = 0.0;
+      RefineSetup R;
+      const DView& vr = s.views[L.images[0]];
+      for (int i = 0; i < 4; ++i) { R.center[i] = coord[i]; R.ray[i] = coord[i] - vr.center[i]; }
+      unitize4(R.ray);
+      R.dscale = dscale;
+      R.ascale = s.ascale;
+      R.ref = L.images[0];
+      double p[3];
+      encode(s, R, coord, normal, p);
+      const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999};
+      const double ub[3] = {HUGE_VAL, 23.99999, 23.99999};
+      for (int i = 0; i < 3; ++i) {
+        const double m = (ub[i] < p[i]) ? ub[i] : p[i];  // std::min(p, ub)
+        job.x0[i] = (m < lb[i]) ? lb[i] : m;             // std::max(., lb)
+      }
+      for (int i = 0; i < 4; ++i) { job.center[i] = R.center[i]; job.ray[i] = R.ray[i]; }
     }
-    __syncthreads();
-    unsigned long long nvalid = 0;
-    for (;;) {
-      if (lane == 0) L.step = (L.bq.resume < 0) ? BQ_DONE : bq_step(L.bq, L.fres);
-      __syncthreads();
-      if (L.step != BQ_NEED_F) break;
-      const double xe[3] = {L.bq.xeval[0], L.bq.xeval[1], L.bq.xeval[2]};
-      __syncthreads();
-      const double f = my_f<WS>(s, L, R, tidx, nidx, xe, &acc[2], &nvalid);
-      evals++;
-      if (lane == 0) L.fres = f;
-      __syncthreads();
+  }
+  if (lane < ni) job.images[lane] = L.images[lane];
+  if (lane == 0) {
+    for (int i = 0; i < 4; ++i) {
+      job.coord[i] = coord[i]; job.normal[i] = normal[i];
+      job.rcoord[i] = coord[i]; job.rnormal[i] = normal[i];
     }
-    refine_code = L.bq.rc;
-    const double xo[3] = {L.bq.xout[0], L.bq.xout[1], L.bq.xout[2]};
-    __syncthreads();
-    if (lane == 0) { acc[0] += evals; acc[1] += nvalid; }
-    const bool success = (refine_code == BQR_SUCCESS || refine_code == 2 || refine_code == 3 || refine_code == BQR_XTOL);
-    if (!success) {
-      if (lane == 0) acc[6] += 1;
-    } else {
-      decode(s, R, xo, coord, normal);
-      const double sc = compute_incc<WS>(s, L, coord, normal, L.images, L.nimg, &acc[2]);
-      ncc = (float)(1.0 - (double)unrobustincc((float)sc));
-    }
-    // ---------------- postProcess (optim.cpp:150-190), depth 0
+    job.dscale = dscale;
+    job.ascale = ascale;
+    job.ncc = -1.0f;
+    job.status = status;
+    job.nimg = ni;
+    job.refine_code = 0;
+    job.evals = 0;
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------- postProcess (kernel 3)
+// COptim::postProcess (optim.cpp:150-190) at depth 0 on the refined job; writes the final
+// pmvs_refined.  acc: [2] grabs [3] accepted [4] fail_pre [5] fail_post [6] refine_failed.
+template <int WS>
+__device__ void post_candidate(const DScene& s, WaveLds<WS>& L, const RefineJob& job, pmvs_refined& cout, float* mat,
+                               unsigned long long* acc) {
+  const int lane = lane_id();
+  float coord[4], normal[4];
+  for (int i = 0; i < 4; ++i) { coord[i] = job.rcoord[i]; normal[i] = job.rnormal[i]; }
+  const float ncc = job.ncc, dscale = job.dscale, ascale = job.ascale;
+  int status = job.status, timages = 0;
+  float tmp = 0.0f;
+  const int ni = job.nimg;
+  if (lane < ni) L.images[lane] = job.images[lane];
+  if (lane == 0) { L.nimg = ni; L.overflow = 0; }
+  __syncthreads();
+  if (status == PMVS_ACCEPTED) {
+    const int rc = job.refine_code;
+    const bool success = (rc == BQR_SUCCESS || rc == 2 || rc == 3 || rc == BQR_XTOL);
+    if (!success && lane == 0) acc[6] += 1;
     int pfail = 0;
     if (L.nimg < s.minImageNum) pfail = 1;
     if (!pfail) {
-      // getMask over all views and insideBimages
-      bool bad = false;
+      bool bad = false;  // CPhotoSetS::getMask over all views + CFindMatch::insideBimages
       if (s.anyMask)
         for (int b = 0; b < s.num; b += WAVE)
           if (b + lane < s.num && get_mask(s, s.views[b + lane], coord, s.level) == 0) bad = true;
@@ -782,9 +797,8 @@ __device__ void refine_candidate(const DScene& s, WaveLds<WS>& L, const pmvs_can
       tmp = smax(0.0f, ncc - s.nccThreshold) * (float)timages;
     }
     if (pfail) status = PMVS_FAIL_POST;
+    if (L.overflow) status = PMVS_FAIL_OVERFLOW;
   }
-  if (L.overflow) status = PMVS_FAIL_OVERFLOW;
-  // ---------------- write result
   const int nout = L.nimg;
   if (lane < nout) {
     cout.images[lane] = L.images[lane];
@@ -793,8 +807,8 @@ __device__ void refine_candidate(const DScene& s, WaveLds<WS>& L, const pmvs_can
   }
   if (lane == 0) {
     cout.status = status;
-    cout.refine_code = refine_code;
-    cout.evals = evals;
+    cout.refine_code = job.refine_code;
+    cout.evals = job.evals;
     cout.num_images = nout;
     for (int i = 0; i < 4; ++i) { cout.coord[i] = coord[i]; cout.normal[i] = normal[i]; }
     cout.ncc = ncc;
@@ -804,10 +818,368 @@ __device__ void refine_candidate(const DScene& s, WaveLds<WS>& L, const pmvs_can
     cout.timages = timages;
     cout.reserved = 0;
     if (status == PMVS_ACCEPTED) acc[3]++;
-    else if (status == PMVS_FAIL_PRE) acc[4]++;
-    else acc[5]++;
+    else if (status == PMVS_FAIL_POST) acc[5]++;
+    else acc[4]++;
   }
   __syncthreads();
+}
+
+// ---------------------------------------------------------------- refinePatchBFGS (kernel 2)
+// One LANE per candidate runs the BOBYQA state machine (state in private memory); every
+// round, the lanes that requested an objective value (COptim::my_f, or the final
+// computeINCC) are evaluated cooperatively by the whole wavefront in chunks of <= TSLOTS
+// textures: lane-per-texture setup, lane-per-(texture,sample) gather issued NB samples at a
+// time, lane-per-texture sequential normalisation, lane-per-pair sequential dots.
+template <int WS, int TSLOTS>
+struct RefLds {
+  static constexpr int S = WS * WS;
+  float tex[TSLOTS][S][4];
+  float ave[TSLOTS][4];
+  long long jbase[TSLOTS];
+  int jvalid[TSLOTS], jW[TSLOTS], jreq[TSLOTS], jidx[TSLOTS];
+  float jleft[TSLOTS][2], jdx[TSLOTS][2], jdy[TSLOTS][2];
+  float jres[TSLOTS];
+  float geo[WAVE][16];               // requesting lane: coord, normal, pxaxis, pyaxis
+  int views[WAVE][PMVS_MAX_TAU];     // requesting lane: first size images
+  int rsize[WAVE], rfirst[WAVE];
+};
+
+__device__ __forceinline__ int wave_excl_scan(int v) {
+  const int lane = lane_id();
+  int incl = v;
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const int t = __shfl_up(incl, d);
+    if (lane >= d) incl += t;
+  }
+  return incl - v;
+}
+
+template <int WS, int TSLOTS>
+__device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS>& C, int njobs) {
+  constexpr int S = WS * WS;
+  constexpr int NB = 4;  // samples per lane whose loads are in flight together
+  const int lane = lane_id();
+  // --- setup: one lane per texture (grabTex optim.cpp:818-846 + grabSafe :783-805)
+  if (lane < njobs) {
+    const int t = lane;
+    const int r = C.jreq[t];
+    const int index = C.views[r][C.jidx[t]];
+    const float* g = C.geo[r];
+    const float coord[4] = {g[0], g[1], g[2], g[3]}, pz[4] = {g[4], g[5], g[6], g[7]};
+    const float px[4] = {g[8], g[9], g[10], g[11]}, py[4] = {g[12], g[13], g[14], g[15]};
+    const DView& v = s.views[index];
+    int ok = 1;
+    float ray[4] = {v.center[0] - coord[0], v.center[1] - coord[1], v.center[2] - coord[2], v.center[3] - coord[3]};
+    unitize4(ray);
+    const float weight = smax(0.0f, dot4(ray, pz));
+    if ((double)weight < s.cosAngle1) ok = 0;
+    float center[3], c1[3], c2[3], tt[4];
+    project(v, coord, s.level, center);
+    for (int i = 0; i < 4; ++i) tt[i] = coord[i] + px[i];
+    project(v, tt, s.level, c1);
+    for (int i = 0; i < 4; ++i) tt[i] = coord[i] + py[i];
+    project(v, tt, s.level, c2);
+    float dx[3] = {c1[0] - center[0], c1[1] - center[1], c1[2] - center[2]};
+    float dy[3] = {c2[0] - center[0], c2[1] - center[1], c2[2] - center[2]};
+    const float ratio = __fdiv_rn(norm3(dx) + norm3(dy), 2.0f);
+    int leveldif = cvt_int_x86(floor(log((double)ratio) / (double)s.log2f + (double)0.5f));
+    leveldif = imax(-s.level, imin(2, leveldif));
+    const float scale = (leveldif >= 0) ? (float)(1 << leveldif) : __fdiv_rn(1.0f, (float)(1 << (-leveldif)));
+    const int newlevel = s.level + leveldif;
+    for (int i = 0; i < 3; ++i) {
+      center[i] = __fdiv_rn(center[i], scale);
+      dx[i] = __fdiv_rn(dx[i], scale);
+      dy[i] = __fdiv_rn(dy[i], scale);
+    }
+    const float fm = (float)(WS / 2);
+    const float dxm[2] = {dx[0] * fm, dx[1] * fm}, dym[2] = {dy[0] * fm, dy[1] * fm};
+    const float tl0 = (center[0] - dxm[0]) - dym[0], tl1 = (center[1] - dxm[1]) - dym[1];
+    const float tr0 = (center[0] + dxm[0]) - dym[0], tr1 = (center[1] + dxm[1]) - dym[1];
+    const float bl0 = (center[0] - dxm[0]) + dym[0], bl1 = (center[1] - dxm[1]) + dym[1];
+    const float br0 = (center[0] + dxm[0]) + dym[0], br1 = (center[1] + dxm[1]) + dym[1];
+    const float minx = smin(tl0, smin(tr0, smin(bl0, br0)));
+    const float maxx = smax(tl0, smax(tr0, smax(bl0, br0)));
+    const float miny = smin(tl1, smin(tr1, smin(bl1, br1)));
+    const float maxy = smax(tl1, smax(tr1, smax(bl1, br1)));
+    if (ok && (minx < 3.0f || (float)(v.w[newlevel] - 1 - 3) <= maxx || miny < 3.0f ||
+               (float)(v.h[newlevel] - 1 - 3) <= maxy))
+      ok = 0;
+    C.jvalid[t] = ok;
+    C.jW[t] = v.w[newlevel];
+    C.jbase[t] = v.pyr_off[newlevel];
+    C.jleft[t][0] = tl0; C.jleft[t][1] = tl1;
+    C.jdx[t][0] = dx[0]; C.jdx[t][1] = dx[1];
+    C.jdy[t][0] = dy[0]; C.jdy[t][1] = dy[1];
+  }
+  __syncthreads();
+  // --- gather: NB samples per lane at a time, all 4*NB texel loads issued before use
+  const int total = njobs * S;
+  for (int u0 = 0; u0 < total; u0 += WAVE * NB) {
+    uint32_t a0[NB], a1[NB], b0[NB], b1[NB];
+    float fx[NB], fy[NB];
+    int lxs[NB], lys[NB];
+    bool live[NB];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int u = u0 + q * WAVE + lane;
+      const int t = u / S, k = u - t * S;
+      live[q] = (u < total) && C.jvalid[t < njobs ? t : 0];
+      long long idx = 0;
+      float lx = 0.f, ly = 0.f;
+      if (live[q]) {
+        const int yy = k / WS, xx = k - yy * WS;
+        lx = C.jleft[t][0]; ly = C.jleft[t][1];
+        const float dyx = C.jdy[t][0], dyy = C.jdy[t][1], dxx = C.jdx[t][0], dxy = C.jdx[t][1];
+        for (int r = 0; r < yy; ++r) { lx = lx + dyx; ly = ly + dyy; }
+        for (int c = 0; c < xx; ++c) { lx = lx + dxx; ly = ly + dxy; }
+        const int ix = (int)lx, iy = (int)ly;
+        idx = C.jbase[t] + (long long)iy * C.jW[t] + ix;
+        lxs[q] = ix; lys[q] = iy;
+      } else {
+        lxs[q] = 0; lys[q] = 0;
+      }
+      fx[q] = lx; fy[q] = ly;
+      const int W = live[q] ? C.jW[t] : 0;
+      const uint32_t* p = s.pyr + idx;
+      a0[q] = p[0]; a1[q] = p[1]; b0[q] = p[W]; b1[q] = p[W + 1];
+    }
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      if (!live[q]) continue;
+      const int u = u0 + q * WAVE + lane;
+      const int t = u / S, k = u - t * S;
+      const float dx1 = fx[q] - (float)lxs[q], dx0 = 1.0f - dx1;
+      const float dy1 = fy[q] - (float)lys[q], dy0 = 1.0f - dy1;
+      const float f00 = dx0 * dy0, f01 = dx0 * dy1, f10 = dx1 * dy0, f11 = dx1 * dy1;
+      float r = 0.0f, g = 0.0f, b = 0.0f;
+      r += (float)(a0[q] & 0xff) * f00 + (float)(b0[q] & 0xff) * f01;
+      g += (float)((a0[q] >> 8) & 0xff) * f00 + (float)((b0[q] >> 8) & 0xff) * f01;
+      b += (float)((a0[q] >> 16) & 0xff) * f00 + (float)((b0[q] >> 16) & 0xff) * f01;
+      r += (float)(a1[q] & 0xff) * f10 + (float)(b1[q] & 0xff) * f11;
+      g += (float)((a1[q] >> 8) & 0xff) * f10 + (float)((b1[q] >> 8) & 0xff) * f11;
+      b += (float)((a1[q] >> 16) & 0xff) * f10 + (float)((b1[q] >> 16) & 0xff) * f11;
+      C.tex[t][k][0] = r; C.tex[t][k][1] = g; C.tex[t][k][2] = b;
+    }
+  }
+  __syncthreads();
+  // --- normalize (optim.cpp:1031-1067), one lane per texture
+  if (lane < njobs && C.jvalid[lane]) {
+    const int t = lane;
+    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+    for (int i = 0; i < S; ++i) {
+      const float4 q = *reinterpret_cast<const float4*>(C.tex[t][i]);
+      a0 += q.x; a1 += q.y; a2 += q.z;
+    }
+    const float fs3 = (float)S;
+    a0 = __fdiv_rn(a0, fs3); a1 = __fdiv_rn(a1, fs3); a2 = __fdiv_rn(a2, fs3);
+    float ave2 = 0.0f;
+    for (int i = 0; i < S; ++i) {
+      const float4 q = *reinterpret_cast<const float4*>(C.tex[t][i]);
+      const float f0 = a0 - q.x, f1 = a1 - q.y, f2 = a2 - q.z;
+      ave2 += f0 * f0 + f1 * f1 + f2 * f2;
+    }
+    ave2 = fsqrt_rn(__fdiv_rn(ave2, (float)(3 * S)));
+    if (ave2 == 0.0f) ave2 = 1.0f;
+    C.ave[t][0] = a0; C.ave[t][1] = a1; C.ave[t][2] = a2; C.ave[t][3] = ave2;
+  }
+  __syncthreads();
+  for (int u = lane; u < total; u += WAVE) {
+    const int t = u / S, k = u - t * S;
+    if (!C.jvalid[t]) continue;
+    const float a2 = C.ave[t][3];
+    C.tex[t][k][0] = __fdiv_rn(C.tex[t][k][0] - C.ave[t][0], a2);
+    C.tex[t][k][1] = __fdiv_rn(C.tex[t][k][1] - C.ave[t][1], a2);
+    C.tex[t][k][2] = __fdiv_rn(C.tex[t][k][2] - C.ave[t][2], a2);
+  }
+  __syncthreads();
+  // --- robust INCC against the request's reference texture (optim.cpp:561-567, 919-929)
+  if (lane < njobs && C.jidx[lane] >= 1) {
+    const int t = lane, ref = C.rfirst[C.jreq[t]];
+    float r = 0.0f;
+    if (C.jvalid[ref] && C.jvalid[t]) {
+      float ans = 0.0f;
+      for (int i = 0; i < S; ++i) {
+        const float4 p = *reinterpret_cast<const float4*>(C.tex[ref][i]);
+        const float4 q = *reinterpret_cast<const float4*>(C.tex[t][i]);
+        ans += p.x * q.x;
+        ans += p.y * q.y;
+        ans += p.z * q.z;
+      }
+      r = robustincc((float)(1.0 - (double)__fdiv_rn(ans, (float)(3 * S))));
+    }
+    C.jres[t] = r;
+  }
+  __syncthreads();
+}
+
+template <int WS, int TSLOTS>
+__global__ __launch_bounds__(64) void refine_v2_kernel(DScene s, RefineJob* __restrict__ jobs, int n, DevStats* st) {
+  __shared__ RefLds<WS, TSLOTS> C;
+  const int lane = lane_id();
+  BqState bq;
+  RefineSetup R;
+  int cand = -1, need = 0, evals = 0, size = 0, nimg = 0, rc = 0;
+  bool exhausted = false;
+  double fv = 0.0;
+  float fcoord[4], fnormal[4];
+  unsigned long long tex_valid = 0, grabs = 0, nevals = 0;
+  const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999};
+  const double ub[3] = {HUGE_VAL, 23.99999, 23.99999};
+  for (;;) {
+    // (a) refill idle lanes from the queue (skipping candidates that failed preProcess)
+    while (cand < 0 && !exhausted) {
+      const unsigned long long c = atomicAdd(&st->queue2, 1ull);
+      if (c >= (unsigned long long)n) {
+        exhausted = true;
+        break;
+      }
+      const RefineJob& J = jobs[c];
+      if (J.status != PMVS_ACCEPTED) continue;
+      cand = (int)c;
+      for (int i = 0; i < 4; ++i) { R.center[i] = J.center[i]; R.ray[i] = J.ray[i]; }
+      R.dscale = J.dscale;
+      R.ascale = s.ascale;
+      R.ref = J.images[0];
+      nimg = J.nimg;
+      size = imin(s.tau, nimg);
+      evals = 0;
+      const double x0[3] = {J.x0[0], J.x0[1], J.x0[2]};
+      bq_begin(bq, x0, lb, ub, 1.e-7, 1000);
+      fv = 0.0;
+      need = 0;
+    }
+    // (b) advance BOBYQA of every lane that holds an objective value (or just started)
+    if (cand >= 0 && need == 0) {
+      const int r = (bq.resume < 0) ? BQ_DONE : bq_step(bq, fv);
+      if (r == BQ_NEED_F) {
+        need = 1;
+        const double xe[3] = {bq.xeval[0], bq.xeval[1], bq.xeval[2]};
+        decode(s, R, xe, fcoord, fnormal);
+      } else {
+        rc = bq.rc;
+        const bool success = (rc == BQR_SUCCESS || rc == 2 || rc == 3 || rc == BQR_XTOL);
+        RefineJob& J = jobs[cand];
+        J.refine_code = rc;
+        J.evals = evals;
+        if (success) {
+          const double xo[3] = {bq.xout[0], bq.xout[1], bq.xout[2]};
+          decode(s, R, xo, fcoord, fnormal);
+          if (nimg < 2) {  // computeINCC returns 2.0 without grabbing (optim.cpp:866)
+            J.ncc = (float)(1.0 - (double)unrobustincc(2.0f));
+            for (int i = 0; i < 4; ++i) { J.rcoord[i] = fcoord[i]; J.rnormal[i] = fnormal[i]; }
+            cand = -1;
+          } else {
+            need = 2;  // final computeINCC (robust, weighted) at the refined geometry
+          }
+        } else {
+          cand = -1;  // geometry and _ncc stay unrefined (optim.cpp:649-655)
+        }
+      }
+    }
+    // (c) publish requests
+    const bool req = (cand >= 0 && need != 0);
+    if (req) {
+      float px[4], py[4];
+      get_paxes(s, s.views[R.ref], fcoord, fnormal, px, py);
+      for (int i = 0; i < 4; ++i) {
+        C.geo[lane][i] = fcoord[i]; C.geo[lane][4 + i] = fnormal[i];
+        C.geo[lane][8 + i] = px[i]; C.geo[lane][12 + i] = py[i];
+      }
+      const RefineJob& J = jobs[cand];
+      for (int i = 0; i < size; ++i) C.views[lane][i] = J.images[i];
+      C.rsize[lane] = size;
+    }
+    const unsigned long long reqmask = __ballot(req);
+    if (reqmask == 0ull) {
+      if (__ballot(cand >= 0 || !exhausted) == 0ull) break;
+      continue;
+    }
+    __syncthreads();
+    // (d) evaluate all requests, packed into chunks of <= TSLOTS textures (lane order)
+    bool pending = req;
+    while (__ballot(pending) != 0ull) {
+      const int sz = pending ? size : 0;
+      const int off = wave_excl_scan(sz);
+      const bool in = pending && (off + sz <= TSLOTS);
+      const int njobs = __shfl(off + sz, 63 - __clzll(__ballot(in)));  // end of the last member
+      if (in) {
+        C.rfirst[lane] = off;
+        for (int i = 0; i < sz; ++i) {
+          C.jreq[off + i] = lane;
+          C.jidx[off + i] = i;
+        }
+      }
+      __syncthreads();
+      eval_chunk<WS, TSLOTS>(s, C, njobs);
+      if (lane == 0) grabs += njobs;
+      if (in) {
+        // reduce this request's per-texture results in the reference's order
+        const int ref = off;
+        int nv = 0;
+        for (int i = 0; i < sz; ++i) nv += C.jvalid[off + i];
+        double f;
+        if (need == 1) {  // COptim::my_f (optim.cpp:527-577)
+          const int mininum = imin(s.minImageNum, sz);
+          tex_valid += nv;
+          if (!C.jvalid[ref]) {
+            f = 2.0;
+          } else {
+            double ans = 0.0f;
+            int denom = 0;
+            for (int i = 1; i < sz; ++i) {
+              if (!C.jvalid[off + i]) continue;
+              ans += (double)C.jres[off + i];
+              denom++;
+            }
+            f = (denom < mininum - 1) ? 2.0f : ans / denom;
+          }
+        } else {  // COptim::computeINCC robust weighted (optim.cpp:875-938)
+          const RefineJob& J = jobs[cand];
+          if (!C.jvalid[ref]) {
+            f = 2.0;
+          } else {
+            double score = 0.0;
+            float totalweight = 0.0f;
+            for (int i = 1; i < sz; ++i) {
+              if (C.jvalid[off + i]) {
+                const float w = J.weights[i];
+                totalweight += w;
+                score += (double)(C.jres[off + i] * w);
+              }
+            }
+            f = (totalweight == 0.0f) ? 2.0 : score / (double)totalweight;
+          }
+        }
+        fv = f;
+        pending = false;
+      }
+      __syncthreads();
+    }
+    // (e) consume results
+    if (req) {
+      if (need == 1) {
+        evals++;
+        nevals++;
+        need = 0;
+      } else {
+        RefineJob& J = jobs[cand];
+        J.ncc = (float)(1.0 - (double)unrobustincc((float)fv));
+        for (int i = 0; i < 4; ++i) { J.rcoord[i] = fcoord[i]; J.rnormal[i] = fnormal[i]; }
+        cand = -1;
+        need = 0;
+      }
+    }
+  }
+  // wave-level reduction of the counters, one atomic each
+  for (int d = 32; d >= 1; d >>= 1) {
+    tex_valid += __shfl_xor(tex_valid, d);
+    nevals += __shfl_xor(nevals, d);
+  }
+  if (lane == 0) {
+    atomicAdd(&st->evals, nevals);
+    atomicAdd(&st->tex_valid, tex_valid);
+    atomicAdd(&st->tex_grabs, grabs);
+  }
 }
 
 }  // namespace pmvsdev
@@ -815,14 +1187,12 @@ __device__ void refine_candidate(const DScene& s, WaveLds<WS>& L, const pmvs_can
 // ==================================================================== kernels
 namespace pmvsdev {
 
-// Persistent refine kernel: each workgroup (one wavefront) dequeues candidates until the
-// batch is exhausted (every wave reaches the exit: the queue head only grows).
+// Kernel 1: preProcess, one wavefront per candidate, persistent with a device work queue.
 template <int WS>
-__global__ __launch_bounds__(64) void refine_kernel(DScene s, const pmvs_candidate* __restrict__ in,
-                                                     pmvs_refined* __restrict__ out, int n, DevStats* st) {
+__global__ __launch_bounds__(64) void pre_kernel(DScene s, const pmvs_candidate* __restrict__ in,
+                                                  RefineJob* __restrict__ jobs, int n, DevStats* st) {
   __shared__ WaveLds<WS> L;
   unsigned long long acc[7] = {0, 0, 0, 0, 0, 0, 0};
-  float* mat = s.scratch + (size_t)blockIdx.x * PMVS_MAX_IMAGES * PMVS_MAX_IMAGES;
   const int lane = lane_id();
   for (;;) {
     if (lane == 0) {
@@ -833,11 +1203,31 @@ __global__ __launch_bounds__(64) void refine_kernel(DScene s, const pmvs_candida
     const int c = L.cand;
     __syncthreads();
     if (c < 0) break;
-    refine_candidate<WS>(s, L, in[c], out[c], mat, acc);
+    pre_candidate<WS>(s, L, in[c], jobs[c], acc);
+  }
+  if (lane == 0) atomicAdd(&st->tex_grabs, acc[2]);
+}
+
+// Kernel 3: postProcess, one wavefront per candidate.
+template <int WS>
+__global__ __launch_bounds__(64) void post_kernel(DScene s, const RefineJob* __restrict__ jobs,
+                                                   pmvs_refined* __restrict__ out, int n, DevStats* st) {
+  __shared__ WaveLds<WS> L;
+  unsigned long long acc[7] = {0, 0, 0, 0, 0, 0, 0};
+  float* mat = s.scratch + (size_t)blockIdx.x * PMVS_MAX_IMAGES * PMVS_MAX_IMAGES;
+  const int lane = lane_id();
+  for (;;) {
+    if (lane == 0) {
+      const unsigned long long c = atomicAdd(&st->queue3, 1ull);
+      L.cand = (c < (unsigned long long)n) ? (int)c : -1;
+    }
+    __syncthreads();
+    const int c = L.cand;
+    __syncthreads();
+    if (c < 0) break;
+    post_candidate<WS>(s, L, jobs[c], out[c], mat, acc);
   }
   if (lane == 0) {
-    atomicAdd(&st->evals, acc[0]);
-    atomicAdd(&st->tex_valid, acc[1]);
     atomicAdd(&st->tex_grabs, acc[2]);
     atomicAdd(&st->accepted, acc[3]);
     atomicAdd(&st->fail_pre, acc[4]);
@@ -974,17 +1364,26 @@ __global__ void unpack_rgba_kernel(const uint32_t* __restrict__ in, uint8_t* __r
 
 namespace pmvsdev {
 
-hipError_t launch_refine(const DScene& s, const pmvs_candidate* d_in, pmvs_refined* d_out, int n, DevStats* d_st,
-                         int grid, hipStream_t stream) {
-  if (n <= 0) return hipSuccess;
+template <int WS>
+static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out,
+                                   int n, DevStats* d_st, int grid, int refine_grid, hipStream_t stream) {
   const int g = grid < n ? grid : n;
+  hipLaunchKernelGGL((pre_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_in, d_jobs, n, d_st);
+  const int rg = refine_grid < (n + 63) / 64 ? refine_grid : (n + 63) / 64;
+  hipLaunchKernelGGL((refine_v2_kernel<WS, REFINE_TSLOTS>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st);
+  hipLaunchKernelGGL((post_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_jobs, d_out, n, d_st);
+  return hipGetLastError();
+}
+
+hipError_t launch_refine(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out, int n,
+                         DevStats* d_st, int grid, int refine_grid, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
   switch (s.wsize) {
-    case 5: hipLaunchKernelGGL((refine_kernel<5>), dim3(g), dim3(64), 0, stream, s, d_in, d_out, n, d_st); break;
-    case 7: hipLaunchKernelGGL((refine_kernel<7>), dim3(g), dim3(64), 0, stream, s, d_in, d_out, n, d_st); break;
-    case 9: hipLaunchKernelGGL((refine_kernel<9>), dim3(g), dim3(64), 0, stream, s, d_in, d_out, n, d_st); break;
+    case 5: return launch_refine_ws<5>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, stream);
+    case 7: return launch_refine_ws<7>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, stream);
+    case 9: return launch_refine_ws<9>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, stream);
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 hipError_t launch_incc_eval(const DScene& s, const pmvs_eval_query* d_q, int n, double* d_out, DevStats* d_st,
@@ -1058,6 +1457,84 @@ __global__ void math_selftest_kernel(int op, const double* __restrict__ in, doub
 hipError_t launch_math_selftest(int op, const double* d_in, double* d_out, int n, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(math_selftest_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, op, d_in, d_out, n);
+  return hipGetLastError();
+}
+}  // namespace pmvsdev
+
+// ==================================================================== BOBYQA self-test
+// Runs the device BOBYQA on analytic test objectives (same as oracle_bobyqa_test) so its
+// trajectories can be checked against the CPU oracle and its cost measured.
+//   mode 0: one problem per LANE, state in private memory (scratch)
+//   mode 1: one problem per WAVE, lane 0 steps the state held in LDS (the v1 refine layout)
+namespace pmvsdev {
+__device__ __forceinline__ double bq_test_f(int kind, const double* v) {
+  if (kind == 0) return (v[0] - 1.5) * (v[0] - 1.5) + 2 * (v[1] - 3) * (v[1] - 3) + 0.5 * (v[2] + 2) * (v[2] + 2) + 0.1 * v[0] * v[1];
+  if (kind == 1) {
+    const double a = 1 - v[0], b = v[1] - v[0] * v[0], c = v[2] - v[1] * v[1];
+    return a * a + 100 * b * b + 100 * c * c;
+  }
+  return (v[0] - 1) * (v[0] - 1) + (v[1] - 40) * (v[1] - 40) + (v[2] + 50) * (v[2] + 50);
+}
+
+__global__ void bobyqa_lane_kernel(int kind, const double* __restrict__ x0, int n, int maxeval, double* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  BqState st;
+  const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999}, ub[3] = {HUGE_VAL, 23.99999, 23.99999};
+  double x[3] = {x0[3 * i], x0[3 * i + 1], x0[3 * i + 2]};
+  bq_begin(st, x, lb, ub, 1e-7, maxeval);
+  double f = 0.0;
+  while (bq_step(st, f) == BQ_NEED_F) f = bq_test_f(kind, st.xeval);
+  out[6 * i + 0] = st.xout[0];
+  out[6 * i + 1] = st.xout[1];
+  out[6 * i + 2] = st.xout[2];
+  out[6 * i + 3] = st.minf;
+  out[6 * i + 4] = (double)st.nevals;
+  out[6 * i + 5] = (double)st.rc;
+}
+
+__global__ __launch_bounds__(64) void bobyqa_wave_kernel(int kind, const double* __restrict__ x0, int n, int maxeval,
+                                                         double* __restrict__ out) {
+  __shared__ BqState st;
+  __shared__ int stepv;
+  __shared__ double fres;
+  const int i = blockIdx.x;
+  if (i >= n) return;
+  const int lane = threadIdx.x;
+  if (lane == 0) {
+    const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999}, ub[3] = {HUGE_VAL, 23.99999, 23.99999};
+    double x[3] = {x0[3 * i], x0[3 * i + 1], x0[3 * i + 2]};
+    bq_begin(st, x, lb, ub, 1e-7, maxeval);
+    fres = 0.0;
+  }
+  __syncthreads();
+  for (;;) {
+    if (lane == 0) stepv = bq_step(st, fres);
+    __syncthreads();
+    if (stepv != BQ_NEED_F) break;
+    const double xe[3] = {st.xeval[0], st.xeval[1], st.xeval[2]};
+    const double f = bq_test_f(kind, xe);
+    __syncthreads();
+    if (lane == 0) fres = f;
+    __syncthreads();
+  }
+  if (lane == 0) {
+    out[6 * i + 0] = st.xout[0];
+    out[6 * i + 1] = st.xout[1];
+    out[6 * i + 2] = st.xout[2];
+    out[6 * i + 3] = st.minf;
+    out[6 * i + 4] = (double)st.nevals;
+    out[6 * i + 5] = (double)st.rc;
+  }
+}
+
+hipError_t launch_bobyqa_selftest(int mode, int kind, const double* d_x0, int n, int maxeval, double* d_out,
+                                  hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (mode == 0)
+    hipLaunchKernelGGL(bobyqa_lane_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, kind, d_x0, n, maxeval, d_out);
+  else
+    hipLaunchKernelGGL(bobyqa_wave_kernel, dim3(n), dim3(64), 0, stream, kind, d_x0, n, maxeval, d_out);
   return hipGetLastError();
 }
 }  // namespace pmvsdev

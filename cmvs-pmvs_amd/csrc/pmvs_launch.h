@@ -4,8 +4,8 @@
 #include "pmvs_device.h"
 
 namespace pmvsdev {
-hipError_t launch_refine(const DScene& s, const pmvs_candidate* d_in, pmvs_refined* d_out, int n, DevStats* d_st,
-                         int grid, hipStream_t stream);
+hipError_t launch_refine(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out, int n,
+                         DevStats* d_st, int grid, int refine_grid, hipStream_t stream);
 hipError_t launch_incc_eval(const DScene& s, const pmvs_eval_query* d_q, int n, double* d_out, DevStats* d_st,
                             hipStream_t stream);
 hipError_t launch_grab_tex(const DScene& s, const pmvs_tex_query* d_q, int n, float* d_out, int* d_valid,
@@ -14,4 +14,6 @@ hipError_t launch_build_level(const uint8_t* d_src, int Wp, int Hp, uint8_t* d_d
 hipError_t launch_pack_rgba(const uint8_t* d_rgb, uint32_t* d_out, long long npix, hipStream_t stream);
 hipError_t launch_unpack_rgba(const uint32_t* d_in, uint8_t* d_rgb, long long npix, hipStream_t stream);
 hipError_t launch_math_selftest(int op, const double* d_in, double* d_out, int n, hipStream_t stream);
+hipError_t launch_bobyqa_selftest(int mode, int kind, const double* d_x0, int n, int maxeval, double* d_out,
+                                  hipStream_t stream);
 }  // namespace pmvsdev

@@ -41,9 +41,25 @@ struct DScene {
   float pad;
 };
 
+// One candidate between the three refine-batch kernels (pre -> refine -> post), in HBM.
+struct RefineJob {
+  float coord[4], normal[4];   // geometry after preProcess (refine input)
+  float center[4], ray[4];     // refinePatchBFGS setup: _centersT, _raysT (optim.cpp:584-586)
+  float dscale, ascale;        // _dscale/_ascale set by setScales in preProcess
+  float ncc;                   // refine output _ncc (-1 when not refined)
+  int status;                  // PMVS_ACCEPTED: refine; PMVS_FAIL_PRE / PMVS_FAIL_OVERFLOW: done
+  int nimg, refine_code, evals, pad;
+  float weights[PMVS_MAX_TAU]; // _weightsT (optim.cpp:592-596), first min(tau, nimg)
+  double x0[3];                // encode()d start point, clamped to the bounds
+  float rcoord[4], rnormal[4]; // refine output geometry (decoded on success, else the input)
+  int images[PMVS_MAX_IMAGES];
+};
+
 struct DevStats {
   unsigned long long evals, tex_valid, tex_grabs, accepted, fail_pre, fail_post, refine_failed;
-  unsigned long long queue;  // dynamic work-queue head
+  unsigned long long queue;   // dynamic work-queue heads of the three kernels
+  unsigned long long queue2;
+  unsigned long long queue3;
 };
 
 }  // namespace pmvsdev

@@ -70,7 +70,7 @@ class SynthParams(C.Structure):
 EXPORTS = ["pmvs_last_error", "pmvs_device_count", "pmvs_scene_create", "pmvs_scene_destroy",
            "pmvs_set_thresholds", "pmvs_scene_get_level", "pmvs_grab_tex", "pmvs_incc_eval",
            "pmvs_refine_batch", "pmvs_refine_batch_device", "pmvs_scene_sync", "pmvs_synth_ring",
-           "pmvs_synth_candidates", "pmvs_selftest_math"]
+           "pmvs_synth_candidates", "pmvs_selftest_math", "pmvs_selftest_bobyqa"]
 
 _lib = None
 
@@ -99,6 +99,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.pmvs_synth_ring.argtypes = [C.POINTER(SynthParams), C.c_void_p, C.c_void_p, C.c_int32]
     lib.pmvs_synth_candidates.argtypes = [C.POINTER(SynthParams), C.c_void_p, C.c_int32, C.c_uint64,
                                           C.c_float, C.c_float, C.c_void_p]
+    lib.pmvs_selftest_bobyqa.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_int32,
+                                         C.c_void_p, C.POINTER(C.c_double)]
     lib.pmvs_selftest_math.argtypes = [C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32]
     for fn in EXPORTS:
         getattr(lib, fn).restype = getattr(lib, fn).restype or C.c_int
@@ -279,6 +281,14 @@ def selftest_math(op: int, x: np.ndarray, device: int = 0) -> np.ndarray:
     out = np.zeros_like(x)
     _check(load_library().pmvs_selftest_math(device, op, _ptr(x), _ptr(out), len(x)))
     return out
+
+
+def selftest_bobyqa(kind: int, x0: np.ndarray, mode: int = 0, maxeval: int = 1000, device: int = 0):
+    x0 = np.ascontiguousarray(x0, np.float64).reshape(-1, 3)
+    out = np.zeros((len(x0), 6), np.float64)
+    ms = C.c_double()
+    _check(load_library().pmvs_selftest_bobyqa(device, mode, kind, _ptr(x0), len(x0), maxeval, _ptr(out), C.byref(ms)))
+    return out, ms.value
 
 
 def device_count() -> int:

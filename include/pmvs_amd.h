@@ -184,6 +184,12 @@ pmvs_status pmvs_scene_sync(pmvs_scene* scene, pmvs_stats* stats);
  * 5 atan, 6 log, 7 f32 sqrt, 8 f32 divide in[i]/in[i+1], 9 floor) on n doubles. */
 pmvs_status pmvs_selftest_math(int32_t device, int32_t op, const double* in, double* out, int32_t n);
 
+/* Self-test: device BOBYQA on analytic objective `kind` (0 quadratic, 1 Rosenbrock-3, 2 bound
+ * active) from n start points x0 (3 doubles each).  mode 0 = one problem per lane, 1 = one per
+ * wavefront.  out: 6 doubles per problem (x[3], minf, nevals, result code); *ms kernel time. */
+pmvs_status pmvs_selftest_bobyqa(int32_t device, int32_t mode, int32_t kind, const double* x0, int32_t n,
+                                 int32_t maxeval, double* out, double* ms);
+
 /* ---------------------------------------------------------------------------------------
  * Synthetic workload generator (NOT a reference interface: the reference ships no data).
  * Textured unit sphere seen by a ring of pinhole cameras. */
