@@ -106,3 +106,22 @@ def test_refine_batch_bit_exact(scenes):
     compare_refined(rg, ro)
     for k in ("accepted", "fail_pre", "fail_post", "refine_failed", "evals", "tex_valid"):
         assert sg[k] == so[k], k
+
+
+def test_full_size_c2_batch_parity(gpu_available, oracle_mod):
+    """BASELINE configs[1] at full size (8 views 1920x1080, level 1, 100k seed candidates):
+    every record of the HIP path equals the oracle's."""
+    import pmvs_amd as P
+    inp, p = P.synth_scene(8, 1920, 1080, level=1, supersample=2, nthreads=16)
+    g = P.Scene(inp)
+    o = oracle_mod.OracleScene(inp)
+    cands = P.synth_candidates(p, inp.projections, 100000, seed=0x5EED)
+    rg, sg = g.refine_batch(cands)
+    ro, so = o.refine_batch(cands, nthreads=16)
+    g.close()
+    o.close()
+    bad = np.flatnonzero(rg["status"] != ro["status"])
+    assert len(bad) == 0, (len(bad), bad[:10])
+    compare_refined(rg, ro)
+    for k in ("accepted", "fail_pre", "fail_post", "refine_failed", "evals", "tex_valid"):
+        assert sg[k] == so[k], k
