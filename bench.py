@@ -96,6 +96,9 @@ def main():
     evals = sum(s["evals"] for s in stats)
     tex_valid = sum(s["tex_valid"] for s in stats)
     kernel_ms = [s["kernel_ms"] for s in stats]
+    prof = {k: sum(s[k] for s in stats) for k in ("opt_cycles", "objective_cycles", "rounds", "chunks")}
+    phase = np.sum([s["prof"] for s in stats], axis=0)
+    phase_names = ("refill", "step", "publish", "chunk_setup", "gather", "normalize", "dot", "reduce")
     totals = torch.tensor([accepted, evals, tex_valid, args.candidates * args.steps], dtype=torch.float64, device=dev)
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if dist:
@@ -159,6 +162,11 @@ def main():
                          "algorithmic_bytes_per_launch": int(bytes_per_launch)},
             "cpu_baseline": cpu,
             "setup_s": {"synth": round(t_synth, 2)},
+            "refine_profile": {"optimizer_cycle_frac": round(prof["opt_cycles"] / max(1, prof["opt_cycles"] + prof["objective_cycles"]), 4),
+                               "rounds": prof["rounds"], "chunks": prof["chunks"],
+                               "phase_frac": {k: round(float(v) / max(1.0, float(phase.sum())), 4) for k, v in zip(phase_names, phase)},
+                               "config": int(os.environ.get("PMVS_REFINE_CONFIG", "1608")),
+                               "waves_per_cu": int(os.environ.get("PMVS_REFINE_WAVES_PER_CU", "4"))},
             "input_bytes_resident": nbytes_in,
         }
         print(json.dumps(result), flush=True)

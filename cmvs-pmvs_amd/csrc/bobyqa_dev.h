@@ -15,7 +15,7 @@
 #pragma once
 
 #if defined(__HIPCC__)
-#define BQ_HD __host__ __device__ inline
+#define BQ_HD __host__ __device__ inline __attribute__((always_inline))
 #else
 #define BQ_HD inline
 #endif

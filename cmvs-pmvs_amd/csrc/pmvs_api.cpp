@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -162,7 +163,7 @@ struct pmvs_scene {
   DBuf<float> scratch;
   DBuf<DevStats> stats;
   DBuf<RefineJob> jobs;
-  int grid = 0, refine_grid = 0;
+  int grid = 0, refine_grid = 0, tslots = 1608;
   // staging for host-pointer calls
   DBuf<pmvs_candidate> cand;
   DBuf<pmvs_refined> res;
@@ -339,7 +340,13 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return bail(fail(PMVS_EDEVICE, "device properties"));
   sc->grid = std::max(1, prop.multiProcessorCount) * 8;
-  sc->refine_grid = std::max(1, prop.multiProcessorCount) * 4;
+  // tuning knobs (defaults measured on MI355X): refine wavefronts per CU and the
+  // number of texture slots one cooperative objective chunk packs
+  int wpc = 4;
+  if (const char* e = getenv("PMVS_REFINE_WAVES_PER_CU")) wpc = std::max(1, std::min(32, atoi(e)));
+  if (const char* e = getenv("PMVS_REFINE_CONFIG")) sc->tslots = atoi(e);
+  if (sc->tslots != 1608 && sc->tslots != 1616 && sc->tslots != 3208 && sc->tslots != 4808 && sc->tslots != 3216) sc->tslots = 1608;
+  sc->refine_grid = std::max(1, prop.multiProcessorCount) * wpc;
   if (sc->scratch.alloc((size_t)sc->grid * PMVS_MAX_IMAGES * PMVS_MAX_IMAGES) != hipSuccess)
     return bail(fail(PMVS_ENOMEM, "scratch"));
 
@@ -440,6 +447,11 @@ static void fill_stats(const DevStats& d, int64_t n, float ms, pmvs_stats* st) {
   st->tex_valid = (int64_t)d.tex_valid;
   st->tex_grabs = (int64_t)d.tex_grabs;
   st->kernel_ms = ms;
+  st->opt_cycles = (int64_t)d.cyc_opt;
+  st->objective_cycles = (int64_t)d.cyc_eval;
+  st->rounds = (int64_t)d.rounds;
+  st->chunks = (int64_t)d.chunks;
+  for (int i = 0; i < 8; ++i) st->prof[i] = (int64_t)d.prof[i];
 }
 
 pmvs_status pmvs_incc_eval(pmvs_scene* sc, const pmvs_eval_query* q, int32_t n, double* out_f, pmvs_stats* stats) {
@@ -485,7 +497,7 @@ pmvs_status pmvs_refine_batch_device(pmvs_scene* sc, const pmvs_candidate* d_in,
   if ((st = ensure(sc->jobs, n))) return st;
   HIPCHK(hipMemsetAsync(sc->stats.p, 0, sizeof(DevStats), sc->stream));
   HIPCHK(hipEventRecord(sc->ev0, sc->stream));
-  HIPCHK(launch_refine(sc->ds, d_in, sc->jobs.p, d_out, n, sc->stats.p, sc->grid, sc->refine_grid, sc->stream));
+  HIPCHK(launch_refine(sc->ds, d_in, sc->jobs.p, d_out, n, sc->stats.p, sc->grid, sc->refine_grid, sc->tslots, sc->stream));
   HIPCHK(hipEventRecord(sc->ev1, sc->stream));
   return PMVS_OK;
 }

@@ -41,9 +41,6 @@ struct WaveLds {
   float fl2[PMVS_MAX_IMAGES];
   float rays[PMVS_MAX_IMAGES][4];
   int grids[PMVS_MAX_IMAGES][2];
-  BqState bq;
-  double fres;
-  int step;
   int cand;
   int overflow;
 };
@@ -830,9 +827,10 @@ __device__ void post_candidate(const DScene& s, WaveLds<WS>& L, const RefineJob&
 // computeINCC) are evaluated cooperatively by the whole wavefront in chunks of <= TSLOTS
 // textures: lane-per-texture setup, lane-per-(texture,sample) gather issued NB samples at a
 // time, lane-per-texture sequential normalisation, lane-per-pair sequential dots.
-template <int WS, int TSLOTS>
+template <int WS, int TSLOTS, int NC>
 struct RefLds {
   static constexpr int S = WS * WS;
+  BqState bq[NC];                    // optimizer state of the wave's NC chains (lane c owns bq[c])
   float tex[TSLOTS][S][4];
   float ave[TSLOTS][4];
   long long jbase[TSLOTS];
@@ -854,8 +852,16 @@ __device__ __forceinline__ int wave_excl_scan(int v) {
   return incl - v;
 }
 
-template <int WS, int TSLOTS>
-__device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS>& C, int njobs) {
+#define PROF_MARK(slot)                                   \
+  do {                                                    \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+    prof[slot] += _t - tprev;                             \
+    tprev = _t;                                           \
+  } while (0)
+
+template <int WS, int TSLOTS, int NC>
+__device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS, NC>& C, int njobs, unsigned long long* prof,
+                           unsigned long long& tprev) {
   constexpr int S = WS * WS;
   constexpr int NB = 4;  // samples per lane whose loads are in flight together
   const int lane = lane_id();
@@ -912,6 +918,7 @@ __device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS>& C, int njobs) {
     C.jdy[t][0] = dy[0]; C.jdy[t][1] = dy[1];
   }
   __syncthreads();
+  PROF_MARK(3);
   // --- gather: NB samples per lane at a time, all 4*NB texel loads issued before use
   const int total = njobs * S;
   for (int u0 = 0; u0 < total; u0 += WAVE * NB) {
@@ -962,6 +969,7 @@ __device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS>& C, int njobs) {
     }
   }
   __syncthreads();
+  PROF_MARK(4);
   // --- normalize (optim.cpp:1031-1067), one lane per texture
   if (lane < njobs && C.jvalid[lane]) {
     const int t = lane;
@@ -992,6 +1000,7 @@ __device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS>& C, int njobs) {
     C.tex[t][k][2] = __fdiv_rn(C.tex[t][k][2] - C.ave[t][2], a2);
   }
   __syncthreads();
+  PROF_MARK(5);
   // --- robust INCC against the request's reference texture (optim.cpp:561-567, 919-929)
   if (lane < njobs && C.jidx[lane] >= 1) {
     const int t = lane, ref = C.rfirst[C.jreq[t]];
@@ -1010,22 +1019,28 @@ __device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS>& C, int njobs) {
     C.jres[t] = r;
   }
   __syncthreads();
+  PROF_MARK(6);
 }
 
-template <int WS, int TSLOTS>
+template <int WS, int TSLOTS, int NC>
 __global__ __launch_bounds__(64) void refine_v2_kernel(DScene s, RefineJob* __restrict__ jobs, int n, DevStats* st) {
-  __shared__ RefLds<WS, TSLOTS> C;
+  __shared__ RefLds<WS, TSLOTS, NC> C;
   const int lane = lane_id();
-  BqState bq;
+  BqState& bq = C.bq[lane < NC ? lane : 0];
   RefineSetup R;
   int cand = -1, need = 0, evals = 0, size = 0, nimg = 0, rc = 0;
-  bool exhausted = false;
+  bool exhausted = lane >= NC;  // lanes >= NC only help evaluate
   double fv = 0.0;
   float fcoord[4], fnormal[4];
   unsigned long long tex_valid = 0, grabs = 0, nevals = 0;
+  unsigned long long cyc_opt = 0, cyc_eval = 0, rounds = 0, chunks = 0;
+  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tprev = 0;
   const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999};
   const double ub[3] = {HUGE_VAL, 23.99999, 23.99999};
   for (;;) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    tprev = t0;
     // (a) refill idle lanes from the queue (skipping candidates that failed preProcess)
     while (cand < 0 && !exhausted) {
       const unsigned long long c = atomicAdd(&st->queue2, 1ull);
@@ -1048,6 +1063,7 @@ __global__ __launch_bounds__(64) void refine_v2_kernel(DScene s, RefineJob* __re
       fv = 0.0;
       need = 0;
     }
+    PROF_MARK(0);
     // (b) advance BOBYQA of every lane that holds an objective value (or just started)
     if (cand >= 0 && need == 0) {
       const int r = (bq.resume < 0) ? BQ_DONE : bq_step(bq, fv);
@@ -1076,6 +1092,7 @@ __global__ __launch_bounds__(64) void refine_v2_kernel(DScene s, RefineJob* __re
         }
       }
     }
+    PROF_MARK(1);
     // (c) publish requests
     const bool req = (cand >= 0 && need != 0);
     if (req) {
@@ -1090,6 +1107,11 @@ __global__ __launch_bounds__(64) void refine_v2_kernel(DScene s, RefineJob* __re
       C.rsize[lane] = size;
     }
     const unsigned long long reqmask = __ballot(req);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    prof[2] += t1 - tprev;
+    tprev = t1;
+    cyc_opt += t1 - t0;
+    rounds++;
     if (reqmask == 0ull) {
       if (__ballot(cand >= 0 || !exhausted) == 0ull) break;
       continue;
@@ -1110,7 +1132,9 @@ __global__ __launch_bounds__(64) void refine_v2_kernel(DScene s, RefineJob* __re
         }
       }
       __syncthreads();
-      eval_chunk<WS, TSLOTS>(s, C, njobs);
+      PROF_MARK(7);
+      eval_chunk<WS, TSLOTS, NC>(s, C, njobs, prof, tprev);
+      chunks++;
       if (lane == 0) grabs += njobs;
       if (in) {
         // reduce this request's per-texture results in the reference's order
@@ -1155,6 +1179,7 @@ __global__ __launch_bounds__(64) void refine_v2_kernel(DScene s, RefineJob* __re
       }
       __syncthreads();
     }
+    cyc_eval += __builtin_amdgcn_s_memtime() - t1;
     // (e) consume results
     if (req) {
       if (need == 1) {
@@ -1179,6 +1204,11 @@ __global__ __launch_bounds__(64) void refine_v2_kernel(DScene s, RefineJob* __re
     atomicAdd(&st->evals, nevals);
     atomicAdd(&st->tex_valid, tex_valid);
     atomicAdd(&st->tex_grabs, grabs);
+    atomicAdd(&st->cyc_opt, cyc_opt);
+    atomicAdd(&st->cyc_eval, cyc_eval);
+    atomicAdd(&st->rounds, rounds);
+    atomicAdd(&st->chunks, chunks);
+    for (int i = 0; i < 8; ++i) atomicAdd(&st->prof[i], prof[i]);
   }
 }
 
@@ -1366,22 +1396,30 @@ namespace pmvsdev {
 
 template <int WS>
 static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out,
-                                   int n, DevStats* d_st, int grid, int refine_grid, hipStream_t stream) {
+                                   int n, DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream) {
   const int g = grid < n ? grid : n;
   hipLaunchKernelGGL((pre_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_in, d_jobs, n, d_st);
-  const int rg = refine_grid < (n + 63) / 64 ? refine_grid : (n + 63) / 64;
-  hipLaunchKernelGGL((refine_v2_kernel<WS, REFINE_TSLOTS>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st);
+  const int nc = tslots % 100;
+  const int rg = refine_grid < (n + nc - 1) / nc ? refine_grid : (n + nc - 1) / nc;
+  // tslots = texture slots per objective chunk * 100 + optimizer chains per wavefront
+  switch (tslots) {
+    case 1608: hipLaunchKernelGGL((refine_v2_kernel<WS, 16, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 1616: hipLaunchKernelGGL((refine_v2_kernel<WS, 16, 16>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 3208: hipLaunchKernelGGL((refine_v2_kernel<WS, 32, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 4808: hipLaunchKernelGGL((refine_v2_kernel<WS, 48, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    default: hipLaunchKernelGGL((refine_v2_kernel<WS, 32, 16>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+  }
   hipLaunchKernelGGL((post_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_jobs, d_out, n, d_st);
   return hipGetLastError();
 }
 
 hipError_t launch_refine(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out, int n,
-                         DevStats* d_st, int grid, int refine_grid, hipStream_t stream) {
+                         DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   switch (s.wsize) {
-    case 5: return launch_refine_ws<5>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, stream);
-    case 7: return launch_refine_ws<7>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, stream);
-    case 9: return launch_refine_ws<9>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, stream);
+    case 5: return launch_refine_ws<5>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, tslots, stream);
+    case 7: return launch_refine_ws<7>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, tslots, stream);
+    case 9: return launch_refine_ws<9>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, tslots, stream);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1493,6 +1531,28 @@ __global__ void bobyqa_lane_kernel(int kind, const double* __restrict__ x0, int 
   out[6 * i + 5] = (double)st.rc;
 }
 
+// Lane-per-problem with the BOBYQA state resident in LDS (C problems per 64-lane workgroup).
+template <int C>
+__global__ __launch_bounds__(64) void bobyqa_lds_kernel(int kind, const double* __restrict__ x0, int n, int maxeval,
+                                                        double* __restrict__ out) {
+  __shared__ BqState sts[C];
+  const int lane = threadIdx.x;
+  const int i = blockIdx.x * C + lane;
+  if (lane >= C || i >= n) return;
+  BqState& st = sts[lane];
+  const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999}, ub[3] = {HUGE_VAL, 23.99999, 23.99999};
+  double x[3] = {x0[3 * i], x0[3 * i + 1], x0[3 * i + 2]};
+  bq_begin(st, x, lb, ub, 1e-7, maxeval);
+  double f = 0.0;
+  while (bq_step(st, f) == BQ_NEED_F) f = bq_test_f(kind, st.xeval);
+  out[6 * i + 0] = st.xout[0];
+  out[6 * i + 1] = st.xout[1];
+  out[6 * i + 2] = st.xout[2];
+  out[6 * i + 3] = st.minf;
+  out[6 * i + 4] = (double)st.nevals;
+  out[6 * i + 5] = (double)st.rc;
+}
+
 __global__ __launch_bounds__(64) void bobyqa_wave_kernel(int kind, const double* __restrict__ x0, int n, int maxeval,
                                                          double* __restrict__ out) {
   __shared__ BqState st;
@@ -1533,8 +1593,14 @@ hipError_t launch_bobyqa_selftest(int mode, int kind, const double* d_x0, int n,
   if (n <= 0) return hipSuccess;
   if (mode == 0)
     hipLaunchKernelGGL(bobyqa_lane_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, kind, d_x0, n, maxeval, d_out);
-  else
+  else if (mode == 1)
     hipLaunchKernelGGL(bobyqa_wave_kernel, dim3(n), dim3(64), 0, stream, kind, d_x0, n, maxeval, d_out);
+  else if (mode == 2)
+    hipLaunchKernelGGL((bobyqa_lds_kernel<16>), dim3((n + 15) / 16), dim3(64), 0, stream, kind, d_x0, n, maxeval, d_out);
+  else if (mode == 3)
+    hipLaunchKernelGGL((bobyqa_lds_kernel<32>), dim3((n + 31) / 32), dim3(64), 0, stream, kind, d_x0, n, maxeval, d_out);
+  else
+    hipLaunchKernelGGL((bobyqa_lds_kernel<64>), dim3((n + 63) / 64), dim3(64), 0, stream, kind, d_x0, n, maxeval, d_out);
   return hipGetLastError();
 }
 }  // namespace pmvsdev

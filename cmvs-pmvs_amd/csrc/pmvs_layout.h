@@ -60,6 +60,8 @@ struct DevStats {
   unsigned long long queue;   // dynamic work-queue heads of the three kernels
   unsigned long long queue2;
   unsigned long long queue3;
+  unsigned long long cyc_opt, cyc_eval, rounds, chunks;  // refine-kernel phase profile (lane 0 of each wave)
+  unsigned long long prof[8];  // refill, step, publish, chunk setup, gather, normalize, dot, reduce
 };
 
 }  // namespace pmvsdev

@@ -54,10 +54,12 @@ class SceneDesc(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("candidates", C.c_int64), ("accepted", C.c_int64), ("fail_pre", C.c_int64),
                 ("fail_post", C.c_int64), ("refine_failed", C.c_int64), ("evals", C.c_int64),
-                ("tex_valid", C.c_int64), ("tex_grabs", C.c_int64), ("kernel_ms", C.c_double)]
+                ("tex_valid", C.c_int64), ("tex_grabs", C.c_int64), ("kernel_ms", C.c_double),
+                ("opt_cycles", C.c_int64), ("objective_cycles", C.c_int64), ("rounds", C.c_int64),
+                ("chunks", C.c_int64), ("prof", C.c_int64 * 8)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        return {k: (list(getattr(self, k)) if k == "prof" else getattr(self, k)) for k, _ in self._fields_}
 
 
 class SynthParams(C.Structure):

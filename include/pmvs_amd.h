@@ -132,6 +132,12 @@ typedef struct pmvs_stats {
   int64_t tex_valid;      /* sum over those evaluations of valid textures (algorithmic bytes = 588*this for wsize 7) */
   int64_t tex_grabs;      /* every grabTex executed (incl. pre/post-processing) */
   double kernel_ms;       /* device time of the last call's kernels (HIP events on the scene stream) */
+  /* refine-kernel phase profile (diagnostics; summed over wavefronts, shader clock cycles) */
+  int64_t opt_cycles;       /* BOBYQA steps, refill and request publication */
+  int64_t objective_cycles; /* cooperative my_f / computeINCC evaluation */
+  int64_t rounds;           /* optimizer rounds (all lanes step once) */
+  int64_t chunks;           /* cooperative objective chunks */
+  int64_t prof[8];          /* cycles: refill, optimizer step, publish, chunk setup, gather, normalize, dot, reduce */
 } pmvs_stats;
 
 typedef struct pmvs_scene pmvs_scene;
