@@ -48,6 +48,22 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(args):
+    """HBM bytes per refine launch from the committed rocprofv3 PMC summary (tools/gpu_round.sh +
+    tools/summarize_profiles.py; FETCH_SIZE x2 per MI355X_MICROARCH.md + WRITE_SIZE) when it was
+    measured on this same default workload; otherwise null."""
+    if (args.candidates, args.views, args.width, args.height, args.level) != (100000, 8, 1920, 1080, 1):
+        return None, None
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+    for f in reversed(files):
+        d = json.load(open(f))
+        for k, v in d.get("kernels", {}).items():
+            if "refine_v2_kernel" in k and k.endswith(os.environ.get("PMVS_REFINE_CONFIG_NAME", "<7, 16, 8>")):
+                return int(v["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT)
+    return None, None
+
+
 def main():
     args = parse()
     import torch
@@ -95,7 +111,8 @@ def main():
     accepted = sum(s["accepted"] for s in stats)
     evals = sum(s["evals"] for s in stats)
     tex_valid = sum(s["tex_valid"] for s in stats)
-    kernel_ms = [s["kernel_ms"] for s in stats]
+    kernel_ms = [s["refine_ms"] for s in stats]
+    stage_ms = {k: round(float(np.mean([s[k] for s in stats])), 3) for k in ("pre_ms", "refine_ms", "post_ms")}
     prof = {k: sum(s[k] for s in stats) for k in ("opt_cycles", "objective_cycles", "rounds", "chunks")}
     phase = np.sum([s["prof"] for s in stats], axis=0)
     phase_names = ("refill", "step", "publish", "chunk_setup", "gather", "normalize", "dot", "reduce")
@@ -107,11 +124,13 @@ def main():
     accepted_all, evals_all, texv_all, cand_all = totals.tolist()
     elapsed_max = tmax.item()
 
-    # ---- roofline of the dominant kernel (refine_kernel), per launch, HIP-event timed
+    # ---- roofline of the dominant kernel (refine_v2_kernel), per launch, HIP-event timed on the
+    # scene stream (events recorded right before and after that launch)
     avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
     bytes_per_launch = tex_valid / args.steps * BYTES_PER_TEXTURE
     achieved = bytes_per_launch / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
 
+    traffic, traffic_src = pmc_traffic(args)
     result = None
     if rank == 0:
         # ---- CPU baseline (oracle restatement on this host, bounded sample)
@@ -157,9 +176,11 @@ def main():
             "accepted_fraction": round(accepted_all / cand_all, 4),
             "evals_per_candidate": round(evals_all / cand_all, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                         "kernel": "refine_kernel<7>", "kernel_ms_avg": round(avg_kernel_s * 1e3, 3),
-                         "algorithmic_bytes_per_launch": int(bytes_per_launch)},
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "kernel": "refine_v2_kernel<7,16,8>", "kernel_ms_avg": round(avg_kernel_s * 1e3, 3),
+                         "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                         "traffic_source": traffic_src},
+            "stage_ms": stage_ms,
             "cpu_baseline": cpu,
             "setup_s": {"synth": round(t_synth, 2)},
             "refine_profile": {"optimizer_cycle_frac": round(prof["opt_cycles"] / max(1, prof["opt_cycles"] + prof["objective_cycles"]), 4),

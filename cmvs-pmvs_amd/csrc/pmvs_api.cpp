@@ -153,6 +153,8 @@ struct pmvs_scene {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t kev[4] = {nullptr, nullptr, nullptr, nullptr};  // around pre / refine / post kernels
+  bool last_refine = false;
   DScene ds{};
   int maxLevel = 0;
   std::vector<DView> hviews;
@@ -178,6 +180,8 @@ struct pmvs_scene {
     evout.release(); tq.release(); tout.release(); tvalid.release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
+    for (hipEvent_t e : kev)
+      if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -229,7 +233,9 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
     return st;
   };
   if (hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&sc->ev0) != hipSuccess || hipEventCreate(&sc->ev1) != hipSuccess)
+      hipEventCreate(&sc->ev0) != hipSuccess || hipEventCreate(&sc->ev1) != hipSuccess ||
+      hipEventCreate(&sc->kev[0]) != hipSuccess || hipEventCreate(&sc->kev[1]) != hipSuccess ||
+      hipEventCreate(&sc->kev[2]) != hipSuccess || hipEventCreate(&sc->kev[3]) != hipSuccess)
     return bail(fail(PMVS_EDEVICE, "stream/event creation failed"));
 
   // ---- views: sizes, cameras, pyramid offsets
@@ -497,8 +503,10 @@ pmvs_status pmvs_refine_batch_device(pmvs_scene* sc, const pmvs_candidate* d_in,
   if ((st = ensure(sc->jobs, n))) return st;
   HIPCHK(hipMemsetAsync(sc->stats.p, 0, sizeof(DevStats), sc->stream));
   HIPCHK(hipEventRecord(sc->ev0, sc->stream));
-  HIPCHK(launch_refine(sc->ds, d_in, sc->jobs.p, d_out, n, sc->stats.p, sc->grid, sc->refine_grid, sc->tslots, sc->stream));
+  HIPCHK(launch_refine(sc->ds, d_in, sc->jobs.p, d_out, n, sc->stats.p, sc->grid, sc->refine_grid, sc->tslots, sc->stream,
+                       sc->kev));
   HIPCHK(hipEventRecord(sc->ev1, sc->stream));
+  sc->last_refine = true;
   return PMVS_OK;
 }
 
@@ -511,6 +519,12 @@ pmvs_status pmvs_scene_sync(pmvs_scene* sc, pmvs_stats* stats) {
   float ms = 0;
   if (hipEventElapsedTime(&ms, sc->ev0, sc->ev1) != hipSuccess) ms = 0;
   fill_stats(ds, (int64_t)(ds.queue > 0 ? ds.queue : 0), ms, stats);
+  if (stats && sc->last_refine) {
+    float a = 0, b = 0, c = 0;
+    if (hipEventElapsedTime(&a, sc->kev[0], sc->kev[1]) == hipSuccess) stats->pre_ms = a;
+    if (hipEventElapsedTime(&b, sc->kev[1], sc->kev[2]) == hipSuccess) stats->refine_ms = b;
+    if (hipEventElapsedTime(&c, sc->kev[2], sc->kev[3]) == hipSuccess) stats->post_ms = c;
+  }
   if (stats) {
     // queue overshoots by one dequeue per workgroup: the candidate count is recorded by the caller
     stats->candidates = (int64_t)(ds.accepted + ds.fail_pre + ds.fail_post);

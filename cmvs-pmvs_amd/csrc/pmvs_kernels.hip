@@ -1396,9 +1396,12 @@ namespace pmvsdev {
 
 template <int WS>
 static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out,
-                                   int n, DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream) {
+                                   int n, DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream,
+                                   hipEvent_t* ev) {
   const int g = grid < n ? grid : n;
+  hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL((pre_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_in, d_jobs, n, d_st);
+  hipEventRecord(ev[1], stream);
   const int nc = tslots % 100;
   const int rg = refine_grid < (n + nc - 1) / nc ? refine_grid : (n + nc - 1) / nc;
   // tslots = texture slots per objective chunk * 100 + optimizer chains per wavefront
@@ -1409,17 +1412,19 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
     case 4808: hipLaunchKernelGGL((refine_v2_kernel<WS, 48, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     default: hipLaunchKernelGGL((refine_v2_kernel<WS, 32, 16>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
   }
+  hipEventRecord(ev[2], stream);
   hipLaunchKernelGGL((post_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_jobs, d_out, n, d_st);
+  hipEventRecord(ev[3], stream);
   return hipGetLastError();
 }
 
 hipError_t launch_refine(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out, int n,
-                         DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream) {
+                         DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream, hipEvent_t* ev) {
   if (n <= 0) return hipSuccess;
   switch (s.wsize) {
-    case 5: return launch_refine_ws<5>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, tslots, stream);
-    case 7: return launch_refine_ws<7>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, tslots, stream);
-    case 9: return launch_refine_ws<9>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, tslots, stream);
+    case 5: return launch_refine_ws<5>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, tslots, stream, ev);
+    case 7: return launch_refine_ws<7>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, tslots, stream, ev);
+    case 9: return launch_refine_ws<9>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, tslots, stream, ev);
     default: return hipErrorInvalidValue;
   }
 }

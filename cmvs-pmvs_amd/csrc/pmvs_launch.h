@@ -5,7 +5,7 @@
 
 namespace pmvsdev {
 hipError_t launch_refine(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out, int n,
-                         DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream);
+                         DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream, hipEvent_t* ev);
 hipError_t launch_incc_eval(const DScene& s, const pmvs_eval_query* d_q, int n, double* d_out, DevStats* d_st,
                             hipStream_t stream);
 hipError_t launch_grab_tex(const DScene& s, const pmvs_tex_query* d_q, int n, float* d_out, int* d_valid,

@@ -56,7 +56,8 @@ class Stats(C.Structure):
                 ("fail_post", C.c_int64), ("refine_failed", C.c_int64), ("evals", C.c_int64),
                 ("tex_valid", C.c_int64), ("tex_grabs", C.c_int64), ("kernel_ms", C.c_double),
                 ("opt_cycles", C.c_int64), ("objective_cycles", C.c_int64), ("rounds", C.c_int64),
-                ("chunks", C.c_int64), ("prof", C.c_int64 * 8)]
+                ("chunks", C.c_int64), ("prof", C.c_int64 * 8), ("pre_ms", C.c_double),
+                ("refine_ms", C.c_double), ("post_ms", C.c_double)]
 
     def as_dict(self):
         return {k: (list(getattr(self, k)) if k == "prof" else getattr(self, k)) for k, _ in self._fields_}

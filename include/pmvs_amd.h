@@ -138,6 +138,7 @@ typedef struct pmvs_stats {
   int64_t rounds;           /* optimizer rounds (all lanes step once) */
   int64_t chunks;           /* cooperative objective chunks */
   int64_t prof[8];          /* cycles: refill, optimizer step, publish, chunk setup, gather, normalize, dot, reduce */
+  double pre_ms, refine_ms, post_ms; /* per-kernel device time of the last refine batch (HIP events) */
 } pmvs_stats;
 
 typedef struct pmvs_scene pmvs_scene;
