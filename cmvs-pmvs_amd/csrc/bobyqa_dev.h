@@ -24,6 +24,23 @@
 
 namespace pmvsdev {
 
+// Diagnostic build only (-DBQ_PROFILE, tools/bq_profile.sh): wave-time spent in the optimizer's
+// sub-steps, accumulated once per wavefront that executes the block.
+#if defined(BQ_PROFILE) && defined(__HIPCC__)
+__device__ unsigned long long bq_prof[8];
+#endif
+#if defined(BQ_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
+#define BQ_PT(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define BQ_PA(slot, v)                                                                 \
+  do {                                                                                 \
+    const unsigned long long _d = __builtin_amdgcn_s_memtime() - v;                    \
+    if ((int)__lane_id() == (int)__builtin_ctzll(__ballot(1))) atomicAdd(&bq_prof[slot], _d); \
+  } while (0)
+#else
+#define BQ_PT(v)
+#define BQ_PA(slot, v)
+#endif
+
 enum { BQ_NEED_F = 1, BQ_DONE = 0 };
 enum {
   BQR_SUCCESS = 1, BQR_XTOL = 4, BQR_MAXEVAL = 5, BQR_INVALID_ARGS = -2, BQR_ROUNDOFF = -4
@@ -665,7 +682,14 @@ BQ_HD int bq_begin(BqState& st, const double* x0, const double* lb, const double
 
 // Advance the optimizer.  fin is the objective value requested by the previous call (ignored
 // on the first call).  Returns BQ_NEED_F with st.xeval set, or BQ_DONE with st.rc/st.xout.
+BQ_HD int bq_step_impl(BqState& st, double fin);
 BQ_HD int bq_step(BqState& st, double fin) {
+  BQ_PT(t_all);
+  const int r = bq_step_impl(st, fin);
+  BQ_PA(3, t_all);
+  return r;
+}
+BQ_HD int bq_step_impl(BqState& st, double fin) {
   const double half = 0.5, one = 1.0, ten = 10.0, tenth = 0.1, two = 2.0, zero = 0.0;
   double temp, sum, suma, sumb, bsum, dx, delsq, scaden, biglsq, hdiag, den, errbig, frhosq,
       bdtol, bdtest, curv, fracsq, sumpq, sumz, sumw, densav, pqold, gqsq, gisq, dist;
@@ -801,8 +825,12 @@ L20:
     }
   }
 L60:
+  {
+  BQ_PT(t_trs);
   bq_trsbox(st.xpt, st.xopt, st.gopt, st.hq, st.pq, st.sl, st.su, st.delta, st.xnew, st.d, st.gnew,
             &st.dsq, &st.crvmin);
+  BQ_PA(0, t_trs);
+  }
   st.dnorm = bq_min(st.delta, sqrt(st.dsq));
   if (st.dnorm < half * st.rho) {
     st.ntrits = -1;
@@ -891,6 +919,9 @@ L90:
   goto L230;
 
 L190:  // ---- RESCUE
+#if defined(BQ_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
+  if ((int)__lane_id() == (int)__builtin_ctzll(__ballot(1))) atomicAdd(&bq_prof[4], 1ull);
+#endif
   st.nfsav = st.nf;
   st.kbase = st.kopt;
   {
@@ -1174,8 +1205,12 @@ R350:
   }
   if (st.ntrits > 0) goto L60;
 L210:
+  {
+  BQ_PT(t_alt);
   bq_altmov(st.xpt, st.xopt, st.bmat, st.zmat, st.sl, st.su, st.kopt, st.knew, st.adelt, st.xnew,
             st.xalt, &st.alpha, &st.cauchy);
+  BQ_PA(1, t_alt);
+  }
   for (int i = 1; i <= BQN; ++i) st.d[i] = st.xnew[i] - st.xopt[i];
 L230:
   for (int k = 1; k <= BQNPT; ++k) {
@@ -1346,7 +1381,11 @@ L360R:
       }
     }
   }
+  {
+  BQ_PT(t_upd);
   bq_update(st.bmat, st.zmat, st.vlag, st.beta, st.denom, st.knew, st.w);
+  BQ_PA(2, t_upd);
+  }
   ih = 0;
   pqold = st.pq[st.knew];
   st.pq[st.knew] = zero;

@@ -351,7 +351,7 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
   int wpc = 4;
   if (const char* e = getenv("PMVS_REFINE_WAVES_PER_CU")) wpc = std::max(1, std::min(32, atoi(e)));
   if (const char* e = getenv("PMVS_REFINE_CONFIG")) sc->tslots = atoi(e);
-  if (sc->tslots != 1608 && sc->tslots != 1616 && sc->tslots != 3208 && sc->tslots != 4808 && sc->tslots != 3216) sc->tslots = 1608;
+  if (sc->tslots != 804 && sc->tslots != 1604 && sc->tslots != 1608 && sc->tslots != 1616 && sc->tslots != 3208 && sc->tslots != 4808 && sc->tslots != 3216) sc->tslots = 1608;
   sc->refine_grid = std::max(1, prop.multiProcessorCount) * wpc;
   if (sc->scratch.alloc((size_t)sc->grid * PMVS_MAX_IMAGES * PMVS_MAX_IMAGES) != hipSuccess)
     return bail(fail(PMVS_ENOMEM, "scratch"));

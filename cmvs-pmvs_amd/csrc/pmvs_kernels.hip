@@ -837,9 +837,9 @@ struct RefLds {
   int jvalid[TSLOTS], jW[TSLOTS], jreq[TSLOTS], jidx[TSLOTS];
   float jleft[TSLOTS][2], jdx[TSLOTS][2], jdy[TSLOTS][2];
   float jres[TSLOTS];
-  float geo[WAVE][16];               // requesting lane: coord, normal, pxaxis, pyaxis
-  int views[WAVE][PMVS_MAX_TAU];     // requesting lane: first size images
-  int rsize[WAVE], rfirst[WAVE];
+  float geo[NC][16];                 // requesting lane: coord, normal, pxaxis, pyaxis
+  int views[NC][PMVS_MAX_TAU];       // requesting lane: first size images
+  int rsize[NC], rfirst[NC];
 };
 
 __device__ __forceinline__ int wave_excl_scan(int v) {
@@ -1023,7 +1023,8 @@ __device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS, NC>& C, int njobs
 }
 
 template <int WS, int TSLOTS, int NC>
-__global__ __launch_bounds__(64) void refine_v2_kernel(DScene s, RefineJob* __restrict__ jobs, int n, DevStats* st) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 4 ? 2 : 1))) void refine_v2_kernel(
+    DScene s, RefineJob* __restrict__ jobs, int n, DevStats* st) {
   __shared__ RefLds<WS, TSLOTS, NC> C;
   const int lane = lane_id();
   BqState& bq = C.bq[lane < NC ? lane : 0];
@@ -1057,6 +1058,8 @@ __global__ __launch_bounds__(64) void refine_v2_kernel(DScene s, RefineJob* __re
       R.ref = J.images[0];
       nimg = J.nimg;
       size = imin(s.tau, nimg);
+      for (int i = 0; i < size; ++i) C.views[lane][i] = J.images[i];  // the chain's texture views
+      C.rsize[lane] = size;
       evals = 0;
       const double x0[3] = {J.x0[0], J.x0[1], J.x0[2]};
       bq_begin(bq, x0, lb, ub, 1.e-7, 1000);
@@ -1102,9 +1105,6 @@ __global__ __launch_bounds__(64) void refine_v2_kernel(DScene s, RefineJob* __re
         C.geo[lane][i] = fcoord[i]; C.geo[lane][4 + i] = fnormal[i];
         C.geo[lane][8 + i] = px[i]; C.geo[lane][12 + i] = py[i];
       }
-      const RefineJob& J = jobs[cand];
-      for (int i = 0; i < size; ++i) C.views[lane][i] = J.images[i];
-      C.rsize[lane] = size;
     }
     const unsigned long long reqmask = __ballot(req);
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -1406,6 +1406,8 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
   const int rg = refine_grid < (n + nc - 1) / nc ? refine_grid : (n + nc - 1) / nc;
   // tslots = texture slots per objective chunk * 100 + optimizer chains per wavefront
   switch (tslots) {
+    case 804: hipLaunchKernelGGL((refine_v2_kernel<WS, 8, 4>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 1604: hipLaunchKernelGGL((refine_v2_kernel<WS, 16, 4>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     case 1608: hipLaunchKernelGGL((refine_v2_kernel<WS, 16, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     case 1616: hipLaunchKernelGGL((refine_v2_kernel<WS, 16, 16>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     case 3208: hipLaunchKernelGGL((refine_v2_kernel<WS, 32, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
@@ -1609,3 +1611,12 @@ hipError_t launch_bobyqa_selftest(int mode, int kind, const double* d_x0, int n,
   return hipGetLastError();
 }
 }  // namespace pmvsdev
+
+#if defined(BQ_PROFILE)
+// Diagnostic build only: read and reset the optimizer sub-step profile.
+extern "C" int pmvs_debug_bq_prof(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pmvsdev::bq_prof), 8 * sizeof(unsigned long long)) != hipSuccess) return 1;
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(pmvsdev::bq_prof), z, sizeof(z)) != hipSuccess;
+}
+#endif

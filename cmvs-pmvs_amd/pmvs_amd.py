@@ -15,7 +15,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpmvs_amd.so")
+LIB_PATH = os.environ.get("PMVS_AMD_LIB", os.path.join(HERE, "libpmvs_amd.so"))
 
 MAX_IMAGES = 64
 MAX_TAU = 16
