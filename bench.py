@@ -64,6 +64,23 @@ def pmc_traffic(args):
     return None, None
 
 
+def rank_candidate_seed(rank: int) -> int:
+    """Each rank refines its own candidate shard (weak scaling, no data-path exchange)."""
+    return 0x5EED + 7919 * rank
+
+
+def reduce_over_ranks(dist, counts, elapsed, device):
+    """SUM the per-rank counters and MAX the per-rank timed-region length over all ranks (the
+    only collectives of the benchmark).  Works with nccl (RCCL) on GPUs and gloo on CPUs."""
+    import torch
+    totals = torch.tensor([float(c) for c in counts], dtype=torch.float64, device=device)
+    tmax = torch.tensor([float(elapsed)], dtype=torch.float64, device=device)
+    if dist is not None:
+        dist.all_reduce(totals, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    return totals.tolist(), tmax.item()
+
+
 def main():
     args = parse()
     import torch
@@ -84,7 +101,7 @@ def main():
     inp, sp = P.synth_scene(args.views, args.width, args.height, level=args.level, supersample=2, nthreads=16)
     t_synth = time.time() - t0
     scene = P.Scene(inp, device=local)
-    cands = P.synth_candidates(sp, inp.projections, args.candidates, seed=0x5EED + 7919 * rank)
+    cands = P.synth_candidates(sp, inp.projections, args.candidates, seed=rank_candidate_seed(rank))
     nbytes_in = cands.nbytes
     d_in = torch.from_numpy(cands.view(np.uint8)).to(dev)
     d_out = torch.empty(args.candidates * P.REFINED_DTYPE.itemsize, dtype=torch.uint8, device=dev)
@@ -116,13 +133,8 @@ def main():
     prof = {k: sum(s[k] for s in stats) for k in ("opt_cycles", "objective_cycles", "rounds", "chunks")}
     phase = np.sum([s["prof"] for s in stats], axis=0)
     phase_names = ("refill", "step", "publish", "chunk_setup", "gather", "normalize", "dot", "reduce")
-    totals = torch.tensor([accepted, evals, tex_valid, args.candidates * args.steps], dtype=torch.float64, device=dev)
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if dist:
-        dist.all_reduce(totals, op=dist.ReduceOp.SUM)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    accepted_all, evals_all, texv_all, cand_all = totals.tolist()
-    elapsed_max = tmax.item()
+    (accepted_all, evals_all, texv_all, cand_all), elapsed_max = reduce_over_ranks(
+        dist, [accepted, evals, tex_valid, args.candidates * args.steps], elapsed, dev)
 
     # ---- roofline of the dominant kernel (refine_v2_kernel), per launch, HIP-event timed on the
     # scene stream (events recorded right before and after that launch)

@@ -1,0 +1,134 @@
+"""GPU parity across the option space the reference exposes for this path (option.cpp keys
+level / csize / wsize / minImageNum / threshold / maxAngle / sequence / timages+oimages /
+useVisData / bimages, plus masks/ and edges/): for every configuration the HIP refine batch,
+grabTex and my_f equal the CPU oracle bit-for-bit."""
+import numpy as np
+import pytest
+
+from pmvs_cases import bits, eval_queries, tex_queries
+
+pytestmark = pytest.mark.gpu
+
+
+def blob_masks(num, h, w, seed, keep=0.85):
+    """Binary images (0/255) with random rectangular holes (for masks/ and edges/)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(num):
+        m = np.full((h, w), 255, np.uint8)
+        area = 0
+        while area < (1 - keep) * h * w:
+            y0, x0 = rng.integers(0, h), rng.integers(0, w)
+            hh, ww = rng.integers(h // 20 + 1, h // 5 + 2), rng.integers(w // 20 + 1, w // 5 + 2)
+            m[y0:y0 + hh, x0:x0 + ww] = 0
+            area = int((m == 0).sum())
+        out.append(m)
+    return out
+
+
+CONFIGS = {
+    "level0_w5_c1": dict(views=6, w=320, h=240, level=0, opts=dict(csize=1, wsize=5)),
+    "level2_w9_c4_min2": dict(views=6, w=640, h=480, level=2, opts=dict(csize=4, wsize=9, min_image_num=2)),
+    "masks_edges_bimages": dict(views=8, w=480, h=360, level=1, masks=True, edges=True,
+                                opts=dict(bindexes=(0, 2, 5))),
+    "targets_vis_seq_angle": dict(views=8, w=480, h=360, level=1, targets=4,
+                                  opts=dict(sequence=3, max_angle_deg=25.0, threshold=0.6),
+                                  vis="ring2"),
+    "min4_thr08": dict(views=10, w=400, h=300, level=1, opts=dict(min_image_num=4, threshold=0.8)),
+}
+
+
+def build(cfg):
+    import pmvs_amd as P
+    inp, p = P.synth_scene(cfg["views"], cfg["w"], cfg["h"], level=cfg["level"], num_targets=cfg.get("targets"),
+                           supersample=2, **cfg.get("opts", {}))
+    V = cfg["views"]
+    if cfg.get("masks"):
+        inp.masks = blob_masks(V, cfg["h"], cfg["w"], 1, keep=0.9)
+    if cfg.get("edges"):
+        inp.edges = blob_masks(V, cfg["h"], cfg["w"], 2, keep=0.8)
+    if cfg.get("vis") == "ring2":
+        inp.visdata2 = [[x for x in range(V) if x != y and min(abs(x - y), V - abs(x - y)) <= 2] for y in range(V)]
+    return inp, p
+
+
+@pytest.fixture(scope="module", params=sorted(CONFIGS), ids=sorted(CONFIGS))
+def pair(request, gpu_available, oracle_mod):
+    import pmvs_amd as P
+    inp, p = build(CONFIGS[request.param])
+    g = P.Scene(inp)
+    o = oracle_mod.OracleScene(inp)
+    yield request.param, inp, p, g, o
+    g.close()
+    o.close()
+
+
+def test_refine_matrix(pair):
+    import pmvs_amd as P
+    name, inp, p, g, o = pair
+    cands = P.synth_candidates(p, inp.projections, 300, seed=77)
+    rg, sg = g.refine_batch(cands)
+    ro, so = o.refine_batch(cands, nthreads=8)
+    assert np.array_equal(rg["status"], ro["status"]), name
+    acc = ro["status"] == 0
+    for f in ("refine_code", "evals", "num_images", "timages"):
+        assert np.array_equal(rg[f][acc], ro[f][acc]), (name, f)
+    for f in ("coord", "normal", "ncc", "dscale", "ascale", "tmp"):
+        assert np.array_equal(bits(rg[f][acc]), bits(ro[f][acc])), (name, f)
+    for i in np.flatnonzero(acc):
+        n = ro["num_images"][i]
+        assert np.array_equal(rg["images"][i][:n], ro["images"][i][:n]), name
+        assert np.array_equal(rg["grids"][i][:n], ro["grids"][i][:n]), name
+    for k in ("accepted", "fail_pre", "fail_post", "refine_failed", "evals", "tex_valid", "tex_grabs"):
+        assert sg[k] == so[k], (name, k)
+
+
+def test_thresholds_matrix(pair):
+    """updateThreshold-style changes (findMatch.cpp:23-28) take effect identically."""
+    import pmvs_amd as P
+    name, inp, p, g, o = pair
+    cands = P.synth_candidates(p, inp.projections, 150, seed=78)
+    for ncc, before in ((0.55, 0.45), (0.8, 0.7)):
+        g.set_thresholds(ncc, before)
+        o.set_thresholds(ncc, before)
+        rg, sg = g.refine_batch(cands)
+        ro, so = o.refine_batch(cands, nthreads=8)
+        assert np.array_equal(rg["status"], ro["status"]), (name, ncc)
+        assert sg["accepted"] == so["accepted"]
+        acc = ro["status"] == 0
+        assert np.array_equal(bits(rg["ncc"][acc]), bits(ro["ncc"][acc]))
+    thr = inp.threshold
+    g.set_thresholds(thr, thr - 0.1)
+    o.set_thresholds(thr, thr - 0.1)
+
+
+def test_grab_and_my_f_matrix(pair):
+    import pmvs_amd as P
+    name, inp, p, g, o = pair
+    V = len(inp.images)
+    cands = P.synth_candidates(p, inp.projections, 60, seed=79)
+    tq = tex_queries(o, V, cands)
+    tg, vg = g.grab_tex(tq)
+    to, vo = o.grab_tex(tq)
+    assert np.array_equal(vg, vo) and np.array_equal(bits(tg), bits(to)), name
+    eq = eval_queries(V, cands, per=3, nimg=min(6, V))
+    fg, _ = g.incc_eval(eq)
+    fo = o.incc_eval(eq)
+    assert np.array_equal(bits(fg), bits(fo)), name
+
+
+def test_empty_and_invalid_batches(gpu_available):
+    import pmvs_amd as P
+    inp, p = P.synth_scene(4, 160, 120, level=1)
+    g = P.Scene(inp)
+    out, st = g.refine_batch(np.zeros(0, P.CANDIDATE_DTYPE))
+    assert len(out) == 0 and st["accepted"] == 0
+    bad = P.synth_candidates(p, inp.projections, 4, seed=1)
+    bad["images"][2][1] = 99  # image index out of range -> PMVS_EINVAL, nothing launched
+    with pytest.raises(P.PmvsError):
+        g.refine_batch(bad)
+    bad = P.synth_candidates(p, inp.projections, 4, seed=1)
+    bad["num_images"][0] = 0
+    with pytest.raises(P.PmvsError):
+        g.refine_batch(bad)
+    g.close()
