@@ -35,6 +35,20 @@ pmvs_status fail(pmvs_status st, const char* fmt, ...) {
   return st;
 }
 
+}  // namespace
+
+pmvs_status pmvs_io_fail(pmvs_status st, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return st;
+}
+
+namespace {
+
 #define HIPCHK(expr)                                                                              \
   do {                                                                                            \
     hipError_t e_ = (expr);                                                                       \
@@ -591,3 +605,35 @@ pmvs_status pmvs_selftest_bobyqa(int32_t device, int32_t mode, int32_t kind, con
 }
 
 }  // extern "C"
+
+pmvs_status pmvs_patch_colors(pmvs_scene* sc, int32_t n, const float* coords4, const int32_t* nimg,
+                              const int32_t* images_flat, int32_t* colors_out) {
+  if (!sc || n < 0 || (n > 0 && (!coords4 || !nimg || !images_flat || !colors_out))) return fail(PMVS_EINVAL, "null argument");
+  if (n == 0) return PMVS_OK;
+  std::vector<int> off(n + 1, 0);
+  for (int i = 0; i < n; ++i) {
+    if (nimg[i] < 1) return fail(PMVS_EINVAL, "patch %d: no images", i);
+    off[i + 1] = off[i] + nimg[i];
+  }
+  for (int k = 0; k < off[n]; ++k)
+    if (images_flat[k] < 0 || images_flat[k] >= sc->ds.num) return fail(PMVS_EINVAL, "image index %d", images_flat[k]);
+  HIPCHK(hipSetDevice(sc->device));
+  float* dc = nullptr;
+  int *doff = nullptr, *dimg = nullptr, *dout = nullptr;
+  hipError_t e = hipMalloc((void**)&dc, (size_t)n * 4 * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc((void**)&doff, (size_t)(n + 1) * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc((void**)&dimg, (size_t)off[n] * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc((void**)&dout, (size_t)n * 3 * sizeof(int));
+  if (e == hipSuccess) e = hipMemcpyAsync(dc, coords4, (size_t)n * 4 * sizeof(float), hipMemcpyHostToDevice, sc->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(doff, off.data(), (size_t)(n + 1) * sizeof(int), hipMemcpyHostToDevice, sc->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dimg, images_flat, (size_t)off[n] * sizeof(int), hipMemcpyHostToDevice, sc->stream);
+  if (e == hipSuccess) e = launch_patch_colors(sc->ds, n, dc, doff, dimg, dout, sc->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(colors_out, dout, (size_t)n * 3 * sizeof(int), hipMemcpyDeviceToHost, sc->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(sc->stream);
+  (void)hipFree(dc);
+  (void)hipFree(doff);
+  (void)hipFree(dimg);
+  (void)hipFree(dout);
+  if (e != hipSuccess) return fail(PMVS_EDEVICE, "patch colours: %s", hipGetErrorString(e));
+  return PMVS_OK;
+}

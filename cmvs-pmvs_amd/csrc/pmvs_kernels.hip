@@ -1399,9 +1399,9 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
                                    int n, DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream,
                                    hipEvent_t* ev) {
   const int g = grid < n ? grid : n;
-  hipEventRecord(ev[0], stream);
+  (void)hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL((pre_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_in, d_jobs, n, d_st);
-  hipEventRecord(ev[1], stream);
+  (void)hipEventRecord(ev[1], stream);
   const int nc = tslots % 100;
   const int rg = refine_grid < (n + nc - 1) / nc ? refine_grid : (n + nc - 1) / nc;
   // tslots = texture slots per objective chunk * 100 + optimizer chains per wavefront
@@ -1414,9 +1414,9 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
     case 4808: hipLaunchKernelGGL((refine_v2_kernel<WS, 48, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     default: hipLaunchKernelGGL((refine_v2_kernel<WS, 32, 16>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
   }
-  hipEventRecord(ev[2], stream);
+  (void)hipEventRecord(ev[2], stream);
   hipLaunchKernelGGL((post_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_jobs, d_out, n, d_st);
-  hipEventRecord(ev[3], stream);
+  (void)hipEventRecord(ev[3], stream);
   return hipGetLastError();
 }
 
@@ -1473,6 +1473,46 @@ hipError_t launch_unpack_rgba(const uint32_t* d_in, uint8_t* d_rgb, long long np
   return hipGetLastError();
 }
 
+}  // namespace pmvsdev
+
+// ==================================================================== .ply colours
+namespace pmvsdev {
+// CPatchOrganizerS::writePLY colour mode 0 (patchOrganizerS.cpp:716-731): Vec3f sum of
+// CPhotoSetS::getColor over the patch's images (project + bilinear at the scene level), divided
+// by the image count, floor(c + 0.5f) clamped to 255.  One thread per patch.  Out-of-image
+// projections (undefined reads in the reference) are clamped to the border texel.
+__global__ void patch_colors_kernel(DScene s, int n, const float* __restrict__ coords, const int* __restrict__ off,
+                                    const int* __restrict__ images, int* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float c[4] = {coords[4 * i], coords[4 * i + 1], coords[4 * i + 2], coords[4 * i + 3]};
+  float acc[3] = {0.0f, 0.0f, 0.0f};
+  int denom = 0;
+  for (int k = off[i]; k < off[i + 1]; ++k) {
+    const DView& v = s.views[images[k]];
+    float ic[3], rgb[3];
+    project(v, c, s.level, ic);
+    const float mx = (float)(v.w[s.level] - 2), my = (float)(v.h[s.level] - 2);
+    const float x = ic[0] < 0.0f ? 0.0f : (ic[0] > mx ? mx : ic[0]);
+    const float y = ic[1] < 0.0f ? 0.0f : (ic[1] > my ? my : ic[1]);
+    get_color(s, v, x, y, s.level, rgb);
+    acc[0] += rgb[0];
+    acc[1] += rgb[1];
+    acc[2] += rgb[2];
+    denom++;
+  }
+  for (int j = 0; j < 3; ++j) {
+    const float m = __fdiv_rn(acc[j], (float)denom);
+    const int q = (int)floor((double)(m + 0.5f));
+    out[3 * i + j] = q < 255 ? q : 255;
+  }
+}
+hipError_t launch_patch_colors(const DScene& s, int n, const float* coords, const int* off, const int* images, int* out,
+                               hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(patch_colors_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, s, n, coords, off, images, out);
+  return hipGetLastError();
+}
 }  // namespace pmvsdev
 
 // ==================================================================== device math self-test

@@ -63,6 +63,15 @@ class Stats(C.Structure):
         return {k: (list(getattr(self, k)) if k == "prof" else getattr(self, k)) for k, _ in self._fields_}
 
 
+class Options(C.Structure):
+    _fields_ = [(k, C.c_int32) for k in ("level", "csize", "wsize", "min_image_num", "cpu", "use_bound",
+                                          "use_vis_data", "sequence", "tflag", "oflag")] + \
+               [(k, C.c_float) for k in ("threshold", "set_edge", "max_angle", "quad")] + \
+               [(k, C.c_int32) for k in ("num_timages", "num_oimages", "num_bindexes")] + \
+               [(k, C.POINTER(C.c_int32)) for k in ("timages", "oimages", "bindexes", "visdata2_offsets",
+                                                      "visdata2")]
+
+
 class SynthParams(C.Structure):
     _fields_ = [("num_views", C.c_int32), ("num_targets", C.c_int32), ("width", C.c_int32),
                 ("height", C.c_int32), ("supersample", C.c_int32), ("level", C.c_int32),
@@ -73,7 +82,9 @@ class SynthParams(C.Structure):
 EXPORTS = ["pmvs_last_error", "pmvs_device_count", "pmvs_scene_create", "pmvs_scene_destroy",
            "pmvs_set_thresholds", "pmvs_scene_get_level", "pmvs_grab_tex", "pmvs_incc_eval",
            "pmvs_refine_batch", "pmvs_refine_batch_device", "pmvs_scene_sync", "pmvs_synth_ring",
-           "pmvs_synth_candidates", "pmvs_selftest_math", "pmvs_selftest_bobyqa"]
+           "pmvs_synth_candidates", "pmvs_selftest_math", "pmvs_selftest_bobyqa", "pmvs_camera_load",
+           "pmvs_ppm_load", "pmvs_options_load", "pmvs_options_free", "pmvs_write_patches", "pmvs_write_pset",
+           "pmvs_write_ply", "pmvs_patch_colors"]
 
 _lib = None
 
@@ -105,11 +116,21 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.pmvs_selftest_bobyqa.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_int32,
                                          C.c_void_p, C.POINTER(C.c_double)]
     lib.pmvs_selftest_math.argtypes = [C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32]
+    lib.pmvs_camera_load.argtypes = [C.c_char_p, C.c_void_p]
+    lib.pmvs_ppm_load.argtypes = [C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_void_p]
+    lib.pmvs_options_load.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.POINTER(Options))]
+    lib.pmvs_options_free.argtypes = [C.POINTER(Options)]
+    lib.pmvs_options_free.restype = None
+    lib.pmvs_write_patches.argtypes = [C.c_char_p, C.c_int32] + [C.c_void_p] * 5
+    lib.pmvs_write_pset.argtypes = [C.c_char_p, C.c_int32, C.c_void_p]
+    lib.pmvs_write_ply.argtypes = [C.c_char_p, C.c_int32, C.c_void_p, C.c_void_p]
+    lib.pmvs_patch_colors.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 4
     for fn in EXPORTS:
         getattr(lib, fn).restype = getattr(lib, fn).restype or C.c_int
     lib.pmvs_last_error.restype = C.c_char_p
     lib.pmvs_device_count.restype = C.c_int32
     lib.pmvs_scene_destroy.restype = None
+    lib.pmvs_options_free.restype = None
     _lib = lib
     return lib
 
@@ -273,6 +294,15 @@ class Scene:
     def refine_batch_device(self, d_in_ptr: int, n: int, d_out_ptr: int):
         _check(self.lib.pmvs_refine_batch_device(self.handle, C.c_void_p(d_in_ptr), n, C.c_void_p(d_out_ptr)))
 
+    def patch_colors(self, coords: np.ndarray, images) -> np.ndarray:
+        """writePLY colour mode 0 for patches (coords [n,4], images: list of view-index lists)."""
+        coords = np.ascontiguousarray(coords, np.float32).reshape(-1, 4)
+        nimg = np.array([len(x) for x in images], np.int32)
+        flat = np.array([v for x in images for v in x] or [0], np.int32)
+        out = np.zeros((len(coords), 3), np.int32)
+        _check(self.lib.pmvs_patch_colors(self.handle, len(coords), _ptr(coords), _ptr(nimg), _ptr(flat), _ptr(out)))
+        return out
+
     def sync(self):
         st = Stats()
         _check(self.lib.pmvs_scene_sync(self.handle, C.byref(st)))
@@ -292,6 +322,66 @@ def selftest_bobyqa(kind: int, x0: np.ndarray, mode: int = 0, maxeval: int = 100
     ms = C.c_double()
     _check(load_library().pmvs_selftest_bobyqa(device, mode, kind, _ptr(x0), len(x0), maxeval, _ptr(out), C.byref(ms)))
     return out, ms.value
+
+
+# ---------------------------------------------------------------------------------- pmvs2 I/O
+def camera_load(path: str) -> np.ndarray:
+    """CONTOUR/CONTOUR2/CONTOUR3 txt -> level-0 3x4 projection (pmvs_camera_load)."""
+    out = np.zeros(12, np.float32)
+    _check(load_library().pmvs_camera_load(path.encode(), _ptr(out)))
+    return out.reshape(3, 4)
+
+
+def ppm_load(path: str) -> np.ndarray:
+    lib = load_library()
+    w, h = C.c_int32(), C.c_int32()
+    _check(lib.pmvs_ppm_load(path.encode(), C.byref(w), C.byref(h), None))
+    img = np.zeros((h.value, w.value, 3), np.uint8)
+    _check(lib.pmvs_ppm_load(path.encode(), C.byref(w), C.byref(h), _ptr(img)))
+    return img
+
+
+def options_load(prefix: str, option_file: str) -> dict:
+    """pmvs2 option file (+ vis.dat / bimages.dat) -> dict (pmvs_options_load)."""
+    lib = load_library()
+    p = C.POINTER(Options)()
+    _check(lib.pmvs_options_load(prefix.encode(), option_file.encode(), C.byref(p)))
+    o = p.contents
+    d = {k: getattr(o, k) for k, _ in Options._fields_[:17]}
+    num = o.num_timages + o.num_oimages
+    d["timages"] = [o.timages[i] for i in range(o.num_timages)]
+    d["oimages"] = [o.oimages[i] for i in range(o.num_oimages)]
+    d["bindexes"] = [o.bindexes[i] for i in range(o.num_bindexes)]
+    off = [o.visdata2_offsets[i] for i in range(num + 1)]
+    d["visdata2"] = [[o.visdata2[k] for k in range(off[r], off[r + 1])] for r in range(num)]
+    lib.pmvs_options_free(p)
+    return d
+
+
+def _patch_arrays(fields, images, vimages):
+    fields = np.ascontiguousarray(fields, np.float32).reshape(-1, 11)
+    nimg = np.array([len(x) for x in images], np.int32)
+    nv = np.array([len(x) for x in vimages], np.int32)
+    ids = np.array([v for x in images for v in x] or [0], np.int32)
+    vids = np.array([v for x in vimages for v in x] or [0], np.int32)
+    return fields, nimg, ids, nv, vids
+
+
+def write_patches(path: str, fields, images, vimages):
+    f, nimg, ids, nv, vids = _patch_arrays(fields, images, vimages)
+    _check(load_library().pmvs_write_patches(path.encode(), len(f), _ptr(f), _ptr(nimg), _ptr(ids), _ptr(nv),
+                                             _ptr(vids)))
+
+
+def write_pset(path: str, fields):
+    f = np.ascontiguousarray(fields, np.float32).reshape(-1, 11)
+    _check(load_library().pmvs_write_pset(path.encode(), len(f), _ptr(f)))
+
+
+def write_ply(path: str, fields, colors):
+    f = np.ascontiguousarray(fields, np.float32).reshape(-1, 11)
+    c = np.ascontiguousarray(colors, np.int32).reshape(-1, 3)
+    _check(load_library().pmvs_write_ply(path.encode(), len(f), _ptr(f), _ptr(c)))
 
 
 def device_count() -> int:

@@ -198,6 +198,49 @@ pmvs_status pmvs_selftest_bobyqa(int32_t device, int32_t mode, int32_t kind, con
                                  int32_t maxeval, double* out, double* ms);
 
 /* ---------------------------------------------------------------------------------------
+ * pmvs2 input / output surface (SURVEY.md §8(b) external boundary, §8 row a19).  Host code;
+ * errors are status codes (the reference exits). */
+
+/* Image::CCamera::init + setProjection (camera.cpp:13-54, 256-360): reads a CONTOUR /
+ * CONTOUR2 / CONTOUR3 txt file and writes the level-0 3x4 projection (row-major). */
+pmvs_status pmvs_camera_load(const char* txt_path, float projection[12]);
+
+/* Binary 8-bit PPM (P6) reader: the PNM path of CImage::readAnyImage (image.cpp:473-506).
+ * rgb may be NULL to query the size; otherwise width*height*3 bytes are written. */
+pmvs_status pmvs_ppm_load(const char* path, int32_t* width, int32_t* height, uint8_t* rgb);
+
+/* PMVS3::SOption (option.cpp:10-307): option file keys and defaults, timages/oimages
+ * (enumeration, -1 range, -2 from vis.dat, -3 none), useVisData (vis.dat), useBound
+ * (bimages.dat).  Image lists are image NUMBERS; visdata2 is CSR over view indexes
+ * (timages first, then oimages); bindexes are target indexes. */
+typedef struct pmvs_options {
+  int32_t level, csize, wsize, min_image_num, cpu, use_bound, use_vis_data, sequence, tflag, oflag;
+  float threshold, set_edge, max_angle /* radians */, quad;
+  int32_t num_timages, num_oimages, num_bindexes;
+  const int32_t* timages;
+  const int32_t* oimages;
+  const int32_t* bindexes;
+  const int32_t* visdata2_offsets; /* num_timages + num_oimages + 1 */
+  const int32_t* visdata2;
+} pmvs_options;
+pmvs_status pmvs_options_load(const char* prefix, const char* option_file, pmvs_options** out);
+void pmvs_options_free(pmvs_options* options);
+
+/* Patch fields for the writers: 11 floats per patch = coord[4], normal[4], ncc, dscale, ascale. */
+/* .patch text exactly as CPatchOrganizerS::writePatches2 + Patch::operator<< (patchOrganizerS.cpp:98-116,
+ * patch.cpp:31-48); ids/vids are image numbers (index2image applied by the caller). */
+pmvs_status pmvs_write_patches(const char* path, int32_t n, const float* fields, const int32_t* nimg,
+                               const int32_t* ids, const int32_t* nvimg, const int32_t* vids);
+/* .pset text (patchOrganizerS.cpp:118-131). */
+pmvs_status pmvs_write_pset(const char* path, int32_t n, const float* fields);
+/* ASCII .ply with colour and quality (CPatchOrganizerS::writePLY, patchOrganizerS.cpp:687-776). */
+pmvs_status pmvs_write_ply(const char* path, int32_t n, const float* fields, const int32_t* colors);
+/* writePLY colour mode 0 on the device: mean of CPhotoSetS::getColor over the patch's images at
+ * the scene level, floor(c + 0.5) clamped to 255.  images_flat holds nimg[i] view indexes per patch. */
+pmvs_status pmvs_patch_colors(pmvs_scene* scene, int32_t n, const float* coords4, const int32_t* nimg,
+                              const int32_t* images_flat, int32_t* colors_out);
+
+/* ---------------------------------------------------------------------------------------
  * Synthetic workload generator (NOT a reference interface: the reference ships no data).
  * Textured unit sphere seen by a ring of pinhole cameras. */
 typedef struct pmvs_synth_params {

@@ -125,3 +125,38 @@ def test_full_size_c2_batch_parity(gpu_available, oracle_mod):
     compare_refined(rg, ro)
     for k in ("accepted", "fail_pre", "fail_post", "refine_failed", "evals", "tex_valid"):
         assert sg[k] == so[k], k
+
+
+def _np_get_color(img, x, y):
+    """CImage::getColor bilinear (image.hpp:435-476) in IEEE float32, same operation order."""
+    f32 = np.float32
+    lx, ly = int(x), int(y)
+    dx1 = f32(x) - f32(lx); dx0 = f32(1) - dx1
+    dy1 = f32(y) - f32(ly); dy0 = f32(1) - dy1
+    f00, f01, f10, f11 = dx0 * dy0, dx0 * dy1, dx1 * dy0, dx1 * dy1
+    a0, a1 = img[ly, lx].astype(np.float32), img[ly, lx + 1].astype(np.float32)
+    b0, b1 = img[ly + 1, lx].astype(np.float32), img[ly + 1, lx + 1].astype(np.float32)
+    out = np.zeros(3, np.float32)
+    out = out + (a0 * f00 + b0 * f01)
+    out = out + (a1 * f10 + b1 * f11)
+    return out
+
+
+def test_patch_colors_match_reference_formula(scenes):
+    """writePLY colour mode 0 on the device == the reference formula evaluated on the oracle's
+    pyramid and projections (patchOrganizerS.cpp:716-731)."""
+    import pmvs_amd as P
+    inp, p, g, o = scenes
+    cands = P.synth_candidates(p, inp.projections, 200, seed=21)
+    images = [list(map(int, c["images"][:c["num_images"]])) for c in cands]
+    got = g.patch_colors(cands["coord"], images)
+    lv = inp.level
+    pyr = {v: o.get_level(v, lv) for v in range(len(inp.images))}
+    for i, c in enumerate(cands):
+        acc = np.zeros(3, np.float32)
+        for v in images[i]:
+            ic = o.project(v, lv, c["coord"][None, :])[0]
+            acc = acc + _np_get_color(pyr[v], ic[0], ic[1])
+        m = acc / np.float32(len(images[i]))
+        exp = [min(255, int(np.floor(np.float64(np.float32(m[j] + np.float32(0.5)))))) for j in range(3)]
+        assert list(got[i]) == exp, i
