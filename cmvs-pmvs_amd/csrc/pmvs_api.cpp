@@ -86,6 +86,7 @@ void setup_camera(DView& v, const float* p12, int maxLevel) {
   const float ftmp = (float)std::sqrt((double)dot4f(oa, oa));
   oa[3] = v.P[0][11];
   for (int i = 0; i < 4; ++i) oa[i] /= ftmp;
+  for (int i = 0; i < 4; ++i) v.oaxis[i] = oa[i];
   if (v.P[0][8] == 0.0 && v.P[0][9] == 0.0 && v.P[0][10] == 0.0) {
     float a[3] = {v.P[0][0], v.P[0][1], v.P[0][2]}, b[3] = {v.P[0][4], v.P[0][5], v.P[0][6]}, c[3];
     cross3f(a, b, c);
@@ -179,6 +180,9 @@ struct pmvs_scene {
   DBuf<float> scratch;
   DBuf<DevStats> stats;
   DBuf<RefineJob> jobs;
+  FilterBuffers fbuf;
+  DBuf<pmvs_patch> fpatches;
+  DBuf<int> fkeep;
   int grid = 0, refine_grid = 0, tslots = 1608;
   // staging for host-pointer calls
   DBuf<pmvs_candidate> cand;
@@ -190,7 +194,7 @@ struct pmvs_scene {
   DBuf<int> tvalid;
   ~pmvs_scene() {
     views.release(); pyr.release(); masks.release(); edges.release(); vis_off.release(); vis.release();
-    bindexes.release(); scratch.release(); stats.release(); jobs.release(); cand.release(); res.release(); evq.release();
+    bindexes.release(); scratch.release(); stats.release(); jobs.release(); fpatches.release(); fkeep.release(); cand.release(); res.release(); evq.release();
     evout.release(); tq.release(); tout.release(); tvalid.release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -399,6 +403,8 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
   s.sortThreshold = (float)(1.0f - std::cos(10.0 * M_PI / 180.0));
   s.ascale = (float)(M_PI / 48.0f);
   s.log2f = (float)std::log(2.0);
+  s.quad = d->quad_threshold;
+  s.depth = 0;
   if (hipStreamSynchronize(sc->stream) != hipSuccess) return bail(fail(PMVS_EDEVICE, "scene upload"));
   *out = sc;
   return PMVS_OK;
@@ -413,7 +419,8 @@ void pmvs_scene_destroy(pmvs_scene* scene) {
 
 pmvs_status pmvs_set_thresholds(pmvs_scene* sc, float ncc, float ncc_before, int32_t depth) {
   if (!sc) return fail(PMVS_EINVAL, "null scene");
-  if (depth != 0) return fail(PMVS_EUNSUPPORTED, "depth %d: only the depth-0 refine path is implemented", depth);
+  if (depth < 0) return fail(PMVS_EINVAL, "depth %d", depth);
+  sc->ds.depth = depth;
   sc->ds.nccThreshold = ncc;
   sc->ds.nccThresholdBefore = ncc_before;
   return PMVS_OK;
@@ -511,6 +518,9 @@ static pmvs_status check_candidates(const pmvs_scene* sc, const pmvs_candidate* 
 
 pmvs_status pmvs_refine_batch_device(pmvs_scene* sc, const pmvs_candidate* d_in, int32_t n, pmvs_refined* d_out) {
   if (!sc || (n > 0 && (!d_in || !d_out))) return fail(PMVS_EINVAL, "null argument");
+  if (sc->ds.depth != 0)
+    return fail(PMVS_EUNSUPPORTED, "refine at depth %d: the depth >= 1 postProcess steps (setVImagesVGrids, check) "
+                "are not part of pmvs_refine_batch in this release", sc->ds.depth);
   if (n <= 0) return PMVS_OK;
   HIPCHK(hipSetDevice(sc->device));
   pmvs_status st;
@@ -635,5 +645,56 @@ pmvs_status pmvs_patch_colors(pmvs_scene* sc, int32_t n, const float* coords4, c
   (void)hipFree(dimg);
   (void)hipFree(dout);
   if (e != hipSuccess) return fail(PMVS_EDEVICE, "patch colours: %s", hipGetErrorString(e));
+  return PMVS_OK;
+}
+
+pmvs_status pmvs_filter_run(pmvs_scene* sc, pmvs_patch* patches, int32_t n, int32_t* keep, pmvs_filter_stats* stats) {
+  if (!sc || n < 0 || (n > 0 && (!patches || !keep))) return fail(PMVS_EINVAL, "null argument");
+  if (sc->ds.tnum > 64) return fail(PMVS_EUNSUPPORTED, "filter pass: more than 64 target images");
+  for (int i = 0; i < n; ++i) {
+    const pmvs_patch& p = patches[i];
+    if (p.num_images < 1 || p.num_images > PMVS_MAX_IMAGES || p.num_vimages < 0 || p.num_vimages > PMVS_MAX_IMAGES)
+      return fail(PMVS_EINVAL, "patch %d: image counts", i);
+    for (int k = 0; k < p.num_images; ++k)
+      if (p.images[k] < 0 || p.images[k] >= sc->ds.num) return fail(PMVS_EINVAL, "patch %d: image %d", i, p.images[k]);
+    for (int k = 0; k < p.num_vimages; ++k)
+      if (p.vimages[k] < 0 || p.vimages[k] >= sc->ds.tnum) return fail(PMVS_EINVAL, "patch %d: vimage", i);
+  }
+  if (stats) std::memset(stats, 0, sizeof(*stats));
+  if (n == 0) return PMVS_OK;
+  HIPCHK(hipSetDevice(sc->device));
+  pmvs_status st;
+  if ((st = ensure(sc->fpatches, n)) || (st = ensure(sc->fkeep, n))) return st;
+  std::vector<long long> tgoff(sc->ds.tnum + 1, 0);
+  for (int t = 0; t < sc->ds.tnum; ++t) {
+    const DView& v = sc->hviews[t];
+    const long long gw = (v.w[sc->ds.level] + sc->ds.csize - 1) / sc->ds.csize;
+    const long long gh = (v.h[sc->ds.level] + sc->ds.csize - 1) / sc->ds.csize;
+    tgoff[t + 1] = tgoff[t] + gw * gh;
+  }
+  HIPCHK(hipMemcpyAsync(sc->fpatches.p, patches, (size_t)n * sizeof(pmvs_patch), hipMemcpyHostToDevice, sc->stream));
+  HIPCHK(hipEventRecord(sc->ev0, sc->stream));
+  int counts[4], overflow = 0;
+  HIPCHK(filter_pass(sc->ds, sc->fbuf, sc->fpatches.p, n, tgoff[sc->ds.tnum], tgoff.data(), sc->grid, sc->stream, counts,
+                     &overflow, sc->fkeep.p));
+  HIPCHK(hipEventRecord(sc->ev1, sc->stream));
+  HIPCHK(hipMemcpyAsync(patches, sc->fpatches.p, (size_t)n * sizeof(pmvs_patch), hipMemcpyDeviceToHost, sc->stream));
+  HIPCHK(hipMemcpyAsync(keep, sc->fkeep.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, sc->stream));
+  HIPCHK(hipStreamSynchronize(sc->stream));
+  if (overflow) return fail(PMVS_EUNSUPPORTED, "filterNeighbor: %d patches with more than 1024 neighbours", overflow);
+  if (stats) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, sc->ev0, sc->ev1);
+    stats->input = n;
+    stats->removed_outside = counts[0];
+    stats->removed_exact = counts[1];
+    stats->removed_neighbor = counts[2];
+    stats->removed_groups = counts[3];
+    int64_t k = 0;
+    for (int i = 0; i < n; ++i) k += keep[i];
+    stats->kept = k;
+    stats->kernel_ms = ms;
+  }
+  sc->last_refine = false;
   return PMVS_OK;
 }

@@ -1475,6 +1475,54 @@ hipError_t launch_unpack_rgba(const uint32_t* d_in, uint8_t* d_rgb, long long np
 
 }  // namespace pmvsdev
 
+// ==================================================================== filterExact setRefImage
+namespace pmvsdev {
+// filterExact's "setRefImage(patch, 0); setGrids(patch)" (filter.cpp:340-343) for the listed
+// patches: one wavefront per patch, the refine path's set_ref_image (pairwise INCC in the
+// workgroup's global scratch), then CPatchOrganizerS::setGrids (patchOrganizerS.cpp:417-426).
+template <int WS>
+__global__ __launch_bounds__(64) void filter_refimage_kernel(DScene s, pmvs_patch* __restrict__ P,
+                                                             const int* __restrict__ list, int m) {
+  __shared__ WaveLds<WS> L;
+  float* mat = s.scratch + (size_t)blockIdx.x * PMVS_MAX_IMAGES * PMVS_MAX_IMAGES;
+  const int lane = lane_id();
+  unsigned long long grabs = 0;
+  for (int k = blockIdx.x; k < m; k += gridDim.x) {
+    pmvs_patch& q = P[list[k]];
+    const int n = q.num_images;
+    if (lane < n) L.images[lane] = q.images[lane];
+    if (lane == 0) { L.nimg = n; L.overflow = 0; }
+    __syncthreads();
+    float coord[4], normal[4];
+    for (int i = 0; i < 4; ++i) { coord[i] = q.coord[i]; normal[i] = q.normal[i]; }
+    set_ref_image<WS>(s, L, coord, normal, mat, &grabs);
+    const int nn = L.nimg;
+    if (lane < nn) {
+      const int img = L.images[lane];
+      float ic[3];
+      project(s.views[img], coord, s.level, ic);
+      q.images[lane] = img;
+      q.grids[lane][0] = ((int)floorf(ic[0] + 0.5f)) / s.csize;
+      q.grids[lane][1] = ((int)floorf(ic[1] + 0.5f)) / s.csize;
+    }
+    if (lane == 0) q.num_images = nn;
+    __syncthreads();
+  }
+}
+
+hipError_t launch_filter_refimage(const DScene& s, pmvs_patch* P, const int* list, int m, int grid, hipStream_t stream) {
+  if (m <= 0) return hipSuccess;
+  const int g = grid < m ? grid : m;
+  switch (s.wsize) {
+    case 5: hipLaunchKernelGGL((filter_refimage_kernel<5>), dim3(g), dim3(64), 0, stream, s, P, list, m); break;
+    case 7: hipLaunchKernelGGL((filter_refimage_kernel<7>), dim3(g), dim3(64), 0, stream, s, P, list, m); break;
+    case 9: hipLaunchKernelGGL((filter_refimage_kernel<9>), dim3(g), dim3(64), 0, stream, s, P, list, m); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+}  // namespace pmvsdev
+
 // ==================================================================== .ply colours
 namespace pmvsdev {
 // CPatchOrganizerS::writePLY colour mode 0 (patchOrganizerS.cpp:716-731): Vec3f sum of

@@ -18,4 +18,25 @@ hipError_t launch_bobyqa_selftest(int mode, int kind, const double* d_x0, int n,
                                   hipStream_t stream);
 hipError_t launch_patch_colors(const DScene& s, int n, const float* coords, const int* off, const int* images, int* out,
                                hipStream_t stream);
+
+// ---- filter pass (pmvs_filter.hip)
+struct FilterBuffers {
+  unsigned long long *preg = nullptr, *vreg = nullptr, *keys = nullptr, *keys2 = nullptr, *dpkey = nullptr,
+                     *safe = nullptr;
+  long long* tgoff = nullptr;
+  int *cnt = nullptr, *off = nullptr, *cellcnt = nullptr, *pg_off = nullptr, *pg_items = nullptr, *vp_off = nullptr,
+      *vp_items = nullptr, *order = nullptr, *rank = nullptr, *flags = nullptr, *need = nullptr, *list = nullptr,
+      *counters = nullptr, *edge_off = nullptr, *edges = nullptr;
+  float* unit0 = nullptr;
+  double* scratch = nullptr;
+  void* temp = nullptr;
+  size_t temp_bytes = 0, edges_cap = 0;
+  int cap_n = 0, cap_grid = 0;
+  long long cap_cells = 0;
+  hipError_t reserve(int n, long long ncells, int tnum, int grid);
+  ~FilterBuffers();
+};
+hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n, long long ncells, const long long* h_tgoff,
+                       int grid, hipStream_t st, int counts[4], int* overflow, int* keep_dev);
+hipError_t launch_filter_refimage(const DScene& s, pmvs_patch* P, const int* list, int m, int grid, hipStream_t stream);
 }  // namespace pmvsdev

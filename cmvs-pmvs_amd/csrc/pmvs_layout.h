@@ -13,6 +13,7 @@ constexpr int TEXCAP = 16;  // textures resident in LDS per wave (>= PMVS_MAX_TA
 struct DView {
   float P[MAXL][12];
   float center[4];
+  float oaxis[4];             // CCamera::_oaxis (optical axis, [3] = P[0][2][3] / |P[0][2][0..2]|)
   float xaxis[3], yaxis[3], zaxis[3];
   float ipscale;
   int w[MAXL], h[MAXL];
@@ -38,7 +39,9 @@ struct DScene {
   float sortThreshold;  // (float)(1.0f - cos(10.0*M_PI/180.0))      optim.cpp:287
   float ascale;         // (float)(M_PI / 48.0f)                      optim.cpp:590
   float log2f;          // static float Log2 = log(2.0f)              optim.cpp:813
-  float pad;
+  float quad;           // _quadThreshold (filterQuad)                 filter.cpp:443
+  int depth;            // CFindMatch::_depth (isVisible, postProcess)  findMatch.hpp
+  int pad2;
 };
 
 // One candidate between the three refine-batch kernels (pre -> refine -> post), in HBM.

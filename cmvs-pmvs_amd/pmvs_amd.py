@@ -33,6 +33,11 @@ REFINED_DTYPE = np.dtype(
 EVAL_QUERY_DTYPE = np.dtype(
     [("coord", "<f4", 4), ("normal", "<f4", 4), ("dscale", "<f4"), ("num_images", "<i4"),
      ("images", "<i4", MAX_TAU), ("x", "<f8", 3)], align=True)
+PATCH_DTYPE = np.dtype(
+    [("coord", "<f4", 4), ("normal", "<f4", 4), ("ncc", "<f4"), ("dscale", "<f4"), ("ascale", "<f4"),
+     ("tmp", "<f4"), ("timages", "<i4"), ("flag", "<i4"), ("fix", "<i4"), ("num_images", "<i4"),
+     ("num_vimages", "<i4"), ("reserved", "<i4"), ("images", "<i4", MAX_IMAGES), ("grids", "<i4", (MAX_IMAGES, 2)),
+     ("vimages", "<i4", MAX_IMAGES), ("vgrids", "<i4", (MAX_IMAGES, 2))], align=True)
 TEX_QUERY_DTYPE = np.dtype(
     [("coord", "<f4", 4), ("pxaxis", "<f4", 4), ("pyaxis", "<f4", 4), ("normal", "<f4", 4),
      ("view", "<i4"), ("normalize", "<i4")], align=True)
@@ -63,6 +68,14 @@ class Stats(C.Structure):
         return {k: (list(getattr(self, k)) if k == "prof" else getattr(self, k)) for k, _ in self._fields_}
 
 
+class FilterStats(C.Structure):
+    _fields_ = [(k, C.c_int64) for k in ("input", "removed_outside", "removed_exact", "removed_neighbor",
+                                          "removed_groups", "kept")] + [("kernel_ms", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class Options(C.Structure):
     _fields_ = [(k, C.c_int32) for k in ("level", "csize", "wsize", "min_image_num", "cpu", "use_bound",
                                           "use_vis_data", "sequence", "tflag", "oflag")] + \
@@ -84,7 +97,7 @@ EXPORTS = ["pmvs_last_error", "pmvs_device_count", "pmvs_scene_create", "pmvs_sc
            "pmvs_refine_batch", "pmvs_refine_batch_device", "pmvs_scene_sync", "pmvs_synth_ring",
            "pmvs_synth_candidates", "pmvs_selftest_math", "pmvs_selftest_bobyqa", "pmvs_camera_load",
            "pmvs_ppm_load", "pmvs_options_load", "pmvs_options_free", "pmvs_write_patches", "pmvs_write_pset",
-           "pmvs_write_ply", "pmvs_patch_colors"]
+           "pmvs_write_ply", "pmvs_patch_colors", "pmvs_filter_run"]
 
 _lib = None
 
@@ -125,6 +138,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.pmvs_write_pset.argtypes = [C.c_char_p, C.c_int32, C.c_void_p]
     lib.pmvs_write_ply.argtypes = [C.c_char_p, C.c_int32, C.c_void_p, C.c_void_p]
     lib.pmvs_patch_colors.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 4
+    lib.pmvs_filter_run.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(FilterStats)]
     for fn in EXPORTS:
         getattr(lib, fn).restype = getattr(lib, fn).restype or C.c_int
     lib.pmvs_last_error.restype = C.c_char_p
@@ -294,6 +308,14 @@ class Scene:
     def refine_batch_device(self, d_in_ptr: int, n: int, d_out_ptr: int):
         _check(self.lib.pmvs_refine_batch_device(self.handle, C.c_void_p(d_in_ptr), n, C.c_void_p(d_out_ptr)))
 
+    def filter_run(self, patches: np.ndarray):
+        """One CFilter::run pass on the device: returns (patches_out, keep, stats)."""
+        pa = np.ascontiguousarray(patches, PATCH_DTYPE).copy()
+        keep = np.zeros(len(pa), np.int32)
+        st = FilterStats()
+        _check(self.lib.pmvs_filter_run(self.handle, _ptr(pa), len(pa), _ptr(keep), C.byref(st)))
+        return pa, keep, st.as_dict()
+
     def patch_colors(self, coords: np.ndarray, images) -> np.ndarray:
         """writePLY colour mode 0 for patches (coords [n,4], images: list of view-index lists)."""
         coords = np.ascontiguousarray(coords, np.float32).reshape(-1, 4)
@@ -382,6 +404,15 @@ def write_ply(path: str, fields, colors):
     f = np.ascontiguousarray(fields, np.float32).reshape(-1, 11)
     c = np.ascontiguousarray(colors, np.int32).reshape(-1, 3)
     _check(load_library().pmvs_write_ply(path.encode(), len(f), _ptr(f), _ptr(c)))
+
+
+def patches_from_refined(refined: np.ndarray) -> np.ndarray:
+    """Accepted pmvs_refined records -> pmvs_patch records (the CPatch fields a filter pass reads)."""
+    acc = refined[refined["status"] == ACCEPTED]
+    p = np.zeros(len(acc), PATCH_DTYPE)
+    for f in ("coord", "normal", "ncc", "dscale", "ascale", "tmp", "timages", "num_images", "images", "grids"):
+        p[f] = acc[f]
+    return p
 
 
 def device_count() -> int:

@@ -198,6 +198,31 @@ pmvs_status pmvs_selftest_bobyqa(int32_t device, int32_t mode, int32_t kind, con
                                  int32_t maxeval, double* out, double* ms);
 
 /* ---------------------------------------------------------------------------------------
+ * Filter pass over a patch set (PMVS3::CFilter::run, filter.cpp:13-27): the cell organizer
+ * (CPatchOrganizerS pgrids / vpgrids / depth maps) is built on the device from the patch
+ * array; insertion order = array index.  Runs at the scene's thresholds and depth
+ * (pmvs_set_thresholds; the reference runs filters at depth >= 1). */
+typedef struct pmvs_patch {
+  float coord[4], normal[4];
+  float ncc, dscale, ascale, tmp;
+  int32_t timages, flag, fix, num_images, num_vimages, reserved;
+  int32_t images[PMVS_MAX_IMAGES];
+  int32_t grids[PMVS_MAX_IMAGES][2];
+  int32_t vimages[PMVS_MAX_IMAGES];
+  int32_t vgrids[PMVS_MAX_IMAGES][2];
+} pmvs_patch;
+
+typedef struct pmvs_filter_stats {
+  int64_t input, removed_outside, removed_exact, removed_neighbor, removed_groups, kept;
+  double kernel_ms;
+} pmvs_filter_stats;
+
+/* patches are updated in place (images/grids/timages/vimages/vgrids as the reference leaves
+ * them); keep[i] = 1 when patch i is still in the organizer (the model) after the pass. */
+pmvs_status pmvs_filter_run(pmvs_scene* scene, pmvs_patch* patches, int32_t n, int32_t* keep,
+                            pmvs_filter_stats* stats);
+
+/* ---------------------------------------------------------------------------------------
  * pmvs2 input / output surface (SURVEY.md §8(b) external boundary, §8 row a19).  Host code;
  * errors are status codes (the reference exits). */
 

@@ -1,0 +1,551 @@
+// oracle/filter_oracle.h -- TEST INFRASTRUCTURE ONLY (included by pmvs_oracle.cpp).
+//
+// CPU restatement of one PMVS filter pass, PMVS3::CFilter::run (filter.cpp:13-27), over a
+// patch set held in a CPatchOrganizerS-style cell organizer (patchOrganizerS.cpp):
+//   setDepthMapsVGridsVPGridsAddPatchV(0)  filter.cpp:727-770 (+ setDepthMaps :668-725,
+//                                           setVImagesVGrids patchOrganizerS.cpp:429-459,
+//                                           addPatchV filter.cpp:795-827)
+//   filterOutside                           filter.cpp:29-86, computeGain :88-146 / thread :148-201
+//   filterExact                             filter.cpp:203-356
+//   filterNeighbor(1)                       filter.cpp:358-518 (findNeighbors
+//                                           patchOrganizerS.cpp:527-631, filterQuad :387-446)
+//   filterSmallGroups                       filter.cpp:520-666
+// each followed by setDepthMapsVGridsVPGridsAddPatchV(1).
+//
+// Ordering.  The reference's cell lists hold shared_ptrs in insertion order and several
+// results depend on iteration order (depth-map ties, BFS labels in filterSmallGroups) or
+// on pointer order (findNeighbors sorts neighbours by address, which feeds the float sums and
+// the least-squares fit of filterQuad).  Here insertion order = patch array index, and
+// neighbour lists are sorted by array index.  Cmylapack::lls (Eigen JacobiSVD, absent from the
+// image) is replaced by a Householder-QR least-squares solve in double: filterQuad decisions
+// are therefore "parity unpinned" against the reference binary.
+#pragma once
+
+#include <array>
+#include <deque>
+
+namespace oracle {
+
+struct FPatch {
+  V4 coord, normal;
+  float ncc, dscale, ascale, tmp;
+  int timages, flag, fix;
+  std::vector<int> images, vimages;
+  std::vector<std::pair<int, int>> grids, vgrids;
+  int id = -1;  // CPatch::_id (collectPatches order)
+};
+
+struct Organizer {
+  const OScene& s;
+  std::vector<std::vector<std::vector<int>>> pgrids, vpgrids;  // [target][cell] -> patch indexes
+  std::vector<std::vector<int>> dpgrids;                         // [target][cell] -> patch or -1
+  std::vector<int> ppatches;                                     // collectPatches order
+  explicit Organizer(const OScene& sc) : s(sc) {
+    pgrids.resize(s.tnum);
+    vpgrids.resize(s.tnum);
+    dpgrids.resize(s.tnum);
+    for (int t = 0; t < s.tnum; ++t) {
+      const size_t n = (size_t)s.gwidths[t] * s.gheights[t];
+      pgrids[t].resize(n);
+      vpgrids[t].resize(n);
+      dpgrids[t].assign(n, -1);
+    }
+  }
+  int cell(int t, int ix, int iy) const { return iy * s.gwidths[t] + ix; }
+  bool in_grid(int t, int ix, int iy) const { return 0 <= ix && ix < s.gwidths[t] && 0 <= iy && iy < s.gheights[t]; }
+};
+
+static inline void erase_from(std::vector<int>& v, int p) { v.erase(std::remove(v.begin(), v.end(), p), v.end()); }
+
+// CPatchOrganizerS::addPatch (patchOrganizerS.cpp:308-346) without the depth-map update (the
+// filter rebuilds depth maps from scratch before every use).
+static void add_patch_p(Organizer& o, const std::vector<FPatch>& P, int p) {
+  const FPatch& q = P[p];
+  for (size_t i = 0; i < q.images.size(); ++i) {
+    const int t = q.images[i];
+    if (o.s.tnum <= t) continue;
+    if (!o.in_grid(t, q.grids[i].first, q.grids[i].second)) continue;  // out-of-grid: undefined in the reference
+    o.pgrids[t][o.cell(t, q.grids[i].first, q.grids[i].second)].push_back(p);
+  }
+}
+
+// CPatchOrganizerS::removePatch (patchOrganizerS.cpp:461-489).
+static void remove_patch(Organizer& o, const std::vector<FPatch>& P, int p) {
+  const FPatch& q = P[p];
+  for (size_t i = 0; i < q.images.size(); ++i) {
+    const int t = q.images[i];
+    if (o.s.tnum <= t || !o.in_grid(t, q.grids[i].first, q.grids[i].second)) continue;
+    erase_from(o.pgrids[t][o.cell(t, q.grids[i].first, q.grids[i].second)], p);
+  }
+  for (size_t i = 0; i < q.vimages.size(); ++i) {
+    const int t = q.vimages[i];
+    erase_from(o.vpgrids[t][o.cell(t, q.vgrids[i].first, q.vgrids[i].second)], p);
+  }
+}
+
+// CPatchOrganizerS::collectPatches(target) (patchOrganizerS.cpp:218-248).
+static void collect_patches(Organizer& o, std::vector<FPatch>& P, int target) {
+  o.ppatches.clear();
+  for (auto& q : P) q.id = -1;
+  int count = 0;
+  for (int t = 0; t < o.s.tnum; ++t)
+    for (auto& cellv : o.pgrids[t])
+      for (int p : cellv)
+        if (P[p].id == -1) {
+          P[p].id = count++;
+          if (target == 0 || P[p].fix == 0) o.ppatches.push_back(p);
+        }
+}
+
+static inline float depth_of(const OScene& s, int t, const V4& c) { return dot4(s.views[t].oaxis, c); }
+
+// CFilter::setDepthMaps / setDepthMapsThread (filter.cpp:668-725).
+static void set_depth_maps(Organizer& o, const std::vector<FPatch>& P) {
+  const OScene& s = o.s;
+  for (int t = 0; t < s.tnum; ++t) {
+    std::fill(o.dpgrids[t].begin(), o.dpgrids[t].end(), -1);
+    for (int p : o.ppatches) {
+      const V3 ic = project(s, t, P[p].coord, s.level);
+      const float fx = ic[0] / s.csize, fy = ic[1] / s.csize;
+      const int xs[2] = {(int)std::floor(fx), (int)std::ceil(fx)};
+      const int ys[2] = {(int)std::floor(fy), (int)std::ceil(fy)};
+      const float depth = depth_of(s, t, P[p].coord);
+      for (int j = 0; j < 2; ++j)
+        for (int i = 0; i < 2; ++i) {
+          if (!o.in_grid(t, xs[i], ys[j])) continue;
+          int& d = o.dpgrids[t][o.cell(t, xs[i], ys[j])];
+          if (d == -1) d = p;
+          else if (depth < depth_of(s, t, P[d].coord)) d = p;
+        }
+    }
+  }
+}
+
+// CPatchOrganizerS::isVisible (patchOrganizerS.cpp:500-525).
+static int is_visible(const Organizer& o, const std::vector<FPatch>& P, const FPatch& q, int t, int ix, int iy,
+                      float strict) {
+  const OScene& s = o.s;
+  if (!o.in_grid(t, ix, iy)) return 0;
+  if (s.depth == 0) return 1;
+  const int d = o.dpgrids[t][o.cell(t, ix, iy)];
+  if (d == -1) return 1;
+  V4 ray = sub4(q.coord, s.views[t].center);
+  unitize4(ray);
+  const float diff = dot4(ray, sub4(q.coord, P[d].coord));
+  const float factor = (float)std::min(2.0, 2.0 + (double)dot4(ray, q.normal));
+  return diff < get_unit(s, t, q.coord) * s.csize * strict * factor ? 1 : 0;
+}
+
+// CPatchOrganizerS::setVImagesVGrids (patchOrganizerS.cpp:429-459) with isVisible0 (:491-498),
+// neighbourThreshold 0.5 (findMatch.cpp:94).
+static void set_vimages_vgrids(const Organizer& o, const std::vector<FPatch>& P, FPatch& q) {
+  const OScene& s = o.s;
+  std::vector<int> used(s.tnum, 0);
+  for (int t : q.images)
+    if (t < s.tnum) used[t] = 1;
+  for (int t : q.vimages) used[t] = 1;
+  for (int t = 0; t < s.tnum; ++t) {
+    if (used[t]) continue;
+    const V3 ic = project(s, t, q.coord, s.level);
+    const int ix = ((int)std::floor(ic[0] + 0.5f)) / s.csize;
+    const int iy = ((int)std::floor(ic[1] + 0.5f)) / s.csize;
+    if (is_visible(o, P, q, t, ix, iy, 0.5f) == 0) continue;
+    if (get_edge(s, q.coord, t, s.level) == 0) continue;
+    q.vimages.push_back(t);
+    q.vgrids.push_back({ix, iy});
+  }
+}
+
+// CFilter::setDepthMapsVGridsVPGridsAddPatchV (filter.cpp:727-770).
+static void set_dm_vgrids(Organizer& o, std::vector<FPatch>& P, int additive) {
+  collect_patches(o, P, 0);
+  set_depth_maps(o, P);
+  for (auto& img : o.vpgrids)
+    for (auto& c : img) c.clear();
+  if (additive == 0)
+    for (int p : o.ppatches) {
+      P[p].vimages.clear();
+      P[p].vgrids.clear();
+    }
+  for (int p : o.ppatches) set_vimages_vgrids(o, P, P[p]);
+  for (int t = 0; t < o.s.tnum; ++t)  // addPatchVThread: first matching entry only
+    for (int p : o.ppatches) {
+      const FPatch& q = P[p];
+      for (size_t i = 0; i < q.vimages.size(); ++i)
+        if (q.vimages[i] == t) {
+          o.vpgrids[t][o.cell(t, q.vgrids[i].first, q.vgrids[i].second)].push_back(p);
+          break;
+        }
+    }
+}
+
+// CFindMatch::isNeighbor / isNeighborRadius (findMatch.cpp:125-185).
+static int is_neighbor_h(const FPatch& l, const FPatch& r, float hunit, float thr, float radius, bool use_radius) {
+  if ((double)dot4(l.normal, r.normal) < std::cos(120.0 * M_PI / 180.0)) return 0;
+  const V4 diff = sub4(r.coord, l.coord);
+  const float vunit = l.dscale + r.dscale;
+  const float f0 = dot4(l.normal, diff), f1 = dot4(r.normal, diff);
+  float ftmp = (float)(((double)std::fabs(f0) + (double)std::fabs(f1)) / 2.0);
+  ftmp /= vunit;
+  V4 v;
+  for (int k = 0; k < 4; ++k) v[k] = (2.0f * diff[k] - l.normal[k] * f0) - r.normal[k] * f1;
+  const float hsize = (float)((double)norm4(v) / 2.0 / (double)hunit);
+  if (use_radius && radius / hunit < hsize) return 0;
+  if (1.0 < hsize) ftmp /= std::min(2.0f, hsize);
+  return ftmp < thr ? 1 : 0;
+}
+static int is_neighbor(const OScene& s, const FPatch& l, const FPatch& r, float thr) {
+  const float hunit =
+      (float)((double)(get_unit(s, l.images[0], l.coord) + get_unit(s, r.images[0], r.coord)) / 2.0 * s.csize);
+  return is_neighbor_h(l, r, hunit, thr, 0.0f, false);
+}
+
+// CPatch::score2 (patch.hpp:49-51).
+static inline float score2(const FPatch& q, float thr) { return std::max(0.0f, q.ncc - thr) * q.timages; }
+
+// CFilter::filterOutsideThread gain (filter.cpp:148-201), neighbourThreshold1 = 1.0.
+static float compute_gain(const Organizer& o, const std::vector<FPatch>& P, const FPatch& q) {
+  const OScene& s = o.s;
+  float gain = score2(q, s.nccThreshold);
+  for (size_t i = 0; i < q.images.size(); ++i) {
+    const int t = q.images[i];
+    if (s.tnum <= t) continue;
+    const int c = o.cell(t, q.grids[i].first, q.grids[i].second);
+    float maxp = 0.0f;
+    for (int j : o.pgrids[t][c])
+      if (!is_neighbor(s, q, P[j], 1.0f)) maxp = std::max(maxp, P[j].ncc - s.nccThreshold);
+    gain -= maxp;
+  }
+  for (size_t i = 0; i < q.vimages.size(); ++i) {
+    const int t = q.vimages[i];
+    if (s.tnum <= t) continue;
+    const float pdepth = depth_of(s, t, q.coord);
+    const int c = o.cell(t, q.vgrids[i].first, q.vgrids[i].second);
+    float maxp = 0.0f;
+    for (int j : o.pgrids[t][c]) {
+      const float bdepth = depth_of(s, t, P[j].coord);
+      if (pdepth < bdepth && !is_neighbor(s, q, P[j], 1.0f)) maxp = std::max(maxp, P[j].ncc - s.nccThreshold);
+    }
+    gain -= maxp;
+  }
+  return gain;
+}
+
+static int filter_outside(Organizer& o, std::vector<FPatch>& P) {
+  collect_patches(o, P, 1);
+  std::vector<float> gains(o.ppatches.size());
+  for (size_t k = 0; k < o.ppatches.size(); ++k) gains[k] = compute_gain(o, P, P[o.ppatches[k]]);
+  int count = 0;
+  for (size_t k = 0; k < o.ppatches.size(); ++k)
+    if (gains[k] < 0.0) {
+      remove_patch(o, P, o.ppatches[k]);
+      count++;
+    }
+  return count;
+}
+
+// CFilter::filterExact (filter.cpp:203-356), neighbourThreshold1 = 1.0.
+static int filter_exact(Organizer& o, std::vector<FPatch>& P, OCtx& ctx) {
+  const OScene& s = o.s;
+  collect_patches(o, P, 0);
+  const int psize = (int)o.ppatches.size();
+  std::vector<std::vector<int>> newimages(psize), removeimages(psize);
+  std::vector<std::vector<std::pair<int, int>>> newgrids(psize), removegrids(psize);
+  for (int t = 0; t < s.tnum; ++t) {
+    const int w = s.gwidths[t], h = s.gheights[t];
+    int index = -1;
+    for (int y = 0; y < h; ++y)
+      for (int x = 0; x < w; ++x) {
+        ++index;
+        for (int p : o.pgrids[t][index]) {
+          const FPatch& q = P[p];
+          if (q.fix) continue;
+          int safe = 0;
+          if (is_visible(o, P, q, t, x, y, 1.0f)) safe = 1;
+          else if (0 < x && is_visible(o, P, q, t, x - 1, y, 1.0f)) safe = 1;
+          else if (x < w - 1 && is_visible(o, P, q, t, x + 1, y, 1.0f)) safe = 1;
+          else if (0 < y && is_visible(o, P, q, t, x, y - 1, 1.0f)) safe = 1;
+          else if (y < h - 1 && is_visible(o, P, q, t, x, y + 1, 1.0f)) safe = 1;
+          if (safe) {
+            newimages[q.id].push_back(t);
+            newgrids[q.id].push_back({x, y});
+          } else {
+            removeimages[q.id].push_back(t);
+            removegrids[q.id].push_back({x, y});
+          }
+        }
+      }
+  }
+  for (int k = 0; k < psize; ++k) {
+    const int p = o.ppatches[k];
+    if (P[p].fix) continue;
+    for (size_t i = 0; i < removeimages[k].size(); ++i) {
+      const int t = removeimages[k][i];
+      erase_from(o.pgrids[t][o.cell(t, removegrids[k][i].first, removegrids[k][i].second)], p);
+    }
+  }
+  int count = 0;
+  for (int k = 0; k < psize; ++k) {
+    const int p = o.ppatches[k];
+    FPatch& q = P[p];
+    if (q.fix) continue;
+    q.timages = (int)newimages[k].size();
+    for (size_t i = 0; i < q.images.size(); ++i)
+      if (s.tnum <= q.images[i]) {
+        newimages[k].push_back(q.images[i]);
+        newgrids[k].push_back(q.grids[i]);
+      }
+    q.images.swap(newimages[k]);
+    q.grids.swap(newgrids[k]);
+    if (s.minImageNum <= (int)q.images.size()) {
+      OPatch op;
+      op.coord = q.coord; op.normal = q.normal; op.images = q.images; op.grids = q.grids;
+      op.dscale = q.dscale; op.ascale = q.ascale; op.ncc = q.ncc;
+      set_ref_image(s, ctx, op);
+      q.images = op.images;
+      OPatch g = op;
+      set_grids(s, g);
+      q.grids = g.grids;
+    }
+    if ((int)q.images.size() < s.minImageNum) {
+      remove_patch(o, P, p);
+      count++;
+    }
+  }
+  return count;
+}
+
+// CExpand::computeRadius (expand.cpp:182-198) with COptim::computeUnits (optim.cpp:446-471).
+static float compute_radius(const OScene& s, const FPatch& q) {
+  OPatch op;
+  op.coord = q.coord; op.normal = q.normal; op.images = q.images;
+  std::vector<float> units;
+  compute_units(s, op, units);
+  std::nth_element(units.begin(), units.begin() + 1, units.end());
+  return units[1] * s.csize;
+}
+
+// CPatchOrganizerS::findNeighbors(patch, neighbors, lock, scale, margin, skipvis)
+// (patchOrganizerS.cpp:527-631); neighbours sorted by patch index (reference: by address).
+static void find_neighbors(const Organizer& o, const std::vector<FPatch>& P, const FPatch& q, std::vector<int>& out,
+                           float scale, int margin, int skipvis) {
+  const OScene& s = o.s;
+  const float radius = (float)(1.5 * margin * (double)compute_radius(s, q));
+  float unit = 0.0f;
+  for (int t : q.images) unit += get_unit(s, t, q.coord);
+  unit /= (int)q.images.size();
+  unit *= s.csize;
+  const float thr = 0.5f * scale;  // _neighborThreshold * scale
+  auto scan = [&](int t, int ix, int iy) {
+    for (int j = -margin; j <= margin; ++j) {
+      const int yt = iy + j;
+      if (yt < 0 || s.gheights[t] <= yt) continue;
+      for (int i = -margin; i <= margin; ++i) {
+        const int xt = ix + i;
+        if (xt < 0 || s.gwidths[t] <= xt) continue;
+        const int c = o.cell(t, xt, yt);
+        for (int p : o.pgrids[t][c])
+          if (is_neighbor_h(q, P[p], unit, thr, radius, true)) out.push_back(p);
+        for (int p : o.vpgrids[t][c])
+          if (is_neighbor_h(q, P[p], unit, thr, radius, true)) out.push_back(p);
+      }
+    }
+  };
+  for (size_t i = 0; i < q.images.size(); ++i)
+    if (q.images[i] < s.tnum) scan(q.images[i], q.grids[i].first, q.grids[i].second);
+  if (skipvis == 0)
+    for (size_t i = 0; i < q.vimages.size(); ++i) scan(q.vimages[i], q.vgrids[i].first, q.vgrids[i].second);
+  std::sort(out.begin(), out.end());
+  out.erase(std::unique(out.begin(), out.end()), out.end());
+}
+
+// ortho (vec4.hpp:303-322) on the patch normal.
+static void ortho4(const V4& z, V4& x, V4& y) {
+  x = {{0, 0, 0, 0}};
+  y = {{0, 0, 0, 0}};
+  if (std::fabs((double)z[0]) > 0.5) {
+    x[0] = z[1]; x[1] = -z[0]; x[2] = 0;
+  } else if (std::fabs((double)z[1]) > 0.5) {
+    x[1] = z[2]; x[2] = -z[1]; x[0] = 0;
+  } else {
+    x[2] = z[0]; x[0] = -z[2]; x[1] = 0;
+  }
+  unitize4(x);
+  y[0] = z[1] * x[2] - z[2] * x[1];
+  y[1] = z[2] * x[0] - z[0] * x[2];
+  y[2] = z[0] * x[1] - z[1] * x[0];
+}
+
+// Least squares min ||A x - b|| for an n x 5 system in double by Householder QR
+// (replaces Cmylapack::lls = Eigen JacobiSVD solve, mylapack.cpp:102-149; parity unpinned).
+static void lls5(const std::vector<std::array<float, 5>>& A, const std::vector<float>& b, float x[5]) {
+  const int n = (int)A.size();
+  std::vector<double> M((size_t)n * 5), r(n);
+  for (int i = 0; i < n; ++i) {
+    for (int j = 0; j < 5; ++j) M[(size_t)i * 5 + j] = A[i][j];
+    r[i] = b[i];
+  }
+  double R[5][5] = {{0}};
+  for (int k = 0; k < 5; ++k) {
+    double nrm = 0.0;
+    for (int i = k; i < n; ++i) nrm += M[(size_t)i * 5 + k] * M[(size_t)i * 5 + k];
+    nrm = std::sqrt(nrm);
+    const double akk = M[(size_t)k * 5 + k];
+    const double alpha = (akk > 0.0) ? -nrm : nrm;
+    // v = a_k - alpha e_k (stored in column k, rows k..n-1)
+    M[(size_t)k * 5 + k] = akk - alpha;
+    double vnorm2 = 0.0;
+    for (int i = k; i < n; ++i) vnorm2 += M[(size_t)i * 5 + k] * M[(size_t)i * 5 + k];
+    if (vnorm2 > 0.0) {
+      for (int j = k + 1; j < 5; ++j) {
+        double dotv = 0.0;
+        for (int i = k; i < n; ++i) dotv += M[(size_t)i * 5 + k] * M[(size_t)i * 5 + j];
+        const double f = 2.0 * dotv / vnorm2;
+        for (int i = k; i < n; ++i) M[(size_t)i * 5 + j] -= f * M[(size_t)i * 5 + k];
+      }
+      double dotb = 0.0;
+      for (int i = k; i < n; ++i) dotb += M[(size_t)i * 5 + k] * r[i];
+      const double f = 2.0 * dotb / vnorm2;
+      for (int i = k; i < n; ++i) r[i] -= f * M[(size_t)i * 5 + k];
+    }
+    R[k][k] = alpha;
+    for (int j = k + 1; j < 5; ++j) R[k][j] = M[(size_t)k * 5 + j];
+  }
+  double xs[5];
+  for (int k = 4; k >= 0; --k) {
+    double v = r[k];
+    for (int j = k + 1; j < 5; ++j) v -= R[k][j] * xs[j];
+    xs[k] = (R[k][k] != 0.0) ? v / R[k][k] : 0.0;
+  }
+  for (int k = 0; k < 5; ++k) x[k] = (float)xs[k];
+}
+
+// CFilter::filterQuad (filter.cpp:387-446).
+static int filter_quad(const OScene& s, const std::vector<FPatch>& P, const FPatch& q, const std::vector<int>& nb) {
+  V4 xdir, ydir;
+  ortho4(q.normal, xdir, ydir);
+  const int nsize = (int)nb.size();
+  float h = 0.0f;
+  for (int n = 0; n < nsize; ++n) h += norm4(sub4(P[nb[n]].coord, q.coord));
+  h /= nsize;
+  std::vector<std::array<float, 5>> A(nsize);
+  std::vector<float> b(nsize), fxs(nsize), fys(nsize), fzs(nsize);
+  for (int n = 0; n < nsize; ++n) {
+    const V4 diff = sub4(P[nb[n]].coord, q.coord);
+    fxs[n] = dot4(diff, xdir) / h;
+    fys[n] = dot4(diff, ydir) / h;
+    fzs[n] = dot4(diff, q.normal);
+    A[n] = {{fxs[n] * fxs[n], fys[n] * fys[n], fxs[n] * fys[n], fxs[n], fys[n]}};
+    b[n] = fzs[n];
+  }
+  float x[5];
+  lls5(A, b, x);
+  const int inum = std::min(s.tau, (int)q.images.size());
+  float unit = 0.0f;
+  for (int i = 0; i < inum; ++i) unit += get_unit(s, q.images[i], q.coord);
+  unit /= inum;
+  float residual = 0.0f;
+  for (int n = 0; n < nsize; ++n) {
+    const float res = x[0] * (fxs[n] * fxs[n]) + x[1] * (fys[n] * fys[n]) + x[2] * (fxs[n] * fys[n]) +
+                      x[3] * fxs[n] + x[4] * fys[n] - fzs[n];
+    residual = (float)((double)residual + std::fabs((double)res) / (double)unit);  // float += double
+  }
+  residual /= (nsize - 5);
+  return residual < s.quad ? 0 : 1;
+}
+
+static int filter_neighbor(Organizer& o, std::vector<FPatch>& P) {
+  collect_patches(o, P, 1);
+  std::vector<int> rejects(o.ppatches.size(), 0);
+  for (size_t k = 0; k < o.ppatches.size(); ++k) {
+    const FPatch& q = P[o.ppatches[k]];
+    std::vector<int> nb;
+    find_neighbors(o, P, q, nb, 4.0f, 2, 1);
+    if ((int)nb.size() < 6) rejects[k] = 1;
+    else if (filter_quad(o.s, P, q, nb)) rejects[k] = 1;
+  }
+  int count = 0;
+  for (size_t k = 0; k < o.ppatches.size(); ++k)
+    if (rejects[k]) {
+      count++;
+      remove_patch(o, P, o.ppatches[k]);
+    }
+  return count;
+}
+
+// CFilter::filterSmallGroups + Sub (filter.cpp:520-666), neighbourThreshold2 = 1.0.
+static int filter_small_groups(Organizer& o, std::vector<FPatch>& P) {
+  const OScene& s = o.s;
+  collect_patches(o, P, 0);
+  const int psize = (int)o.ppatches.size();
+  if (psize == 0) return 0;
+  std::vector<int> label(psize, -1);
+  for (int k = 0; k < psize; ++k) P[o.ppatches[k]].flag = k;
+  int id = -1;
+  for (int pid = 0; pid < psize; ++pid) {
+    if (label[pid] != -1) continue;
+    label[pid] = ++id;
+    std::deque<int> ltmp;
+    ltmp.push_back(pid);
+    while (!ltmp.empty()) {
+      const int ptmp = ltmp.front();
+      ltmp.pop_front();
+      const FPatch& q = P[o.ppatches[ptmp]];
+      const int t = q.images[0], ix = q.grids[0].first, iy = q.grids[0].second;
+      for (int y = -1; y <= 1; ++y) {
+        const int yt = iy + y;
+        if (yt < 0 || s.gheights[t] <= yt) continue;
+        for (int x = -1; x <= 1; ++x) {
+          const int xt = ix + x;
+          if (xt < 0 || s.gwidths[t] <= xt) continue;
+          const int c = o.cell(t, xt, yt);
+          for (int lst = 0; lst < 2; ++lst)
+            for (int p : (lst == 0 ? o.pgrids[t][c] : o.vpgrids[t][c])) {
+              const int itmp = P[p].flag;
+              if (label[itmp] != -1) continue;
+              if (is_neighbor(s, q, P[p], 1.0f)) {
+                label[itmp] = id;
+                ltmp.push_back(itmp);
+              }
+            }
+        }
+      }
+    }
+  }
+  id++;
+  std::vector<int> size(id, 0);
+  for (int l : label) ++size[l];
+  const int threshold = std::max(20, psize / 10000);
+  int count = 0;
+  for (int k = 0; k < psize; ++k) {
+    const int p = o.ppatches[k];
+    if (P[p].fix) continue;
+    if (size[label[k]] < threshold) {
+      remove_patch(o, P, p);
+      count++;
+    }
+  }
+  return count;
+}
+
+// CFilter::run (filter.cpp:13-27).  counts[0..3] = removed by outside/exact/neighbor/groups.
+static void filter_run(const OScene& s, std::vector<FPatch>& P, std::vector<int>& keep, int counts[4]) {
+  Organizer o(s);
+  OCtx ctx;
+  init_ctx(s, ctx);
+  for (int p = 0; p < (int)P.size(); ++p) add_patch_p(o, P, p);
+  set_dm_vgrids(o, P, 0);
+  counts[0] = filter_outside(o, P);
+  set_dm_vgrids(o, P, 1);
+  counts[1] = filter_exact(o, P, ctx);
+  set_dm_vgrids(o, P, 1);
+  counts[2] = filter_neighbor(o, P);
+  set_dm_vgrids(o, P, 1);
+  counts[3] = filter_small_groups(o, P);
+  set_dm_vgrids(o, P, 1);
+  collect_patches(o, P, 0);
+  keep.assign(P.size(), 0);
+  for (int p : o.ppatches) keep[p] = 1;
+}
+
+}  // namespace oracle

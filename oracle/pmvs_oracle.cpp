@@ -852,6 +852,8 @@ static void init_ctx(const OScene& s, OCtx& c) {
 
 }  // namespace oracle
 
+#include "filter_oracle.h"
+
 using namespace oracle;
 
 extern "C" {
@@ -1072,6 +1074,34 @@ int oracle_bobyqa_test(int kind, const double* x0, int maxeval, double* xout, do
   *fout = minf;
   *nrec = cnt;
   return rc;
+}
+
+// One CFilter::run pass (filter_oracle.h).  counts[4]: removed by outside/exact/neighbor/groups.
+void oracle_filter_run(void* h, pmvs_patch* patches, int n, int* keep, int* counts) {
+  const OScene& s = *static_cast<const OScene*>(h);
+  std::vector<FPatch> P(n);
+  for (int i = 0; i < n; ++i) {
+    const pmvs_patch& a = patches[i];
+    FPatch& q = P[i];
+    for (int k = 0; k < 4; ++k) { q.coord[k] = a.coord[k]; q.normal[k] = a.normal[k]; }
+    q.ncc = a.ncc; q.dscale = a.dscale; q.ascale = a.ascale; q.tmp = a.tmp;
+    q.timages = a.timages; q.flag = a.flag; q.fix = a.fix;
+    for (int k = 0; k < a.num_images; ++k) { q.images.push_back(a.images[k]); q.grids.push_back({a.grids[k][0], a.grids[k][1]}); }
+    for (int k = 0; k < a.num_vimages; ++k) { q.vimages.push_back(a.vimages[k]); q.vgrids.push_back({a.vgrids[k][0], a.vgrids[k][1]}); }
+  }
+  std::vector<int> kp;
+  filter_run(s, P, kp, counts);
+  for (int i = 0; i < n; ++i) {
+    pmvs_patch& a = patches[i];
+    const FPatch& q = P[i];
+    a.timages = q.timages;
+    a.flag = q.flag;
+    a.num_images = (int)std::min<size_t>(q.images.size(), PMVS_MAX_IMAGES);
+    for (int k = 0; k < a.num_images; ++k) { a.images[k] = q.images[k]; a.grids[k][0] = q.grids[k].first; a.grids[k][1] = q.grids[k].second; }
+    a.num_vimages = (int)std::min<size_t>(q.vimages.size(), PMVS_MAX_IMAGES);
+    for (int k = 0; k < a.num_vimages; ++k) { a.vimages[k] = q.vimages[k]; a.vgrids[k][0] = q.vgrids[k].first; a.vgrids[k][1] = q.vgrids[k].second; }
+    keep[i] = kp[i];
+  }
 }
 
 }  // extern "C"

@@ -44,6 +44,7 @@ def lib():
         L.oracle_paxes.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.oracle_incc_eval.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         L.oracle_refine_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.POINTER(P.Stats)]
+        L.oracle_filter_run.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         L.oracle_bobyqa_test.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_int, C.POINTER(C.c_int)]
         _lib = L
@@ -131,6 +132,14 @@ class OracleScene:
         enc = np.zeros((len(q), 3), np.float64) if want_encode else None
         lib().oracle_incc_eval(self.h, _p(q), len(q), _p(out), _p(enc))
         return (out, enc) if want_encode else out
+
+    def filter_run(self, patches):
+        """One CFilter::run pass; returns (patches_out, keep, counts[outside, exact, neighbor, groups])."""
+        pa = np.ascontiguousarray(patches, P.PATCH_DTYPE).copy()
+        keep = np.zeros(len(pa), np.int32)
+        counts = np.zeros(4, np.int32)
+        lib().oracle_filter_run(self.h, _p(pa), len(pa), _p(keep), _p(counts))
+        return pa, keep, counts
 
     def refine_batch(self, cands, nthreads=1):
         cands = np.ascontiguousarray(cands, P.CANDIDATE_DTYPE)

@@ -24,6 +24,11 @@ int main(void) {
   S(pmvs_tex_query); O(pmvs_tex_query, coord); O(pmvs_tex_query, pxaxis); O(pmvs_tex_query, pyaxis);
   O(pmvs_tex_query, normal); O(pmvs_tex_query, view); O(pmvs_tex_query, normalize);
   S(pmvs_stats); O(pmvs_stats, kernel_ms); O(pmvs_stats, tex_grabs);
+  S(pmvs_patch); O(pmvs_patch, ncc); O(pmvs_patch, timages); O(pmvs_patch, num_images); O(pmvs_patch, images);
+  O(pmvs_patch, grids); O(pmvs_patch, vimages); O(pmvs_patch, vgrids);
+  S(pmvs_filter_stats); O(pmvs_filter_stats, kernel_ms);
+  S(pmvs_options); O(pmvs_options, threshold); O(pmvs_options, num_timages); O(pmvs_options, timages);
+  O(pmvs_options, visdata2);
   S(pmvs_synth_params); O(pmvs_synth_params, seed); O(pmvs_synth_params, arc_step_deg);
   return 0;
 }

@@ -47,7 +47,8 @@ def test_python_mirror_layout_matches_c(tmp_path):
         c[k if rest[0] != "sizeof" else k + ".sizeof"] = int(rest[-1])
     import pmvs_amd as P
     np_types = {"pmvs_candidate": P.CANDIDATE_DTYPE, "pmvs_refined": P.REFINED_DTYPE,
-                "pmvs_eval_query": P.EVAL_QUERY_DTYPE, "pmvs_tex_query": P.TEX_QUERY_DTYPE}
+                "pmvs_eval_query": P.EVAL_QUERY_DTYPE, "pmvs_tex_query": P.TEX_QUERY_DTYPE,
+                "pmvs_patch": P.PATCH_DTYPE}
     for name, dt in np_types.items():
         assert dt.itemsize == c[name + ".sizeof"], name
         for f in dt.names:
@@ -55,7 +56,7 @@ def test_python_mirror_layout_matches_c(tmp_path):
             if key in c:
                 assert dt.fields[f][1] == c[key], key
     ct_types = {"pmvs_view_desc": P.ViewDesc, "pmvs_scene_desc": P.SceneDesc, "pmvs_stats": P.Stats,
-                "pmvs_synth_params": P.SynthParams}
+                "pmvs_synth_params": P.SynthParams, "pmvs_filter_stats": P.FilterStats, "pmvs_options": P.Options}
     for name, T in ct_types.items():
         assert C.sizeof(T) == c[name + ".sizeof"], name
         for f, _ in T._fields_:
