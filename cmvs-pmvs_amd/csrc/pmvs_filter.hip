@@ -23,6 +23,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <deque>
 #include <vector>
 
@@ -51,7 +53,12 @@ struct FilterDev {
   const int* rank;   // patch -> collect rank or -1
   int nalive;
   const float* unit0;  // getUnit(images[0], coord) per patch
+  long long ncells;
+  int npg, nvp;        // entries in the pgrids / vpgrids lists
+  int* err;            // [0] count, [1] first code (defensive bounds checks)
 };
+
+
 
 // --------------------------------------------------------------------------- small helpers
 __device__ __forceinline__ unsigned int depth_bits(float d) {
@@ -469,20 +476,49 @@ __device__ void lls5_wave(NbLds& L, double* M, double* r, int n) {
   __syncthreads();
 }
 
+// Sort a[0..n) ascending (bitonic over the next power of two, padded with INT_MAX) and drop
+// duplicates; returns the unique count.  All 64 lanes call it.
+__device__ int sort_unique_lds(int* a, int n, int* cnt_slot) {
+  const int lane = lane_id_w();
+  int N = 1;
+  while (N < n) N <<= 1;
+  for (int i = n + lane; i < N; i += 64) a[i] = 0x7fffffff;
+  __syncthreads();
+  for (int k = 2; k <= N; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = lane; i < N; i += 64) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const bool up = (i & k) == 0;
+          const int x = a[i], y = a[ixj];
+          if ((x > y) == up) { a[i] = y; a[ixj] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  if (lane == 0) {
+    int u = 0;
+    for (int i = 0; i < n; ++i)
+      if (u == 0 || a[i] != a[u - 1]) a[u++] = a[i];
+    *cnt_slot = u;
+  }
+  __syncthreads();
+  return *cnt_slot;
+}
+
 // CFilter::filterNeighborThread (filter.cpp:358-385) + findNeighbors(..., 0, 4, 2, 1)
 // (patchOrganizerS.cpp:527-631) + filterQuad (filter.cpp:387-446), one wavefront per patch.
 __global__ __launch_bounds__(64) void neighbor_kernel(DScene s, FilterDev F, double* __restrict__ scratch,
                                                       int* __restrict__ reject, int* __restrict__ overflow,
-                                                      int* __restrict__ queue) {
+                                                      int* __restrict__ queue, int* __restrict__ dbg_counts) {
   __shared__ NbLds L;
   const int lane = threadIdx.x;
   double* M = scratch + (size_t)blockIdx.x * NB_CAP * 6;
   double* r = M + (size_t)NB_CAP * 5;
   for (;;) {
-    if (lane == 0) L.cnt = atomicAdd(queue, 1);
-    __syncthreads();
-    const int i = L.cnt;
-    __syncthreads();
+    int i = 0;
+    if (lane == 0) i = atomicAdd(queue, 1);
+    i = __shfl(i, 0);  // work-queue index broadcast in registers
     if (i >= F.nalive) break;
     const int p = F.order[i];
     const pmvs_patch& q = F.P[p];
@@ -490,8 +526,10 @@ __global__ __launch_bounds__(64) void neighbor_kernel(DScene s, FilterDev F, dou
       if (lane == 0) reject[p] = 0;
       continue;
     }
+    __syncthreads();  // the previous patch's LDS reads are complete before L is reused
     // computeRadius: 2nd smallest of computeUnits (optim.cpp:446-471) times csize
-    const int ni = q.num_images;
+    int ni = q.num_images;
+    if (ni < 1 || ni > PMVS_MAX_IMAGES) { if (lane == 0) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 31); } ni = 1; }
     if (lane < ni) {
       const DView& v = s.views[q.images[lane]];
       float u = get_unit(s, v, q.coord);
@@ -529,17 +567,24 @@ __global__ __launch_bounds__(64) void neighbor_kernel(DScene s, FilterDev F, dou
           const int xt = q.grids[k][0] + dx;
           if (xt < 0 || gw <= xt) continue;
           const long long c = F.tgoff[t] + (long long)yt * gw + xt;
+          if (c < 0 || c >= F.ncells) { if (lane == 0) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 11); } continue; }
           for (int lst = 0; lst < 2; ++lst) {
             const int* off = lst ? F.vp_off : F.pg_off;
             const int* items = lst ? F.vp_items : F.pg_items;
-            const int b = off[c], e = off[c + 1];
+            const int lim = lst ? F.nvp : F.npg;
+            int b = off[c], e = off[c + 1];
+            if (b < 0 || e > lim || b > e) {
+              if (lane == 0) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 12 + lst); }
+              b = 0; e = 0;
+            }
             for (int base = b; base < e; base += 64) {
               const int idx = base + lane;
               bool hit = false;
               int j = 0;
               if (idx < e) {
                 j = items[idx];
-                hit = is_neighbor_h(q, F.P[j], unit, thr, radius, true) != 0;
+                if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 14); j = 0; }
+                else hit = is_neighbor_h(q, F.P[j], unit, thr, radius, true) != 0;
               }
               const unsigned long long mask = __ballot(hit);
               const int before = __popcll(mask & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
@@ -551,29 +596,24 @@ __global__ __launch_bounds__(64) void neighbor_kernel(DScene s, FilterDev F, dou
               __syncthreads();
               if (lane == 0) L.cnt += __popcll(mask);
               __syncthreads();
+              // duplicates (one entry per image/cell registration) are compacted when the
+              // buffer fills; the reference sorts and uniques once at the end (same set)
+              if (L.cnt > NB_CAP - 64 && !L.overflow) sort_unique_lds(L.nb, imin(L.cnt, NB_CAP), &L.cnt);
             }
           }
         }
       }
     }
     int n = L.cnt < NB_CAP ? L.cnt : NB_CAP;
-    // sort ascending (odd-even transposition over the wave), then unique
-    for (int pass = 0; pass < n; ++pass) {
-      for (int a = 2 * lane + (pass & 1); a + 1 < n; a += 128) {
-        const int x0 = L.nb[a], x1 = L.nb[a + 1];
-        if (x1 < x0) { L.nb[a] = x1; L.nb[a + 1] = x0; }
-      }
-      __syncthreads();
-    }
-    if (lane == 0) {
-      int u = 0;
-      for (int a = 0; a < n; ++a)
-        if (u == 0 || L.nb[a] != L.nb[u - 1]) L.nb[u++] = L.nb[a];
-      L.cnt = u;
-      if (L.overflow) atomicAdd(overflow, 1);
-    }
+    n = sort_unique_lds(L.nb, n, &L.cnt);
+    if (lane == 0 && L.overflow) atomicAdd(overflow, 1);
+    if (lane == 0 && dbg_counts) dbg_counts[p] = L.overflow ? -n : n;
     __syncthreads();
     n = L.cnt;
+    if (n > NB_CAP || n < 0) { if (lane == 0) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 21); } n = 0; }
+    for (int a = lane; a < n; a += 64)
+      if (L.nb[a] < 0 || L.nb[a] >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 22); L.nb[a] = p; }
+    __syncthreads();
     int rej = 0;
     if (n < 6) {
       rej = 1;
@@ -683,6 +723,14 @@ __global__ void group_edges_kernel(DScene s, FilterDev F, int pass, const int* _
 
 static inline unsigned nblk(long long n, int b = 256) { return (unsigned)((n + b - 1) / b); }
 
+static void dbg(hipStream_t st, const char* what) {
+  static const bool on = getenv("PMVS_FILTER_DEBUG") != nullptr;
+  if (!on) return;
+  const hipError_t e = hipStreamSynchronize(st);
+  fprintf(stderr, "[filter] %s: %s\n", what, hipGetErrorString(e));
+  fflush(stderr);
+}
+
 template <class T>
 static hipError_t dalloc(T*& p, size_t n) {
   if (p) (void)hipFree(p);
@@ -734,12 +782,13 @@ struct Ctx {
   long long ncells;
   int grid;
   hipStream_t st;
-  int nalive = 0;
+  int nalive = 0, npg = 0, nvp = 0;
   FilterDev dev() const {
     FilterDev F{};
     F.P = P; F.n = n; F.preg = B.preg; F.vreg = B.vreg; F.tgoff = B.tgoff; F.tnum = s.tnum;
     F.pg_off = B.pg_off; F.pg_items = B.pg_items; F.vp_off = B.vp_off; F.vp_items = B.vp_items;
     F.dpkey = B.dpkey; F.order = B.order; F.rank = B.rank; F.nalive = nalive; F.unit0 = B.unit0;
+    F.ncells = ncells; F.npg = npg; F.nvp = nvp; F.err = B.counters + 6;
     return F;
   }
 };
@@ -761,6 +810,7 @@ static hipError_t build_lists(Ctx& c, int vis) {
   FCHK(hipcub::DeviceScan::ExclusiveSum(B.temp, tb, B.cnt, B.off, c.n + 1, c.st));
   int e = 0;
   FCHK(read_int(B.off + c.n, &e, c.st));
+  (vis ? c.nvp : c.npg) = e;
   hipLaunchKernelGGL(emit_entries_kernel, dim3(nblk(c.n)), dim3(256), 0, c.st, c.s, c.P, c.n, reg, vis, B.off, B.tgoff,
                      B.keys);
   tb = B.temp_bytes;
@@ -795,15 +845,20 @@ static hipError_t collect(Ctx& c) {
 static hipError_t set_dm_vgrids(Ctx& c, int additive) {
   FilterBuffers& B = c.B;
   FCHK(build_lists(c, 0));
+  dbg(c.st, "  lists");
   FCHK(collect(c));
+  dbg(c.st, "  collect");
   FCHK(hipMemsetAsync(B.dpkey, 0xff, c.ncells * sizeof(unsigned long long), c.st));
   if (c.nalive > 0)
     hipLaunchKernelGGL(depth_map_kernel, dim3(nblk((long long)c.nalive * c.s.tnum)), dim3(256), 0, c.st, c.s, c.dev(),
                        B.dpkey);
+  dbg(c.st, "  depth");
   FCHK(hipMemsetAsync(B.vreg, 0, c.n * sizeof(unsigned long long), c.st));
   if (c.nalive > 0)
     hipLaunchKernelGGL(vimages_kernel, dim3(nblk(c.nalive)), dim3(256), 0, c.st, c.s, c.dev(), additive, B.vreg);
+  dbg(c.st, "  vimages");
   FCHK(build_lists(c, 1));
+  dbg(c.st, "  vlists");
   return hipGetLastError();
 }
 
@@ -819,17 +874,21 @@ static hipError_t apply_flags(Ctx& c, int* removed) {
 
 hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n, long long ncells, const long long* h_tgoff,
                        int grid, hipStream_t st, int counts[4], int* overflow, int* keep_dev) {
+  dbg(st, "start");
   FCHK(B.reserve(n, ncells, s.tnum, grid));
+  dbg(st, "reserve");
   FCHK(hipMemcpyAsync(B.tgoff, h_tgoff, (s.tnum + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
   Ctx c{s, B, dP, n, ncells, grid, st};
   for (int k = 0; k < 4; ++k) counts[k] = 0;
   *overflow = 0;
   hipLaunchKernelGGL(init_reg_kernel, dim3(nblk(n)), dim3(256), 0, st, s, dP, n, B.preg, B.vreg);
   FCHK(set_dm_vgrids(c, 0));
+  dbg(st, "set_dm_vgrids(0)");
   // ---- filterOutside
   FCHK(hipMemsetAsync(B.flags, 0, n * sizeof(int), st));
   if (c.nalive) hipLaunchKernelGGL(gain_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, s, c.dev(), B.flags);
   FCHK(apply_flags(c, &counts[0]));
+  dbg(st, "outside");
   FCHK(set_dm_vgrids(c, 1));
   // ---- filterExact
   FCHK(hipMemsetAsync(B.safe, 0, n * sizeof(unsigned long long), st));
@@ -855,14 +914,38 @@ hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n,
     }
     FCHK(read_int(B.counters + 2, &counts[1], st));
   }
+  dbg(st, "exact");
   FCHK(set_dm_vgrids(c, 1));
+  dbg(st, "set_dm_vgrids(1) after exact");
   // ---- filterNeighbor(1)
   FCHK(hipMemsetAsync(B.flags, 0, n * sizeof(int), st));
-  FCHK(hipMemsetAsync(B.counters + 3, 0, 2 * sizeof(int), st));
+  FCHK(hipMemsetAsync(B.counters + 3, 0, 5 * sizeof(int), st));
   if (c.nalive)
     hipLaunchKernelGGL(neighbor_kernel, dim3(std::min(grid, c.nalive)), dim3(64), 0, st, s, c.dev(), B.scratch, B.flags,
-                       B.counters + 3, B.counters + 4);
+                       B.counters + 3, B.counters + 4, getenv("PMVS_FILTER_DEBUG") ? B.need : nullptr);
+  dbg(st, "neighbor kernel");
+  if (getenv("PMVS_FILTER_DEBUG")) {
+    std::vector<int> cnts(n), ord(c.nalive);
+    (void)hipMemcpy(cnts.data(), B.need, n * sizeof(int), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(ord.data(), B.order, c.nalive * sizeof(int), hipMemcpyDeviceToHost);
+    int mx = 0, ov = 0;
+    for (int k = 0; k < c.nalive; ++k) {
+      const int v = cnts[ord[k]];
+      if (v < 0) ++ov;
+      mx = std::max(mx, v < 0 ? -v : v);
+    }
+    fprintf(stderr, "[filter] neighbours: max unique %d, overflowed %d of %d; first: %d %d %d\n", mx, ov, c.nalive,
+            cnts[ord[0]], c.nalive > 1 ? cnts[ord[1]] : 0, c.nalive > 2 ? cnts[ord[2]] : 0);
+  }
   FCHK(read_int(B.counters + 3, overflow, st));
+  {
+    int errs[2] = {0, 0};
+    FCHK(hipMemcpy(errs, B.counters + 6, 2 * sizeof(int), hipMemcpyDeviceToHost));
+    if (errs[0]) {
+      fprintf(stderr, "[filter] neighbor kernel bounds violations: %d (first code %d)\n", errs[0], errs[1]);
+      return hipErrorIllegalAddress;
+    }
+  }
   FCHK(apply_flags(c, &counts[2]));
   FCHK(set_dm_vgrids(c, 1));
   // ---- filterSmallGroups
@@ -916,6 +999,7 @@ hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n,
     hipLaunchKernelGGL(clear_fixed_kernel, dim3(nblk(n)), dim3(256), 0, st, dP, n, B.flags);
     FCHK(apply_flags(c, &counts[3]));
   }
+  dbg(st, "groups");
   FCHK(set_dm_vgrids(c, 1));
   FCHK(build_lists(c, 0));
   FCHK(collect(c));

@@ -1104,4 +1104,28 @@ void oracle_filter_run(void* h, pmvs_patch* patches, int n, int* keep, int* coun
   }
 }
 
+// Diagnostic: filterNeighbor's neighbour-list sizes (raw with duplicates, unique) on the
+// organizer state right before filterNeighbor in a pass that skips outside/exact.
+void oracle_neighbor_sizes(void* h, pmvs_patch* patches, int n, int* raw, int* uniq) {
+  const OScene& s = *static_cast<const OScene*>(h);
+  std::vector<FPatch> P(n);
+  for (int i = 0; i < n; ++i) {
+    const pmvs_patch& a = patches[i];
+    FPatch& q = P[i];
+    for (int k = 0; k < 4; ++k) { q.coord[k] = a.coord[k]; q.normal[k] = a.normal[k]; }
+    q.ncc = a.ncc; q.dscale = a.dscale; q.ascale = a.ascale; q.tmp = a.tmp;
+    q.timages = a.timages; q.flag = a.flag; q.fix = a.fix;
+    for (int k = 0; k < a.num_images; ++k) { q.images.push_back(a.images[k]); q.grids.push_back({a.grids[k][0], a.grids[k][1]}); }
+  }
+  Organizer o(s);
+  for (int p = 0; p < n; ++p) add_patch_p(o, P, p);
+  set_dm_vgrids(o, P, 0);
+  for (int p = 0; p < n; ++p) {
+    std::vector<int> nb;
+    find_neighbors(o, P, P[p], nb, 4.0f, 2, 1);
+    uniq[p] = (int)nb.size();
+    raw[p] = 0;
+  }
+}
+
 }  // extern "C"

@@ -51,7 +51,7 @@ def compare(out_g, keep_g, st_g, out_o, keep_o, counts_o):
 
 
 @pytest.mark.parametrize("cfg", [dict(views=8, w=960, h=540, level=1, n=100000, seed=5),
-                                 dict(views=6, w=640, h=480, level=2, n=40000, seed=6, csize=4)],
+                                 dict(views=6, w=640, h=480, level=2, n=4000, seed=6, csize=4)],
                          ids=["ring8_level1", "ring6_level2_c4"])
 def test_filter_pass_matches_oracle(gpu_available, oracle_mod, cfg):
     import pmvs_amd as P
