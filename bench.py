@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-filter", action="store_true", help="skip the filter-pass side measurement")
     return ap.parse_args()
 
 
@@ -142,6 +143,20 @@ def main():
     bytes_per_launch = tex_valid / args.steps * BYTES_PER_TEXTURE
     achieved = bytes_per_launch / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
 
+    # ---- side measurement: one CFilter::run pass (depth 1) over this rank's refined patches
+    filt = None
+    if not args.no_filter:
+        res = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=P.REFINED_DTYPE)
+        patches = P.patches_from_refined(res)
+        scene.set_thresholds(0.7, 0.4, 1)
+        t0 = time.perf_counter()
+        _, keep, fst = scene.filter_run(patches)
+        tf = time.perf_counter() - t0
+        scene.set_thresholds(0.7, 0.4, 0)
+        filt = {"patches": int(len(patches)), "kept": int(fst["kept"]), "device_ms": round(fst["kernel_ms"], 3),
+                "wall_ms": round(tf * 1e3, 3), "patches_per_s": round(len(patches) / (fst["kernel_ms"] / 1e3), 1),
+                "removed": [int(fst[k]) for k in ("removed_outside", "removed_exact", "removed_neighbor",
+                                                  "removed_groups")]}
     traffic, traffic_src = pmc_traffic(args)
     result = None
     if rank == 0:
@@ -193,6 +208,7 @@ def main():
                          "algorithmic_bytes_per_launch": int(bytes_per_launch),
                          "traffic_source": traffic_src},
             "stage_ms": stage_ms,
+            "filter_pass": filt,
             "cpu_baseline": cpu,
             "setup_s": {"synth": round(t_synth, 2)},
             "refine_profile": {"optimizer_cycle_frac": round(prof["opt_cycles"] / max(1, prof["opt_cycles"] + prof["objective_cycles"]), 4),
