@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -181,6 +182,7 @@ struct pmvs_scene {
   DBuf<DevStats> stats;
   DBuf<RefineJob> jobs;
   FilterBuffers fbuf;
+  ExpandBuffers xbuf;
   DBuf<pmvs_patch> fpatches;
   DBuf<int> fkeep;
   int grid = 0, refine_grid = 0, tslots = 1608;
@@ -694,6 +696,67 @@ pmvs_status pmvs_filter_run(pmvs_scene* sc, pmvs_patch* patches, int32_t n, int3
     for (int i = 0; i < n; ++i) k += keep[i];
     stats->kept = k;
     stats->kernel_ms = ms;
+  }
+  sc->last_refine = false;
+  return PMVS_OK;
+}
+
+pmvs_status pmvs_expand_run(pmvs_scene* sc, const pmvs_patch* patches, const int32_t* alive, int32_t n, int32_t wave,
+                            int32_t count_threshold, pmvs_patch* out, int32_t* alive_out, int32_t cap, int32_t* n_out,
+                            pmvs_expand_stats* stats) {
+  if (!sc || n < 0 || (n > 0 && (!patches || !alive)) || !out || !alive_out || !n_out || cap < n)
+    return fail(PMVS_EINVAL, "invalid argument");
+  if (wave < 1 || wave > kMaxWave) return fail(PMVS_EINVAL, "wave must be in [1, %d]", kMaxWave);
+  if (sc->ds.tnum > 64) return fail(PMVS_EUNSUPPORTED, "expansion: more than 64 target images");
+  for (int i = 0; i < n; ++i) {
+    const pmvs_patch& p = patches[i];
+    if (p.num_images < 1 || p.num_images > PMVS_MAX_IMAGES || p.num_vimages < 0 || p.num_vimages > PMVS_MAX_IMAGES)
+      return fail(PMVS_EINVAL, "patch %d: image counts", i);
+    for (int k = 0; k < p.num_images; ++k)
+      if (p.images[k] < 0 || p.images[k] >= sc->ds.num) return fail(PMVS_EINVAL, "patch %d: image %d", i, p.images[k]);
+    for (int k = 0; k < p.num_vimages; ++k)
+      if (p.vimages[k] < 0 || p.vimages[k] >= sc->ds.tnum) return fail(PMVS_EINVAL, "patch %d: vimage", i);
+  }
+  if (stats) std::memset(stats, 0, sizeof(*stats));
+  *n_out = 0;
+  if (n == 0) return PMVS_OK;
+  HIPCHK(hipSetDevice(sc->device));
+  pmvs_status st;
+  if ((st = ensure(sc->fpatches, cap))) return st;
+  std::vector<long long> tgoff(sc->ds.tnum + 1, 0);
+  sc->xbuf.gw.assign(sc->ds.tnum, 0);
+  sc->xbuf.gh.assign(sc->ds.tnum, 0);
+  for (int t = 0; t < sc->ds.tnum; ++t) {
+    const DView& v = sc->hviews[t];
+    sc->xbuf.gw[t] = (v.w[sc->ds.level] + sc->ds.csize - 1) / sc->ds.csize;
+    sc->xbuf.gh[t] = (v.h[sc->ds.level] + sc->ds.csize - 1) / sc->ds.csize;
+    tgoff[t + 1] = tgoff[t] + (long long)sc->xbuf.gw[t] * sc->xbuf.gh[t];
+  }
+  std::vector<pmvs_patch> H(patches, patches + n);
+  std::vector<int> al(alive, alive + n);
+  RefineFn refine = [sc](const pmvs_candidate* d_in, int m, pmvs_refined* d_out) -> hipError_t {
+    if (ensure(sc->jobs, m)) return hipErrorOutOfMemory;
+    hipError_t e = hipMemsetAsync(sc->stats.p, 0, sizeof(DevStats), sc->stream);
+    if (e != hipSuccess) return e;
+    return launch_refine(sc->ds, d_in, sc->jobs.p, d_out, m, sc->stats.p, sc->grid, sc->refine_grid, sc->tslots,
+                         sc->stream, sc->kev);
+  };
+  long long sv[8];
+  const auto t0 = std::chrono::steady_clock::now();
+  const hipError_t e = expand_pass(sc->ds, sc->fbuf, sc->xbuf, sc->fpatches.p, H, al, cap, tgoff[sc->ds.tnum],
+                                   tgoff.data(), wave, count_threshold, sc->grid, sc->stream, refine, sv);
+  if (e == hipErrorOutOfMemory)
+    return fail(PMVS_EUNSUPPORTED, "expansion: capacity %d exceeded or a patch has more than 1024 neighbours", cap);
+  HIPCHK(e);
+  HIPCHK(hipStreamSynchronize(sc->stream));
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  std::memcpy(out, H.data(), H.size() * sizeof(pmvs_patch));
+  std::memcpy(alive_out, al.data(), al.size() * sizeof(int));
+  *n_out = (int32_t)H.size();
+  if (stats) {
+    stats->parents = sv[0]; stats->candidates = sv[1]; stats->fail_prep = sv[2]; stats->fail_pre = sv[3];
+    stats->fail_post = sv[4]; stats->fail_commit = sv[5]; stats->added = sv[6]; stats->waves = sv[7];
+    stats->wall_ms = ms;
   }
   sc->last_refine = false;
   return PMVS_OK;

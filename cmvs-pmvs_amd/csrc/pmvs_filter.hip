@@ -26,6 +26,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <deque>
+#include <functional>
+#include <queue>
 #include <vector>
 
 #include "pmvs_device.h"
@@ -96,13 +98,13 @@ __device__ int is_neighbor(const DScene& s, const FilterDev& F, int a, int b, fl
 }
 
 // CPatchOrganizerS::isVisible (patchOrganizerS.cpp:500-525).
-__device__ int is_visible(const DScene& s, const FilterDev& F, int p, int t, int ix, int iy, float strict) {
+__device__ int is_visible_q(const DScene& s, const FilterDev& F, const pmvs_patch& q, int t, int ix, int iy,
+                             float strict) {
   if (!in_grid(s, t, ix, iy)) return 0;
   if (s.depth == 0) return 1;
   const unsigned long long key = F.dpkey[F.tgoff[t] + (long long)iy * gwidth(s, t) + ix];
   if (key == ~0ull) return 1;
   const int d = F.order[(int)(key & 0xffffffffull)];
-  const pmvs_patch& q = F.P[p];
   const DView& v = s.views[t];
   float ray[4] = {q.coord[0] - v.center[0], q.coord[1] - v.center[1], q.coord[2] - v.center[2], q.coord[3] - v.center[3]};
   unitize4(ray);
@@ -112,6 +114,9 @@ __device__ int is_visible(const DScene& s, const FilterDev& F, int p, int t, int
   const double fd = 2.0 + (double)dot4(ray, q.normal);
   const float factor = (float)((fd < 2.0) ? fd : 2.0);  // std::min(2.0, .)
   return diff < get_unit(s, v, q.coord) * (float)s.csize * strict * factor ? 1 : 0;
+}
+__device__ int is_visible(const DScene& s, const FilterDev& F, int p, int t, int ix, int iy, float strict) {
+  return is_visible_q(s, F, F.P[p], t, ix, iy, strict);
 }
 
 // --------------------------------------------------------------------------- organizer build
@@ -508,6 +513,160 @@ __device__ int sort_unique_lds(int* a, int n, int* cnt_slot) {
 
 // CFilter::filterNeighborThread (filter.cpp:358-385) + findNeighbors(..., 0, 4, 2, 1)
 // (patchOrganizerS.cpp:527-631) + filterQuad (filter.cpp:387-446), one wavefront per patch.
+// CExpand::computeRadius (expand.cpp:182-198): second smallest of COptim::computeUnits
+// (optim.cpp:446-471) times csize.  All lanes call; result in every lane.
+__device__ float compute_radius_wave(const DScene& s, NbLds& L, const pmvs_patch& q) {
+  const int lane = lane_id_w();
+  const int ni = q.num_images;
+  __syncthreads();
+  if (lane < ni) {
+    const DView& v = s.views[q.images[lane]];
+    float u = get_unit(s, v, q.coord);
+    float ray[4] = {v.center[0] - q.coord[0], v.center[1] - q.coord[1], v.center[2] - q.coord[2], v.center[3] - q.coord[3]};
+    unitize4(ray);
+    const float den = dot4(ray, q.normal);
+    u = (0.0f < den) ? __fdiv_rn(u, den) : 1073741824.0f;
+    L.units[lane] = u;
+  }
+  __syncthreads();
+  float m1 = 3.0e38f, m2 = 3.0e38f;  // two smallest (nth_element(begin, begin + 1, end))
+  for (int k = 0; k < ni; ++k) {
+    const float u = L.units[k];
+    if (u < m1) { m2 = m1; m1 = u; }
+    else if (u < m2) m2 = u;
+  }
+  return m2 * (float)s.csize;
+}
+
+// CPatchOrganizerS::findNeighbors(patch, neighbors, lock, scale, margin, skipvis)
+// (patchOrganizerS.cpp:527-631) into L.nb[0..n), sorted by patch index and unique.  Returns n;
+// L.overflow is set when more than NB_CAP unique neighbours exist.
+__device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, const pmvs_patch& q, float scale,
+                                int margin, int skipvis) {
+  const int lane = lane_id_w();
+  const int ni = q.num_images;
+  const float radius = (float)(1.5 * margin * (double)compute_radius_wave(s, L, q));
+  float unit = 0.0f;
+  for (int k = 0; k < ni; ++k) unit += get_unit(s, s.views[q.images[k]], q.coord);
+  unit = __fdiv_rn(unit, (float)ni);
+  unit *= (float)s.csize;
+  const float thr = 0.5f * scale;
+  if (lane == 0) { L.cnt = 0; L.overflow = 0; }
+  __syncthreads();
+  const int nlists = skipvis ? ni : ni + q.num_vimages;
+  for (int k = 0; k < nlists; ++k) {
+    const bool vis = k >= ni;
+    const int t = vis ? q.vimages[k - ni] : q.images[k];
+    if (s.tnum <= t) continue;
+    const int gx = vis ? q.vgrids[k - ni][0] : q.grids[k][0];
+    const int gy = vis ? q.vgrids[k - ni][1] : q.grids[k][1];
+    const int gw = gwidth(s, t), gh = gheight(s, t);
+    for (int dy = -margin; dy <= margin; ++dy) {
+      const int yt = gy + dy;
+      if (yt < 0 || gh <= yt) continue;
+      for (int dx = -margin; dx <= margin; ++dx) {
+        const int xt = gx + dx;
+        if (xt < 0 || gw <= xt) continue;
+        const long long c = F.tgoff[t] + (long long)yt * gw + xt;
+        for (int lst = 0; lst < 2; ++lst) {
+          const int* off = lst ? F.vp_off : F.pg_off;
+          const int* items = lst ? F.vp_items : F.pg_items;
+          const int lim = lst ? F.nvp : F.npg;
+          int b = off[c], e = off[c + 1];
+          if (b < 0 || e > lim || b > e) {
+            if (lane == 0) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 12 + lst); }
+            b = 0; e = 0;
+          }
+          for (int base = b; base < e; base += 64) {
+            const int idx = base + lane;
+            bool hit = false;
+            int j = 0;
+            if (idx < e) {
+              j = items[idx];
+              if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 14); j = 0; }
+              else hit = is_neighbor_h(q, F.P[j], unit, thr, radius, true) != 0;
+            }
+            const unsigned long long mask = __ballot(hit);
+            const int before = __popcll(mask & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+            const int pos = L.cnt + before;
+            if (hit) {
+              if (pos < NB_CAP) L.nb[pos] = j;
+              else L.overflow = 1;
+            }
+            __syncthreads();
+            if (lane == 0) L.cnt += __popcll(mask);
+            __syncthreads();
+            // duplicates (one entry per image/cell registration) are compacted when the buffer
+            // fills; the reference sorts and uniques once at the end (same set)
+            if (L.cnt > NB_CAP - 64 && !L.overflow) sort_unique_lds(L.nb, imin(L.cnt, NB_CAP), &L.cnt);
+          }
+        }
+      }
+    }
+  }
+  const int n = L.cnt < NB_CAP ? L.cnt : NB_CAP;
+  return sort_unique_lds(L.nb, n, &L.cnt);
+}
+
+// CFilter::filterQuad (filter.cpp:387-446) on the neighbours in L.nb[0..n); returns 1 = reject.
+__device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, double* M, double* r,
+                                const pmvs_patch& q, int n) {
+  const int lane = lane_id_w();
+  float xdir[4] = {0, 0, 0, 0}, ydir[4] = {0, 0, 0, 0};
+  const float* z = q.normal;
+  if (fabs((double)z[0]) > 0.5) { xdir[0] = z[1]; xdir[1] = -z[0]; xdir[2] = 0; }
+  else if (fabs((double)z[1]) > 0.5) { xdir[1] = z[2]; xdir[2] = -z[1]; xdir[0] = 0; }
+  else { xdir[2] = z[0]; xdir[0] = -z[2]; xdir[1] = 0; }
+  unitize4(xdir);
+  ydir[0] = z[1] * xdir[2] - z[2] * xdir[1];
+  ydir[1] = z[2] * xdir[0] - z[0] * xdir[2];
+  ydir[2] = z[0] * xdir[1] - z[1] * xdir[0];
+  if (lane == 0) {
+    float h = 0.0f;
+    for (int a = 0; a < n; ++a) {
+      float d[4];
+      for (int k = 0; k < 4; ++k) d[k] = F.P[L.nb[a]].coord[k] - q.coord[k];
+      h += norm4(d);
+    }
+    L.f[1] = (double)__fdiv_rn(h, (float)n);
+  }
+  __syncthreads();
+  const float h = (float)L.f[1];
+  for (int a = lane; a < n; a += 64) {
+    float d[4];
+    for (int k = 0; k < 4; ++k) d[k] = F.P[L.nb[a]].coord[k] - q.coord[k];
+    const float fx = __fdiv_rn(dot4(d, xdir), h), fy = __fdiv_rn(dot4(d, ydir), h), fz = dot4(d, q.normal);
+    L.fx[a] = fx; L.fy[a] = fy; L.fz[a] = fz;
+    M[(size_t)a * 5 + 0] = (double)(fx * fx);
+    M[(size_t)a * 5 + 1] = (double)(fy * fy);
+    M[(size_t)a * 5 + 2] = (double)(fx * fy);
+    M[(size_t)a * 5 + 3] = (double)fx;
+    M[(size_t)a * 5 + 4] = (double)fy;
+    r[a] = (double)fz;
+  }
+  __threadfence_block();
+  __syncthreads();
+  lls5_wave(L, M, r, n);
+  if (lane == 0) {
+    const int inum = imin(s.tau, q.num_images);
+    float u2 = 0.0f;
+    for (int k = 0; k < inum; ++k) u2 += get_unit(s, s.views[q.images[k]], q.coord);
+    u2 = __fdiv_rn(u2, (float)inum);
+    float residual = 0.0f;
+    for (int a = 0; a < n; ++a) {
+      const float fx = L.fx[a], fy = L.fy[a];
+      const float res = L.x[0] * (fx * fx) + L.x[1] * (fy * fy) + L.x[2] * (fx * fy) + L.x[3] * fx + L.x[4] * fy - L.fz[a];
+      residual = (float)((double)residual + fabs((double)res) / (double)u2);  // float += double
+    }
+    residual = __fdiv_rn(residual, (float)(n - 5));
+    L.cnt = (residual < s.quad ? 0 : 1);
+  }
+  __syncthreads();
+  return L.cnt;
+}
+
+// CFilter::filterNeighborThread (filter.cpp:358-385): findNeighbors(patch, ., 0, 4, 2, 1), reject
+// with fewer than 6 neighbours or a failed quadric fit.  One wavefront per patch.
 __global__ __launch_bounds__(64) void neighbor_kernel(DScene s, FilterDev F, double* __restrict__ scratch,
                                                       int* __restrict__ reject, int* __restrict__ overflow,
                                                       int* __restrict__ queue, int* __restrict__ dbg_counts) {
@@ -526,151 +685,10 @@ __global__ __launch_bounds__(64) void neighbor_kernel(DScene s, FilterDev F, dou
       if (lane == 0) reject[p] = 0;
       continue;
     }
-    __syncthreads();  // the previous patch's LDS reads are complete before L is reused
-    // computeRadius: 2nd smallest of computeUnits (optim.cpp:446-471) times csize
-    int ni = q.num_images;
-    if (ni < 1 || ni > PMVS_MAX_IMAGES) { if (lane == 0) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 31); } ni = 1; }
-    if (lane < ni) {
-      const DView& v = s.views[q.images[lane]];
-      float u = get_unit(s, v, q.coord);
-      float ray[4] = {v.center[0] - q.coord[0], v.center[1] - q.coord[1], v.center[2] - q.coord[2], v.center[3] - q.coord[3]};
-      unitize4(ray);
-      const float den = dot4(ray, q.normal);
-      u = (0.0f < den) ? __fdiv_rn(u, den) : 1073741824.0f;
-      L.units[lane] = u;
-    }
-    if (lane == 0) { L.cnt = 0; L.overflow = 0; }
-    __syncthreads();
-    float radius = 0.0f, unit = 0.0f;
-    {
-      float m1 = 3.0e38f, m2 = 3.0e38f;  // two smallest (nth_element(begin, begin + 1, end))
-      for (int k = 0; k < ni; ++k) {
-        const float u = L.units[k];
-        if (u < m1) { m2 = m1; m1 = u; }
-        else if (u < m2) m2 = u;
-      }
-      radius = (float)(1.5 * 2 * (double)(m2 * (float)s.csize));
-      for (int k = 0; k < ni; ++k) unit += get_unit(s, s.views[q.images[k]], q.coord);
-      unit = __fdiv_rn(unit, (float)ni);
-      unit *= (float)s.csize;
-    }
-    const float thr = 0.5f * 4.0f;
-    // gather: target entries of images[], 5x5 cells, pgrids then vpgrids
-    for (int k = 0; k < ni; ++k) {
-      const int t = q.images[k];
-      if (s.tnum <= t) continue;
-      const int gw = gwidth(s, t), gh = gheight(s, t);
-      for (int dy = -2; dy <= 2; ++dy) {
-        const int yt = q.grids[k][1] + dy;
-        if (yt < 0 || gh <= yt) continue;
-        for (int dx = -2; dx <= 2; ++dx) {
-          const int xt = q.grids[k][0] + dx;
-          if (xt < 0 || gw <= xt) continue;
-          const long long c = F.tgoff[t] + (long long)yt * gw + xt;
-          if (c < 0 || c >= F.ncells) { if (lane == 0) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 11); } continue; }
-          for (int lst = 0; lst < 2; ++lst) {
-            const int* off = lst ? F.vp_off : F.pg_off;
-            const int* items = lst ? F.vp_items : F.pg_items;
-            const int lim = lst ? F.nvp : F.npg;
-            int b = off[c], e = off[c + 1];
-            if (b < 0 || e > lim || b > e) {
-              if (lane == 0) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 12 + lst); }
-              b = 0; e = 0;
-            }
-            for (int base = b; base < e; base += 64) {
-              const int idx = base + lane;
-              bool hit = false;
-              int j = 0;
-              if (idx < e) {
-                j = items[idx];
-                if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 14); j = 0; }
-                else hit = is_neighbor_h(q, F.P[j], unit, thr, radius, true) != 0;
-              }
-              const unsigned long long mask = __ballot(hit);
-              const int before = __popcll(mask & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
-              const int pos = L.cnt + before;
-              if (hit) {
-                if (pos < NB_CAP) L.nb[pos] = j;
-                else L.overflow = 1;
-              }
-              __syncthreads();
-              if (lane == 0) L.cnt += __popcll(mask);
-              __syncthreads();
-              // duplicates (one entry per image/cell registration) are compacted when the
-              // buffer fills; the reference sorts and uniques once at the end (same set)
-              if (L.cnt > NB_CAP - 64 && !L.overflow) sort_unique_lds(L.nb, imin(L.cnt, NB_CAP), &L.cnt);
-            }
-          }
-        }
-      }
-    }
-    int n = L.cnt < NB_CAP ? L.cnt : NB_CAP;
-    n = sort_unique_lds(L.nb, n, &L.cnt);
+    const int n = gather_neighbors(s, F, L, q, 4.0f, 2, 1);
     if (lane == 0 && L.overflow) atomicAdd(overflow, 1);
     if (lane == 0 && dbg_counts) dbg_counts[p] = L.overflow ? -n : n;
-    __syncthreads();
-    n = L.cnt;
-    if (n > NB_CAP || n < 0) { if (lane == 0) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 21); } n = 0; }
-    for (int a = lane; a < n; a += 64)
-      if (L.nb[a] < 0 || L.nb[a] >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 22); L.nb[a] = p; }
-    __syncthreads();
-    int rej = 0;
-    if (n < 6) {
-      rej = 1;
-    } else {
-      // filterQuad (filter.cpp:387-446)
-      float xdir[4] = {0, 0, 0, 0}, ydir[4] = {0, 0, 0, 0};
-      const float* z = q.normal;
-      if (fabs((double)z[0]) > 0.5) { xdir[0] = z[1]; xdir[1] = -z[0]; xdir[2] = 0; }
-      else if (fabs((double)z[1]) > 0.5) { xdir[1] = z[2]; xdir[2] = -z[1]; xdir[0] = 0; }
-      else { xdir[2] = z[0]; xdir[0] = -z[2]; xdir[1] = 0; }
-      unitize4(xdir);
-      ydir[0] = z[1] * xdir[2] - z[2] * xdir[1];
-      ydir[1] = z[2] * xdir[0] - z[0] * xdir[2];
-      ydir[2] = z[0] * xdir[1] - z[1] * xdir[0];
-      if (lane == 0) {
-        float h = 0.0f;
-        for (int a = 0; a < n; ++a) {
-          float d[4];
-          for (int k = 0; k < 4; ++k) d[k] = F.P[L.nb[a]].coord[k] - q.coord[k];
-          h += norm4(d);
-        }
-        L.f[1] = (double)__fdiv_rn(h, (float)n);
-      }
-      __syncthreads();
-      const float h = (float)L.f[1];
-      for (int a = lane; a < n; a += 64) {
-        float d[4];
-        for (int k = 0; k < 4; ++k) d[k] = F.P[L.nb[a]].coord[k] - q.coord[k];
-        const float fx = __fdiv_rn(dot4(d, xdir), h), fy = __fdiv_rn(dot4(d, ydir), h), fz = dot4(d, q.normal);
-        L.fx[a] = fx; L.fy[a] = fy; L.fz[a] = fz;
-        M[(size_t)a * 5 + 0] = (double)(fx * fx);
-        M[(size_t)a * 5 + 1] = (double)(fy * fy);
-        M[(size_t)a * 5 + 2] = (double)(fx * fy);
-        M[(size_t)a * 5 + 3] = (double)fx;
-        M[(size_t)a * 5 + 4] = (double)fy;
-        r[a] = (double)fz;
-      }
-      __threadfence_block();
-      __syncthreads();
-      lls5_wave(L, M, r, n);
-      if (lane == 0) {
-        const int inum = imin(s.tau, q.num_images);
-        float u2 = 0.0f;
-        for (int k = 0; k < inum; ++k) u2 += get_unit(s, s.views[q.images[k]], q.coord);
-        u2 = __fdiv_rn(u2, (float)inum);
-        float residual = 0.0f;
-        for (int a = 0; a < n; ++a) {
-          const float fx = L.fx[a], fy = L.fy[a];
-          const float res = L.x[0] * (fx * fx) + L.x[1] * (fy * fy) + L.x[2] * (fx * fy) + L.x[3] * fx + L.x[4] * fy - L.fz[a];
-          residual = (float)((double)residual + fabs((double)res) / (double)u2);  // float += double
-        }
-        residual = __fdiv_rn(residual, (float)(n - 5));
-        L.cnt = (residual < s.quad ? 0 : 1);
-      }
-      __syncthreads();
-      rej = L.cnt;
-    }
+    const int rej = (n < 6) ? 1 : filter_quad_wave(s, F, L, M, r, q, n);
     if (lane == 0) reject[p] = rej;
     __syncthreads();
   }
@@ -713,6 +731,296 @@ __global__ void group_edges_kernel(DScene s, FilterDev F, int pass, const int* _
   if (!pass) cnt[i] = k;
 }
 
+
+// ============================================================================ expansion
+// CExpand::findEmptyBlocks (expand.cpp:95-180), one wavefront per parent: the six angular
+// bins around the patch that hold no neighbour (findNeighbors(patch, ., 1, 4.0f), margin 1,
+// vimages included) and were not tried before (_dflag) get a candidate at `radius`.
+__global__ __launch_bounds__(64) void empty_blocks_kernel(DScene s, FilterDev F, const int* __restrict__ parents, int np,
+                                                          float* __restrict__ cand_coord, int* __restrict__ cand_ok,
+                                                          int* __restrict__ queue, int* __restrict__ overflow) {
+  __shared__ NbLds L;
+  const int lane = threadIdx.x;
+  for (;;) {
+    int k = 0;
+    if (lane == 0) k = atomicAdd(queue, 1);
+    k = __shfl(k, 0);
+    if (k >= np) break;
+    const pmvs_patch& q = F.P[parents[k]];
+    const float radius = compute_radius_wave(s, L, q);
+    const int n = gather_neighbors(s, F, L, q, 4.0f, 1, 0);
+    if (lane == 0) {
+      if (L.overflow) atomicAdd(overflow, 1);
+      float xdir[4] = {0, 0, 0, 0}, ydir[4] = {0, 0, 0, 0};
+      const float* z = q.normal;
+      if (fabs((double)z[0]) > 0.5) { xdir[0] = z[1]; xdir[1] = -z[0]; xdir[2] = 0; }
+      else if (fabs((double)z[1]) > 0.5) { xdir[1] = z[2]; xdir[2] = -z[1]; xdir[0] = 0; }
+      else { xdir[2] = z[0]; xdir[0] = -z[2]; xdir[1] = 0; }
+      unitize4(xdir);
+      ydir[0] = z[1] * xdir[2] - z[2] * xdir[1];
+      ydir[1] = z[2] * xdir[0] - z[0] * xdir[2];
+      ydir[2] = z[0] * xdir[1] - z[1] * xdir[0];
+      float fill[6] = {0, 0, 0, 0, 0, 0};
+      const float radiuslow = __fdiv_rn(radius, 6.0f), radiushigh = radius * 2.5f;
+      for (int a = 0; a < n; ++a) {
+        float d[4];
+        for (int c = 0; c < 4; ++c) d[c] = F.P[L.nb[a]].coord[c] - q.coord[c];
+        float f0 = dot4(d, xdir), f1 = dot4(d, ydir);
+        const float len = (float)sqrt((double)(f0 * f0 + f1 * f1));
+        if (len < radiuslow || radiushigh < len) continue;
+        f0 = __fdiv_rn(f0, len);
+        f1 = __fdiv_rn(f1, len);
+        float angle = (float)atan2((double)f1, (double)f0);
+        if (angle < 0.0) angle = (float)((double)angle + 2 * M_PI);
+        const float findex = (float)((double)angle / (2 * M_PI / 6));
+        const int lindex = (int)floor((double)findex);
+        const int hindex = lindex + 1;
+        fill[lindex % 6] += (float)hindex - findex;
+        fill[hindex % 6] += findex - (float)lindex;
+      }
+      for (int i = 0; i < 6; ++i) {
+        int ok = 1;
+        if (0.0f < fill[i]) ok = 0;
+        if (q.dflag & (0x0001 << i)) ok = 0;
+        cand_ok[6 * k + i] = ok;
+        if (ok) {
+          const double angle = 2 * M_PI * i / 6;
+          const double cr = cos(angle) * (double)radius, sr = sin(angle) * (double)radius;
+          for (int c = 0; c < 4; ++c)
+            cand_coord[4 * (6 * k + i) + c] = (q.coord[c] + (float)((double)xdir[c] * cr)) + (float)((double)ydir[c] * sr);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// CExpand::expandSub up to the refine (expand.cpp:200-226), one thread per candidate slot:
+// setGridsImages from the parent's images, mask / bimages, checkCounts, removeImagesEdge.
+// status: -1 no candidate, 1 rejected, 0 goes to preProcess (pmvs_candidate written).
+__global__ void prepare_kernel(DScene s, FilterDev F, const unsigned char* __restrict__ counts, const int* __restrict__ parents,
+                               int np, const float* __restrict__ cand_coord, const int* __restrict__ cand_ok,
+                               pmvs_candidate* __restrict__ cout, pmvs_patch* __restrict__ prep, int* __restrict__ status,
+                               int cthr, int only) {
+  const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+  if (slot >= np * 6) return;
+  if (!cand_ok[slot] || (only >= 0 && slot != only)) { status[slot] = -1; return; }
+  const pmvs_patch& par = F.P[parents[slot / 6]];
+  float coord[4];
+  for (int c = 0; c < 4; ++c) coord[c] = cand_coord[4 * slot + c];
+  pmvs_patch& q = prep[slot];
+  for (int c = 0; c < 4; ++c) { q.coord[c] = coord[c]; q.normal[c] = par.normal[c]; }
+  int ni = 0;
+  for (int k = 0; k < par.num_images; ++k) {  // setGridsImages (patchOrganizerS.cpp:383-399)
+    const int t = par.images[k];
+    float ic[3];
+    project(s.views[t], coord, s.level, ic);
+    const int ix = ((int)floorf(ic[0] + 0.5f)) / s.csize;
+    const int iy = ((int)floorf(ic[1] + 0.5f)) / s.csize;
+    if (0 <= ix && ix < gwidth(s, t) && 0 <= iy && iy < gheight(s, t)) {
+      q.images[ni] = t;
+      q.grids[ni][0] = ix;
+      q.grids[ni][1] = iy;
+      ni++;
+    }
+  }
+  q.num_images = ni;
+  int st = 0;
+  if (ni == 0) st = 1;
+  if (!st) {
+    bool bad = false;
+    if (s.anyMask)
+      for (int v = 0; v < s.num; ++v)
+        if (get_mask(s, s.views[v], coord, s.level) == 0) bad = true;
+    for (int b = 0; b < s.nb; ++b) {
+      const DView& v = s.views[s.bindexes[b]];
+      float ic[3];
+      project(v, coord, s.level, ic);
+      if (ic[0] < 0.0f || (float)(v.w[s.level] - 1) < ic[0] || ic[1] < 0.0f || (float)(v.h[s.level] - 1) < ic[1]) bad = true;
+    }
+    if (bad) st = 1;
+  }
+  if (!st) {  // checkCounts (expand.cpp:268-323)
+    int full = 0, empty = 0;
+    for (int k = 0; k < ni; ++k) {
+      const int t = q.images[k];
+      if (s.tnum <= t) continue;
+      const long long c = F.tgoff[t] + (long long)q.grids[k][1] * gwidth(s, t) + q.grids[k][0];
+      if (F.pg_off[c + 1] > F.pg_off[c]) { ++full; continue; }
+      if (cthr <= counts[c]) ++full;
+      else ++empty;
+    }
+    if (s.depth <= 1) { if (empty < s.minImageNum && full != 0) st = 1; }
+    else if (empty < s.minImageNum - 1 && full != 0) st = 1;
+  }
+  int ne = 0;
+  if (!st) {  // removeImagesEdge (optim.cpp:384-396)
+    for (int k = 0; k < ni; ++k)
+      if (get_edge(s, s.views[q.images[k]], coord, s.level)) cout[slot].images[ne++] = q.images[k];
+    if (ne == 0) st = 1;
+  }
+  status[slot] = st;
+  if (!st) {
+    for (int c = 0; c < 4; ++c) { cout[slot].coord[c] = coord[c]; cout[slot].normal[c] = par.normal[c]; }
+    cout[slot].dscale = 0.0f;
+    cout[slot].num_images = ne;
+  }
+}
+
+// COptim::postProcess depth >= 1 steps (optim.cpp:178-188) on refined candidates, one wavefront
+// each: setVImagesVGrids against the model's depth maps and, at depth >= 2, check() =
+// computeGain + findNeighbors(patch, ., 1, 4, 2) + filterQuad.  out_status: 0 accepted,
+// 2 preProcess failed, 3 postProcess failed.
+__global__ __launch_bounds__(64) void depth_post_kernel(DScene s, FilterDev F, const pmvs_refined* __restrict__ res,
+                                                        int m, pmvs_patch* __restrict__ outp, int* __restrict__ out_status,
+                                                        double* __restrict__ scratch, int* __restrict__ queue,
+                                                        int* __restrict__ overflow) {
+  __shared__ NbLds L;
+  const int lane = threadIdx.x;
+  double* M = scratch + (size_t)blockIdx.x * NB_CAP * 6;
+  double* r = M + (size_t)NB_CAP * 5;
+  for (;;) {
+    int k = 0;
+    if (lane == 0) k = atomicAdd(queue, 1);
+    k = __shfl(k, 0);
+    if (k >= m) break;
+    const pmvs_refined& rr = res[k];
+    pmvs_patch& q = outp[k];
+    if (rr.status != PMVS_ACCEPTED) {
+      if (lane == 0) out_status[k] = (rr.status == PMVS_FAIL_POST) ? 3 : 2;
+      continue;
+    }
+    if (lane == 0) {
+      for (int c = 0; c < 4; ++c) { q.coord[c] = rr.coord[c]; q.normal[c] = rr.normal[c]; }
+      q.ncc = rr.ncc; q.dscale = rr.dscale; q.ascale = rr.ascale; q.tmp = rr.tmp; q.timages = rr.timages;
+      q.flag = 1; q.fix = 0; q.dflag = 0; q.num_images = rr.num_images; q.num_vimages = 0;
+    }
+    if (lane < rr.num_images) {
+      q.images[lane] = rr.images[lane];
+      q.grids[lane][0] = rr.grids[lane][0];
+      q.grids[lane][1] = rr.grids[lane][1];
+    }
+    __threadfence_block();
+    __syncthreads();
+    int st = 0;
+    if (s.depth) {
+      // setVImagesVGrids (patchOrganizerS.cpp:429-459): lane t tests target image t
+      bool take = false;
+      int ix = 0, iy = 0;
+      for (int base = 0; base < s.tnum; base += 64) {
+        const int t = base + lane;
+        take = false;
+        if (t < s.tnum) {
+          bool used = false;
+          for (int i = 0; i < q.num_images; ++i)
+            if (q.images[i] == t) used = true;
+          if (!used) {
+            float ic[3];
+            project(s.views[t], q.coord, s.level, ic);
+            ix = ((int)floorf(ic[0] + 0.5f)) / s.csize;
+            iy = ((int)floorf(ic[1] + 0.5f)) / s.csize;
+            take = is_visible_q(s, F, q, t, ix, iy, 0.5f) && get_edge(s, s.views[t], q.coord, s.level);
+          }
+        }
+        const unsigned long long mask = __ballot(take);
+        const int pos = __popcll(mask & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+        const int nv = q.num_vimages;
+        __syncthreads();
+        if (take && nv + pos < PMVS_MAX_IMAGES) {
+          q.vimages[nv + pos] = t;
+          q.vgrids[nv + pos][0] = ix;
+          q.vgrids[nv + pos][1] = iy;
+        }
+        __syncthreads();
+        if (lane == 0) q.num_vimages = imin(PMVS_MAX_IMAGES, nv + __popcll(mask));
+        __threadfence_block();
+        __syncthreads();
+      }
+      if (2 <= s.depth) {
+        // COptim::check (optim.cpp:363-381): computeGain (filter.cpp:88-146) ...
+        const int ne = q.num_images + q.num_vimages;
+        const float u0 = get_unit(s, s.views[q.images[0]], q.coord);
+        if (lane == 0) L.f[2] = (double)(smax(0.0f, q.ncc - s.nccThreshold) * (float)q.timages);
+        for (int base = 0; base < ne; base += 64) {
+          const int en = base + lane;
+          float maxp = 0.0f;
+          if (en < ne) {
+            const bool vis = en >= q.num_images;
+            const int t = vis ? q.vimages[en - q.num_images] : q.images[en];
+            if (t < s.tnum) {
+              const int gx = vis ? q.vgrids[en - q.num_images][0] : q.grids[en][0];
+              const int gy = vis ? q.vgrids[en - q.num_images][1] : q.grids[en][1];
+              const long long c = F.tgoff[t] + (long long)gy * gwidth(s, t) + gx;
+              const float pdepth = depth_of(s.views[t], q.coord);
+              for (int e = F.pg_off[c]; e < F.pg_off[c + 1]; ++e) {
+                const int j = F.pg_items[e];
+                if (vis && !(pdepth < depth_of(s.views[t], F.P[j].coord))) continue;
+                const float hunit = (float)((double)(u0 + F.unit0[j]) / 2.0 * s.csize);
+                if (!is_neighbor_h(q, F.P[j], hunit, 1.0f, 0.0f, false)) maxp = smax(maxp, F.P[j].ncc - s.nccThreshold);
+              }
+            }
+          }
+          L.units[lane] = maxp;
+          __syncthreads();
+          if (lane == 0) {
+            float gain = (float)L.f[2];
+            for (int i = 0; i < 64 && base + i < ne; ++i) gain -= L.units[i];
+            L.f[2] = (double)gain;
+          }
+          __syncthreads();
+        }
+        if (lane == 0) q.tmp = (float)L.f[2];
+        __syncthreads();
+        if ((float)L.f[2] < 0.0f) {
+          st = 3;
+        } else {
+          // ... findNeighbors(patch, neighbors, 1, 4, 2) + filterQuad when more than 6 neighbours
+          const int n = gather_neighbors(s, F, L, q, 4.0f, 2, 0);
+          if (lane == 0 && L.overflow) atomicAdd(overflow, 1);
+          if (6 < n && filter_quad_wave(s, F, L, M, r, q, n)) st = 3;
+        }
+      }
+    }
+    if (lane == 0) out_status[k] = st;
+    __syncthreads();
+  }
+}
+
+// CPatchOrganizerS::addPatch of the committed patches (patchOrganizerS.cpp:308-381): registration
+// bits and depth-map updates; rank codes are larger than every loaded patch's, so equal depths
+// keep the older patch as the reference's strict "depth < dtmp".
+__global__ void add_patches_kernel(DScene s, FilterDev F, int first, int count, int rank0, unsigned long long* __restrict__ preg,
+                                   unsigned long long* __restrict__ vreg, int* __restrict__ order,
+                                   unsigned long long* __restrict__ dpkey, float* __restrict__ unit0) {
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (long long)count * s.tnum) return;
+  const int k = (int)(g / s.tnum), t = (int)(g - (long long)k * s.tnum);
+  const int p = first + k;
+  const pmvs_patch& q = F.P[p];
+  if (t == 0) {
+    unsigned long long m = 0ull;
+    for (int i = 0; i < q.num_images; ++i)
+      if (q.images[i] < s.tnum && in_grid(s, q.images[i], q.grids[i][0], q.grids[i][1])) m |= 1ull << i;
+    preg[p] = m;
+    vreg[p] = (q.num_vimages >= 64) ? ~0ull : ((1ull << q.num_vimages) - 1ull);
+    order[rank0 + k] = p;
+    unit0[p] = get_unit(s, s.views[q.images[0]], q.coord);
+  }
+  if (s.depth == 0) return;  // addPatch keeps no depth maps at depth 0 (patchOrganizerS.cpp:331)
+  const DView& v = s.views[t];
+  float ic[3];
+  project(v, q.coord, s.level, ic);
+  const float fx = __fdiv_rn(ic[0], (float)s.csize), fy = __fdiv_rn(ic[1], (float)s.csize);
+  const int xs[2] = {(int)floor((double)fx), (int)ceil((double)fx)};
+  const int ys[2] = {(int)floor((double)fy), (int)ceil((double)fy)};
+  const unsigned long long key = ((unsigned long long)depth_bits(depth_of(v, q.coord)) << 32) | (unsigned)(rank0 + k);
+  const int gw = gwidth(s, t), gh = gheight(s, t);
+  for (int j = 0; j < 2; ++j)
+    for (int i = 0; i < 2; ++i) {
+      if (xs[i] < 0 || gw <= xs[i] || ys[j] < 0 || gh <= ys[j]) continue;
+      atomicMin(&dpkey[F.tgoff[t] + (long long)ys[j] * gw + xs[i]], key);
+    }
+}
 
 // ============================================================================ host orchestration
 #define FCHK(x)                          \
@@ -1007,4 +1315,242 @@ hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n,
   return hipGetLastError();
 }
 
+
+// ============================================================================ expansion (host)
+namespace {
+
+struct QItem {
+  float tmp;
+  long long seq;
+  int p;
+};
+struct QCmp {  // max-heap on _tmp (P_compare, patchOrganizerS.hpp:10-15); ties: earlier push first
+  bool operator()(const QItem& a, const QItem& b) const {
+    if (a.tmp != b.tmp) return a.tmp < b.tmp;
+    return a.seq > b.seq;
+  }
+};
+
+__global__ void gather_slots_kernel(const int* __restrict__ slots, int m, const pmvs_candidate* __restrict__ cin,
+                                    const pmvs_patch* __restrict__ prep, pmvs_candidate* __restrict__ cout,
+                                    pmvs_patch* __restrict__ pout) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= m) return;
+  cout[k] = cin[slots[k]];
+  pout[k] = prep[slots[k]];
+}
+
+__global__ void alive_reg_kernel(int n, const int* __restrict__ alive, unsigned long long* __restrict__ preg,
+                                 unsigned long long* __restrict__ vreg, const pmvs_patch* __restrict__ P) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  if (!alive[p]) {
+    preg[p] = 0ull;
+    vreg[p] = 0ull;
+  } else {
+    const int nv = P[p].num_vimages;
+    vreg[p] = (nv >= 64) ? ~0ull : ((1ull << nv) - 1ull);
+  }
+}
+
+template <class T>
+static hipError_t grow(T*& p, size_t& cap, size_t need) {
+  if (need <= cap && p) return hipSuccess;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = need;
+  return hipMalloc((void**)&p, (need ? need : 1) * sizeof(T));
+}
+
+}  // namespace
+
+ExpandBuffers::~ExpandBuffers() {
+  void* ps[] = {parents, cand_coord, cand_ok, cand, prep, status, slots, cand2, prep2, res, outp, ostatus, counts, alive};
+  for (void* p : ps)
+    if (p) (void)hipFree(p);
+}
+
+hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs_patch* dP, std::vector<pmvs_patch>& H,
+                       std::vector<int>& alive, int cap, long long ncells, const long long* h_tgoff, int wave, int cthr,
+                       int grid, hipStream_t st, const RefineFn& refine, long long stats[8]) {
+  for (int k = 0; k < 8; ++k) stats[k] = 0;
+  const int n0 = (int)H.size();
+  FCHK(B.reserve(cap, ncells, s.tnum, grid));
+  FCHK(hipMemcpyAsync(B.tgoff, h_tgoff, (s.tnum + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
+  FCHK(hipMemcpyAsync(dP, H.data(), (size_t)n0 * sizeof(pmvs_patch), hipMemcpyHostToDevice, st));
+  FCHK(grow(X.alive, X.cap_alive, (size_t)n0));
+  FCHK(hipMemcpyAsync(X.alive, alive.data(), (size_t)n0 * sizeof(int), hipMemcpyHostToDevice, st));
+  Ctx c{s, B, dP, n0, ncells, grid, st};
+  // ---- model load (the state CFilter::run leaves): registrations, collect order, depth maps, lists
+  hipLaunchKernelGGL(init_reg_kernel, dim3(nblk(n0)), dim3(256), 0, st, s, dP, n0, B.preg, B.vreg);
+  hipLaunchKernelGGL(alive_reg_kernel, dim3(nblk(n0)), dim3(256), 0, st, n0, X.alive, B.preg, B.vreg, dP);
+  FCHK(build_lists(c, 0));
+  FCHK(collect(c));
+  FCHK(hipMemsetAsync(B.dpkey, 0xff, ncells * sizeof(unsigned long long), st));
+  if (c.nalive > 0)
+    hipLaunchKernelGGL(depth_map_kernel, dim3(nblk((long long)c.nalive * s.tnum)), dim3(256), 0, st, s, c.dev(), B.dpkey);
+  FCHK(build_lists(c, 1));
+  // host mirrors: pgrids occupancy per cell, counts (clearCounts), collect order (queue)
+  std::vector<int> pgoff(ncells + 1), order(c.nalive);
+  FCHK(hipMemcpyAsync(pgoff.data(), B.pg_off, (ncells + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
+  if (c.nalive) FCHK(hipMemcpyAsync(order.data(), B.order, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
+  FCHK(hipStreamSynchronize(st));
+  std::vector<int> occ(ncells);
+  for (long long k = 0; k < ncells; ++k) occ[k] = pgoff[k + 1] - pgoff[k];
+  std::vector<unsigned char> counts(ncells, 0);
+  std::priority_queue<QItem, std::vector<QItem>, QCmp> queue;
+  long long seq = 0;
+  for (int i = 0; i < c.nalive; ++i) H[order[i]].flag = 0;  // clearFlags (the collected patches)
+  for (int i = 0; i < c.nalive; ++i) {  // collectPatches(queue)
+    const int p = order[i];
+    if (H[p].flag == 0) {
+      H[p].flag = 1;
+      queue.push({H[p].tmp, seq++, p});
+    }
+  }
+  int rank_next = c.nalive;
+  const int W = std::max(1, std::min(wave, kMaxWave));
+  FCHK(grow(X.counts, X.cap_cnt, (size_t)ncells));
+  while (!queue.empty()) {
+    stats[7]++;
+    std::vector<int> parents;
+    while (!queue.empty() && (int)parents.size() < W) {
+      parents.push_back(queue.top().p);
+      queue.pop();
+    }
+    const int np = (int)parents.size();
+    stats[0] += np;
+    FCHK(grow(X.parents, X.cap_par, (size_t)np));
+    FCHK(grow(X.cand_coord, X.cap_coord, (size_t)np * 24));
+    FCHK(grow(X.cand_ok, X.cap_ok, (size_t)np * 6));
+    FCHK(grow(X.cand, X.cap_cand, (size_t)np * 6));
+    FCHK(grow(X.prep, X.cap_prep, (size_t)np * 6));
+    FCHK(grow(X.status, X.cap_status, (size_t)np * 6));
+    FCHK(hipMemcpyAsync(X.parents, parents.data(), np * sizeof(int), hipMemcpyHostToDevice, st));
+    c.n = (int)H.size();
+    FCHK(hipMemsetAsync(B.counters + 3, 0, 5 * sizeof(int), st));
+    hipLaunchKernelGGL(empty_blocks_kernel, dim3(std::min(grid, np)), dim3(64), 0, st, s, c.dev(), X.parents, np,
+                       X.cand_coord, X.cand_ok, B.counters + 4, B.counters + 3);
+    // wave = 1 is the reference's schedule: the parent's directions are prepared, refined and
+    // committed one after the other (expand.cpp:92-101); wider waves batch every candidate.
+    std::vector<int> batches{-1};
+    if (W == 1) {
+      std::vector<int> ok(6);
+      FCHK(hipMemcpyAsync(ok.data(), X.cand_ok, 6 * sizeof(int), hipMemcpyDeviceToHost, st));
+      FCHK(hipStreamSynchronize(st));
+      batches.clear();
+      for (int k = 0; k < 6; ++k)
+        if (ok[k]) batches.push_back(k);
+    }
+    for (const int only : batches) {
+      c.n = (int)H.size();
+      FCHK(hipMemcpyAsync(X.counts, counts.data(), ncells, hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(prepare_kernel, dim3(nblk((long long)np * 6)), dim3(256), 0, st, s, c.dev(), X.counts, X.parents,
+                         np, X.cand_coord, X.cand_ok, X.cand, X.prep, X.status, cthr, only);
+      std::vector<int> status((size_t)np * 6);
+      FCHK(hipMemcpyAsync(status.data(), X.status, (size_t)np * 6 * sizeof(int), hipMemcpyDeviceToHost, st));
+      FCHK(hipStreamSynchronize(st));
+      std::vector<int> slots, slot2surv((size_t)np * 6, -1);
+      for (int k = 0; k < np * 6; ++k) {
+        if (status[k] >= 0) stats[1]++;
+        if (status[k] == 0) {
+          slot2surv[k] = (int)slots.size();
+          slots.push_back(k);
+        }
+      }
+      const int m = (int)slots.size();
+      std::vector<int> ostatus(m);
+      std::vector<pmvs_patch> outp(m), prep(m);
+      if (m > 0) {
+        FCHK(grow(X.slots, X.cap_slots, (size_t)m));
+        FCHK(grow(X.cand2, X.cap_cand2, (size_t)m));
+        FCHK(grow(X.prep2, X.cap_prep2, (size_t)m));
+        FCHK(grow(X.res, X.cap_res, (size_t)m));
+        FCHK(grow(X.outp, X.cap_outp, (size_t)m));
+        FCHK(grow(X.ostatus, X.cap_ost, (size_t)m));
+        FCHK(hipMemcpyAsync(X.slots, slots.data(), m * sizeof(int), hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(gather_slots_kernel, dim3(nblk(m)), dim3(256), 0, st, X.slots, m, X.cand, X.prep, X.cand2, X.prep2);
+        FCHK(refine(X.cand2, m, X.res));
+        FCHK(hipMemsetAsync(B.counters + 4, 0, sizeof(int), st));
+        hipLaunchKernelGGL(depth_post_kernel, dim3(std::min(grid, m)), dim3(64), 0, st, s, c.dev(), X.res, m, X.outp,
+                           X.ostatus, B.scratch, B.counters + 4, B.counters + 3);
+        FCHK(hipMemcpyAsync(ostatus.data(), X.ostatus, m * sizeof(int), hipMemcpyDeviceToHost, st));
+        FCHK(hipMemcpyAsync(outp.data(), X.outp, (size_t)m * sizeof(pmvs_patch), hipMemcpyDeviceToHost, st));
+        FCHK(hipMemcpyAsync(prep.data(), X.prep2, (size_t)m * sizeof(pmvs_patch), hipMemcpyDeviceToHost, st));
+      }
+      int ovf = 0;
+      FCHK(read_int(B.counters + 3, &ovf, st));
+      if (ovf) return hipErrorOutOfMemory;  // more than NB_CAP neighbours (reported by the API)
+      // ---- commit in (parent priority, direction) order
+      const int first = (int)H.size();
+      for (int k = 0; k < np * 6; ++k) {
+        if (status[k] < 0) continue;
+        const int par = parents[k / 6], dir = k % 6;
+        int stc = status[k];  // 1 = prepare failed
+        int j = slot2surv[k];
+        if (stc == 0) stc = ostatus[j];
+        if (stc == 0 && only < 0) {  // checkCounts again with the committed state
+          const pmvs_patch& q = prep[j];
+          int full = 0, empty = 0;
+          for (int i = 0; i < q.num_images; ++i) {
+            const int t = q.images[i];
+            if (s.tnum <= t || q.grids[i][0] < 0 || X.gw[t] <= q.grids[i][0] || q.grids[i][1] < 0 ||
+                X.gh[t] <= q.grids[i][1])
+              continue;
+            const long long cidx = h_tgoff[t] + (long long)q.grids[i][1] * X.gw[t] + q.grids[i][0];
+            if (occ[cidx] > 0) { ++full; continue; }
+            if (cthr <= counts[cidx]) ++full;
+            else ++empty;
+          }
+          const bool fail = (s.depth <= 1) ? (empty < s.minImageNum && full != 0) : (empty < s.minImageNum - 1 && full != 0);
+          if (fail) stc = 4;
+        }
+        if (stc != 0) {
+          H[par].dflag |= 0x0001 << dir;
+          stats[1 + std::min(stc, 4)]++;  // 2 fail_prep, 3 fail_pre, 4 fail_post, 5 fail_commit
+          continue;
+        }
+        pmvs_patch np_ = outp[j];
+        np_.flag = 1;
+        np_.fix = 0;
+        np_.dflag = 0;
+        // CExpand::updateCounts (expand.cpp:325-406)
+        int full = 0, empty = 0;
+        auto touch = [&](int t, int ix, int iy) {
+          if (ix < 0 || ix >= X.gw[t] || iy < 0 || iy >= X.gh[t]) return;
+          unsigned char& cc = counts[h_tgoff[t] + (long long)iy * X.gw[t] + ix];
+          if (cthr <= cc) ++full;
+          else ++empty;
+          ++cc;
+        };
+        for (int i = 0; i < np_.num_images; ++i)
+          if (np_.images[i] < s.tnum) touch(np_.images[i], np_.grids[i][0], np_.grids[i][1]);
+        for (int i = 0; i < np_.num_vimages; ++i) touch(np_.vimages[i], np_.vgrids[i][0], np_.vgrids[i][1]);
+        const int add = empty != 0;
+        for (int i = 0; i < np_.num_images; ++i) {  // addPatch: pgrids registration
+          const int t = np_.images[i];
+          if (t < s.tnum && 0 <= np_.grids[i][0] && np_.grids[i][0] < X.gw[t] && 0 <= np_.grids[i][1] &&
+              np_.grids[i][1] < X.gh[t])
+            occ[h_tgoff[t] + (long long)np_.grids[i][1] * X.gw[t] + np_.grids[i][0]]++;
+        }
+        if ((int)H.size() >= cap) return hipErrorOutOfMemory;
+        H.push_back(np_);
+        alive.push_back(1);
+        stats[6]++;
+        if (add) queue.push({np_.tmp, seq++, (int)H.size() - 1});
+      }
+      const int added = (int)H.size() - first;
+      if (added > 0) {
+        FCHK(hipMemcpyAsync(dP + first, H.data() + first, (size_t)added * sizeof(pmvs_patch), hipMemcpyHostToDevice, st));
+        c.n = (int)H.size();
+        hipLaunchKernelGGL(add_patches_kernel, dim3(nblk((long long)added * s.tnum)), dim3(256), 0, st, s, c.dev(), first,
+                           added, rank_next, B.preg, B.vreg, B.order, B.dpkey, B.unit0);
+        rank_next += added;
+        FCHK(build_lists(c, 0));
+        FCHK(build_lists(c, 1));
+      }
+    }
+  }
+  return hipGetLastError();
+}
 }  // namespace pmvsdev

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include "pmvs_device.h"
+#include <functional>
+#include <vector>
 
 namespace pmvsdev {
 hipError_t launch_refine(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out, int n,
@@ -39,4 +41,23 @@ struct FilterBuffers {
 hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n, long long ncells, const long long* h_tgoff,
                        int grid, hipStream_t st, int counts[4], int* overflow, int* keep_dev);
 hipError_t launch_filter_refimage(const DScene& s, pmvs_patch* P, const int* list, int m, int grid, hipStream_t stream);
+
+// ---- expansion run (pmvs_filter.hip)
+constexpr int kMaxWave = 16384;  // parents per expansion wave (device slot arrays are sized by it)
+struct ExpandBuffers {
+  int *parents = nullptr, *cand_ok = nullptr, *status = nullptr, *slots = nullptr, *ostatus = nullptr, *alive = nullptr;
+  float* cand_coord = nullptr;
+  pmvs_candidate *cand = nullptr, *cand2 = nullptr;
+  pmvs_patch *prep = nullptr, *prep2 = nullptr, *outp = nullptr;
+  pmvs_refined* res = nullptr;
+  unsigned char* counts = nullptr;
+  size_t cap_coord = 0, cap_ok = 0, cap_cand = 0, cap_prep = 0, cap_slots = 0, cap_prep2 = 0, cap_res = 0, cap_outp = 0,
+         cap_ost = 0, cap_par = 0, cap_status = 0, cap_cand2 = 0, cap_alive = 0, cap_cnt = 0;
+  std::vector<int> gw, gh;  // grid sizes of the target images
+  ~ExpandBuffers();
+};
+using RefineFn = std::function<hipError_t(const pmvs_candidate* d_in, int n, pmvs_refined* d_out)>;
+hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs_patch* dP, std::vector<pmvs_patch>& H,
+                       std::vector<int>& alive, int cap, long long ncells, const long long* h_tgoff, int wave, int cthr,
+                       int grid, hipStream_t st, const RefineFn& refine, long long stats[8]);
 }  // namespace pmvsdev

@@ -36,7 +36,7 @@ EVAL_QUERY_DTYPE = np.dtype(
 PATCH_DTYPE = np.dtype(
     [("coord", "<f4", 4), ("normal", "<f4", 4), ("ncc", "<f4"), ("dscale", "<f4"), ("ascale", "<f4"),
      ("tmp", "<f4"), ("timages", "<i4"), ("flag", "<i4"), ("fix", "<i4"), ("num_images", "<i4"),
-     ("num_vimages", "<i4"), ("reserved", "<i4"), ("images", "<i4", MAX_IMAGES), ("grids", "<i4", (MAX_IMAGES, 2)),
+     ("num_vimages", "<i4"), ("dflag", "<i4"), ("images", "<i4", MAX_IMAGES), ("grids", "<i4", (MAX_IMAGES, 2)),
      ("vimages", "<i4", MAX_IMAGES), ("vgrids", "<i4", (MAX_IMAGES, 2))], align=True)
 TEX_QUERY_DTYPE = np.dtype(
     [("coord", "<f4", 4), ("pxaxis", "<f4", 4), ("pyaxis", "<f4", 4), ("normal", "<f4", 4),
@@ -76,6 +76,14 @@ class FilterStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class ExpandStats(C.Structure):
+    _fields_ = [(k, C.c_int64) for k in ("parents", "candidates", "fail_prep", "fail_pre", "fail_post",
+                                          "fail_commit", "added", "waves")] + [("wall_ms", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class Options(C.Structure):
     _fields_ = [(k, C.c_int32) for k in ("level", "csize", "wsize", "min_image_num", "cpu", "use_bound",
                                           "use_vis_data", "sequence", "tflag", "oflag")] + \
@@ -97,7 +105,8 @@ EXPORTS = ["pmvs_last_error", "pmvs_device_count", "pmvs_scene_create", "pmvs_sc
            "pmvs_refine_batch", "pmvs_refine_batch_device", "pmvs_scene_sync", "pmvs_synth_ring",
            "pmvs_synth_candidates", "pmvs_selftest_math", "pmvs_selftest_bobyqa", "pmvs_camera_load",
            "pmvs_ppm_load", "pmvs_options_load", "pmvs_options_free", "pmvs_write_patches", "pmvs_write_pset",
-           "pmvs_write_ply", "pmvs_patch_colors", "pmvs_filter_run"]
+           "pmvs_write_ply", "pmvs_patch_colors", "pmvs_filter_run",
+           "pmvs_expand_run"]
 
 _lib = None
 
@@ -139,6 +148,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.pmvs_write_ply.argtypes = [C.c_char_p, C.c_int32, C.c_void_p, C.c_void_p]
     lib.pmvs_patch_colors.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 4
     lib.pmvs_filter_run.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(FilterStats)]
+    lib.pmvs_expand_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
+                                    C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(ExpandStats)]
     for fn in EXPORTS:
         getattr(lib, fn).restype = getattr(lib, fn).restype or C.c_int
     lib.pmvs_last_error.restype = C.c_char_p
@@ -315,6 +326,21 @@ class Scene:
         st = FilterStats()
         _check(self.lib.pmvs_filter_run(self.handle, _ptr(pa), len(pa), _ptr(keep), C.byref(st)))
         return pa, keep, st.as_dict()
+
+    def expand_run(self, patches: np.ndarray, alive=None, wave: int = 1, count_threshold: int = 4, cap=None):
+        """One CExpand::run on the device (expand.cpp:17-406): returns (patches, alive, stats).
+
+        The result holds the input patches (flags updated) followed by the new ones."""
+        pa = np.ascontiguousarray(patches, PATCH_DTYPE)
+        al = np.ones(len(pa), np.int32) if alive is None else np.ascontiguousarray(alive, np.int32)
+        cap = int(cap or max(4 * len(pa), len(pa) + 1024))
+        out = np.zeros(cap, PATCH_DTYPE)
+        aout = np.zeros(cap, np.int32)
+        n_out = C.c_int32(0)
+        st = ExpandStats()
+        _check(self.lib.pmvs_expand_run(self.handle, _ptr(pa), _ptr(al), len(pa), wave, count_threshold,
+                                        _ptr(out), _ptr(aout), cap, C.byref(n_out), C.byref(st)))
+        return out[:n_out.value].copy(), aout[:n_out.value].copy(), st.as_dict()
 
     def patch_colors(self, coords: np.ndarray, images) -> np.ndarray:
         """writePLY colour mode 0 for patches (coords [n,4], images: list of view-index lists)."""

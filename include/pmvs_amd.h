@@ -205,7 +205,7 @@ pmvs_status pmvs_selftest_bobyqa(int32_t device, int32_t mode, int32_t kind, con
 typedef struct pmvs_patch {
   float coord[4], normal[4];
   float ncc, dscale, ascale, tmp;
-  int32_t timages, flag, fix, num_images, num_vimages, reserved;
+  int32_t timages, flag, fix, num_images, num_vimages, dflag; /* dflag: CPatch::_dflag (failed expansion directions) */
   int32_t images[PMVS_MAX_IMAGES];
   int32_t grids[PMVS_MAX_IMAGES][2];
   int32_t vimages[PMVS_MAX_IMAGES];
@@ -221,6 +221,22 @@ typedef struct pmvs_filter_stats {
  * them); keep[i] = 1 when patch i is still in the organizer (the model) after the pass. */
 pmvs_status pmvs_filter_run(pmvs_scene* scene, pmvs_patch* patches, int32_t n, int32_t* keep,
                             pmvs_filter_stats* stats);
+
+/* One expansion run (PMVS3::CExpand::run, expand.cpp:17-406) on a model = patches[i] with
+ * alive[i] (the state a filter pass leaves: pgrids/vpgrids/depth maps are rebuilt from it).  The
+ * max-_tmp queue is expanded in waves of `wave` parents (1 = the reference's single-thread
+ * schedule), candidates are refined with preProcess -> refinePatch ->
+ * postProcess including the depth >= 1 steps (setVImagesVGrids; check() at depth >= 2) and
+ * committed in (parent priority, direction) order.  count_threshold = _countThreshold1 (4 at the
+ * first expansion, 2 after updateThreshold).  out/alive_out (capacity cap) receive the old
+ * patches (with updated _flag/_dflag) followed by the new ones; *n_out their number. */
+typedef struct pmvs_expand_stats {
+  int64_t parents, candidates, fail_prep, fail_pre, fail_post, fail_commit, added, waves;
+  double wall_ms;
+} pmvs_expand_stats;
+pmvs_status pmvs_expand_run(pmvs_scene* scene, const pmvs_patch* patches, const int32_t* alive, int32_t n,
+                            int32_t wave, int32_t count_threshold, pmvs_patch* out, int32_t* alive_out, int32_t cap,
+                            int32_t* n_out, pmvs_expand_stats* stats);
 
 /* ---------------------------------------------------------------------------------------
  * pmvs2 input / output surface (SURVEY.md §8(b) external boundary, §8 row a19).  Host code;

@@ -29,7 +29,7 @@ namespace oracle {
 struct FPatch {
   V4 coord, normal;
   float ncc, dscale, ascale, tmp;
-  int timages, flag, fix;
+  int timages, flag, fix, dflag = 0;
   std::vector<int> images, vimages;
   std::vector<std::pair<int, int>> grids, vgrids;
   int id = -1;  // CPatch::_id (collectPatches order)

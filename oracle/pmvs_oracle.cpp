@@ -853,6 +853,7 @@ static void init_ctx(const OScene& s, OCtx& c) {
 }  // namespace oracle
 
 #include "filter_oracle.h"
+#include "expand_oracle.h"
 
 using namespace oracle;
 
@@ -1085,7 +1086,7 @@ void oracle_filter_run(void* h, pmvs_patch* patches, int n, int* keep, int* coun
     FPatch& q = P[i];
     for (int k = 0; k < 4; ++k) { q.coord[k] = a.coord[k]; q.normal[k] = a.normal[k]; }
     q.ncc = a.ncc; q.dscale = a.dscale; q.ascale = a.ascale; q.tmp = a.tmp;
-    q.timages = a.timages; q.flag = a.flag; q.fix = a.fix;
+    q.timages = a.timages; q.flag = a.flag; q.fix = a.fix; q.dflag = a.dflag;
     for (int k = 0; k < a.num_images; ++k) { q.images.push_back(a.images[k]); q.grids.push_back({a.grids[k][0], a.grids[k][1]}); }
     for (int k = 0; k < a.num_vimages; ++k) { q.vimages.push_back(a.vimages[k]); q.vgrids.push_back({a.vgrids[k][0], a.vgrids[k][1]}); }
   }
@@ -1126,6 +1127,48 @@ void oracle_neighbor_sizes(void* h, pmvs_patch* patches, int n, int* raw, int* u
     uniq[p] = (int)nb.size();
     raw[p] = 0;
   }
+}
+
+static void to_fpatch(const pmvs_patch& a, FPatch& q) {
+  for (int k = 0; k < 4; ++k) { q.coord[k] = a.coord[k]; q.normal[k] = a.normal[k]; }
+  q.ncc = a.ncc; q.dscale = a.dscale; q.ascale = a.ascale; q.tmp = a.tmp;
+  q.timages = a.timages; q.flag = a.flag; q.fix = a.fix; q.dflag = a.dflag;
+  q.images.clear(); q.grids.clear(); q.vimages.clear(); q.vgrids.clear();
+  for (int k = 0; k < a.num_images; ++k) { q.images.push_back(a.images[k]); q.grids.push_back({a.grids[k][0], a.grids[k][1]}); }
+  for (int k = 0; k < a.num_vimages; ++k) { q.vimages.push_back(a.vimages[k]); q.vgrids.push_back({a.vgrids[k][0], a.vgrids[k][1]}); }
+}
+static void from_fpatch(const FPatch& q, pmvs_patch& a) {
+  std::memset(&a, 0, sizeof(a));
+  for (int k = 0; k < 4; ++k) { a.coord[k] = q.coord[k]; a.normal[k] = q.normal[k]; }
+  a.ncc = q.ncc; a.dscale = q.dscale; a.ascale = q.ascale; a.tmp = q.tmp;
+  a.timages = q.timages; a.flag = q.flag; a.fix = q.fix; a.dflag = q.dflag;
+  a.num_images = (int)std::min<size_t>(q.images.size(), PMVS_MAX_IMAGES);
+  for (int k = 0; k < a.num_images; ++k) { a.images[k] = q.images[k]; a.grids[k][0] = q.grids[k].first; a.grids[k][1] = q.grids[k].second; }
+  a.num_vimages = (int)std::min<size_t>(q.vimages.size(), PMVS_MAX_IMAGES);
+  for (int k = 0; k < a.num_vimages; ++k) { a.vimages[k] = q.vimages[k]; a.vgrids[k][0] = q.vgrids[k].first; a.vgrids[k][1] = q.vgrids[k].second; }
+}
+
+// One CExpand::run (expand_oracle.h) on the model (patches[i], alive[i]).  Writes the updated
+// model (old patches first, new ones appended) to out/alive_out (capacity cap); returns the new
+// patch count or -1 when cap is too small.  stats: parents, candidates, fail_prep, fail_pre,
+// fail_post, fail_commit, added, waves.
+int oracle_expand_run(void* h, const pmvs_patch* patches, const int* alive, int n, int wave, int cthr,
+                      pmvs_patch* out, int* alive_out, int cap, int64_t* stats) {
+  const OScene& s = *static_cast<const OScene*>(h);
+  std::vector<FPatch> P(n);
+  std::vector<int> al(alive, alive + n);
+  for (int i = 0; i < n; ++i) to_fpatch(patches[i], P[i]);
+  ExpandStats st;
+  expand_run(s, P, al, wave, cthr, st);
+  if ((int)P.size() > cap) return -1;
+  for (size_t i = 0; i < P.size(); ++i) {
+    from_fpatch(P[i], out[i]);
+    alive_out[i] = al[i];
+  }
+  const int64_t v[8] = {st.parents, st.candidates, st.fail_prep, st.fail_pre, st.fail_post, st.fail_commit, st.added,
+                        st.waves};
+  for (int k = 0; k < 8; ++k) stats[k] = v[k];
+  return (int)P.size();
 }
 
 }  // extern "C"

@@ -45,6 +45,8 @@ def lib():
         L.oracle_incc_eval.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         L.oracle_refine_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.POINTER(P.Stats)]
         L.oracle_filter_run.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        L.oracle_expand_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                        C.c_void_p, C.c_int, C.c_void_p]
         L.oracle_bobyqa_test.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_int, C.POINTER(C.c_int)]
         _lib = L
@@ -140,6 +142,21 @@ class OracleScene:
         counts = np.zeros(4, np.int32)
         lib().oracle_filter_run(self.h, _p(pa), len(pa), _p(keep), _p(counts))
         return pa, keep, counts
+
+    def expand_run(self, patches, alive=None, wave=1, count_threshold=4, cap=None):
+        """One CExpand::run; returns (patches_out, alive_out, stats dict)."""
+        pa = np.ascontiguousarray(patches, P.PATCH_DTYPE)
+        al = np.ones(len(pa), np.int32) if alive is None else np.ascontiguousarray(alive, np.int32)
+        cap = cap or max(4 * len(pa), 1024)
+        out = np.zeros(cap, P.PATCH_DTYPE)
+        alo = np.zeros(cap, np.int32)
+        st = np.zeros(8, np.int64)
+        m = lib().oracle_expand_run(self.h, _p(pa), _p(al), len(pa), wave, count_threshold, _p(out), _p(alo), cap,
+                                    _p(st))
+        if m < 0:
+            raise RuntimeError("expand_run: capacity too small")
+        keys = ("parents", "candidates", "fail_prep", "fail_pre", "fail_post", "fail_commit", "added", "waves")
+        return out[:m].copy(), alo[:m].copy(), dict(zip(keys, st.tolist()))
 
     def refine_batch(self, cands, nthreads=1):
         cands = np.ascontiguousarray(cands, P.CANDIDATE_DTYPE)

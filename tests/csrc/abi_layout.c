@@ -27,6 +27,8 @@ int main(void) {
   S(pmvs_patch); O(pmvs_patch, ncc); O(pmvs_patch, timages); O(pmvs_patch, num_images); O(pmvs_patch, images);
   O(pmvs_patch, grids); O(pmvs_patch, vimages); O(pmvs_patch, vgrids);
   S(pmvs_filter_stats); O(pmvs_filter_stats, kernel_ms);
+  S(pmvs_expand_stats); O(pmvs_expand_stats, added); O(pmvs_expand_stats, wall_ms);
+  O(pmvs_patch, dflag);
   S(pmvs_options); O(pmvs_options, threshold); O(pmvs_options, num_timages); O(pmvs_options, timages);
   O(pmvs_options, visdata2);
   S(pmvs_synth_params); O(pmvs_synth_params, seed); O(pmvs_synth_params, arc_step_deg);

@@ -1,0 +1,92 @@
+"""GPU parity of one expansion run (PMVS3::CExpand::run, expand.cpp:17-406) against the CPU
+oracle (oracle/expand_oracle.h) on the same seed model: identical patch count, statistics, and
+every field of every patch (new patches bit-for-bit: coord, normal, ncc, scales, images, grids,
+vimages, vgrids; old patches' _flag).
+
+The seed model is a set of refined patches of a synthetic ring (HIP refine path).  wave = 1 is
+the reference's single-thread schedule; wave > 1 pops that many parents per round (DESIGN.md,
+"Expansion"), and the oracle runs the same wave schedule."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("coord", "normal", "ncc", "dscale", "ascale", "tmp", "timages", "flag", "fix", "num_images",
+          "num_vimages", "dflag")
+
+
+def seed_model(P, g, inp, p, n, seed):
+    cands = P.synth_candidates(p, inp.projections, n, seed=seed)
+    r, _ = g.refine_batch(cands)
+    return P.patches_from_refined(r)
+
+
+def compare(out_g, al_g, st_g, out_o, al_o, st_o):
+    assert len(out_g) == len(out_o), (len(out_g), len(out_o))
+    for k in st_o:
+        assert st_g[k] == st_o[k], (k, st_g[k], st_o[k])
+    assert np.array_equal(al_g, al_o)
+    for f in FIELDS:
+        a, b = out_g[f], out_o[f]
+        if a.dtype.kind == "f":
+            a, b = a.view(np.uint32), b.view(np.uint32)
+        bad = np.nonzero((a != b).reshape(len(a), -1).any(1))[0]
+        assert len(bad) == 0, (f, len(bad), bad[:8])
+    for i in range(len(out_o)):
+        n, m = out_o["num_images"][i], out_o["num_vimages"][i]
+        assert np.array_equal(out_g["images"][i][:n], out_o["images"][i][:n]), i
+        assert np.array_equal(out_g["grids"][i][:n], out_o["grids"][i][:n]), i
+        assert np.array_equal(out_g["vimages"][i][:m], out_o["vimages"][i][:m]), i
+        assert np.array_equal(out_g["vgrids"][i][:m], out_o["vgrids"][i][:m]), i
+
+
+@pytest.mark.parametrize("depth,wave", [(1, 1), (2, 64), (1, 4096)], ids=["d1_w1", "d2_w64", "d1_w4096"])
+def test_expand_matches_oracle(gpu_available, oracle_mod, depth, wave):
+    import pmvs_amd as P
+    inp, p = P.synth_scene(6, 480, 360, level=1, supersample=2)
+    g = P.Scene(inp)
+    o = oracle_mod.OracleScene(inp)
+    pa = seed_model(P, g, inp, p, 300, 3)
+    for sc in (g, o):
+        sc.set_thresholds(inp.threshold, inp.threshold - 0.3, depth)
+    out_g, al_g, st_g = g.expand_run(pa, wave=wave, cap=100000)
+    out_o, al_o, st_o = o.expand_run(pa, wave=wave, cap=100000)
+    g.close()
+    o.close()
+    assert st_g["added"] > 5 * len(pa)
+    compare(out_g, al_g, st_g, out_o, al_o, st_o)
+
+
+def test_expand_after_filter_with_dead_patches(gpu_available, oracle_mod):
+    """Second expansion of a model a filter pass thinned (alive = keep), count threshold 2
+    (the value after updateThreshold), including _fix patches."""
+    import pmvs_amd as P
+    inp, p = P.synth_scene(6, 480, 360, level=1, supersample=2)
+    g = P.Scene(inp)
+    o = oracle_mod.OracleScene(inp)
+    pa = seed_model(P, g, inp, p, 300, 4)
+    for sc in (g, o):
+        sc.set_thresholds(inp.threshold, inp.threshold - 0.3, 1)
+    m, al, _ = g.expand_run(pa, wave=256, cap=100000)
+    assert (al == 1).all()
+    m, keep, _ = g.filter_run(m)
+    m["fix"][::97] = 1
+    out_g, al_g, st_g = g.expand_run(m, alive=keep, wave=256, count_threshold=2, cap=200000)
+    out_o, al_o, st_o = o.expand_run(m, alive=keep, wave=256, count_threshold=2, cap=200000)
+    g.close()
+    o.close()
+    assert (keep == 0).any()
+    compare(out_g, al_g, st_g, out_o, al_o, st_o)
+
+
+def test_expand_capacity_error(gpu_available):
+    import pmvs_amd as P
+    inp, p = P.synth_scene(6, 480, 360, level=1, supersample=2)
+    g = P.Scene(inp)
+    pa = seed_model(P, g, inp, p, 100, 5)
+    g.set_thresholds(inp.threshold, inp.threshold - 0.3, 1)
+    with pytest.raises(RuntimeError):
+        g.expand_run(pa, wave=64, cap=len(pa) + 10)
+    out, al, st = g.expand_run(pa[:0], wave=64, cap=16)
+    assert len(out) == 0 and st["parents"] == 0
+    g.close()
