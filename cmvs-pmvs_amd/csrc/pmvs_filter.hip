@@ -38,6 +38,10 @@ namespace pmvsdev {
 
 constexpr int NB_CAP = 1024;  // neighbours per patch in filterNeighbor (overflow is reported)
 __device__ __forceinline__ int lane_id_w() { return threadIdx.x & 63; }
+// Wave-uniform copies (SGPR) of values that are uniform by construction but loaded from memory:
+// every branch or loop around a barrier is driven by one of these, never by a VGPR value.
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ float uni_f(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
 
 struct FilterDev {
   const DScene* dummy;
@@ -485,6 +489,7 @@ __device__ void lls5_wave(NbLds& L, double* M, double* r, int n) {
 // duplicates; returns the unique count.  All 64 lanes call it.
 __device__ int sort_unique_lds(int* a, int n, int* cnt_slot) {
   const int lane = lane_id_w();
+  n = uni(n);
   int N = 1;
   while (N < n) N <<= 1;
   for (int i = n + lane; i < N; i += 64) a[i] = 0x7fffffff;
@@ -508,7 +513,7 @@ __device__ int sort_unique_lds(int* a, int n, int* cnt_slot) {
     *cnt_slot = u;
   }
   __syncthreads();
-  return *cnt_slot;
+  return uni(*cnt_slot);
 }
 
 // CFilter::filterNeighborThread (filter.cpp:358-385) + findNeighbors(..., 0, 4, 2, 1)
@@ -517,7 +522,7 @@ __device__ int sort_unique_lds(int* a, int n, int* cnt_slot) {
 // (optim.cpp:446-471) times csize.  All lanes call; result in every lane.
 __device__ float compute_radius_wave(const DScene& s, NbLds& L, const pmvs_patch& q) {
   const int lane = lane_id_w();
-  const int ni = q.num_images;
+  const int ni = uni(q.num_images);
   __syncthreads();
   if (lane < ni) {
     const DView& v = s.views[q.images[lane]];
@@ -544,7 +549,7 @@ __device__ float compute_radius_wave(const DScene& s, NbLds& L, const pmvs_patch
 __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, const pmvs_patch& q, float scale,
                                 int margin, int skipvis) {
   const int lane = lane_id_w();
-  const int ni = q.num_images;
+  const int ni = uni(q.num_images);
   const float radius = (float)(1.5 * margin * (double)compute_radius_wave(s, L, q));
   float unit = 0.0f;
   for (int k = 0; k < ni; ++k) unit += get_unit(s, s.views[q.images[k]], q.coord);
@@ -553,13 +558,13 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, c
   const float thr = 0.5f * scale;
   if (lane == 0) { L.cnt = 0; L.overflow = 0; }
   __syncthreads();
-  const int nlists = skipvis ? ni : ni + q.num_vimages;
+  const int nlists = skipvis ? ni : ni + uni(q.num_vimages);
   for (int k = 0; k < nlists; ++k) {
     const bool vis = k >= ni;
-    const int t = vis ? q.vimages[k - ni] : q.images[k];
+    const int t = uni(vis ? q.vimages[k - ni] : q.images[k]);
     if (s.tnum <= t) continue;
-    const int gx = vis ? q.vgrids[k - ni][0] : q.grids[k][0];
-    const int gy = vis ? q.vgrids[k - ni][1] : q.grids[k][1];
+    const int gx = uni(vis ? q.vgrids[k - ni][0] : q.grids[k][0]);
+    const int gy = uni(vis ? q.vgrids[k - ni][1] : q.grids[k][1]);
     const int gw = gwidth(s, t), gh = gheight(s, t);
     for (int dy = -margin; dy <= margin; ++dy) {
       const int yt = gy + dy;
@@ -572,7 +577,7 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, c
           const int* off = lst ? F.vp_off : F.pg_off;
           const int* items = lst ? F.vp_items : F.pg_items;
           const int lim = lst ? F.nvp : F.npg;
-          int b = off[c], e = off[c + 1];
+          int b = uni(off[c]), e = uni(off[c + 1]);
           if (b < 0 || e > lim || b > e) {
             if (lane == 0) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 12 + lst); }
             b = 0; e = 0;
@@ -598,13 +603,14 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, c
             __syncthreads();
             // duplicates (one entry per image/cell registration) are compacted when the buffer
             // fills; the reference sorts and uniques once at the end (same set)
-            if (L.cnt > NB_CAP - 64 && !L.overflow) sort_unique_lds(L.nb, imin(L.cnt, NB_CAP), &L.cnt);
+            const int cnt = uni(L.cnt);
+            if (cnt > NB_CAP - 64 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(cnt, NB_CAP), &L.cnt);
           }
         }
       }
     }
   }
-  const int n = L.cnt < NB_CAP ? L.cnt : NB_CAP;
+  const int n = imin(uni(L.cnt), NB_CAP);
   return sort_unique_lds(L.nb, n, &L.cnt);
 }
 
@@ -612,6 +618,7 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, c
 __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, double* M, double* r,
                                 const pmvs_patch& q, int n) {
   const int lane = lane_id_w();
+  n = uni(n);
   float xdir[4] = {0, 0, 0, 0}, ydir[4] = {0, 0, 0, 0};
   const float* z = q.normal;
   if (fabs((double)z[0]) > 0.5) { xdir[0] = z[1]; xdir[1] = -z[0]; xdir[2] = 0; }
@@ -662,7 +669,7 @@ __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, d
     L.cnt = (residual < s.quad ? 0 : 1);
   }
   __syncthreads();
-  return L.cnt;
+  return uni(L.cnt);
 }
 
 // CFilter::filterNeighborThread (filter.cpp:358-385): findNeighbors(patch, ., 0, 4, 2, 1), reject
@@ -677,18 +684,17 @@ __global__ __launch_bounds__(64) void neighbor_kernel(DScene s, FilterDev F, dou
   for (;;) {
     int i = 0;
     if (lane == 0) i = atomicAdd(queue, 1);
-    i = __shfl(i, 0);  // work-queue index broadcast in registers
+    i = __builtin_amdgcn_readfirstlane(i);  // work-queue index, wave-uniform (SGPR)
     if (i >= F.nalive) break;
     const int p = F.order[i];
     const pmvs_patch& q = F.P[p];
-    if (q.fix) {
-      if (lane == 0) reject[p] = 0;
-      continue;
+    int rej = 0;  // _fix patches are kept; no early `continue` (see depth_post_kernel)
+    if (!uni(q.fix)) {
+      const int n = gather_neighbors(s, F, L, q, 4.0f, 2, 1);
+      if (lane == 0 && L.overflow) atomicAdd(overflow, 1);
+      if (lane == 0 && dbg_counts) dbg_counts[p] = L.overflow ? -n : n;
+      rej = (n < 6) ? 1 : filter_quad_wave(s, F, L, M, r, q, n);
     }
-    const int n = gather_neighbors(s, F, L, q, 4.0f, 2, 1);
-    if (lane == 0 && L.overflow) atomicAdd(overflow, 1);
-    if (lane == 0 && dbg_counts) dbg_counts[p] = L.overflow ? -n : n;
-    const int rej = (n < 6) ? 1 : filter_quad_wave(s, F, L, M, r, q, n);
     if (lane == 0) reject[p] = rej;
     __syncthreads();
   }
@@ -744,7 +750,7 @@ __global__ __launch_bounds__(64) void empty_blocks_kernel(DScene s, FilterDev F,
   for (;;) {
     int k = 0;
     if (lane == 0) k = atomicAdd(queue, 1);
-    k = __shfl(k, 0);
+    k = __builtin_amdgcn_readfirstlane(k);
     if (k >= np) break;
     const pmvs_patch& q = F.P[parents[k]];
     const float radius = compute_radius_wave(s, L, q);
@@ -876,33 +882,36 @@ __global__ __launch_bounds__(64) void depth_post_kernel(DScene s, FilterDev F, c
                                                         double* __restrict__ scratch, int* __restrict__ queue,
                                                         int* __restrict__ overflow) {
   __shared__ NbLds L;
+  __shared__ pmvs_patch Q;  // the patch is built in LDS and stored once (no global read-back)
   const int lane = threadIdx.x;
   double* M = scratch + (size_t)blockIdx.x * NB_CAP * 6;
   double* r = M + (size_t)NB_CAP * 5;
   for (;;) {
     int k = 0;
     if (lane == 0) k = atomicAdd(queue, 1);
-    k = __shfl(k, 0);
+    k = __builtin_amdgcn_readfirstlane(k);
     if (k >= m) break;
     const pmvs_refined& rr = res[k];
-    pmvs_patch& q = outp[k];
-    if (rr.status != PMVS_ACCEPTED) {
-      if (lane == 0) out_status[k] = (rr.status == PMVS_FAIL_POST) ? 3 : 2;
-      continue;
-    }
+    pmvs_patch& q = Q;
+    // wave-uniform (SGPR) status: the branch below holds barriers, so it must not be divergent
+    // No `continue` out of a lane-divergent region anywhere in this loop: lanes that leave early
+    // are not guaranteed to reconverge with lane 0 before the next ticket is broadcast.
+    const int rstatus = uni(rr.status);
+    int st = (rstatus == PMVS_FAIL_POST) ? 3 : 2;
+    if (rstatus == PMVS_ACCEPTED) {
+    st = 0;
     if (lane == 0) {
       for (int c = 0; c < 4; ++c) { q.coord[c] = rr.coord[c]; q.normal[c] = rr.normal[c]; }
       q.ncc = rr.ncc; q.dscale = rr.dscale; q.ascale = rr.ascale; q.tmp = rr.tmp; q.timages = rr.timages;
       q.flag = 1; q.fix = 0; q.dflag = 0; q.num_images = rr.num_images; q.num_vimages = 0;
     }
-    if (lane < rr.num_images) {
-      q.images[lane] = rr.images[lane];
-      q.grids[lane][0] = rr.grids[lane][0];
-      q.grids[lane][1] = rr.grids[lane][1];
-    }
-    __threadfence_block();
+    q.images[lane] = (lane < rr.num_images) ? rr.images[lane] : 0;
+    q.grids[lane][0] = (lane < rr.num_images) ? rr.grids[lane][0] : 0;
+    q.grids[lane][1] = (lane < rr.num_images) ? rr.grids[lane][1] : 0;
+    q.vimages[lane] = 0;
+    q.vgrids[lane][0] = 0;
+    q.vgrids[lane][1] = 0;
     __syncthreads();
-    int st = 0;
     if (s.depth) {
       // setVImagesVGrids (patchOrganizerS.cpp:429-459): lane t tests target image t
       bool take = false;
@@ -933,12 +942,11 @@ __global__ __launch_bounds__(64) void depth_post_kernel(DScene s, FilterDev F, c
         }
         __syncthreads();
         if (lane == 0) q.num_vimages = imin(PMVS_MAX_IMAGES, nv + __popcll(mask));
-        __threadfence_block();
         __syncthreads();
       }
       if (2 <= s.depth) {
         // COptim::check (optim.cpp:363-381): computeGain (filter.cpp:88-146) ...
-        const int ne = q.num_images + q.num_vimages;
+        const int ne = uni(q.num_images + q.num_vimages);
         const float u0 = get_unit(s, s.views[q.images[0]], q.coord);
         if (lane == 0) L.f[2] = (double)(smax(0.0f, q.ncc - s.nccThreshold) * (float)q.timages);
         for (int base = 0; base < ne; base += 64) {
@@ -971,7 +979,7 @@ __global__ __launch_bounds__(64) void depth_post_kernel(DScene s, FilterDev F, c
         }
         if (lane == 0) q.tmp = (float)L.f[2];
         __syncthreads();
-        if ((float)L.f[2] < 0.0f) {
+        if (uni_f((float)L.f[2]) < 0.0f) {
           st = 3;
         } else {
           // ... findNeighbors(patch, neighbors, 1, 4, 2) + filterQuad when more than 6 neighbours
@@ -980,6 +988,10 @@ __global__ __launch_bounds__(64) void depth_post_kernel(DScene s, FilterDev F, c
           if (6 < n && filter_quad_wave(s, F, L, M, r, q, n)) st = 3;
         }
       }
+    }
+    const unsigned* src = reinterpret_cast<const unsigned*>(&Q);
+    unsigned* dst = reinterpret_cast<unsigned*>(&outp[k]);
+    for (int w = lane; w < (int)(sizeof(pmvs_patch) / 4); w += 64) dst[w] = src[w];
     }
     if (lane == 0) out_status[k] = st;
     __syncthreads();
@@ -1447,6 +1459,7 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
       FCHK(hipMemcpyAsync(X.counts, counts.data(), ncells, hipMemcpyHostToDevice, st));
       hipLaunchKernelGGL(prepare_kernel, dim3(nblk((long long)np * 6)), dim3(256), 0, st, s, c.dev(), X.counts, X.parents,
                          np, X.cand_coord, X.cand_ok, X.cand, X.prep, X.status, cthr, only);
+      FCHK(hipPeekAtLastError());
       std::vector<int> status((size_t)np * 6);
       FCHK(hipMemcpyAsync(status.data(), X.status, (size_t)np * 6 * sizeof(int), hipMemcpyDeviceToHost, st));
       FCHK(hipStreamSynchronize(st));
@@ -1474,6 +1487,7 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
         FCHK(hipMemsetAsync(B.counters + 4, 0, sizeof(int), st));
         hipLaunchKernelGGL(depth_post_kernel, dim3(std::min(grid, m)), dim3(64), 0, st, s, c.dev(), X.res, m, X.outp,
                            X.ostatus, B.scratch, B.counters + 4, B.counters + 3);
+        FCHK(hipPeekAtLastError());
         FCHK(hipMemcpyAsync(ostatus.data(), X.ostatus, m * sizeof(int), hipMemcpyDeviceToHost, st));
         FCHK(hipMemcpyAsync(outp.data(), X.outp, (size_t)m * sizeof(pmvs_patch), hipMemcpyDeviceToHost, st));
         FCHK(hipMemcpyAsync(prep.data(), X.prep2, (size_t)m * sizeof(pmvs_patch), hipMemcpyDeviceToHost, st));
@@ -1511,6 +1525,15 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
           continue;
         }
         pmvs_patch np_ = outp[j];
+        bool sane = np_.num_images >= 1 && np_.num_images <= PMVS_MAX_IMAGES && np_.num_vimages >= 0 &&
+                    np_.num_vimages <= PMVS_MAX_IMAGES;
+        for (int i = 0; sane && i < np_.num_images; ++i) sane = np_.images[i] >= 0 && np_.images[i] < s.num;
+        for (int i = 0; sane && i < np_.num_vimages; ++i) sane = np_.vimages[i] >= 0 && np_.vimages[i] < s.tnum;
+        if (!sane) {  // a device result that cannot come from the refine path
+          fprintf(stderr, "expand: insane patch k=%d j=%d m=%d ni=%d nv=%d ncc=%g img0=%d vim0=%d\n", k, j, m,
+                  np_.num_images, np_.num_vimages, np_.ncc, np_.images[0], np_.vimages[0]);
+          return hipErrorIllegalState;
+        }
         np_.flag = 1;
         np_.fix = 0;
         np_.dflag = 0;

@@ -1230,7 +1230,7 @@ __global__ __launch_bounds__(64) void pre_kernel(DScene s, const pmvs_candidate*
       L.cand = (c < (unsigned long long)n) ? (int)c : -1;
     }
     __syncthreads();
-    const int c = L.cand;
+    const int c = __builtin_amdgcn_readfirstlane(L.cand);
     __syncthreads();
     if (c < 0) break;
     pre_candidate<WS>(s, L, in[c], jobs[c], acc);
@@ -1252,7 +1252,7 @@ __global__ __launch_bounds__(64) void post_kernel(DScene s, const RefineJob* __r
       L.cand = (c < (unsigned long long)n) ? (int)c : -1;
     }
     __syncthreads();
-    const int c = L.cand;
+    const int c = __builtin_amdgcn_readfirstlane(L.cand);
     __syncthreads();
     if (c < 0) break;
     post_candidate<WS>(s, L, jobs[c], out[c], mat, acc);
