@@ -702,8 +702,8 @@ pmvs_status pmvs_filter_run(pmvs_scene* sc, pmvs_patch* patches, int32_t n, int3
 }
 
 pmvs_status pmvs_expand_run(pmvs_scene* sc, const pmvs_patch* patches, const int32_t* alive, int32_t n, int32_t wave,
-                            int32_t count_threshold, pmvs_patch* out, int32_t* alive_out, int32_t cap, int32_t* n_out,
-                            pmvs_expand_stats* stats) {
+                            int32_t count_threshold, int32_t flags, pmvs_patch* out, int32_t* alive_out, int32_t cap,
+                            int32_t* n_out, pmvs_expand_stats* stats) {
   if (!sc || n < 0 || (n > 0 && (!patches || !alive)) || !out || !alive_out || !n_out || cap < n)
     return fail(PMVS_EINVAL, "invalid argument");
   if (wave < 1 || wave > kMaxWave) return fail(PMVS_EINVAL, "wave must be in [1, %d]", kMaxWave);
@@ -744,7 +744,7 @@ pmvs_status pmvs_expand_run(pmvs_scene* sc, const pmvs_patch* patches, const int
   long long sv[8];
   const auto t0 = std::chrono::steady_clock::now();
   const hipError_t e = expand_pass(sc->ds, sc->fbuf, sc->xbuf, sc->fpatches.p, H, al, cap, tgoff[sc->ds.tnum],
-                                   tgoff.data(), wave, count_threshold, sc->grid, sc->stream, refine, sv);
+                                   tgoff.data(), wave, count_threshold, flags, sc->grid, sc->stream, refine, sv);
   if (e == hipErrorOutOfMemory)
     return fail(PMVS_EUNSUPPORTED, "expansion: capacity %d exceeded or a patch has more than 1024 neighbours", cap);
   HIPCHK(e);

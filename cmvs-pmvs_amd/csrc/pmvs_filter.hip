@@ -1384,7 +1384,7 @@ ExpandBuffers::~ExpandBuffers() {
 
 hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs_patch* dP, std::vector<pmvs_patch>& H,
                        std::vector<int>& alive, int cap, long long ncells, const long long* h_tgoff, int wave, int cthr,
-                       int grid, hipStream_t st, const RefineFn& refine, long long stats[8]) {
+                       int flags, int grid, hipStream_t st, const RefineFn& refine, long long stats[8]) {
   for (int k = 0; k < 8; ++k) stats[k] = 0;
   const int n0 = (int)H.size();
   FCHK(B.reserve(cap, ncells, s.tnum, grid));
@@ -1399,7 +1399,7 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
   FCHK(build_lists(c, 0));
   FCHK(collect(c));
   FCHK(hipMemsetAsync(B.dpkey, 0xff, ncells * sizeof(unsigned long long), st));
-  if (c.nalive > 0)
+  if (c.nalive > 0 && !(flags & 1))  // after the seed phase the depth maps are still empty
     hipLaunchKernelGGL(depth_map_kernel, dim3(nblk((long long)c.nalive * s.tnum)), dim3(256), 0, st, s, c.dev(), B.dpkey);
   FCHK(build_lists(c, 1));
   // host mirrors: pgrids occupancy per cell, counts (clearCounts), collect order (queue)

@@ -59,5 +59,5 @@ struct ExpandBuffers {
 using RefineFn = std::function<hipError_t(const pmvs_candidate* d_in, int n, pmvs_refined* d_out)>;
 hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs_patch* dP, std::vector<pmvs_patch>& H,
                        std::vector<int>& alive, int cap, long long ncells, const long long* h_tgoff, int wave, int cthr,
-                       int grid, hipStream_t st, const RefineFn& refine, long long stats[8]);
+                       int flags, int grid, hipStream_t st, const RefineFn& refine, long long stats[8]);
 }  // namespace pmvsdev

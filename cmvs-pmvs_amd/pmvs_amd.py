@@ -148,7 +148,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.pmvs_write_ply.argtypes = [C.c_char_p, C.c_int32, C.c_void_p, C.c_void_p]
     lib.pmvs_patch_colors.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 4
     lib.pmvs_filter_run.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(FilterStats)]
-    lib.pmvs_expand_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32,
+    lib.pmvs_expand_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                     C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(ExpandStats)]
     for fn in EXPORTS:
         getattr(lib, fn).restype = getattr(lib, fn).restype or C.c_int
@@ -327,7 +327,8 @@ class Scene:
         _check(self.lib.pmvs_filter_run(self.handle, _ptr(pa), len(pa), _ptr(keep), C.byref(st)))
         return pa, keep, st.as_dict()
 
-    def expand_run(self, patches: np.ndarray, alive=None, wave: int = 1, count_threshold: int = 4, cap=None):
+    def expand_run(self, patches: np.ndarray, alive=None, wave: int = 1, count_threshold: int = 4, cap=None,
+                   after_seeds: bool = False):
         """One CExpand::run on the device (expand.cpp:17-406): returns (patches, alive, stats).
 
         The result holds the input patches (flags updated) followed by the new ones."""
@@ -339,8 +340,33 @@ class Scene:
         n_out = C.c_int32(0)
         st = ExpandStats()
         _check(self.lib.pmvs_expand_run(self.handle, _ptr(pa), _ptr(al), len(pa), wave, count_threshold,
-                                        _ptr(out), _ptr(aout), cap, C.byref(n_out), C.byref(st)))
+                                        int(after_seeds), _ptr(out), _ptr(aout), cap, C.byref(n_out), C.byref(st)))
         return out[:n_out.value].copy(), aout[:n_out.value].copy(), st.as_dict()
+
+    def run_loop(self, seeds: np.ndarray, threshold: float, iterations: int = 3, wave: int = 4096, cap=None,
+                 after_seeds: bool = True):
+        """CFindMatch::run after the seed phase (findMatch.cpp:196-217): depth 1, then `iterations` x
+        (CExpand::run, CFilter::run, updateThreshold, ++depth).  Thresholds follow the reference's
+        float arithmetic: before = threshold - 0.3f (findMatch.cpp:104), -= 0.05f per iteration and
+        _countThreshold1 4 -> 2 (findMatch.cpp:23-28).  Returns (patches, per-iteration stats)."""
+        ncc = np.float32(threshold)
+        before = np.float32(ncc - np.float32(0.3))
+        cthr, depth = 4, 1
+        model = np.ascontiguousarray(seeds, PATCH_DTYPE)
+        cap = int(cap or max(64 * len(model), 1 << 16))
+        log = []
+        for t in range(iterations):
+            self.set_thresholds(float(ncc), float(before), depth)
+            model, alive, st_e = self.expand_run(model, wave=wave, count_threshold=cthr, cap=cap,
+                                                 after_seeds=after_seeds and t == 0)
+            model, keep, st_f = self.filter_run(model)
+            model = model[keep == 1]
+            log.append({"depth": depth, "expand": st_e, "filter": st_f, "patches": len(model)})
+            ncc = np.float32(ncc - np.float32(0.05))
+            before = np.float32(before - np.float32(0.05))
+            cthr = 2
+            depth += 1
+        return model, log
 
     def patch_colors(self, coords: np.ndarray, images) -> np.ndarray:
         """writePLY colour mode 0 for patches (coords [n,4], images: list of view-index lists)."""

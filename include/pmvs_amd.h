@@ -230,13 +230,14 @@ pmvs_status pmvs_filter_run(pmvs_scene* scene, pmvs_patch* patches, int32_t n, i
  * committed in (parent priority, direction) order.  count_threshold = _countThreshold1 (4 at the
  * first expansion, 2 after updateThreshold).  out/alive_out (capacity cap) receive the old
  * patches (with updated _flag/_dflag) followed by the new ones; *n_out their number. */
+#define PMVS_EXPAND_AFTER_SEEDS 1 /* model straight from the seed phase: no depth maps yet (findMatch.cpp:193-202) */
 typedef struct pmvs_expand_stats {
   int64_t parents, candidates, fail_prep, fail_pre, fail_post, fail_commit, added, waves;
   double wall_ms;
 } pmvs_expand_stats;
 pmvs_status pmvs_expand_run(pmvs_scene* scene, const pmvs_patch* patches, const int32_t* alive, int32_t n,
-                            int32_t wave, int32_t count_threshold, pmvs_patch* out, int32_t* alive_out, int32_t cap,
-                            int32_t* n_out, pmvs_expand_stats* stats);
+                            int32_t wave, int32_t count_threshold, int32_t flags, pmvs_patch* out, int32_t* alive_out,
+                            int32_t cap, int32_t* n_out, pmvs_expand_stats* stats);
 
 /* ---------------------------------------------------------------------------------------
  * pmvs2 input / output surface (SURVEY.md §8(b) external boundary, §8 row a19).  Host code;

@@ -36,11 +36,11 @@ struct Model {
 
 // Organizer state of a model given by its alive patches (as CFilter::run leaves it:
 // pgrids = target entries, dpgrids = setDepthMaps over collect order, vpgrids = addPatchV).
-static void model_load(Model& m, std::vector<FPatch>& P, const std::vector<int>& alive) {
+static void model_load(Model& m, std::vector<FPatch>& P, const std::vector<int>& alive, bool depth_maps) {
   for (int p = 0; p < (int)P.size(); ++p)
     if (alive[p]) add_patch_p(m.o, P, p);
   collect_patches(m.o, P, 0);
-  set_depth_maps(m.o, P);
+  if (depth_maps) set_depth_maps(m.o, P);  // none after the seed phase (addPatch at depth 0)
   for (int t = 0; t < m.s.tnum; ++t)
     for (int p : m.o.ppatches) {
       const FPatch& q = P[p];
@@ -242,12 +242,12 @@ struct QCmp {
 };
 
 // CExpand::run (expand.cpp:17-72) in waves.
-static void expand_run(const OScene& s, std::vector<FPatch>& P, std::vector<int>& alive, int wave, int cthr,
+static void expand_run(const OScene& s, std::vector<FPatch>& P, std::vector<int>& alive, int wave, int cthr, int flags,
                        ExpandStats& st) {
   Model m(s);
   OCtx ctx;
   init_ctx(s, ctx);
-  model_load(m, P, alive);
+  model_load(m, P, alive, (flags & 1) == 0);
   for (int p : m.o.ppatches) P[p].flag = 0;  // clearFlags
   std::priority_queue<QItem, std::vector<QItem>, QCmp> queue;
   int64_t seq = 0;

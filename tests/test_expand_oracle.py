@@ -52,3 +52,13 @@ def test_expand_deterministic_and_empty(seeds):
     assert np.array_equal(a[0].view(np.uint8), b[0].view(np.uint8)) and a[2] == b[2]
     out, alive, st = o.expand_run(pa[:0], wave=16, cap=16)
     assert len(out) == 0 and st["parents"] == 0
+
+
+def test_loop_oracle(seeds):
+    """Three (expand, filter, updateThreshold) iterations from seeds grow then thin the model."""
+    P, inp, o, pa = seeds
+    model, log = o.run_loop(pa, inp.threshold, iterations=3, wave=256)
+    assert [x["depth"] for x in log] == [1, 2, 3]
+    assert log[0]["expand"]["added"] > 5 * len(pa)
+    assert len(model) == log[-1]["patches"] > len(pa)
+    assert all(x["expand"]["parents"] > 0 for x in log)

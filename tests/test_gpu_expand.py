@@ -90,3 +90,25 @@ def test_expand_capacity_error(gpu_available):
     out, al, st = g.expand_run(pa[:0], wave=64, cap=16)
     assert len(out) == 0 and st["parents"] == 0
     g.close()
+
+
+@pytest.mark.parametrize("wave", [1, 512])
+def test_full_loop_matches_oracle(gpu_available, oracle_mod, wave):
+    """CFindMatch::run after the seed phase (findMatch.cpp:196-217): 3 x (expand, filter,
+    updateThreshold) from refined seeds, first expansion with the seed phase's empty depth maps."""
+    import pmvs_amd as P
+    inp, p = P.synth_scene(6, 480, 360, level=1, supersample=2)
+    g = P.Scene(inp)
+    o = oracle_mod.OracleScene(inp)
+    pa = seed_model(P, g, inp, p, 200, 7)
+    out_g, log_g = g.run_loop(pa, inp.threshold, wave=wave)
+    out_o, log_o = o.run_loop(pa, inp.threshold, wave=wave)
+    g.close()
+    o.close()
+    for a, b in zip(log_g, log_o):
+        assert a["patches"] == b["patches"], (a, b)
+        assert {k: v for k, v in a["expand"].items() if k != "wall_ms"} == b["expand"]
+        assert [a["filter"][k] for k in ("removed_outside", "removed_exact", "removed_neighbor",
+                                         "removed_groups")] == b["filter"]
+    assert log_g[-1]["patches"] > 5 * len(pa)
+    compare(out_g, np.ones(len(out_g), np.int32), {}, out_o, np.ones(len(out_o), np.int32), {})
