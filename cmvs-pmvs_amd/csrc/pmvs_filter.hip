@@ -1034,6 +1034,11 @@ __global__ void add_patches_kernel(DScene s, FilterDev F, int first, int count, 
     }
 }
 
+__global__ void flag_rank_kernel(pmvs_patch* __restrict__ P, const int* __restrict__ order, int na) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < na) P[order[k]].flag = k;
+}
+
 // ============================================================================ host orchestration
 #define FCHK(x)                          \
   do {                                   \
@@ -1315,6 +1320,8 @@ hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n,
     for (int k = 0; k < na; ++k)
       if (size[label[k]] < threshold) flags[order[k]] = 1;
     FCHK(hipMemcpyAsync(B.flags, flags.data(), n * sizeof(int), hipMemcpyHostToDevice, st));
+    // _flag = collect index of every collected patch (filter.cpp:538-542)
+    hipLaunchKernelGGL(flag_rank_kernel, dim3(nblk(na)), dim3(256), 0, st, dP, B.order, na);
     // fixed patches are never removed (filter.cpp:590)
     hipLaunchKernelGGL(clear_fixed_kernel, dim3(nblk(n)), dim3(256), 0, st, dP, n, B.flags);
     FCHK(apply_flags(c, &counts[3]));

@@ -40,7 +40,7 @@ def compare(out_g, keep_g, st_g, out_o, keep_o, counts_o):
     assert np.array_equal(keep_g, keep_o), int((keep_g != keep_o).sum())
     assert [st_g["removed_outside"], st_g["removed_exact"], st_g["removed_neighbor"], st_g["removed_groups"]] == \
         list(counts_o)
-    for f in ("timages", "num_images", "num_vimages"):
+    for f in ("timages", "num_images", "num_vimages", "flag"):
         assert np.array_equal(out_g[f], out_o[f]), f
     for i in range(len(out_o)):
         n, m = out_o["num_images"][i], out_o["num_vimages"][i]
