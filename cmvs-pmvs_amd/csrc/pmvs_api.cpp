@@ -14,6 +14,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -186,6 +188,12 @@ struct pmvs_scene {
   DBuf<pmvs_patch> fpatches;
   DBuf<int> fkeep;
   int grid = 0, refine_grid = 0, tslots = 1608;
+  // expansion sharding (pmvs_scene_set_shard) and the kept result of pmvs_expand_run(out = NULL)
+  int shard_rank = 0, shard_world = 1;
+  pmvs_allgather_fn shard_fn = nullptr;
+  void* shard_ctx = nullptr;
+  std::vector<pmvs_patch> xres;
+  std::vector<int> xalive;
   // staging for host-pointer calls
   DBuf<pmvs_candidate> cand;
   DBuf<pmvs_refined> res;
@@ -704,7 +712,8 @@ pmvs_status pmvs_filter_run(pmvs_scene* sc, pmvs_patch* patches, int32_t n, int3
 pmvs_status pmvs_expand_run(pmvs_scene* sc, const pmvs_patch* patches, const int32_t* alive, int32_t n, int32_t wave,
                             int32_t count_threshold, int32_t flags, pmvs_patch* out, int32_t* alive_out, int32_t cap,
                             int32_t* n_out, pmvs_expand_stats* stats) {
-  if (!sc || n < 0 || (n > 0 && (!patches || !alive)) || !out || !alive_out || !n_out || cap < n)
+  const bool keep = !out && !alive_out;
+  if (!sc || n < 0 || (n > 0 && (!patches || !alive)) || (!keep && (!out || !alive_out)) || !n_out || cap < n)
     return fail(PMVS_EINVAL, "invalid argument");
   if (wave < 1 || wave > kMaxWave) return fail(PMVS_EINVAL, "wave must be in [1, %d]", kMaxWave);
   if (sc->ds.tnum > 64) return fail(PMVS_EUNSUPPORTED, "expansion: more than 64 target images");
@@ -719,10 +728,10 @@ pmvs_status pmvs_expand_run(pmvs_scene* sc, const pmvs_patch* patches, const int
   }
   if (stats) std::memset(stats, 0, sizeof(*stats));
   *n_out = 0;
+  sc->xres.clear();
+  sc->xalive.clear();
   if (n == 0) return PMVS_OK;
   HIPCHK(hipSetDevice(sc->device));
-  pmvs_status st;
-  if ((st = ensure(sc->fpatches, cap))) return st;
   std::vector<long long> tgoff(sc->ds.tnum + 1, 0);
   sc->xbuf.gw.assign(sc->ds.tnum, 0);
   sc->xbuf.gh.assign(sc->ds.tnum, 0);
@@ -734,30 +743,145 @@ pmvs_status pmvs_expand_run(pmvs_scene* sc, const pmvs_patch* patches, const int
   }
   std::vector<pmvs_patch> H(patches, patches + n);
   std::vector<int> al(alive, alive + n);
-  RefineFn refine = [sc](const pmvs_candidate* d_in, int m, pmvs_refined* d_out) -> hipError_t {
+  // refine-work accounting: device counters accumulate over the run (only the work-queue heads
+  // are reset per launch); the refine-kernel time of each launch is read at the next one, when
+  // the host has synchronised in between.
+  double refine_ms = 0.0;
+  int64_t refined = 0;
+  bool pending = false;
+  auto take_time = [&]() {
+    if (!pending) return;
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, sc->kev[1], sc->kev[2]) == hipSuccess) refine_ms += ms;
+    pending = false;
+  };
+  HIPCHK(hipMemsetAsync(sc->stats.p, 0, sizeof(DevStats), sc->stream));
+  RefineFn refine = [&](const pmvs_candidate* d_in, int m, pmvs_refined* d_out) -> hipError_t {
     if (ensure(sc->jobs, m)) return hipErrorOutOfMemory;
-    hipError_t e = hipMemsetAsync(sc->stats.p, 0, sizeof(DevStats), sc->stream);
+    take_time();
+    hipError_t e = hipMemsetAsync(&sc->stats.p->queue, 0, 3 * sizeof(unsigned long long), sc->stream);
     if (e != hipSuccess) return e;
+    refined += m;
+    pending = true;
     return launch_refine(sc->ds, d_in, sc->jobs.p, d_out, m, sc->stats.p, sc->grid, sc->refine_grid, sc->tslots,
                          sc->stream, sc->kev);
   };
+  Shard sh;
+  if (sc->shard_fn && sc->shard_world > 1) {
+    sh.rank = sc->shard_rank;
+    sh.world = sc->shard_world;
+    pmvs_allgather_fn fn = sc->shard_fn;
+    void* ctx = sc->shard_ctx;
+    sh.exchange = [fn, ctx](const void* send, size_t bytes, void* recv) { return fn(ctx, send, (int64_t)bytes, recv); };
+  }
   long long sv[8];
   const auto t0 = std::chrono::steady_clock::now();
-  const hipError_t e = expand_pass(sc->ds, sc->fbuf, sc->xbuf, sc->fpatches.p, H, al, cap, tgoff[sc->ds.tnum],
-                                   tgoff.data(), wave, count_threshold, flags, sc->grid, sc->stream, refine, sv);
+  const hipError_t e = expand_pass(sc->ds, sc->fbuf, sc->xbuf, sc->fpatches.p, sc->fpatches.n, H, al, cap,
+                                   tgoff[sc->ds.tnum], tgoff.data(), wave, count_threshold, flags, sc->grid, sc->stream,
+                                   refine, sh, sv);
   if (e == hipErrorOutOfMemory)
     return fail(PMVS_EUNSUPPORTED, "expansion: capacity %d exceeded or a patch has more than 1024 neighbours", cap);
+  if (e == hipErrorUnknown && sh.world > 1) return fail(PMVS_EDEVICE, "expansion: the shard exchange or another rank failed");
   HIPCHK(e);
   HIPCHK(hipStreamSynchronize(sc->stream));
+  take_time();
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  std::memcpy(out, H.data(), H.size() * sizeof(pmvs_patch));
-  std::memcpy(alive_out, al.data(), al.size() * sizeof(int));
+  DevStats ds{};
+  HIPCHK(hipMemcpy(&ds, sc->stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));
   *n_out = (int32_t)H.size();
+  if (keep) {
+    sc->xres.swap(H);
+    sc->xalive.swap(al);
+  } else {
+    std::memcpy(out, H.data(), H.size() * sizeof(pmvs_patch));
+    std::memcpy(alive_out, al.data(), al.size() * sizeof(int));
+  }
   if (stats) {
     stats->parents = sv[0]; stats->candidates = sv[1]; stats->fail_prep = sv[2]; stats->fail_pre = sv[3];
     stats->fail_post = sv[4]; stats->fail_commit = sv[5]; stats->added = sv[6]; stats->waves = sv[7];
     stats->wall_ms = ms;
+    stats->refined = refined;
+    stats->evals = (int64_t)ds.evals;
+    stats->tex_valid = (int64_t)ds.tex_valid;
+    stats->refine_ms = refine_ms;
   }
   sc->last_refine = false;
   return PMVS_OK;
 }
+
+pmvs_status pmvs_expand_fetch(pmvs_scene* sc, pmvs_patch* out, int32_t* alive_out, int32_t n) {
+  if (!sc || n < 0 || (n > 0 && (!out || !alive_out))) return fail(PMVS_EINVAL, "invalid argument");
+  if ((size_t)n != sc->xres.size()) return fail(PMVS_EINVAL, "expand_fetch: %d patches kept, %d asked", (int)sc->xres.size(), n);
+  if (n) {
+    std::memcpy(out, sc->xres.data(), (size_t)n * sizeof(pmvs_patch));
+    std::memcpy(alive_out, sc->xalive.data(), (size_t)n * sizeof(int));
+  }
+  std::vector<pmvs_patch>().swap(sc->xres);
+  std::vector<int>().swap(sc->xalive);
+  return PMVS_OK;
+}
+
+pmvs_status pmvs_scene_set_shard(pmvs_scene* sc, int32_t rank, int32_t world, pmvs_allgather_fn fn, void* ctx) {
+  if (!sc || world < 1 || rank < 0 || rank >= world || (world > 1 && !fn)) return fail(PMVS_EINVAL, "invalid shard");
+  sc->shard_rank = rank;
+  sc->shard_world = world;
+  sc->shard_fn = fn;
+  sc->shard_ctx = ctx;
+  return PMVS_OK;
+}
+
+// ---- in-process all-gather among threads (generation-counted barrier)
+struct pmvs_thread_exchange {
+  int world = 1;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0, leaving = 0;
+  long long gen = 0;
+  std::vector<const void*> send;
+  int64_t bytes = -1;
+  bool bad = false;
+  std::vector<std::pair<pmvs_thread_exchange*, int>> ctx;
+};
+
+pmvs_thread_exchange* pmvs_thread_exchange_create(int32_t world) {
+  if (world < 1) return nullptr;
+  auto* g = new pmvs_thread_exchange();
+  g->world = world;
+  g->send.assign(world, nullptr);
+  for (int r = 0; r < world; ++r) g->ctx.push_back({g, r});
+  return g;
+}
+
+void* pmvs_thread_exchange_ctx(pmvs_thread_exchange* g, int32_t rank) {
+  if (!g || rank < 0 || rank >= g->world) return nullptr;
+  return &g->ctx[rank];
+}
+
+int pmvs_thread_allgather(void* ctx, const void* send, int64_t bytes, void* recv) {
+  auto* c = static_cast<std::pair<pmvs_thread_exchange*, int>*>(ctx);
+  if (!c) return -1;
+  pmvs_thread_exchange* g = c->first;
+  const int r = c->second;
+  std::unique_lock<std::mutex> lk(g->mu);
+  g->cv.wait(lk, [&] { return g->leaving == 0; });  // the previous round has fully drained
+  if (g->arrived == 0) { g->bytes = bytes; g->bad = false; }
+  if (bytes != g->bytes) g->bad = true;
+  g->send[r] = send;
+  const long long my = g->gen;
+  if (++g->arrived == g->world) {
+    g->leaving = g->world;
+    g->arrived = 0;
+    ++g->gen;
+    g->cv.notify_all();
+  } else {
+    g->cv.wait(lk, [&] { return g->gen != my; });
+  }
+  const bool bad = g->bad;
+  if (!bad)
+    for (int k = 0; k < g->world; ++k) std::memcpy((char*)recv + (size_t)k * bytes, g->send[k], (size_t)bytes);
+  if (--g->leaving == 0) g->cv.notify_all();  // nobody returns before every copy is done
+  else g->cv.wait(lk, [&] { return g->leaving == 0; });
+  return bad ? -1 : 0;
+}
+
+void pmvs_thread_exchange_destroy(pmvs_thread_exchange* g) { delete g; }

@@ -25,6 +25,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <deque>
 #include <functional>
 #include <queue>
@@ -62,6 +63,13 @@ struct FilterDev {
   long long ncells;
   int npg, nvp;        // entries in the pgrids / vpgrids lists
   int* err;            // [0] count, [1] first code (defensive bounds checks)
+  // Expansion only: registrations committed since the CSR lists were built, as per-cell chains
+  // (head per cell, -1 = empty; item/next in a shared entry pool).  Every expansion reader is
+  // insensitive to the order inside a cell list (findNeighbors sorts and uniques, computeGain
+  // takes a max per cell, checkCounts tests occupancy), so chains need no insertion order.
+  // nullptr in the filter pass.
+  const int* pg_dhead; const int* vp_dhead;
+  const int* d_item; const int* d_next;
 };
 
 
@@ -606,6 +614,32 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, c
             const int cnt = uni(L.cnt);
             if (cnt > NB_CAP - 64 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(cnt, NB_CAP), &L.cnt);
           }
+          if (F.pg_dhead) {  // entries committed by earlier expansion waves: up to 64 per round
+            int ent = uni((lst ? F.vp_dhead : F.pg_dhead)[c]);
+            while (ent >= 0) {
+              int j = -1;
+              for (int w = 0; w < 64 && ent >= 0; ++w) {
+                const int it = uni(F.d_item[ent]);
+                if (lane == w) j = it;
+                ent = uni(F.d_next[ent]);
+              }
+              bool hit = false;
+              if (j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 15); j = -1; }
+              if (j >= 0) hit = is_neighbor_h(q, F.P[j], unit, thr, radius, true) != 0;
+              const unsigned long long mask = __ballot(hit);
+              const int before = __popcll(mask & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+              const int pos = L.cnt + before;
+              if (hit) {
+                if (pos < NB_CAP) L.nb[pos] = j;
+                else L.overflow = 1;
+              }
+              __syncthreads();
+              if (lane == 0) L.cnt += __popcll(mask);
+              __syncthreads();
+              const int cnt = uni(L.cnt);
+              if (cnt > NB_CAP - 64 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(cnt, NB_CAP), &L.cnt);
+            }
+          }
         }
       }
     }
@@ -852,7 +886,7 @@ __global__ void prepare_kernel(DScene s, FilterDev F, const unsigned char* __res
       const int t = q.images[k];
       if (s.tnum <= t) continue;
       const long long c = F.tgoff[t] + (long long)q.grids[k][1] * gwidth(s, t) + q.grids[k][0];
-      if (F.pg_off[c + 1] > F.pg_off[c]) { ++full; continue; }
+      if (F.pg_off[c + 1] > F.pg_off[c] || (F.pg_dhead && F.pg_dhead[c] >= 0)) { ++full; continue; }
       if (cthr <= counts[c]) ++full;
       else ++empty;
     }
@@ -960,8 +994,11 @@ __global__ __launch_bounds__(64) void depth_post_kernel(DScene s, FilterDev F, c
               const int gy = vis ? q.vgrids[en - q.num_images][1] : q.grids[en][1];
               const long long c = F.tgoff[t] + (long long)gy * gwidth(s, t) + gx;
               const float pdepth = depth_of(s.views[t], q.coord);
-              for (int e = F.pg_off[c]; e < F.pg_off[c + 1]; ++e) {
-                const int j = F.pg_items[e];
+              const int eb = F.pg_off[c], ee = F.pg_off[c + 1];
+              for (int e = eb, ent = F.pg_dhead ? F.pg_dhead[c] : -1; e < ee || ent >= 0;) {
+                int j;
+                if (e < ee) j = F.pg_items[e++];
+                else { j = F.d_item[ent]; ent = F.d_next[ent]; }
                 if (vis && !(pdepth < depth_of(s.views[t], F.P[j].coord))) continue;
                 const float hunit = (float)((double)(u0 + F.unit0[j]) / 2.0 * s.csize);
                 if (!is_neighbor_h(q, F.P[j], hunit, 1.0f, 0.0f, false)) maxp = smax(maxp, F.P[j].ncc - s.nccThreshold);
@@ -1001,9 +1038,24 @@ __global__ __launch_bounds__(64) void depth_post_kernel(DScene s, FilterDev F, c
 // CPatchOrganizerS::addPatch of the committed patches (patchOrganizerS.cpp:308-381): registration
 // bits and depth-map updates; rank codes are larger than every loaded patch's, so equal depths
 // keep the older patch as the reference's strict "depth < dtmp".
+struct DeltaLists {  // the per-cell chains of FilterDev (expansion), writable
+  int* pg_head;
+  int* vp_head;
+  int* item;
+  int* next;
+  int* used;  // entries taken from the pool
+  int cap;
+};
+__device__ __forceinline__ void chain_push(const DeltaLists& D, int* head, long long cell, int p) {
+  const int e = atomicAdd(D.used, 1);
+  if (e >= D.cap) return;  // the host sizes the pool from the committed patches; never taken
+  D.item[e] = p;
+  D.next[e] = atomicExch(&head[cell], e);
+}
+
 __global__ void add_patches_kernel(DScene s, FilterDev F, int first, int count, int rank0, unsigned long long* __restrict__ preg,
                                    unsigned long long* __restrict__ vreg, int* __restrict__ order,
-                                   unsigned long long* __restrict__ dpkey, float* __restrict__ unit0) {
+                                   unsigned long long* __restrict__ dpkey, float* __restrict__ unit0, DeltaLists D) {
   const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= (long long)count * s.tnum) return;
   const int k = (int)(g / s.tnum), t = (int)(g - (long long)k * s.tnum);
@@ -1012,9 +1064,15 @@ __global__ void add_patches_kernel(DScene s, FilterDev F, int first, int count, 
   if (t == 0) {
     unsigned long long m = 0ull;
     for (int i = 0; i < q.num_images; ++i)
-      if (q.images[i] < s.tnum && in_grid(s, q.images[i], q.grids[i][0], q.grids[i][1])) m |= 1ull << i;
+      if (q.images[i] < s.tnum && in_grid(s, q.images[i], q.grids[i][0], q.grids[i][1])) {
+        m |= 1ull << i;
+        chain_push(D, D.pg_head, F.tgoff[q.images[i]] + (long long)q.grids[i][1] * gwidth(s, q.images[i]) + q.grids[i][0], p);
+      }
     preg[p] = m;
     vreg[p] = (q.num_vimages >= 64) ? ~0ull : ((1ull << q.num_vimages) - 1ull);
+    for (int i = 0; i < q.num_vimages; ++i)
+      if (in_grid(s, q.vimages[i], q.vgrids[i][0], q.vgrids[i][1]))
+        chain_push(D, D.vp_head, F.tgoff[q.vimages[i]] + (long long)q.vgrids[i][1] * gwidth(s, q.vimages[i]) + q.vgrids[i][0], p);
     order[rank0 + k] = p;
     unit0[p] = get_unit(s, s.views[q.images[0]], q.coord);
   }
@@ -1108,12 +1166,14 @@ struct Ctx {
   int grid;
   hipStream_t st;
   int nalive = 0, npg = 0, nvp = 0;
+  const int *pg_dhead = nullptr, *vp_dhead = nullptr, *d_item = nullptr, *d_next = nullptr;
   FilterDev dev() const {
     FilterDev F{};
     F.P = P; F.n = n; F.preg = B.preg; F.vreg = B.vreg; F.tgoff = B.tgoff; F.tnum = s.tnum;
     F.pg_off = B.pg_off; F.pg_items = B.pg_items; F.vp_off = B.vp_off; F.vp_items = B.vp_items;
     F.dpkey = B.dpkey; F.order = B.order; F.rank = B.rank; F.nalive = nalive; F.unit0 = B.unit0;
     F.ncells = ncells; F.npg = npg; F.nvp = nvp; F.err = B.counters + 6;
+    F.pg_dhead = pg_dhead; F.vp_dhead = vp_dhead; F.d_item = d_item; F.d_next = d_next;
     return F;
   }
 };
@@ -1372,6 +1432,13 @@ __global__ void alive_reg_kernel(int n, const int* __restrict__ alive, unsigned 
   }
 }
 
+// CExpand::updateCounts results of one commit (host-computed): counts[cell] = value.
+__global__ void counts_scatter_kernel(const long long* __restrict__ cells, const unsigned char* __restrict__ vals, int n,
+                                      unsigned char* __restrict__ counts) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) counts[cells[k]] = vals[k];
+}
+
 template <class T>
 static hipError_t grow(T*& p, size_t& cap, size_t need) {
   if (need <= cap && p) return hipSuccess;
@@ -1384,17 +1451,45 @@ static hipError_t grow(T*& p, size_t& cap, size_t need) {
 }  // namespace
 
 ExpandBuffers::~ExpandBuffers() {
-  void* ps[] = {parents, cand_coord, cand_ok, cand, prep, status, slots, cand2, prep2, res, outp, ostatus, counts, alive};
+  void* ps[] = {parents, cand_coord, cand_ok, cand, prep, status, slots, cand2, prep2, res, outp, ostatus, counts, alive,
+                pg_head, vp_head, d_item, d_next, pool_used, tcells, tvals};
   for (void* p : ps)
     if (p) (void)hipFree(p);
 }
 
-hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs_patch* dP, std::vector<pmvs_patch>& H,
-                       std::vector<int>& alive, int cap, long long ncells, const long long* h_tgoff, int wave, int cthr,
-                       int flags, int grid, hipStream_t st, const RefineFn& refine, long long stats[8]) {
+// Grows a device array keeping its contents (the delta-chain entry pool).
+template <class T>
+static hipError_t grow_keep(T*& p, size_t& cap, size_t need, size_t used, hipStream_t st) {
+  if (need <= cap && p) return hipSuccess;
+  const size_t ncap = std::max(need, cap * 2 + 1024);
+  T* q = nullptr;
+  FCHK(hipMalloc((void**)&q, ncap * sizeof(T)));
+  if (p && used) FCHK(hipMemcpyAsync(q, p, used * sizeof(T), hipMemcpyDeviceToDevice, st));
+  FCHK(hipStreamSynchronize(st));
+  if (p) (void)hipFree(p);
+  p = q;
+  cap = ncap;
+  return hipSuccess;
+}
+
+// One CExpand::run (expand.cpp:17-406) in waves; see pmvs_amd.h (pmvs_expand_run) and DESIGN.md.
+// Sharded (sh.world > 1): every rank holds the same model and runs the same schedule; the cheap
+// organizer steps (findEmptyBlocks, expandSub up to the refine) run on every rank, the refine +
+// depth >= 1 postProcess of a wave's candidates is split into contiguous rank ranges, and the
+// per-candidate results are all-gathered (sh.exchange) before the identical commit -- so the
+// model after the run is bit-identical to the one-rank run with the same wave.
+hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs_patch*& dP, size_t& dP_cap,
+                       std::vector<pmvs_patch>& H, std::vector<int>& alive, int cap, long long ncells,
+                       const long long* h_tgoff, int wave, int cthr, int flags, int grid, hipStream_t st,
+                       const RefineFn& refine, const Shard& sh, long long stats[8]) {
   for (int k = 0; k < 8; ++k) stats[k] = 0;
   const int n0 = (int)H.size();
-  FCHK(B.reserve(cap, ncells, s.tnum, grid));
+  const int W = std::max(1, std::min(wave, kMaxWave));
+  // device patch capacity: the model plus a few waves, doubled when the commits need more
+  size_t pcap = std::min<size_t>((size_t)cap, (size_t)n0 + 12 * (size_t)W + 1024);
+  FCHK(B.reserve((int)pcap, ncells, s.tnum, grid));
+  pcap = (size_t)B.cap_n;
+  FCHK(grow_keep(dP, dP_cap, pcap, 0, st));
   FCHK(hipMemcpyAsync(B.tgoff, h_tgoff, (s.tnum + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
   FCHK(hipMemcpyAsync(dP, H.data(), (size_t)n0 * sizeof(pmvs_patch), hipMemcpyHostToDevice, st));
   FCHK(grow(X.alive, X.cap_alive, (size_t)n0));
@@ -1409,14 +1504,30 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
   if (c.nalive > 0 && !(flags & 1))  // after the seed phase the depth maps are still empty
     hipLaunchKernelGGL(depth_map_kernel, dim3(nblk((long long)c.nalive * s.tnum)), dim3(256), 0, st, s, c.dev(), B.dpkey);
   FCHK(build_lists(c, 1));
-  // host mirrors: pgrids occupancy per cell, counts (clearCounts), collect order (queue)
+  // ---- registrations committed by this run: per-cell chains (no per-wave rebuild of the CSR)
+  FCHK(grow(X.pg_head, X.cap_pghead, (size_t)ncells));
+  FCHK(grow(X.vp_head, X.cap_vphead, (size_t)ncells));
+  FCHK(hipMemsetAsync(X.pg_head, 0xff, ncells * sizeof(int), st));
+  FCHK(hipMemsetAsync(X.vp_head, 0xff, ncells * sizeof(int), st));
+  FCHK(grow(X.pool_used, X.cap_pused, 1));
+  FCHK(hipMemsetAsync(X.pool_used, 0, sizeof(int), st));
+  size_t pool_need = 0;
+  X.pool_host = 0;
+  auto set_delta = [&]() {
+    c.pg_dhead = X.pg_head; c.vp_dhead = X.vp_head; c.d_item = X.d_item; c.d_next = X.d_next;
+  };
+  set_delta();
+  // ---- host mirrors: pgrids occupancy per cell, counts (clearCounts), collect order (queue)
   std::vector<int> pgoff(ncells + 1), order(c.nalive);
   FCHK(hipMemcpyAsync(pgoff.data(), B.pg_off, (ncells + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
   if (c.nalive) FCHK(hipMemcpyAsync(order.data(), B.order, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
   FCHK(hipStreamSynchronize(st));
   std::vector<int> occ(ncells);
   for (long long k = 0; k < ncells; ++k) occ[k] = pgoff[k + 1] - pgoff[k];
+  std::vector<int>().swap(pgoff);
   std::vector<unsigned char> counts(ncells, 0);
+  FCHK(grow(X.counts, X.cap_cnt, (size_t)ncells));
+  FCHK(hipMemsetAsync(X.counts, 0, ncells, st));
   std::priority_queue<QItem, std::vector<QItem>, QCmp> queue;
   long long seq = 0;
   for (int i = 0; i < c.nalive; ++i) H[order[i]].flag = 0;  // clearFlags (the collected patches)
@@ -1428,8 +1539,10 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
     }
   }
   int rank_next = c.nalive;
-  const int W = std::max(1, std::min(wave, kMaxWave));
-  FCHK(grow(X.counts, X.cap_cnt, (size_t)ncells));
+  const int G = std::max(1, sh.world), R = std::min(std::max(0, sh.rank), G - 1);
+  std::vector<long long> touched;
+  std::vector<unsigned char> tvals;
+  std::vector<char> xsend, xrecv;
   while (!queue.empty()) {
     stats[7]++;
     std::vector<int> parents;
@@ -1463,7 +1576,6 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
     }
     for (const int only : batches) {
       c.n = (int)H.size();
-      FCHK(hipMemcpyAsync(X.counts, counts.data(), ncells, hipMemcpyHostToDevice, st));
       hipLaunchKernelGGL(prepare_kernel, dim3(nblk((long long)np * 6)), dim3(256), 0, st, s, c.dev(), X.counts, X.parents,
                          np, X.cand_coord, X.cand_ok, X.cand, X.prep, X.status, cthr, only);
       FCHK(hipPeekAtLastError());
@@ -1479,31 +1591,68 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
         }
       }
       const int m = (int)slots.size();
+      // this rank's contiguous share of the survivors
+      const int chunk = (m + G - 1) / G;
+      const int lo = std::min(m, R * chunk), hi = std::min(m, lo + chunk), mine = hi - lo;
       std::vector<int> ostatus(m);
       std::vector<pmvs_patch> outp(m), prep(m);
-      if (m > 0) {
-        FCHK(grow(X.slots, X.cap_slots, (size_t)m));
-        FCHK(grow(X.cand2, X.cap_cand2, (size_t)m));
-        FCHK(grow(X.prep2, X.cap_prep2, (size_t)m));
-        FCHK(grow(X.res, X.cap_res, (size_t)m));
-        FCHK(grow(X.outp, X.cap_outp, (size_t)m));
-        FCHK(grow(X.ostatus, X.cap_ost, (size_t)m));
-        FCHK(hipMemcpyAsync(X.slots, slots.data(), m * sizeof(int), hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(gather_slots_kernel, dim3(nblk(m)), dim3(256), 0, st, X.slots, m, X.cand, X.prep, X.cand2, X.prep2);
-        FCHK(refine(X.cand2, m, X.res));
-        FCHK(hipMemsetAsync(B.counters + 4, 0, sizeof(int), st));
-        hipLaunchKernelGGL(depth_post_kernel, dim3(std::min(grid, m)), dim3(64), 0, st, s, c.dev(), X.res, m, X.outp,
-                           X.ostatus, B.scratch, B.counters + 4, B.counters + 3);
-        FCHK(hipPeekAtLastError());
-        FCHK(hipMemcpyAsync(ostatus.data(), X.ostatus, m * sizeof(int), hipMemcpyDeviceToHost, st));
-        FCHK(hipMemcpyAsync(outp.data(), X.outp, (size_t)m * sizeof(pmvs_patch), hipMemcpyDeviceToHost, st));
-        FCHK(hipMemcpyAsync(prep.data(), X.prep2, (size_t)m * sizeof(pmvs_patch), hipMemcpyDeviceToHost, st));
-      }
       int ovf = 0;
-      FCHK(read_int(B.counters + 3, &ovf, st));
+      hipError_t lerr = hipSuccess;
+      auto local = [&]() -> hipError_t {
+        if (m > 0) {
+          FCHK(grow(X.slots, X.cap_slots, (size_t)m));
+          FCHK(grow(X.cand2, X.cap_cand2, (size_t)m));
+          FCHK(grow(X.prep2, X.cap_prep2, (size_t)m));
+          FCHK(grow(X.res, X.cap_res, (size_t)m));
+          FCHK(grow(X.outp, X.cap_outp, (size_t)m));
+          FCHK(grow(X.ostatus, X.cap_ost, (size_t)m));
+          FCHK(hipMemcpyAsync(X.slots, slots.data(), m * sizeof(int), hipMemcpyHostToDevice, st));
+          hipLaunchKernelGGL(gather_slots_kernel, dim3(nblk(m)), dim3(256), 0, st, X.slots, m, X.cand, X.prep, X.cand2, X.prep2);
+          if (mine > 0) {
+            FCHK(refine(X.cand2 + lo, mine, X.res + lo));
+            FCHK(hipMemsetAsync(B.counters + 4, 0, sizeof(int), st));
+            hipLaunchKernelGGL(depth_post_kernel, dim3(std::min(grid, mine)), dim3(64), 0, st, s, c.dev(), X.res + lo, mine,
+                               X.outp + lo, X.ostatus + lo, B.scratch, B.counters + 4, B.counters + 3);
+            FCHK(hipPeekAtLastError());
+            FCHK(hipMemcpyAsync(ostatus.data() + lo, X.ostatus + lo, mine * sizeof(int), hipMemcpyDeviceToHost, st));
+            FCHK(hipMemcpyAsync(outp.data() + lo, X.outp + lo, (size_t)mine * sizeof(pmvs_patch), hipMemcpyDeviceToHost, st));
+          }
+          FCHK(hipMemcpyAsync(prep.data(), X.prep2, (size_t)m * sizeof(pmvs_patch), hipMemcpyDeviceToHost, st));
+        }
+        return read_int(B.counters + 3, &ovf, st);
+      };
+      lerr = local();
+      if (G > 1) {
+        // all-gather of [error, overflow, status[chunk], patch[chunk]] per rank
+        const size_t rec = sizeof(int) + sizeof(pmvs_patch);
+        const size_t bytes = 2 * sizeof(int) + (size_t)chunk * rec;
+        xsend.assign(bytes, 0);
+        xrecv.assign(bytes * G, 0);
+        int hdr[2] = {(int)lerr, ovf};
+        std::memcpy(xsend.data(), hdr, sizeof(hdr));
+        if (lerr == hipSuccess && mine > 0) {
+          std::memcpy(xsend.data() + 2 * sizeof(int), ostatus.data() + lo, mine * sizeof(int));
+          std::memcpy(xsend.data() + 2 * sizeof(int) + (size_t)chunk * sizeof(int), outp.data() + lo,
+                      (size_t)mine * sizeof(pmvs_patch));
+        }
+        if (sh.exchange(xsend.data(), bytes, xrecv.data()) != 0) return hipErrorUnknown;
+        for (int r = 0; r < G; ++r) {
+          const char* b = xrecv.data() + (size_t)r * bytes;
+          std::memcpy(hdr, b, sizeof(hdr));
+          if (hdr[0] != 0 && lerr == hipSuccess) lerr = hipErrorUnknown;  // another rank failed
+          ovf |= hdr[1];
+          const int rlo = std::min(m, r * chunk), rhi = std::min(m, rlo + chunk);
+          if (r == R || rhi <= rlo) continue;
+          std::memcpy(ostatus.data() + rlo, b + 2 * sizeof(int), (rhi - rlo) * sizeof(int));
+          std::memcpy(outp.data() + rlo, b + 2 * sizeof(int) + (size_t)chunk * sizeof(int),
+                      (size_t)(rhi - rlo) * sizeof(pmvs_patch));
+        }
+      }
+      FCHK(lerr);
       if (ovf) return hipErrorOutOfMemory;  // more than NB_CAP neighbours (reported by the API)
       // ---- commit in (parent priority, direction) order
       const int first = (int)H.size();
+      touched.clear();
       for (int k = 0; k < np * 6; ++k) {
         if (status[k] < 0) continue;
         const int par = parents[k / 6], dir = k % 6;
@@ -1548,10 +1697,12 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
         int full = 0, empty = 0;
         auto touch = [&](int t, int ix, int iy) {
           if (ix < 0 || ix >= X.gw[t] || iy < 0 || iy >= X.gh[t]) return;
-          unsigned char& cc = counts[h_tgoff[t] + (long long)iy * X.gw[t] + ix];
+          const long long cidx = h_tgoff[t] + (long long)iy * X.gw[t] + ix;
+          unsigned char& cc = counts[cidx];
           if (cthr <= cc) ++full;
           else ++empty;
           ++cc;
+          touched.push_back(cidx);
         };
         for (int i = 0; i < np_.num_images; ++i)
           if (np_.images[i] < s.tnum) touch(np_.images[i], np_.grids[i][0], np_.grids[i][1]);
@@ -1560,24 +1711,54 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
         for (int i = 0; i < np_.num_images; ++i) {  // addPatch: pgrids registration
           const int t = np_.images[i];
           if (t < s.tnum && 0 <= np_.grids[i][0] && np_.grids[i][0] < X.gw[t] && 0 <= np_.grids[i][1] &&
-              np_.grids[i][1] < X.gh[t])
+              np_.grids[i][1] < X.gh[t]) {
             occ[h_tgoff[t] + (long long)np_.grids[i][1] * X.gw[t] + np_.grids[i][0]]++;
+            ++pool_need;
+          }
         }
+        pool_need += np_.num_vimages;
         if ((int)H.size() >= cap) return hipErrorOutOfMemory;
         H.push_back(np_);
         alive.push_back(1);
         stats[6]++;
         if (add) queue.push({np_.tmp, seq++, (int)H.size() - 1});
       }
+      // device counts: the cells this commit touched (final values)
+      if (!touched.empty()) {
+        const int nt = (int)touched.size();
+        tvals.resize(nt);
+        for (int k = 0; k < nt; ++k) tvals[k] = counts[touched[k]];
+        FCHK(grow(X.tcells, X.cap_tcells, (size_t)nt));
+        FCHK(grow(X.tvals, X.cap_tvals, (size_t)nt));
+        FCHK(hipMemcpyAsync(X.tcells, touched.data(), nt * sizeof(long long), hipMemcpyHostToDevice, st));
+        FCHK(hipMemcpyAsync(X.tvals, tvals.data(), nt, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(counts_scatter_kernel, dim3(nblk(nt)), dim3(256), 0, st, X.tcells, X.tvals, nt, X.counts);
+      }
       const int added = (int)H.size() - first;
       if (added > 0) {
+        const size_t used_before = X.pool_host;
+        FCHK(grow_keep(X.d_item, X.cap_item, pool_need, used_before, st));
+        FCHK(grow_keep(X.d_next, X.cap_next, pool_need, used_before, st));
+        set_delta();
+        if (H.size() > pcap) {  // per-patch arrays the waves write, grown keeping their contents
+          const size_t ncap = std::min<size_t>((size_t)cap, std::max(H.size(), 2 * pcap));
+          size_t c1 = pcap, c2 = pcap, c3 = pcap, c4 = pcap;
+          FCHK(grow_keep(dP, dP_cap, ncap, (size_t)first, st));
+          FCHK(grow_keep(B.preg, c1, ncap, (size_t)first, st));
+          FCHK(grow_keep(B.vreg, c2, ncap, (size_t)first, st));
+          FCHK(grow_keep(B.order, c3, ncap, (size_t)rank_next, st));
+          FCHK(grow_keep(B.unit0, c4, ncap, (size_t)first, st));
+          B.cap_n = 0;  // the other per-patch buffers are re-reserved by the next pass
+          pcap = ncap;
+          c.P = dP;
+        }
         FCHK(hipMemcpyAsync(dP + first, H.data() + first, (size_t)added * sizeof(pmvs_patch), hipMemcpyHostToDevice, st));
         c.n = (int)H.size();
+        DeltaLists D{X.pg_head, X.vp_head, X.d_item, X.d_next, X.pool_used, (int)std::min<size_t>(X.cap_item, INT32_MAX)};
         hipLaunchKernelGGL(add_patches_kernel, dim3(nblk((long long)added * s.tnum)), dim3(256), 0, st, s, c.dev(), first,
-                           added, rank_next, B.preg, B.vreg, B.order, B.dpkey, B.unit0);
+                           added, rank_next, B.preg, B.vreg, B.order, B.dpkey, B.unit0, D);
+        X.pool_host = pool_need;
         rank_next += added;
-        FCHK(build_lists(c, 0));
-        FCHK(build_lists(c, 1));
       }
     }
   }

@@ -51,13 +51,28 @@ struct ExpandBuffers {
   pmvs_patch *prep = nullptr, *prep2 = nullptr, *outp = nullptr;
   pmvs_refined* res = nullptr;
   unsigned char* counts = nullptr;
+  // registrations committed during the run: per-cell chain heads + entry pool (FilterDev delta)
+  int *pg_head = nullptr, *vp_head = nullptr, *d_item = nullptr, *d_next = nullptr, *pool_used = nullptr;
+  long long* tcells = nullptr;  // cells whose counts a commit changed, and their values
+  unsigned char* tvals = nullptr;
+  size_t pool_host = 0;
   size_t cap_coord = 0, cap_ok = 0, cap_cand = 0, cap_prep = 0, cap_slots = 0, cap_prep2 = 0, cap_res = 0, cap_outp = 0,
-         cap_ost = 0, cap_par = 0, cap_status = 0, cap_cand2 = 0, cap_alive = 0, cap_cnt = 0;
+         cap_ost = 0, cap_par = 0, cap_status = 0, cap_cand2 = 0, cap_alive = 0, cap_cnt = 0, cap_pghead = 0,
+         cap_vphead = 0, cap_item = 0, cap_next = 0, cap_pused = 0, cap_tcells = 0, cap_tvals = 0;
   std::vector<int> gw, gh;  // grid sizes of the target images
   ~ExpandBuffers();
 };
 using RefineFn = std::function<hipError_t(const pmvs_candidate* d_in, int n, pmvs_refined* d_out)>;
-hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs_patch* dP, std::vector<pmvs_patch>& H,
-                       std::vector<int>& alive, int cap, long long ncells, const long long* h_tgoff, int wave, int cthr,
-                       int flags, int grid, hipStream_t st, const RefineFn& refine, long long stats[8]);
+// All-gather of `bytes` per rank into recv (world * bytes, rank order); 0 = OK.
+using ExchangeFn = std::function<int(const void* send, size_t bytes, void* recv)>;
+struct Shard {
+  int rank = 0, world = 1;
+  ExchangeFn exchange;
+};
+// dP/dP_cap: the device patch array (grown, contents kept, as the model grows); cap bounds the
+// result size.
+hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs_patch*& dP, size_t& dP_cap,
+                       std::vector<pmvs_patch>& H, std::vector<int>& alive, int cap, long long ncells,
+                       const long long* h_tgoff, int wave, int cthr, int flags, int grid, hipStream_t st,
+                       const RefineFn& refine, const Shard& sh, long long stats[8]);
 }  // namespace pmvsdev

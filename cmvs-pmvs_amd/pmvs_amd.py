@@ -78,7 +78,10 @@ class FilterStats(C.Structure):
 
 class ExpandStats(C.Structure):
     _fields_ = [(k, C.c_int64) for k in ("parents", "candidates", "fail_prep", "fail_pre", "fail_post",
-                                          "fail_commit", "added", "waves")] + [("wall_ms", C.c_double)]
+                                          "fail_commit", "added", "waves")] + [("wall_ms", C.c_double)] + \
+               [(k, C.c_int64) for k in ("refined", "evals", "tex_valid")] + [("refine_ms", C.c_double)]
+
+    WORK = ("wall_ms", "refined", "evals", "tex_valid", "refine_ms")  # timing / per-rank work fields
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -106,7 +109,11 @@ EXPORTS = ["pmvs_last_error", "pmvs_device_count", "pmvs_scene_create", "pmvs_sc
            "pmvs_synth_candidates", "pmvs_selftest_math", "pmvs_selftest_bobyqa", "pmvs_camera_load",
            "pmvs_ppm_load", "pmvs_options_load", "pmvs_options_free", "pmvs_write_patches", "pmvs_write_pset",
            "pmvs_write_ply", "pmvs_patch_colors", "pmvs_filter_run",
-           "pmvs_expand_run"]
+           "pmvs_expand_run", "pmvs_expand_fetch", "pmvs_scene_set_shard", "pmvs_thread_exchange_create",
+           "pmvs_thread_exchange_ctx", "pmvs_thread_allgather", "pmvs_thread_exchange_destroy"]
+
+# int fn(void* ctx, const void* send, int64_t bytes, void* recv): all-gather (pmvs_allgather_fn)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p)
 
 _lib = None
 
@@ -150,12 +157,24 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.pmvs_filter_run.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(FilterStats)]
     lib.pmvs_expand_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                     C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(ExpandStats)]
+    lib.pmvs_expand_fetch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32]
+    lib.pmvs_scene_set_shard.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
+    lib.pmvs_thread_exchange_create.argtypes = [C.c_int32]
+    lib.pmvs_thread_exchange_create.restype = C.c_void_p
+    lib.pmvs_thread_exchange_ctx.argtypes = [C.c_void_p, C.c_int32]
+    lib.pmvs_thread_exchange_ctx.restype = C.c_void_p
+    lib.pmvs_thread_allgather.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
+    lib.pmvs_thread_exchange_destroy.argtypes = [C.c_void_p]
+    lib.pmvs_thread_exchange_destroy.restype = None
     for fn in EXPORTS:
         getattr(lib, fn).restype = getattr(lib, fn).restype or C.c_int
     lib.pmvs_last_error.restype = C.c_char_p
     lib.pmvs_device_count.restype = C.c_int32
     lib.pmvs_scene_destroy.restype = None
     lib.pmvs_options_free.restype = None
+    lib.pmvs_thread_exchange_create.restype = C.c_void_p
+    lib.pmvs_thread_exchange_ctx.restype = C.c_void_p
+    lib.pmvs_thread_exchange_destroy.restype = None
     _lib = lib
     return lib
 
@@ -331,17 +350,27 @@ class Scene:
                    after_seeds: bool = False):
         """One CExpand::run on the device (expand.cpp:17-406): returns (patches, alive, stats).
 
-        The result holds the input patches (flags updated) followed by the new ones."""
+        The result holds the input patches (flags updated) followed by the new ones; `cap` bounds
+        its size (default: 2^30).  Collective when a shard is set (set_shard)."""
         pa = np.ascontiguousarray(patches, PATCH_DTYPE)
         al = np.ones(len(pa), np.int32) if alive is None else np.ascontiguousarray(alive, np.int32)
-        cap = int(cap or max(4 * len(pa), len(pa) + 1024))
-        out = np.zeros(cap, PATCH_DTYPE)
-        aout = np.zeros(cap, np.int32)
+        cap = int(cap or (1 << 30))
         n_out = C.c_int32(0)
         st = ExpandStats()
         _check(self.lib.pmvs_expand_run(self.handle, _ptr(pa), _ptr(al), len(pa), wave, count_threshold,
-                                        int(after_seeds), _ptr(out), _ptr(aout), cap, C.byref(n_out), C.byref(st)))
-        return out[:n_out.value].copy(), aout[:n_out.value].copy(), st.as_dict()
+                                        int(after_seeds), None, None, cap, C.byref(n_out), C.byref(st)))
+        out = np.empty(n_out.value, PATCH_DTYPE)
+        aout = np.empty(n_out.value, np.int32)
+        _check(self.lib.pmvs_expand_fetch(self.handle, _ptr(out), _ptr(aout), n_out.value))
+        return out, aout, st.as_dict()
+
+    def set_shard(self, rank: int, world: int, fn=None, ctx=None):
+        """Shard the expansion over `world` ranks (pmvs_scene_set_shard); fn is a C function
+        pointer (pmvs_allgather_fn: the library's pmvs_thread_allgather, or an ALLGATHER_FN
+        callback such as DistExchange's).  The callback object must outlive the scene's use."""
+        self._shard_keep = fn
+        ptr = None if fn is None else (fn if isinstance(fn, int) else C.cast(fn, C.c_void_p).value)
+        _check(self.lib.pmvs_scene_set_shard(self.handle, rank, world, ptr, ctx))
 
     def run_loop(self, seeds: np.ndarray, threshold: float, iterations: int = 3, wave: int = 4096, cap=None,
                  after_seeds: bool = True):
@@ -353,7 +382,6 @@ class Scene:
         before = np.float32(ncc - np.float32(0.3))
         cthr, depth = 4, 1
         model = np.ascontiguousarray(seeds, PATCH_DTYPE)
-        cap = int(cap or max(64 * len(model), 1 << 16))
         log = []
         for t in range(iterations):
             self.set_thresholds(float(ncc), float(before), depth)
@@ -512,3 +540,64 @@ def synth_scene(num_views: int, width: int, height: int, level: int = 1, num_tar
     rgb, proj = synth_ring(p, nthreads=nthreads)
     return SceneInputs(images=[rgb[i] for i in range(num_views)], projections=proj,
                        num_targets=p.num_targets, level=level, **opts), p
+
+
+class ThreadExchange:
+    """In-process all-gather among `world` threads (pmvs_thread_exchange): scene r of a group uses
+    set_shard(r, world, *group.endpoint(r)).  Used to run several sharded scenes on one GPU."""
+
+    def __init__(self, world: int):
+        self.lib = load_library()
+        self.world = world
+        self.handle = self.lib.pmvs_thread_exchange_create(world)
+        if not self.handle:
+            raise PmvsError("pmvs_thread_exchange_create failed")
+
+    def endpoint(self, rank: int):
+        fn = C.cast(self.lib.pmvs_thread_allgather, C.c_void_p).value
+        return fn, self.lib.pmvs_thread_exchange_ctx(self.handle, rank)
+
+    def close(self):
+        if self.handle:
+            self.lib.pmvs_thread_exchange_destroy(self.handle)
+            self.handle = None
+
+
+class DistExchange:
+    """pmvs_allgather_fn over torch.distributed: one process per GPU (RCCL over xGMI when the
+    process group's backend is nccl; gloo on CPUs).  The host buffer of each expansion wave is
+    staged through a device tensor for RCCL.  Keep the object alive while the scene uses it."""
+
+    def __init__(self, group=None, device=None):
+        import torch
+        import torch.distributed as dist
+        self.dist, self.torch, self.group = dist, torch, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        backend = dist.get_backend(group)
+        self.device = device if device is not None else (
+            torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu"))
+        self.error = None
+        self.fn = ALLGATHER_FN(self._allgather)
+
+    def _allgather(self, ctx, send, nbytes, recv):
+        try:
+            torch = self.torch
+            src = np.ctypeslib.as_array(C.cast(send, C.POINTER(C.c_uint8)), shape=(nbytes,))
+            t = torch.from_numpy(src.copy()).to(self.device)
+            if self.device.type == "cpu":  # gloo: list form
+                parts = [torch.empty_like(t) for _ in range(self.world)]
+                self.dist.all_gather(parts, t, group=self.group)
+                res = torch.cat(parts).numpy()
+            else:
+                out = torch.empty(nbytes * self.world, dtype=torch.uint8, device=self.device)
+                self.dist.all_gather_into_tensor(out, t, group=self.group)
+                res = out.cpu().numpy()
+            C.memmove(recv, res.ctypes.data, nbytes * self.world)
+            return 0
+        except Exception as e:  # reported by pmvs_expand_run as a failed exchange
+            self.error = e
+            return -1
+
+    def attach(self, scene: "Scene"):
+        scene.set_shard(self.rank, self.world, self.fn, None)

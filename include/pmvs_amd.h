@@ -228,16 +228,44 @@ pmvs_status pmvs_filter_run(pmvs_scene* scene, pmvs_patch* patches, int32_t n, i
  * schedule), candidates are refined with preProcess -> refinePatch ->
  * postProcess including the depth >= 1 steps (setVImagesVGrids; check() at depth >= 2) and
  * committed in (parent priority, direction) order.  count_threshold = _countThreshold1 (4 at the
- * first expansion, 2 after updateThreshold).  out/alive_out (capacity cap) receive the old
- * patches (with updated _flag/_dflag) followed by the new ones; *n_out their number. */
+ * first expansion, 2 after updateThreshold).  The result is the old patches (with updated
+ * _flag/_dflag) followed by the new ones, at most `cap` in all; *n_out is their number.
+ * out/alive_out receive it when non-NULL; with out == alive_out == NULL the scene keeps it and
+ * pmvs_expand_fetch copies it out (so the caller can size its arrays after the run).
+ * With a shard set (pmvs_scene_set_shard) the call is collective: every rank passes the same
+ * model and arguments and gets the same result. */
 #define PMVS_EXPAND_AFTER_SEEDS 1 /* model straight from the seed phase: no depth maps yet (findMatch.cpp:193-202) */
 typedef struct pmvs_expand_stats {
   int64_t parents, candidates, fail_prep, fail_pre, fail_post, fail_commit, added, waves;
   double wall_ms;
+  /* this rank's refine work (preProcess -> refinePatch -> postProcess of its candidate share):
+   * candidates refined, my_f + computeINCC evaluations, valid textures over them, summed
+   * refine-kernel time (HIP events) */
+  int64_t refined, evals, tex_valid;
+  double refine_ms;
 } pmvs_expand_stats;
 pmvs_status pmvs_expand_run(pmvs_scene* scene, const pmvs_patch* patches, const int32_t* alive, int32_t n,
                             int32_t wave, int32_t count_threshold, int32_t flags, pmvs_patch* out, int32_t* alive_out,
                             int32_t cap, int32_t* n_out, pmvs_expand_stats* stats);
+/* Copies the result the last pmvs_expand_run kept (out == NULL) and releases it; n = *n_out. */
+pmvs_status pmvs_expand_fetch(pmvs_scene* scene, pmvs_patch* out, int32_t* alive_out, int32_t n);
+
+/* Multi-GPU sharding of the expansion: one scene per GPU/rank, all holding the
+ * same model.  Each wave's candidates are split into contiguous rank ranges for the refine and
+ * the per-candidate results are all-gathered through `fn` before the (replicated) commit.
+ * fn(ctx, send, bytes, recv): all-gather of `bytes` from every rank into recv (world * bytes, in
+ * rank order), host memory, returns 0 on success; it is called from the thread that called
+ * pmvs_expand_run.  world = 1 (or fn = NULL) turns sharding off. */
+typedef int (*pmvs_allgather_fn)(void* ctx, const void* send, int64_t bytes, void* recv);
+pmvs_status pmvs_scene_set_shard(pmvs_scene* scene, int32_t rank, int32_t world, pmvs_allgather_fn fn, void* ctx);
+
+/* An in-process all-gather among `world` threads (one scene per thread, e.g. several scenes on
+ * one GPU): pmvs_thread_allgather with ctx = pmvs_thread_exchange_ctx(group, rank). */
+typedef struct pmvs_thread_exchange pmvs_thread_exchange;
+pmvs_thread_exchange* pmvs_thread_exchange_create(int32_t world);
+void* pmvs_thread_exchange_ctx(pmvs_thread_exchange* group, int32_t rank);
+int pmvs_thread_allgather(void* ctx, const void* send, int64_t bytes, void* recv);
+void pmvs_thread_exchange_destroy(pmvs_thread_exchange* group);
 
 /* ---------------------------------------------------------------------------------------
  * pmvs2 input / output surface (SURVEY.md §8(b) external boundary, §8 row a19).  Host code;

@@ -107,8 +107,92 @@ def test_full_loop_matches_oracle(gpu_available, oracle_mod, wave):
     o.close()
     for a, b in zip(log_g, log_o):
         assert a["patches"] == b["patches"], (a, b)
-        assert {k: v for k, v in a["expand"].items() if k != "wall_ms"} == b["expand"]
+        assert {k: v for k, v in a["expand"].items() if k not in P.ExpandStats.WORK} == b["expand"]
         assert [a["filter"][k] for k in ("removed_outside", "removed_exact", "removed_neighbor",
                                          "removed_groups")] == b["filter"]
     assert log_g[-1]["patches"] > 5 * len(pa)
     compare(out_g, np.ones(len(out_g), np.int32), {}, out_o, np.ones(len(out_o), np.int32), {})
+
+
+def test_expand_device_growth_small_waves(gpu_available, oracle_mod):
+    """wave = 8: the device patch arrays start at (model + 12 waves + 1024) and are regrown
+    (contents kept) several times during the run; the result still equals the oracle's."""
+    import pmvs_amd as P
+    inp, p = P.synth_scene(6, 480, 360, level=1, supersample=2)
+    g = P.Scene(inp)
+    o = oracle_mod.OracleScene(inp)
+    pa = seed_model(P, g, inp, p, 120, 9)
+    for sc in (g, o):
+        sc.set_thresholds(inp.threshold, inp.threshold - 0.3, 1)
+    out_g, al_g, st_g = g.expand_run(pa, wave=8)
+    out_o, al_o, st_o = o.expand_run(pa, wave=8, cap=200000)
+    g.close()
+    o.close()
+    assert len(out_g) > 2 * (len(pa) + 12 * 8 + 1024)
+    compare(out_g, al_g, st_g, out_o, al_o, st_o)
+
+
+def run_sharded(P, inp, model, world, fn, **kw):
+    """`world` scenes on GPU 0, one per thread, sharing one in-process all-gather (the same
+    protocol bench.py runs with one process per GPU over RCCL)."""
+    import threading
+    ex = P.ThreadExchange(world)
+    scenes = [P.Scene(inp) for _ in range(world)]
+    for r, sc in enumerate(scenes):
+        sc.set_shard(r, world, *ex.endpoint(r))
+    res, errs = [None] * world, []
+
+    def work(r):
+        try:
+            res[r] = fn(scenes[r], model, **kw)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    for sc in scenes:
+        sc.close()
+    ex.close()
+    assert not errs, errs
+    return res
+
+
+@pytest.mark.parametrize("world,wave", [(2, 256), (3, 64)])
+def test_sharded_expand_matches_single_rank(gpu_available, world, wave):
+    """Sharded expansion: every rank's model after the run is bit-identical to
+    the one-rank run with the same wave, and the ranks' refine shares add up to the candidates."""
+    import pmvs_amd as P
+    inp, p = P.synth_scene(6, 480, 360, level=1, supersample=2)
+    g = P.Scene(inp)
+    pa = seed_model(P, g, inp, p, 300, 3)
+    g.set_thresholds(inp.threshold, inp.threshold - 0.3, 2)
+    ref, al_ref, st_ref = g.expand_run(pa, wave=wave)
+    g.close()
+
+    def fn(sc, model, **kw):
+        sc.set_thresholds(inp.threshold, inp.threshold - 0.3, 2)
+        return sc.expand_run(model, **kw)
+
+    res = run_sharded(P, inp, pa, world, fn, wave=wave)
+    for out, al, st in res:
+        compare(out, al, {k: v for k, v in st.items() if k not in P.ExpandStats.WORK}, ref, al_ref,
+                {k: v for k, v in st_ref.items() if k not in P.ExpandStats.WORK})
+    assert sum(r[2]["refined"] for r in res) == st_ref["refined"]
+    assert sum(r[2]["evals"] for r in res) == st_ref["evals"]
+    assert all(r[2]["refined"] > 0 for r in res)
+
+
+def test_sharded_full_loop_matches_single_rank(gpu_available):
+    import pmvs_amd as P
+    inp, p = P.synth_scene(6, 480, 360, level=1, supersample=2)
+    g = P.Scene(inp)
+    pa = seed_model(P, g, inp, p, 200, 7)
+    ref, log_ref = g.run_loop(pa, inp.threshold, wave=512)
+    g.close()
+    res = run_sharded(P, inp, pa, 2, lambda sc, m, **kw: sc.run_loop(m, inp.threshold, **kw), wave=512)
+    for out, log in res:
+        assert [x["patches"] for x in log] == [x["patches"] for x in log_ref]
+        compare(out, np.ones(len(out), np.int32), {}, ref, np.ones(len(ref), np.int32), {})
