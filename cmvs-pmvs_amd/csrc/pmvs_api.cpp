@@ -192,8 +192,9 @@ struct pmvs_scene {
   int shard_rank = 0, shard_world = 1;
   pmvs_allgather_fn shard_fn = nullptr;
   void* shard_ctx = nullptr;
-  std::vector<pmvs_patch> xres;
+  int xkept = -1, lkept = -1;   // models kept on the device for pmvs_expand_fetch / pmvs_loop_fetch
   std::vector<int> xalive;
+  DBuf<pmvs_patch> fpatches2;   // compaction target of pmvs_run_loop
   // staging for host-pointer calls
   DBuf<pmvs_candidate> cand;
   DBuf<pmvs_refined> res;
@@ -203,7 +204,7 @@ struct pmvs_scene {
   DBuf<float> tout;
   DBuf<int> tvalid;
   ~pmvs_scene() {
-    views.release(); pyr.release(); masks.release(); edges.release(); vis_off.release(); vis.release();
+    fpatches2.release(); views.release(); pyr.release(); masks.release(); edges.release(); vis_off.release(); vis.release();
     bindexes.release(); scratch.release(); stats.release(); jobs.release(); fpatches.release(); fkeep.release(); cand.release(); res.release(); evq.release();
     evout.release(); tq.release(); tout.release(); tvalid.release();
     if (ev0) (void)hipEventDestroy(ev0);
@@ -221,6 +222,16 @@ pmvs_status ensure(DBuf<T>& b, size_t n) {
   hipError_t e = b.alloc(n);
   if (e != hipSuccess) return fail(PMVS_ENOMEM, "hipMalloc(%zu bytes): %s", n * sizeof(T), hipGetErrorString(e));
   return PMVS_OK;
+}
+template <class T>
+pmvs_status ensure_keep_data(pmvs_scene*, DBuf<T>& b, size_t n) { return ensure(b, n); }
+int grow_alive(pmvs_scene* sc, int n) {
+  ExpandBuffers& X = sc->xbuf;
+  if ((size_t)n <= X.cap_alive && X.alive) return 0;
+  if (X.alive) (void)hipFree(X.alive);
+  X.alive = nullptr;
+  X.cap_alive = (size_t)n;
+  return hipMalloc((void**)&X.alive, (size_t)n * sizeof(int)) == hipSuccess ? 0 : 1;
 }
 }  // namespace
 
@@ -709,14 +720,10 @@ pmvs_status pmvs_filter_run(pmvs_scene* sc, pmvs_patch* patches, int32_t n, int3
   return PMVS_OK;
 }
 
-pmvs_status pmvs_expand_run(pmvs_scene* sc, const pmvs_patch* patches, const int32_t* alive, int32_t n, int32_t wave,
-                            int32_t count_threshold, int32_t flags, pmvs_patch* out, int32_t* alive_out, int32_t cap,
-                            int32_t* n_out, pmvs_expand_stats* stats) {
-  const bool keep = !out && !alive_out;
-  if (!sc || n < 0 || (n > 0 && (!patches || !alive)) || (!keep && (!out || !alive_out)) || !n_out || cap < n)
-    return fail(PMVS_EINVAL, "invalid argument");
-  if (wave < 1 || wave > kMaxWave) return fail(PMVS_EINVAL, "wave must be in [1, %d]", kMaxWave);
-  if (sc->ds.tnum > 64) return fail(PMVS_EUNSUPPORTED, "expansion: more than 64 target images");
+namespace {
+
+// validation of a caller's patch set (image counts and indexes)
+pmvs_status check_patches(const pmvs_scene* sc, const pmvs_patch* patches, int n) {
   for (int i = 0; i < n; ++i) {
     const pmvs_patch& p = patches[i];
     if (p.num_images < 1 || p.num_images > PMVS_MAX_IMAGES || p.num_vimages < 0 || p.num_vimages > PMVS_MAX_IMAGES)
@@ -726,12 +733,10 @@ pmvs_status pmvs_expand_run(pmvs_scene* sc, const pmvs_patch* patches, const int
     for (int k = 0; k < p.num_vimages; ++k)
       if (p.vimages[k] < 0 || p.vimages[k] >= sc->ds.tnum) return fail(PMVS_EINVAL, "patch %d: vimage", i);
   }
-  if (stats) std::memset(stats, 0, sizeof(*stats));
-  *n_out = 0;
-  sc->xres.clear();
-  sc->xalive.clear();
-  if (n == 0) return PMVS_OK;
-  HIPCHK(hipSetDevice(sc->device));
+  return PMVS_OK;
+}
+
+std::vector<long long> target_cells(pmvs_scene* sc) {
   std::vector<long long> tgoff(sc->ds.tnum + 1, 0);
   sc->xbuf.gw.assign(sc->ds.tnum, 0);
   sc->xbuf.gh.assign(sc->ds.tnum, 0);
@@ -741,8 +746,14 @@ pmvs_status pmvs_expand_run(pmvs_scene* sc, const pmvs_patch* patches, const int
     sc->xbuf.gh[t] = (v.h[sc->ds.level] + sc->ds.csize - 1) / sc->ds.csize;
     tgoff[t + 1] = tgoff[t] + (long long)sc->xbuf.gw[t] * sc->xbuf.gh[t];
   }
-  std::vector<pmvs_patch> H(patches, patches + n);
-  std::vector<int> al(alive, alive + n);
+  return tgoff;
+}
+
+// One expansion run on the device-resident model sc->fpatches[0, n0) with alive flags
+// sc->xbuf.alive; *n_out patches afterwards.
+pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int cthr, int flags, int cap, int* n_out,
+                          pmvs_expand_stats* stats) {
+  const std::vector<long long> tgoff = target_cells(sc);
   // refine-work accounting: device counters accumulate over the run (only the work-queue heads
   // are reset per launch); the refine-kernel time of each launch is read at the next one, when
   // the host has synchronised in between.
@@ -776,9 +787,9 @@ pmvs_status pmvs_expand_run(pmvs_scene* sc, const pmvs_patch* patches, const int
   }
   long long sv[8];
   const auto t0 = std::chrono::steady_clock::now();
-  const hipError_t e = expand_pass(sc->ds, sc->fbuf, sc->xbuf, sc->fpatches.p, sc->fpatches.n, H, al, cap,
-                                   tgoff[sc->ds.tnum], tgoff.data(), wave, count_threshold, flags, sc->grid, sc->stream,
-                                   refine, sh, sv);
+  const hipError_t e = expand_pass(sc->ds, sc->fbuf, sc->xbuf, sc->fpatches.p, sc->fpatches.n, n0, sc->xbuf.alive, cap,
+                                   tgoff[sc->ds.tnum], tgoff.data(), wave, cthr, flags, sc->grid, sc->stream, refine, sh,
+                                   sv, n_out, min_cands);
   if (e == hipErrorOutOfMemory)
     return fail(PMVS_EUNSUPPORTED, "expansion: capacity %d exceeded or a patch has more than 1024 neighbours", cap);
   if (e == hipErrorUnknown && sh.world > 1) return fail(PMVS_EDEVICE, "expansion: the shard exchange or another rank failed");
@@ -788,15 +799,8 @@ pmvs_status pmvs_expand_run(pmvs_scene* sc, const pmvs_patch* patches, const int
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   DevStats ds{};
   HIPCHK(hipMemcpy(&ds, sc->stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));
-  *n_out = (int32_t)H.size();
-  if (keep) {
-    sc->xres.swap(H);
-    sc->xalive.swap(al);
-  } else {
-    std::memcpy(out, H.data(), H.size() * sizeof(pmvs_patch));
-    std::memcpy(alive_out, al.data(), al.size() * sizeof(int));
-  }
   if (stats) {
+    std::memset(stats, 0, sizeof(*stats));
     stats->parents = sv[0]; stats->candidates = sv[1]; stats->fail_prep = sv[2]; stats->fail_pre = sv[3];
     stats->fail_post = sv[4]; stats->fail_commit = sv[5]; stats->added = sv[6]; stats->waves = sv[7];
     stats->wall_ms = ms;
@@ -809,15 +813,146 @@ pmvs_status pmvs_expand_run(pmvs_scene* sc, const pmvs_patch* patches, const int
   return PMVS_OK;
 }
 
+// One filter pass on the device-resident model sc->fpatches[0, n); keep flags in sc->fkeep.
+pmvs_status filter_device(pmvs_scene* sc, int n, pmvs_filter_stats* stats) {
+  if (stats) std::memset(stats, 0, sizeof(*stats));
+  if (n == 0) return PMVS_OK;
+  pmvs_status st;
+  if ((st = ensure(sc->fkeep, n))) return st;
+  std::vector<long long> tgoff = target_cells(sc);
+  HIPCHK(hipEventRecord(sc->ev0, sc->stream));
+  int counts[4], overflow = 0;
+  HIPCHK(filter_pass(sc->ds, sc->fbuf, sc->fpatches.p, n, tgoff[sc->ds.tnum], tgoff.data(), sc->grid, sc->stream, counts,
+                     &overflow, sc->fkeep.p));
+  HIPCHK(hipEventRecord(sc->ev1, sc->stream));
+  HIPCHK(hipStreamSynchronize(sc->stream));
+  if (overflow) return fail(PMVS_EUNSUPPORTED, "filterNeighbor: %d patches with more than 1024 neighbours", overflow);
+  if (stats) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, sc->ev0, sc->ev1);
+    stats->input = n;
+    stats->removed_outside = counts[0];
+    stats->removed_exact = counts[1];
+    stats->removed_neighbor = counts[2];
+    stats->removed_groups = counts[3];
+    stats->kept = n - counts[0] - counts[1] - counts[2] - counts[3];
+    stats->kernel_ms = ms;
+  }
+  sc->last_refine = false;
+  return PMVS_OK;
+}
+
+}  // namespace
+
+pmvs_status pmvs_expand_run(pmvs_scene* sc, const pmvs_patch* patches, const int32_t* alive, int32_t n, int32_t wave,
+                            int32_t min_candidates, int32_t count_threshold, int32_t flags, pmvs_patch* out, int32_t* alive_out, int32_t cap,
+                            int32_t* n_out, pmvs_expand_stats* stats) {
+  const bool keep = !out && !alive_out;
+  if (!sc || n < 0 || (n > 0 && (!patches || !alive)) || (!keep && (!out || !alive_out)) || !n_out || cap < n)
+    return fail(PMVS_EINVAL, "invalid argument");
+  if (wave < 1 || wave > kMaxWave) return fail(PMVS_EINVAL, "wave must be in [1, %d]", kMaxWave);
+  if (sc->ds.tnum > 64) return fail(PMVS_EUNSUPPORTED, "expansion: more than 64 target images");
+  pmvs_status st;
+  if ((st = check_patches(sc, patches, n))) return st;
+  if (stats) std::memset(stats, 0, sizeof(*stats));
+  *n_out = 0;
+  sc->xkept = keep ? 0 : -1;
+  sc->xalive.clear();
+  if (n == 0) return PMVS_OK;
+  HIPCHK(hipSetDevice(sc->device));
+  if ((st = ensure(sc->fpatches, n))) return st;
+  if (grow_alive(sc, n)) return fail(PMVS_ENOMEM, "alive flags");
+  HIPCHK(hipMemcpyAsync(sc->fpatches.p, patches, (size_t)n * sizeof(pmvs_patch), hipMemcpyHostToDevice, sc->stream));
+  HIPCHK(hipMemcpyAsync(sc->xbuf.alive, alive, (size_t)n * sizeof(int), hipMemcpyHostToDevice, sc->stream));
+  int nn = 0;
+  if (min_candidates < 0) return fail(PMVS_EINVAL, "min_candidates %d", min_candidates);
+  if ((st = expand_device(sc, n, wave, min_candidates, count_threshold, flags, cap, &nn, stats))) return st;
+  *n_out = nn;
+  std::vector<int> al(alive, alive + n);
+  al.resize(nn, 1);
+  if (keep) {
+    sc->xkept = nn;
+    sc->xalive.swap(al);
+    return PMVS_OK;
+  }
+  HIPCHK(hipMemcpy(out, sc->fpatches.p, (size_t)nn * sizeof(pmvs_patch), hipMemcpyDeviceToHost));
+  std::memcpy(alive_out, al.data(), (size_t)nn * sizeof(int));
+  return PMVS_OK;
+}
+
 pmvs_status pmvs_expand_fetch(pmvs_scene* sc, pmvs_patch* out, int32_t* alive_out, int32_t n) {
   if (!sc || n < 0 || (n > 0 && (!out || !alive_out))) return fail(PMVS_EINVAL, "invalid argument");
-  if ((size_t)n != sc->xres.size()) return fail(PMVS_EINVAL, "expand_fetch: %d patches kept, %d asked", (int)sc->xres.size(), n);
+  if (n != sc->xkept) return fail(PMVS_EINVAL, "expand_fetch: %d patches kept, %d asked", sc->xkept, n);
   if (n) {
-    std::memcpy(out, sc->xres.data(), (size_t)n * sizeof(pmvs_patch));
-    std::memcpy(alive_out, sc->xalive.data(), (size_t)n * sizeof(int));
+    HIPCHK(hipSetDevice(sc->device));
+    HIPCHK(hipMemcpy(out, sc->fpatches.p, (size_t)n * sizeof(pmvs_patch), hipMemcpyDeviceToHost));
+    if (alive_out) std::memcpy(alive_out, sc->xalive.data(), (size_t)n * sizeof(int));
   }
-  std::vector<pmvs_patch>().swap(sc->xres);
+  sc->xkept = -1;
   std::vector<int>().swap(sc->xalive);
+  return PMVS_OK;
+}
+
+pmvs_status pmvs_run_loop(pmvs_scene* sc, const pmvs_patch* seeds, int32_t n, float threshold, int32_t iterations,
+                          int32_t wave, int32_t min_candidates, int32_t flags, int32_t cap, int32_t* n_out, pmvs_loop_iter* iters) {
+  if (!sc || n < 0 || (n > 0 && !seeds) || !n_out || iterations < 0 || cap < n || min_candidates < 0)
+    return fail(PMVS_EINVAL, "invalid argument");
+  if (wave < 1 || wave > kMaxWave) return fail(PMVS_EINVAL, "wave must be in [1, %d]", kMaxWave);
+  if (sc->ds.tnum > 64) return fail(PMVS_EUNSUPPORTED, "expansion: more than 64 target images");
+  pmvs_status st;
+  if ((st = check_patches(sc, seeds, n))) return st;
+  *n_out = 0;
+  sc->lkept = -1;
+  if (iters) std::memset(iters, 0, sizeof(pmvs_loop_iter) * (size_t)iterations);
+  HIPCHK(hipSetDevice(sc->device));
+  if ((st = ensure(sc->fpatches, std::max(n, 1)))) return st;
+  if (n) HIPCHK(hipMemcpyAsync(sc->fpatches.p, seeds, (size_t)n * sizeof(pmvs_patch), hipMemcpyHostToDevice, sc->stream));
+  // CFindMatch::run after the seed phase (findMatch.cpp:196-217); updateThreshold in float
+  // (findMatch.cpp:23-28): before = threshold - 0.3f (findMatch.cpp:104)
+  float ncc = threshold, before = threshold - 0.3f;
+  int cthr = 4, depth = 1, cur = n;
+  for (int it = 0; it < iterations; ++it) {
+    sc->ds.depth = depth;
+    sc->ds.nccThreshold = ncc;
+    sc->ds.nccThresholdBefore = before;
+    if (grow_alive(sc, std::max(cur, 1))) return fail(PMVS_ENOMEM, "alive flags");
+    HIPCHK(fill_int(sc->xbuf.alive, cur, 1, sc->stream));
+    pmvs_loop_iter li{};
+    li.depth = depth;
+    int nn = cur;
+    if (cur > 0 && (st = expand_device(sc, cur, wave, min_candidates, cthr, (it == 0 && (flags & PMVS_EXPAND_AFTER_SEEDS)) ? 1 : 0, cap,
+                                       &nn, &li.expand)))
+      return st;
+    if ((st = filter_device(sc, nn, &li.filter))) return st;
+    int kept = 0;
+    if (nn > 0) {
+      if ((st = ensure_keep_data(sc, sc->fpatches2, sc->fpatches.n))) return st;
+      HIPCHK(compact_model(sc->fbuf, sc->fpatches.p, nn, sc->fkeep.p, sc->fpatches2.p, &kept, sc->stream));
+      std::swap(sc->fpatches.p, sc->fpatches2.p);
+      std::swap(sc->fpatches.n, sc->fpatches2.n);
+    }
+    cur = kept;
+    li.patches = kept;
+    if (iters) iters[it] = li;
+    ncc -= 0.05f;
+    before -= 0.05f;
+    cthr = 2;
+    ++depth;
+  }
+  HIPCHK(hipStreamSynchronize(sc->stream));
+  *n_out = cur;
+  sc->lkept = cur;
+  return PMVS_OK;
+}
+
+pmvs_status pmvs_loop_fetch(pmvs_scene* sc, pmvs_patch* out, int32_t n) {
+  if (!sc || n < 0 || (n > 0 && !out)) return fail(PMVS_EINVAL, "invalid argument");
+  if (n != sc->lkept) return fail(PMVS_EINVAL, "loop_fetch: %d patches kept, %d asked", sc->lkept, n);
+  if (n) {
+    HIPCHK(hipSetDevice(sc->device));
+    HIPCHK(hipMemcpy(out, sc->fpatches.p, (size_t)n * sizeof(pmvs_patch), hipMemcpyDeviceToHost));
+  }
+  sc->lkept = -1;
   return PMVS_OK;
 }
 

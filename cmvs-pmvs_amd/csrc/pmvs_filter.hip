@@ -22,8 +22,10 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -1398,6 +1400,12 @@ hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n,
 // ============================================================================ expansion (host)
 namespace {
 
+static inline float __int_as_float_h(int v) {
+  float f;
+  std::memcpy(&f, &v, sizeof(f));
+  return f;
+}
+
 struct QItem {
   float tmp;
   long long seq;
@@ -1417,6 +1425,84 @@ __global__ void gather_slots_kernel(const int* __restrict__ slots, int m, const 
   if (k >= m) return;
   cout[k] = cin[slots[k]];
   pout[k] = prep[slots[k]];
+}
+
+// Collected patches: flag = 1 (clearFlags + collectPatches(queue), patchOrganizerS.cpp) and their
+// _tmp in collect order (the queue's initial contents).
+__global__ void collect_flags_kernel(pmvs_patch* __restrict__ P, const int* __restrict__ order, int na,
+                                     float* __restrict__ qtmp) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= na) return;
+  pmvs_patch& q = P[order[i]];
+  q.flag = 1;
+  qtmp[i] = q.tmp;
+}
+
+// Compact per-candidate record the host commit reads (instead of two full patch records):
+// [status, tmp bits, nprep, nimg, nvis | prep cells[64] | image cells[64] | vimage cells[64]],
+// cells as global target-cell indexes.  prep cells: the in-grid target entries of the prepared
+// candidate (the commit-time checkCounts); image / vimage cells: the in-grid target entries of
+// the refined patch (updateCounts, addPatch).  status 9 = a record the refine path cannot produce.
+constexpr int kRecInts = 5 + 3 * PMVS_MAX_IMAGES;
+__global__ void commit_rec_kernel(DScene s, const long long* __restrict__ tgoff, const pmvs_patch* __restrict__ outp,
+                                  const int* __restrict__ ostatus, const pmvs_patch* __restrict__ prep, int m,
+                                  int* __restrict__ rec) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  int* r = rec + (size_t)j * kRecInts;
+  const pmvs_patch& pp = prep[j];
+  int np = 0;
+  for (int i = 0; i < pp.num_images && i < PMVS_MAX_IMAGES; ++i) {
+    const int t = pp.images[i];
+    if (t < s.tnum && in_grid(s, t, pp.grids[i][0], pp.grids[i][1]))
+      r[5 + np++] = (int)(tgoff[t] + (long long)pp.grids[i][1] * gwidth(s, t) + pp.grids[i][0]);
+  }
+  r[2] = np;
+  int st = ostatus[j];
+  int ni = 0, nv = 0;
+  if (st == 0) {
+    const pmvs_patch& q = outp[j];
+    if (q.num_images < 1 || q.num_images > PMVS_MAX_IMAGES || q.num_vimages < 0 || q.num_vimages > PMVS_MAX_IMAGES) {
+      st = 9;
+    } else {
+      for (int i = 0; i < q.num_images; ++i) {
+        const int t = q.images[i];
+        if (t < 0 || t >= s.num) st = 9;
+        else if (t < s.tnum && in_grid(s, t, q.grids[i][0], q.grids[i][1]))
+          r[5 + PMVS_MAX_IMAGES + ni++] = (int)(tgoff[t] + (long long)q.grids[i][1] * gwidth(s, t) + q.grids[i][0]);
+      }
+      for (int i = 0; i < q.num_vimages; ++i) {
+        const int t = q.vimages[i];
+        if (t < 0 || t >= s.tnum) st = 9;
+        else if (in_grid(s, t, q.vgrids[i][0], q.vgrids[i][1]))
+          r[5 + 2 * PMVS_MAX_IMAGES + nv++] = (int)(tgoff[t] + (long long)q.vgrids[i][1] * gwidth(s, t) + q.vgrids[i][0]);
+      }
+      r[1] = __float_as_int(q.tmp);
+    }
+  }
+  r[0] = st;
+  r[3] = ni;
+  r[4] = nv;
+}
+
+// Committed candidates appended to the model: P[first + k] = outp[acc[k]] with _flag = 1,
+// _fix = 0, _dflag = 0 (CExpand::expandSub -> addPatch).  One wavefront per record.
+__global__ __launch_bounds__(64) void append_kernel(pmvs_patch* __restrict__ P, int first, const int* __restrict__ acc,
+                                                    int nacc, const pmvs_patch* __restrict__ outp) {
+  const int k = blockIdx.x;
+  if (k >= nacc) return;
+  const unsigned* src = reinterpret_cast<const unsigned*>(&outp[acc[k]]);
+  unsigned* dst = reinterpret_cast<unsigned*>(&P[first + k]);
+  constexpr int kFlag = offsetof(pmvs_patch, flag) / 4, kFix = offsetof(pmvs_patch, fix) / 4,
+                kDflag = offsetof(pmvs_patch, dflag) / 4;
+  for (int w = threadIdx.x; w < (int)(sizeof(pmvs_patch) / 4); w += 64)
+    dst[w] = (w == kFlag) ? 1u : (w == kFix || w == kDflag) ? 0u : src[w];
+}
+
+// _dflag |= bits of the parents whose directions failed this wave (distinct parents per wave).
+__global__ void dflag_kernel(pmvs_patch* __restrict__ P, const int2* __restrict__ upd, int n) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) P[upd[k].x].dflag |= upd[k].y;
 }
 
 __global__ void alive_reg_kernel(int n, const int* __restrict__ alive, unsigned long long* __restrict__ preg,
@@ -1452,7 +1538,7 @@ static hipError_t grow(T*& p, size_t& cap, size_t need) {
 
 ExpandBuffers::~ExpandBuffers() {
   void* ps[] = {parents, cand_coord, cand_ok, cand, prep, status, slots, cand2, prep2, res, outp, ostatus, counts, alive,
-                pg_head, vp_head, d_item, d_next, pool_used, tcells, tvals};
+                pg_head, vp_head, d_item, d_next, pool_used, tcells, tvals, qtmp, crec, acc, dupd};
   for (void* p : ps)
     if (p) (void)hipFree(p);
 }
@@ -1472,32 +1558,58 @@ static hipError_t grow_keep(T*& p, size_t& cap, size_t need, size_t used, hipStr
   return hipSuccess;
 }
 
-// One CExpand::run (expand.cpp:17-406) in waves; see pmvs_amd.h (pmvs_expand_run) and DESIGN.md.
-// Sharded (sh.world > 1): every rank holds the same model and runs the same schedule; the cheap
+// PMVS_EXPAND_PROFILE=1: host wall time per expansion phase (synchronising at phase ends), to stderr.
+struct PhaseTimer {
+  bool on = getenv("PMVS_EXPAND_PROFILE") != nullptr;
+  hipStream_t st;
+  double acc[10] = {0};
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  explicit PhaseTimer(hipStream_t s) : st(s) {}
+  void mark(int k) {
+    if (!on) return;
+    (void)hipStreamSynchronize(st);
+    const auto now = std::chrono::steady_clock::now();
+    acc[k] += std::chrono::duration<double, std::milli>(now - t).count();
+    t = now;
+  }
+  ~PhaseTimer() {
+    if (!on) return;
+    static const char* names[10] = {"load", "pop", "empty_blocks", "prepare", "gather+refine", "depth_post+d2h",
+                                    "exchange", "commit", "upload", "other"};
+    fprintf(stderr, "[expand profile ms]");
+    for (int k = 0; k < 10; ++k) fprintf(stderr, " %s=%.1f", names[k], acc[k]);
+    fprintf(stderr, "\n");
+  }
+};
+
+// One CExpand::run (expand.cpp:17-406) in waves on a device-resident model; see pmvs_amd.h
+// (pmvs_expand_run) and DESIGN.md.  dP[0, n0) holds the model (d_alive marks the patches the
+// organizer holds); on return dP[0, *n_out) holds it with the new patches appended and _flag /
+// _dflag updated.  The host keeps only the queue, the per-cell counts and occupancy, and reads
+// compact per-candidate commit records (commit_rec_kernel) -- no patch records cross PCIe on one
+// rank.  Sharded (sh.world > 1): every rank holds the same model and runs the same schedule; the
 // organizer steps (findEmptyBlocks, expandSub up to the refine) run on every rank, the refine +
 // depth >= 1 postProcess of a wave's candidates is split into contiguous rank ranges, and the
-// per-candidate results are all-gathered (sh.exchange) before the identical commit -- so the
-// model after the run is bit-identical to the one-rank run with the same wave.
-hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs_patch*& dP, size_t& dP_cap,
-                       std::vector<pmvs_patch>& H, std::vector<int>& alive, int cap, long long ncells,
-                       const long long* h_tgoff, int wave, int cthr, int flags, int grid, hipStream_t st,
-                       const RefineFn& refine, const Shard& sh, long long stats[8]) {
+// refined records are all-gathered (sh.exchange) before the identical commit -- so the model is
+// bit-identical to the one-rank run with the same wave.
+hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs_patch*& dP, size_t& dP_cap, int n0,
+                       const int* d_alive, int cap, long long ncells, const long long* h_tgoff, int wave, int cthr,
+                       int flags, int grid, hipStream_t st, const RefineFn& refine, const Shard& sh, long long stats[8],
+                       int* n_out, int min_cands) {
   for (int k = 0; k < 8; ++k) stats[k] = 0;
-  const int n0 = (int)H.size();
+  *n_out = n0;
+  PhaseTimer T(st);
   const int W = std::max(1, std::min(wave, kMaxWave));
   // device patch capacity: the model plus a few waves, doubled when the commits need more
   size_t pcap = std::min<size_t>((size_t)cap, (size_t)n0 + 12 * (size_t)W + 1024);
   FCHK(B.reserve((int)pcap, ncells, s.tnum, grid));
-  pcap = (size_t)B.cap_n;
-  FCHK(grow_keep(dP, dP_cap, pcap, 0, st));
+  pcap = std::min<size_t>((size_t)B.cap_n, (size_t)cap);
+  FCHK(grow_keep(dP, dP_cap, pcap, (size_t)n0, st));
   FCHK(hipMemcpyAsync(B.tgoff, h_tgoff, (s.tnum + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
-  FCHK(hipMemcpyAsync(dP, H.data(), (size_t)n0 * sizeof(pmvs_patch), hipMemcpyHostToDevice, st));
-  FCHK(grow(X.alive, X.cap_alive, (size_t)n0));
-  FCHK(hipMemcpyAsync(X.alive, alive.data(), (size_t)n0 * sizeof(int), hipMemcpyHostToDevice, st));
   Ctx c{s, B, dP, n0, ncells, grid, st};
   // ---- model load (the state CFilter::run leaves): registrations, collect order, depth maps, lists
   hipLaunchKernelGGL(init_reg_kernel, dim3(nblk(n0)), dim3(256), 0, st, s, dP, n0, B.preg, B.vreg);
-  hipLaunchKernelGGL(alive_reg_kernel, dim3(nblk(n0)), dim3(256), 0, st, n0, X.alive, B.preg, B.vreg, dP);
+  hipLaunchKernelGGL(alive_reg_kernel, dim3(nblk(n0)), dim3(256), 0, st, n0, d_alive, B.preg, B.vreg, dP);
   FCHK(build_lists(c, 0));
   FCHK(collect(c));
   FCHK(hipMemsetAsync(B.dpkey, 0xff, ncells * sizeof(unsigned long long), st));
@@ -1517,52 +1629,80 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
     c.pg_dhead = X.pg_head; c.vp_dhead = X.vp_head; c.d_item = X.d_item; c.d_next = X.d_next;
   };
   set_delta();
-  // ---- host mirrors: pgrids occupancy per cell, counts (clearCounts), collect order (queue)
-  std::vector<int> pgoff(ncells + 1), order(c.nalive);
-  FCHK(hipMemcpyAsync(pgoff.data(), B.pg_off, (ncells + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
-  if (c.nalive) FCHK(hipMemcpyAsync(order.data(), B.order, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
+  // ---- host mirrors: pgrids occupancy per cell, counts (clearCounts), the queue
+  std::vector<int> occ(ncells + 1), order(c.nalive);
+  std::vector<float> qtmp(c.nalive);
+  FCHK(grow(X.qtmp, X.cap_qtmp, (size_t)std::max(1, c.nalive)));
+  if (c.nalive)
+    hipLaunchKernelGGL(collect_flags_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, dP, B.order, c.nalive, X.qtmp);
+  FCHK(hipMemcpyAsync(occ.data(), B.pg_off, (ncells + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
+  if (c.nalive) {
+    FCHK(hipMemcpyAsync(order.data(), B.order, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
+    FCHK(hipMemcpyAsync(qtmp.data(), X.qtmp, c.nalive * sizeof(float), hipMemcpyDeviceToHost, st));
+  }
   FCHK(hipStreamSynchronize(st));
-  std::vector<int> occ(ncells);
-  for (long long k = 0; k < ncells; ++k) occ[k] = pgoff[k + 1] - pgoff[k];
-  std::vector<int>().swap(pgoff);
+  for (long long k = 0; k < ncells; ++k) occ[k] = occ[k + 1] - occ[k];
   std::vector<unsigned char> counts(ncells, 0);
   FCHK(grow(X.counts, X.cap_cnt, (size_t)ncells));
   FCHK(hipMemsetAsync(X.counts, 0, ncells, st));
+  // The max-_tmp queue (P_compare; ties: earlier push first): the collected patches as a sorted
+  // run, the patches pushed during the run in a heap, popped by merging the two.
+  std::vector<QItem> initial(c.nalive);
+  for (int i = 0; i < c.nalive; ++i) initial[i] = {qtmp[i], (long long)i, order[i]};
+  const QCmp less;  // less(a, b): a has lower priority than b
+  std::sort(initial.begin(), initial.end(), [&](const QItem& a, const QItem& b) { return less(b, a); });
+  size_t ihead = 0;
   std::priority_queue<QItem, std::vector<QItem>, QCmp> queue;
-  long long seq = 0;
-  for (int i = 0; i < c.nalive; ++i) H[order[i]].flag = 0;  // clearFlags (the collected patches)
-  for (int i = 0; i < c.nalive; ++i) {  // collectPatches(queue)
-    const int p = order[i];
-    if (H[p].flag == 0) {
-      H[p].flag = 1;
-      queue.push({H[p].tmp, seq++, p});
-    }
-  }
+  long long seq = c.nalive;
+  auto q_empty = [&]() { return ihead >= initial.size() && queue.empty(); };
+  auto q_pop = [&]() -> int {
+    if (ihead < initial.size() && (queue.empty() || !less(initial[ihead], queue.top()))) return initial[ihead++].p;
+    const int p = queue.top().p;
+    queue.pop();
+    return p;
+  };
   int rank_next = c.nalive;
+  int nmodel = n0;
   const int G = std::max(1, sh.world), R = std::min(std::max(0, sh.rank), G - 1);
   std::vector<long long> touched;
   std::vector<unsigned char> tvals;
   std::vector<char> xsend, xrecv;
-  while (!queue.empty()) {
+  std::vector<int> rec, acc;
+  std::vector<int2> dupd;
+  T.mark(0);
+  std::vector<int> okh;
+  while (!q_empty()) {
     stats[7]++;
+    // A wave: chunks of W parents (queue order) until it holds min_cands candidate directions
+    // (findEmptyBlocks against the start-of-wave model; min_cands = 0 or W = 1: one chunk).
     std::vector<int> parents;
-    while (!queue.empty() && (int)parents.size() < W) {
-      parents.push_back(queue.top().p);
-      queue.pop();
-    }
+    long long ndirs = 0;
+    c.n = nmodel;
+    do {
+      const int off = (int)parents.size();
+      while (!q_empty() && (int)parents.size() - off < W) parents.push_back(q_pop());
+      const int nc = (int)parents.size() - off;
+      T.mark(1);
+      FCHK(grow_keep(X.parents, X.cap_par, parents.size(), (size_t)off, st));
+      FCHK(grow_keep(X.cand_coord, X.cap_coord, parents.size() * 24, (size_t)off * 24, st));
+      FCHK(grow_keep(X.cand_ok, X.cap_ok, parents.size() * 6, (size_t)off * 6, st));
+      FCHK(hipMemcpyAsync(X.parents + off, parents.data() + off, nc * sizeof(int), hipMemcpyHostToDevice, st));
+      FCHK(hipMemsetAsync(B.counters + 3, 0, 5 * sizeof(int), st));
+      hipLaunchKernelGGL(empty_blocks_kernel, dim3(std::min(grid, nc)), dim3(64), 0, st, s, c.dev(), X.parents + off, nc,
+                         X.cand_coord + (size_t)off * 24, X.cand_ok + (size_t)off * 6, B.counters + 4, B.counters + 3);
+      if (W > 1 && min_cands > 0) {
+        okh.resize((size_t)nc * 6);
+        FCHK(hipMemcpyAsync(okh.data(), X.cand_ok + (size_t)off * 6, (size_t)nc * 6 * sizeof(int), hipMemcpyDeviceToHost, st));
+        FCHK(hipStreamSynchronize(st));
+        for (int v : okh) ndirs += v;
+      }
+      T.mark(2);
+    } while (W > 1 && ndirs < min_cands && !q_empty());
     const int np = (int)parents.size();
     stats[0] += np;
-    FCHK(grow(X.parents, X.cap_par, (size_t)np));
-    FCHK(grow(X.cand_coord, X.cap_coord, (size_t)np * 24));
-    FCHK(grow(X.cand_ok, X.cap_ok, (size_t)np * 6));
     FCHK(grow(X.cand, X.cap_cand, (size_t)np * 6));
     FCHK(grow(X.prep, X.cap_prep, (size_t)np * 6));
     FCHK(grow(X.status, X.cap_status, (size_t)np * 6));
-    FCHK(hipMemcpyAsync(X.parents, parents.data(), np * sizeof(int), hipMemcpyHostToDevice, st));
-    c.n = (int)H.size();
-    FCHK(hipMemsetAsync(B.counters + 3, 0, 5 * sizeof(int), st));
-    hipLaunchKernelGGL(empty_blocks_kernel, dim3(std::min(grid, np)), dim3(64), 0, st, s, c.dev(), X.parents, np,
-                       X.cand_coord, X.cand_ok, B.counters + 4, B.counters + 3);
     // wave = 1 is the reference's schedule: the parent's directions are prepared, refined and
     // committed one after the other (expand.cpp:92-101); wider waves batch every candidate.
     std::vector<int> batches{-1};
@@ -1574,14 +1714,16 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
       for (int k = 0; k < 6; ++k)
         if (ok[k]) batches.push_back(k);
     }
+    int pbits = 0;  // wave = 1: failed directions of the single parent, written after its batches
     for (const int only : batches) {
-      c.n = (int)H.size();
+      c.n = nmodel;
       hipLaunchKernelGGL(prepare_kernel, dim3(nblk((long long)np * 6)), dim3(256), 0, st, s, c.dev(), X.counts, X.parents,
                          np, X.cand_coord, X.cand_ok, X.cand, X.prep, X.status, cthr, only);
       FCHK(hipPeekAtLastError());
       std::vector<int> status((size_t)np * 6);
       FCHK(hipMemcpyAsync(status.data(), X.status, (size_t)np * 6 * sizeof(int), hipMemcpyDeviceToHost, st));
       FCHK(hipStreamSynchronize(st));
+      T.mark(3);
       std::vector<int> slots, slot2surv((size_t)np * 6, -1);
       for (int k = 0; k < np * 6; ++k) {
         if (status[k] >= 0) stats[1]++;
@@ -1594,10 +1736,7 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
       // this rank's contiguous share of the survivors
       const int chunk = (m + G - 1) / G;
       const int lo = std::min(m, R * chunk), hi = std::min(m, lo + chunk), mine = hi - lo;
-      std::vector<int> ostatus(m);
-      std::vector<pmvs_patch> outp(m), prep(m);
       int ovf = 0;
-      hipError_t lerr = hipSuccess;
       auto local = [&]() -> hipError_t {
         if (m > 0) {
           FCHK(grow(X.slots, X.cap_slots, (size_t)m));
@@ -1610,30 +1749,33 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
           hipLaunchKernelGGL(gather_slots_kernel, dim3(nblk(m)), dim3(256), 0, st, X.slots, m, X.cand, X.prep, X.cand2, X.prep2);
           if (mine > 0) {
             FCHK(refine(X.cand2 + lo, mine, X.res + lo));
+            T.mark(4);
             FCHK(hipMemsetAsync(B.counters + 4, 0, sizeof(int), st));
             hipLaunchKernelGGL(depth_post_kernel, dim3(std::min(grid, mine)), dim3(64), 0, st, s, c.dev(), X.res + lo, mine,
                                X.outp + lo, X.ostatus + lo, B.scratch, B.counters + 4, B.counters + 3);
             FCHK(hipPeekAtLastError());
-            FCHK(hipMemcpyAsync(ostatus.data() + lo, X.ostatus + lo, mine * sizeof(int), hipMemcpyDeviceToHost, st));
-            FCHK(hipMemcpyAsync(outp.data() + lo, X.outp + lo, (size_t)mine * sizeof(pmvs_patch), hipMemcpyDeviceToHost, st));
           }
-          FCHK(hipMemcpyAsync(prep.data(), X.prep2, (size_t)m * sizeof(pmvs_patch), hipMemcpyDeviceToHost, st));
         }
         return read_int(B.counters + 3, &ovf, st);
       };
-      lerr = local();
+      hipError_t lerr = local();
+      T.mark(5);
       if (G > 1) {
-        // all-gather of [error, overflow, status[chunk], patch[chunk]] per rank
-        const size_t rec = sizeof(int) + sizeof(pmvs_patch);
-        const size_t bytes = 2 * sizeof(int) + (size_t)chunk * rec;
+        // all-gather of [error, overflow, status[chunk], patch[chunk]] per rank; the other ranks'
+        // ranges are then uploaded so every rank holds all m refined records
+        const size_t bytes = 2 * sizeof(int) + (size_t)chunk * (sizeof(int) + sizeof(pmvs_patch));
         xsend.assign(bytes, 0);
         xrecv.assign(bytes * G, 0);
         int hdr[2] = {(int)lerr, ovf};
         std::memcpy(xsend.data(), hdr, sizeof(hdr));
         if (lerr == hipSuccess && mine > 0) {
-          std::memcpy(xsend.data() + 2 * sizeof(int), ostatus.data() + lo, mine * sizeof(int));
-          std::memcpy(xsend.data() + 2 * sizeof(int) + (size_t)chunk * sizeof(int), outp.data() + lo,
-                      (size_t)mine * sizeof(pmvs_patch));
+          lerr = hipMemcpyAsync(xsend.data() + 2 * sizeof(int), X.ostatus + lo, mine * sizeof(int), hipMemcpyDeviceToHost, st);
+          if (lerr == hipSuccess)
+            lerr = hipMemcpyAsync(xsend.data() + 2 * sizeof(int) + (size_t)chunk * sizeof(int), X.outp + lo,
+                                  (size_t)mine * sizeof(pmvs_patch), hipMemcpyDeviceToHost, st);
+          if (lerr == hipSuccess) lerr = hipStreamSynchronize(st);
+          hdr[0] = (int)lerr;
+          std::memcpy(xsend.data(), hdr, sizeof(hdr));
         }
         if (sh.exchange(xsend.data(), bytes, xrecv.data()) != 0) return hipErrorUnknown;
         for (int r = 0; r < G; ++r) {
@@ -1641,88 +1783,83 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
           std::memcpy(hdr, b, sizeof(hdr));
           if (hdr[0] != 0 && lerr == hipSuccess) lerr = hipErrorUnknown;  // another rank failed
           ovf |= hdr[1];
+        }
+        for (int r = 0; r < G && lerr == hipSuccess && !ovf; ++r) {
+          const char* b = xrecv.data() + (size_t)r * bytes;
           const int rlo = std::min(m, r * chunk), rhi = std::min(m, rlo + chunk);
           if (r == R || rhi <= rlo) continue;
-          std::memcpy(ostatus.data() + rlo, b + 2 * sizeof(int), (rhi - rlo) * sizeof(int));
-          std::memcpy(outp.data() + rlo, b + 2 * sizeof(int) + (size_t)chunk * sizeof(int),
-                      (size_t)(rhi - rlo) * sizeof(pmvs_patch));
+          FCHK(hipMemcpyAsync(X.ostatus + rlo, b + 2 * sizeof(int), (rhi - rlo) * sizeof(int), hipMemcpyHostToDevice, st));
+          FCHK(hipMemcpyAsync(X.outp + rlo, b + 2 * sizeof(int) + (size_t)chunk * sizeof(int),
+                              (size_t)(rhi - rlo) * sizeof(pmvs_patch), hipMemcpyHostToDevice, st));
         }
       }
       FCHK(lerr);
       if (ovf) return hipErrorOutOfMemory;  // more than NB_CAP neighbours (reported by the API)
-      // ---- commit in (parent priority, direction) order
-      const int first = (int)H.size();
-      touched.clear();
-      for (int k = 0; k < np * 6; ++k) {
-        if (status[k] < 0) continue;
-        const int par = parents[k / 6], dir = k % 6;
-        int stc = status[k];  // 1 = prepare failed
-        int j = slot2surv[k];
-        if (stc == 0) stc = ostatus[j];
-        if (stc == 0 && only < 0) {  // checkCounts again with the committed state
-          const pmvs_patch& q = prep[j];
-          int full = 0, empty = 0;
-          for (int i = 0; i < q.num_images; ++i) {
-            const int t = q.images[i];
-            if (s.tnum <= t || q.grids[i][0] < 0 || X.gw[t] <= q.grids[i][0] || q.grids[i][1] < 0 ||
-                X.gh[t] <= q.grids[i][1])
-              continue;
-            const long long cidx = h_tgoff[t] + (long long)q.grids[i][1] * X.gw[t] + q.grids[i][0];
-            if (occ[cidx] > 0) { ++full; continue; }
-            if (cthr <= counts[cidx]) ++full;
-            else ++empty;
-          }
-          const bool fail = (s.depth <= 1) ? (empty < s.minImageNum && full != 0) : (empty < s.minImageNum - 1 && full != 0);
-          if (fail) stc = 4;
-        }
-        if (stc != 0) {
-          H[par].dflag |= 0x0001 << dir;
-          stats[1 + std::min(stc, 4)]++;  // 2 fail_prep, 3 fail_pre, 4 fail_post, 5 fail_commit
-          continue;
-        }
-        pmvs_patch np_ = outp[j];
-        bool sane = np_.num_images >= 1 && np_.num_images <= PMVS_MAX_IMAGES && np_.num_vimages >= 0 &&
-                    np_.num_vimages <= PMVS_MAX_IMAGES;
-        for (int i = 0; sane && i < np_.num_images; ++i) sane = np_.images[i] >= 0 && np_.images[i] < s.num;
-        for (int i = 0; sane && i < np_.num_vimages; ++i) sane = np_.vimages[i] >= 0 && np_.vimages[i] < s.tnum;
-        if (!sane) {  // a device result that cannot come from the refine path
-          fprintf(stderr, "expand: insane patch k=%d j=%d m=%d ni=%d nv=%d ncc=%g img0=%d vim0=%d\n", k, j, m,
-                  np_.num_images, np_.num_vimages, np_.ncc, np_.images[0], np_.vimages[0]);
-          return hipErrorIllegalState;
-        }
-        np_.flag = 1;
-        np_.fix = 0;
-        np_.dflag = 0;
-        // CExpand::updateCounts (expand.cpp:325-406)
-        int full = 0, empty = 0;
-        auto touch = [&](int t, int ix, int iy) {
-          if (ix < 0 || ix >= X.gw[t] || iy < 0 || iy >= X.gh[t]) return;
-          const long long cidx = h_tgoff[t] + (long long)iy * X.gw[t] + ix;
-          unsigned char& cc = counts[cidx];
-          if (cthr <= cc) ++full;
-          else ++empty;
-          ++cc;
-          touched.push_back(cidx);
-        };
-        for (int i = 0; i < np_.num_images; ++i)
-          if (np_.images[i] < s.tnum) touch(np_.images[i], np_.grids[i][0], np_.grids[i][1]);
-        for (int i = 0; i < np_.num_vimages; ++i) touch(np_.vimages[i], np_.vgrids[i][0], np_.vgrids[i][1]);
-        const int add = empty != 0;
-        for (int i = 0; i < np_.num_images; ++i) {  // addPatch: pgrids registration
-          const int t = np_.images[i];
-          if (t < s.tnum && 0 <= np_.grids[i][0] && np_.grids[i][0] < X.gw[t] && 0 <= np_.grids[i][1] &&
-              np_.grids[i][1] < X.gh[t]) {
-            occ[h_tgoff[t] + (long long)np_.grids[i][1] * X.gw[t] + np_.grids[i][0]]++;
-            ++pool_need;
-          }
-        }
-        pool_need += np_.num_vimages;
-        if ((int)H.size() >= cap) return hipErrorOutOfMemory;
-        H.push_back(np_);
-        alive.push_back(1);
-        stats[6]++;
-        if (add) queue.push({np_.tmp, seq++, (int)H.size() - 1});
+      if (m > 0) {
+        FCHK(grow(X.crec, X.cap_crec, (size_t)m * kRecInts));
+        hipLaunchKernelGGL(commit_rec_kernel, dim3(nblk(m)), dim3(256), 0, st, s, B.tgoff, X.outp, X.ostatus, X.prep2, m,
+                           X.crec);
+        rec.resize((size_t)m * kRecInts);
+        FCHK(hipMemcpyAsync(rec.data(), X.crec, (size_t)m * kRecInts * sizeof(int), hipMemcpyDeviceToHost, st));
+        FCHK(hipStreamSynchronize(st));
       }
+      T.mark(6);
+      // ---- commit in (parent priority, direction) order
+      touched.clear();
+      acc.clear();
+      dupd.clear();
+      for (int pi = 0; pi < np; ++pi) {
+        int bits = 0;
+        for (int dir = 0; dir < 6; ++dir) {
+          const int k = 6 * pi + dir;
+          if (status[k] < 0) continue;
+          int stc = status[k];  // 1 = prepare failed
+          const int j = slot2surv[k];
+          const int* r = (stc == 0) ? &rec[(size_t)j * kRecInts] : nullptr;
+          if (stc == 0) stc = r[0];
+          if (stc == 9) {
+            fprintf(stderr, "expand: refined record %d of %d is not a valid patch\n", j, m);
+            return hipErrorIllegalState;
+          }
+          if (stc == 0 && only < 0) {  // checkCounts again with the committed state
+            int full = 0, empty = 0;
+            for (int i = 0; i < r[2]; ++i) {
+              const int cidx = r[5 + i];
+              if (occ[cidx] > 0) { ++full; continue; }
+              if (cthr <= counts[cidx]) ++full;
+              else ++empty;
+            }
+            const bool fail = (s.depth <= 1) ? (empty < s.minImageNum && full != 0) : (empty < s.minImageNum - 1 && full != 0);
+            if (fail) stc = 4;
+          }
+          if (stc != 0) {
+            bits |= 0x0001 << dir;
+            stats[1 + std::min(stc, 4)]++;  // 2 fail_prep, 3 fail_pre, 4 fail_post, 5 fail_commit
+            continue;
+          }
+          // CExpand::updateCounts (expand.cpp:325-406) + addPatch (pgrids registration)
+          int full = 0, empty = 0;
+          auto touch = [&](int cidx) {
+            unsigned char& cc = counts[cidx];
+            if (cthr <= cc) ++full;
+            else ++empty;
+            ++cc;
+            touched.push_back(cidx);
+          };
+          for (int i = 0; i < r[3]; ++i) touch(r[5 + PMVS_MAX_IMAGES + i]);
+          for (int i = 0; i < r[4]; ++i) touch(r[5 + 2 * PMVS_MAX_IMAGES + i]);
+          for (int i = 0; i < r[3]; ++i) occ[r[5 + PMVS_MAX_IMAGES + i]]++;
+          pool_need += (size_t)r[3] + (size_t)r[4];
+          if (nmodel + (int)acc.size() >= cap) return hipErrorOutOfMemory;
+          const int newp = nmodel + (int)acc.size();
+          acc.push_back(j);
+          stats[6]++;
+          if (empty != 0) queue.push({__int_as_float_h(r[1]), seq++, newp});
+        }
+        if (W == 1) pbits |= bits;
+        else if (bits) dupd.push_back(make_int2(parents[pi], bits));
+      }
+      T.mark(7);
       // device counts: the cells this commit touched (final values)
       if (!touched.empty()) {
         const int nt = (int)touched.size();
@@ -1734,14 +1871,19 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
         FCHK(hipMemcpyAsync(X.tvals, tvals.data(), nt, hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(counts_scatter_kernel, dim3(nblk(nt)), dim3(256), 0, st, X.tcells, X.tvals, nt, X.counts);
       }
-      const int added = (int)H.size() - first;
+      if (!dupd.empty()) {
+        FCHK(grow(X.dupd, X.cap_dupd, dupd.size()));
+        FCHK(hipMemcpyAsync(X.dupd, dupd.data(), dupd.size() * sizeof(int2), hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(dflag_kernel, dim3(nblk((long long)dupd.size())), dim3(256), 0, st, dP, X.dupd, (int)dupd.size());
+      }
+      const int added = (int)acc.size();
       if (added > 0) {
-        const size_t used_before = X.pool_host;
-        FCHK(grow_keep(X.d_item, X.cap_item, pool_need, used_before, st));
-        FCHK(grow_keep(X.d_next, X.cap_next, pool_need, used_before, st));
+        const int first = nmodel;
+        FCHK(grow_keep(X.d_item, X.cap_item, pool_need, X.pool_host, st));
+        FCHK(grow_keep(X.d_next, X.cap_next, pool_need, X.pool_host, st));
         set_delta();
-        if (H.size() > pcap) {  // per-patch arrays the waves write, grown keeping their contents
-          const size_t ncap = std::min<size_t>((size_t)cap, std::max(H.size(), 2 * pcap));
+        if ((size_t)(first + added) > pcap) {  // per-patch arrays the waves write, grown keeping their contents
+          const size_t ncap = std::min<size_t>((size_t)cap, std::max((size_t)(first + added), 2 * pcap));
           size_t c1 = pcap, c2 = pcap, c3 = pcap, c4 = pcap;
           FCHK(grow_keep(dP, dP_cap, ncap, (size_t)first, st));
           FCHK(grow_keep(B.preg, c1, ncap, (size_t)first, st));
@@ -1752,16 +1894,64 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
           pcap = ncap;
           c.P = dP;
         }
-        FCHK(hipMemcpyAsync(dP + first, H.data() + first, (size_t)added * sizeof(pmvs_patch), hipMemcpyHostToDevice, st));
-        c.n = (int)H.size();
+        FCHK(grow(X.acc, X.cap_acc, (size_t)added));
+        FCHK(hipMemcpyAsync(X.acc, acc.data(), added * sizeof(int), hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(append_kernel, dim3(added), dim3(64), 0, st, dP, first, X.acc, added, X.outp);
+        nmodel += added;
+        c.n = nmodel;
         DeltaLists D{X.pg_head, X.vp_head, X.d_item, X.d_next, X.pool_used, (int)std::min<size_t>(X.cap_item, INT32_MAX)};
         hipLaunchKernelGGL(add_patches_kernel, dim3(nblk((long long)added * s.tnum)), dim3(256), 0, st, s, c.dev(), first,
                            added, rank_next, B.preg, B.vreg, B.order, B.dpkey, B.unit0, D);
         X.pool_host = pool_need;
         rank_next += added;
       }
+      T.mark(8);
+    }
+    if (W == 1 && pbits) {
+      const int2 u = make_int2(parents[0], pbits);
+      FCHK(grow(X.dupd, X.cap_dupd, 1));
+      FCHK(hipMemcpyAsync(X.dupd, &u, sizeof(int2), hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(dflag_kernel, dim3(1), dim3(64), 0, st, dP, X.dupd, 1);
+      FCHK(hipStreamSynchronize(st));
     }
   }
+  *n_out = nmodel;
+  return hipGetLastError();
+}
+
+// ============================================================================ loop helpers
+__global__ __launch_bounds__(64) void compact_kernel(const pmvs_patch* __restrict__ src, int n, const int* __restrict__ keep,
+                                                     const int* __restrict__ pos, pmvs_patch* __restrict__ dst) {
+  const int k = blockIdx.x;
+  if (k >= n || !keep[k]) return;
+  const unsigned* a = reinterpret_cast<const unsigned*>(&src[k]);
+  unsigned* b = reinterpret_cast<unsigned*>(&dst[pos[k]]);
+  for (int w = threadIdx.x; w < (int)(sizeof(pmvs_patch) / 4); w += 64) b[w] = a[w];
+}
+
+__global__ void fill_int_kernel(int* __restrict__ a, int n, int v) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) a[k] = v;
+}
+
+// The patches a filter pass kept (keep[k] = 1), in order, into dst (CFindMatch::run keeps the
+// model in the organizer; here the removed records are dropped between passes).
+hipError_t compact_model(FilterBuffers& B, const pmvs_patch* src, int n, const int* keep, pmvs_patch* dst, int* nkept,
+                         hipStream_t st) {
+  *nkept = 0;
+  if (n <= 0) return hipSuccess;
+  FCHK(B.reserve(n, B.cap_cells, 0, B.cap_grid));
+  FCHK(hipMemcpyAsync(B.cnt, keep, n * sizeof(int), hipMemcpyDeviceToDevice, st));
+  FCHK(hipMemsetAsync(B.cnt + n, 0, sizeof(int), st));
+  size_t tb = B.temp_bytes;
+  FCHK(hipcub::DeviceScan::ExclusiveSum(B.temp, tb, B.cnt, B.off, n + 1, st));
+  FCHK(read_int(B.off + n, nkept, st));
+  hipLaunchKernelGGL(compact_kernel, dim3(n), dim3(64), 0, st, src, n, keep, B.off, dst);
+  return hipGetLastError();
+}
+
+hipError_t fill_int(int* a, int n, int v, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(fill_int_kernel, dim3(nblk(n)), dim3(256), 0, st, a, n, v);
   return hipGetLastError();
 }
 }  // namespace pmvsdev

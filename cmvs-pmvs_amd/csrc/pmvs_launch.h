@@ -43,7 +43,7 @@ hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n,
 hipError_t launch_filter_refimage(const DScene& s, pmvs_patch* P, const int* list, int m, int grid, hipStream_t stream);
 
 // ---- expansion run (pmvs_filter.hip)
-constexpr int kMaxWave = 16384;  // parents per expansion wave (device slot arrays are sized by it)
+constexpr int kMaxWave = 65536;  // parents per expansion wave (device slot arrays are sized by it)
 struct ExpandBuffers {
   int *parents = nullptr, *cand_ok = nullptr, *status = nullptr, *slots = nullptr, *ostatus = nullptr, *alive = nullptr;
   float* cand_coord = nullptr;
@@ -54,11 +54,15 @@ struct ExpandBuffers {
   // registrations committed during the run: per-cell chain heads + entry pool (FilterDev delta)
   int *pg_head = nullptr, *vp_head = nullptr, *d_item = nullptr, *d_next = nullptr, *pool_used = nullptr;
   long long* tcells = nullptr;  // cells whose counts a commit changed, and their values
+  float* qtmp = nullptr;        // _tmp of the collected patches (queue)
+  int *crec = nullptr, *acc = nullptr;  // commit records; committed record indexes
+  int2* dupd = nullptr;         // (parent, failed-direction bits) of a wave
   unsigned char* tvals = nullptr;
   size_t pool_host = 0;
   size_t cap_coord = 0, cap_ok = 0, cap_cand = 0, cap_prep = 0, cap_slots = 0, cap_prep2 = 0, cap_res = 0, cap_outp = 0,
          cap_ost = 0, cap_par = 0, cap_status = 0, cap_cand2 = 0, cap_alive = 0, cap_cnt = 0, cap_pghead = 0,
-         cap_vphead = 0, cap_item = 0, cap_next = 0, cap_pused = 0, cap_tcells = 0, cap_tvals = 0;
+         cap_vphead = 0, cap_item = 0, cap_next = 0, cap_pused = 0, cap_tcells = 0, cap_tvals = 0,
+         cap_qtmp = 0, cap_crec = 0, cap_acc = 0, cap_dupd = 0;
   std::vector<int> gw, gh;  // grid sizes of the target images
   ~ExpandBuffers();
 };
@@ -69,10 +73,13 @@ struct Shard {
   int rank = 0, world = 1;
   ExchangeFn exchange;
 };
-// dP/dP_cap: the device patch array (grown, contents kept, as the model grows); cap bounds the
-// result size.
-hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs_patch*& dP, size_t& dP_cap,
-                       std::vector<pmvs_patch>& H, std::vector<int>& alive, int cap, long long ncells,
-                       const long long* h_tgoff, int wave, int cthr, int flags, int grid, hipStream_t st,
-                       const RefineFn& refine, const Shard& sh, long long stats[8]);
+// dP[0, n0): the device-resident model (grown in place, contents kept); d_alive[0, n0) marks the
+// patches the organizer holds; cap bounds the result size *n_out.
+hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs_patch*& dP, size_t& dP_cap, int n0,
+                       const int* d_alive, int cap, long long ncells, const long long* h_tgoff, int wave, int cthr,
+                       int flags, int grid, hipStream_t st, const RefineFn& refine, const Shard& sh, long long stats[8],
+                       int* n_out, int min_cands = 0);
+hipError_t compact_model(FilterBuffers& B, const pmvs_patch* src, int n, const int* keep, pmvs_patch* dst, int* nkept,
+                         hipStream_t st);
+hipError_t fill_int(int* a, int n, int v, hipStream_t st);
 }  // namespace pmvsdev

@@ -87,6 +87,14 @@ class ExpandStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class LoopIter(C.Structure):
+    _fields_ = [("depth", C.c_int32), ("patches", C.c_int32), ("expand", ExpandStats), ("filter", FilterStats)]
+
+    def as_dict(self):
+        return {"depth": self.depth, "expand": self.expand.as_dict(), "filter": self.filter.as_dict(),
+                "patches": self.patches}
+
+
 class Options(C.Structure):
     _fields_ = [(k, C.c_int32) for k in ("level", "csize", "wsize", "min_image_num", "cpu", "use_bound",
                                           "use_vis_data", "sequence", "tflag", "oflag")] + \
@@ -109,7 +117,7 @@ EXPORTS = ["pmvs_last_error", "pmvs_device_count", "pmvs_scene_create", "pmvs_sc
            "pmvs_synth_candidates", "pmvs_selftest_math", "pmvs_selftest_bobyqa", "pmvs_camera_load",
            "pmvs_ppm_load", "pmvs_options_load", "pmvs_options_free", "pmvs_write_patches", "pmvs_write_pset",
            "pmvs_write_ply", "pmvs_patch_colors", "pmvs_filter_run",
-           "pmvs_expand_run", "pmvs_expand_fetch", "pmvs_scene_set_shard", "pmvs_thread_exchange_create",
+           "pmvs_expand_run", "pmvs_expand_fetch", "pmvs_run_loop", "pmvs_loop_fetch", "pmvs_scene_set_shard", "pmvs_thread_exchange_create",
            "pmvs_thread_exchange_ctx", "pmvs_thread_allgather", "pmvs_thread_exchange_destroy"]
 
 # int fn(void* ctx, const void* send, int64_t bytes, void* recv): all-gather (pmvs_allgather_fn)
@@ -155,9 +163,12 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.pmvs_write_ply.argtypes = [C.c_char_p, C.c_int32, C.c_void_p, C.c_void_p]
     lib.pmvs_patch_colors.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 4
     lib.pmvs_filter_run.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(FilterStats)]
-    lib.pmvs_expand_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+    lib.pmvs_expand_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                     C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(ExpandStats)]
     lib.pmvs_expand_fetch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32]
+    lib.pmvs_run_loop.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_float, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                  C.c_int32, C.POINTER(C.c_int32), C.c_void_p]
+    lib.pmvs_loop_fetch.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     lib.pmvs_scene_set_shard.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
     lib.pmvs_thread_exchange_create.argtypes = [C.c_int32]
     lib.pmvs_thread_exchange_create.restype = C.c_void_p
@@ -347,7 +358,7 @@ class Scene:
         return pa, keep, st.as_dict()
 
     def expand_run(self, patches: np.ndarray, alive=None, wave: int = 1, count_threshold: int = 4, cap=None,
-                   after_seeds: bool = False):
+                   after_seeds: bool = False, min_candidates: int = 0):
         """One CExpand::run on the device (expand.cpp:17-406): returns (patches, alive, stats).
 
         The result holds the input patches (flags updated) followed by the new ones; `cap` bounds
@@ -357,7 +368,7 @@ class Scene:
         cap = int(cap or (1 << 30))
         n_out = C.c_int32(0)
         st = ExpandStats()
-        _check(self.lib.pmvs_expand_run(self.handle, _ptr(pa), _ptr(al), len(pa), wave, count_threshold,
+        _check(self.lib.pmvs_expand_run(self.handle, _ptr(pa), _ptr(al), len(pa), wave, min_candidates, count_threshold,
                                         int(after_seeds), None, None, cap, C.byref(n_out), C.byref(st)))
         out = np.empty(n_out.value, PATCH_DTYPE)
         aout = np.empty(n_out.value, np.int32)
@@ -373,20 +384,31 @@ class Scene:
         _check(self.lib.pmvs_scene_set_shard(self.handle, rank, world, ptr, ctx))
 
     def run_loop(self, seeds: np.ndarray, threshold: float, iterations: int = 3, wave: int = 4096, cap=None,
-                 after_seeds: bool = True):
+                 after_seeds: bool = True, native: bool = True, min_candidates: int = 0):
         """CFindMatch::run after the seed phase (findMatch.cpp:196-217): depth 1, then `iterations` x
         (CExpand::run, CFilter::run, updateThreshold, ++depth).  Thresholds follow the reference's
         float arithmetic: before = threshold - 0.3f (findMatch.cpp:104), -= 0.05f per iteration and
-        _countThreshold1 4 -> 2 (findMatch.cpp:23-28).  Returns (patches, per-iteration stats)."""
+        _countThreshold1 4 -> 2 (findMatch.cpp:23-28).  native=True runs the whole loop in the
+        library with the model resident in HBM (pmvs_run_loop); native=False composes expand_run
+        and filter_run through host memory (same result).  Returns (patches, per-iteration stats)."""
+        model = np.ascontiguousarray(seeds, PATCH_DTYPE)
+        if native:
+            iters = (LoopIter * max(1, iterations))()
+            n_out = C.c_int32(0)
+            _check(self.lib.pmvs_run_loop(self.handle, _ptr(model), len(model), float(np.float32(threshold)),
+                                          iterations, wave, min_candidates, 1 if after_seeds else 0, int(cap or (1 << 30)),
+                                          C.byref(n_out), iters))
+            out = np.empty(n_out.value, PATCH_DTYPE)
+            _check(self.lib.pmvs_loop_fetch(self.handle, _ptr(out), n_out.value))
+            return out, [iters[t].as_dict() for t in range(iterations)]
         ncc = np.float32(threshold)
         before = np.float32(ncc - np.float32(0.3))
         cthr, depth = 4, 1
-        model = np.ascontiguousarray(seeds, PATCH_DTYPE)
         log = []
         for t in range(iterations):
             self.set_thresholds(float(ncc), float(before), depth)
             model, alive, st_e = self.expand_run(model, wave=wave, count_threshold=cthr, cap=cap,
-                                                 after_seeds=after_seeds and t == 0)
+                                                 after_seeds=after_seeds and t == 0, min_candidates=min_candidates)
             model, keep, st_f = self.filter_run(model)
             model = model[keep == 1]
             log.append({"depth": depth, "expand": st_e, "filter": st_f, "patches": len(model)})

@@ -227,7 +227,9 @@ pmvs_status pmvs_filter_run(pmvs_scene* scene, pmvs_patch* patches, int32_t n, i
  * max-_tmp queue is expanded in waves of `wave` parents (1 = the reference's single-thread
  * schedule), candidates are refined with preProcess -> refinePatch ->
  * postProcess including the depth >= 1 steps (setVImagesVGrids; check() at depth >= 2) and
- * committed in (parent priority, direction) order.  count_threshold = _countThreshold1 (4 at the
+ * committed in (parent priority, direction) order; with min_candidates > 0 (and wave > 1) a wave
+ * takes further chunks of `wave` parents until its parents have that many free directions
+ * (findEmptyBlocks against the start-of-wave model).  count_threshold = _countThreshold1 (4 at the
  * first expansion, 2 after updateThreshold).  The result is the old patches (with updated
  * _flag/_dflag) followed by the new ones, at most `cap` in all; *n_out is their number.
  * out/alive_out receive it when non-NULL; with out == alive_out == NULL the scene keeps it and
@@ -245,10 +247,27 @@ typedef struct pmvs_expand_stats {
   double refine_ms;
 } pmvs_expand_stats;
 pmvs_status pmvs_expand_run(pmvs_scene* scene, const pmvs_patch* patches, const int32_t* alive, int32_t n,
-                            int32_t wave, int32_t count_threshold, int32_t flags, pmvs_patch* out, int32_t* alive_out,
+                            int32_t wave, int32_t min_candidates, int32_t count_threshold, int32_t flags, pmvs_patch* out, int32_t* alive_out,
                             int32_t cap, int32_t* n_out, pmvs_expand_stats* stats);
 /* Copies the result the last pmvs_expand_run kept (out == NULL) and releases it; n = *n_out. */
 pmvs_status pmvs_expand_fetch(pmvs_scene* scene, pmvs_patch* out, int32_t* alive_out, int32_t n);
+
+/* The dense-matching loop after the seed phase, PMVS3::CFindMatch::run (findMatch.cpp:196-217):
+ * `iterations` x (CExpand::run, CFilter::run, updateThreshold) from the seed patches, with the
+ * model resident in HBM between the passes (only the final model crosses PCIe).  Thresholds as
+ * the reference: depth 1 upwards, ncc = threshold and before = threshold - 0.3f, both -= 0.05f
+ * and _countThreshold1 4 -> 2 after each iteration (findMatch.cpp:23-28, 104).  flags:
+ * PMVS_EXPAND_AFTER_SEEDS for the first expansion.  cap bounds the model size.  *n_out = the final
+ * model's size; pmvs_loop_fetch copies it out.  iters (may be NULL) receives per-iteration stats.
+ * Collective when a shard is set. */
+typedef struct pmvs_loop_iter {
+  int32_t depth, patches; /* patches kept after the filter pass */
+  pmvs_expand_stats expand;
+  pmvs_filter_stats filter;
+} pmvs_loop_iter;
+pmvs_status pmvs_run_loop(pmvs_scene* scene, const pmvs_patch* seeds, int32_t n, float threshold, int32_t iterations,
+                          int32_t wave, int32_t min_candidates, int32_t flags, int32_t cap, int32_t* n_out, pmvs_loop_iter* iters);
+pmvs_status pmvs_loop_fetch(pmvs_scene* scene, pmvs_patch* out, int32_t n);
 
 /* Multi-GPU sharding of the expansion: one scene per GPU/rank, all holding the
  * same model.  Each wave's candidates are split into contiguous rank ranges for the refine and

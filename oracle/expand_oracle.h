@@ -242,8 +242,12 @@ struct QCmp {
 };
 
 // CExpand::run (expand.cpp:17-72) in waves.
+// A wave is `wave` parents, extended by further chunks of `wave` parents (popped in queue order,
+// their free directions found against the same start-of-wave model) while it holds fewer than
+// `min_cands` candidate directions: late passes, where most parents are already surrounded, then
+// batch enough refinements per wave.  min_cands = 0 (or wave = 1) keeps plain waves.
 static void expand_run(const OScene& s, std::vector<FPatch>& P, std::vector<int>& alive, int wave, int cthr, int flags,
-                       ExpandStats& st) {
+                       ExpandStats& st, int min_cands = 0) {
   Model m(s);
   OCtx ctx;
   init_ctx(s, ctx);
@@ -261,28 +265,32 @@ static void expand_run(const OScene& s, std::vector<FPatch>& P, std::vector<int>
   const int W = std::max(1, wave);
   while (!queue.empty()) {
     st.waves++;
-    std::vector<int> parents;
-    while (!queue.empty() && (int)parents.size() < W) {
-      parents.push_back(queue.top().p);
-      queue.pop();
-    }
-    st.parents += (int64_t)parents.size();
     // Every parent's free directions are found against the model at the start of the wave
     // (expand.cpp:92-93); wave = 1 then prepares, refines and commits them one after the other
     // (expand.cpp:95-101, the single-thread schedule), wider waves do so as one batch and
     // re-run checkCounts at commit.
+    std::vector<int> parents;
     std::vector<Cand> dirs;
-    for (int par : parents) {
-      std::vector<std::pair<int, V4>> d;
-      find_empty_blocks(m, P, P[par], P[par].dflag, d);
-      for (auto& x : d) {
-        Cand c;
-        c.parent = par;
-        c.dir = x.first;
-        c.coord = x.second;
-        dirs.push_back(std::move(c));
+    do {
+      std::vector<int> chunk;
+      while (!queue.empty() && (int)chunk.size() < W) {
+        chunk.push_back(queue.top().p);
+        queue.pop();
       }
-    }
+      for (int par : chunk) {
+        std::vector<std::pair<int, V4>> d;
+        find_empty_blocks(m, P, P[par], P[par].dflag, d);
+        for (auto& x : d) {
+          Cand c;
+          c.parent = par;
+          c.dir = x.first;
+          c.coord = x.second;
+          dirs.push_back(std::move(c));
+        }
+      }
+      parents.insert(parents.end(), chunk.begin(), chunk.end());
+    } while (W > 1 && (int64_t)dirs.size() < min_cands && !queue.empty());
+    st.parents += (int64_t)parents.size();
     auto batch = [&](size_t b, size_t e, bool recheck) {
       for (size_t i = b; i < e; ++i) {
         Cand& c = dirs[i];

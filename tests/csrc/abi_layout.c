@@ -30,6 +30,7 @@ int main(void) {
   S(pmvs_expand_stats); O(pmvs_expand_stats, added); O(pmvs_expand_stats, wall_ms);
   O(pmvs_expand_stats, refined); O(pmvs_expand_stats, tex_valid); O(pmvs_expand_stats, refine_ms);
   O(pmvs_patch, dflag);
+  S(pmvs_loop_iter); O(pmvs_loop_iter, patches); O(pmvs_loop_iter, expand); O(pmvs_loop_iter, filter);
   S(pmvs_options); O(pmvs_options, threshold); O(pmvs_options, num_timages); O(pmvs_options, timages);
   O(pmvs_options, visdata2);
   S(pmvs_synth_params); O(pmvs_synth_params, seed); O(pmvs_synth_params, arc_step_deg);

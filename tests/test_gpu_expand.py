@@ -92,8 +92,8 @@ def test_expand_capacity_error(gpu_available):
     g.close()
 
 
-@pytest.mark.parametrize("wave", [1, 512])
-def test_full_loop_matches_oracle(gpu_available, oracle_mod, wave):
+@pytest.mark.parametrize("wave,native", [(1, True), (512, True), (512, False)])
+def test_full_loop_matches_oracle(gpu_available, oracle_mod, wave, native):
     """CFindMatch::run after the seed phase (findMatch.cpp:196-217): 3 x (expand, filter,
     updateThreshold) from refined seeds, first expansion with the seed phase's empty depth maps."""
     import pmvs_amd as P
@@ -101,7 +101,7 @@ def test_full_loop_matches_oracle(gpu_available, oracle_mod, wave):
     g = P.Scene(inp)
     o = oracle_mod.OracleScene(inp)
     pa = seed_model(P, g, inp, p, 200, 7)
-    out_g, log_g = g.run_loop(pa, inp.threshold, wave=wave)
+    out_g, log_g = g.run_loop(pa, inp.threshold, wave=wave, native=native)
     out_o, log_o = o.run_loop(pa, inp.threshold, wave=wave)
     g.close()
     o.close()
@@ -196,3 +196,38 @@ def test_sharded_full_loop_matches_single_rank(gpu_available):
     for out, log in res:
         assert [x["patches"] for x in log] == [x["patches"] for x in log_ref]
         compare(out, np.ones(len(out), np.int32), {}, ref, np.ones(len(ref), np.int32), {})
+
+
+@pytest.mark.parametrize("depth", [1, 2])
+def test_expand_min_candidates_matches_oracle(gpu_available, oracle_mod, depth):
+    """Waves extended by further parent chunks until they hold min_candidates free directions
+    (the schedule bench.py uses for C3): device and oracle run the same schedule."""
+    import pmvs_amd as P
+    inp, p = P.synth_scene(6, 480, 360, level=1, supersample=2)
+    g = P.Scene(inp)
+    o = oracle_mod.OracleScene(inp)
+    pa = seed_model(P, g, inp, p, 300, 5)
+    for sc in (g, o):
+        sc.set_thresholds(inp.threshold, inp.threshold - 0.3, depth)
+    out_g, al_g, st_g = g.expand_run(pa, wave=16, min_candidates=300)
+    out_o, al_o, st_o = o.expand_run(pa, wave=16, min_candidates=300, cap=200000)
+    g.close()
+    o.close()
+    assert st_o["waves"] < st_o["parents"] / 16
+    compare(out_g, al_g, st_g, out_o, al_o, st_o)
+
+
+def test_full_loop_min_candidates_matches_oracle(gpu_available, oracle_mod):
+    import pmvs_amd as P
+    inp, p = P.synth_scene(6, 480, 360, level=1, supersample=2)
+    g = P.Scene(inp)
+    o = oracle_mod.OracleScene(inp)
+    pa = seed_model(P, g, inp, p, 200, 8)
+    out_g, log_g = g.run_loop(pa, inp.threshold, wave=64, min_candidates=256)
+    out_o, log_o = o.run_loop(pa, inp.threshold, wave=64, min_candidates=256)
+    g.close()
+    o.close()
+    for a, b in zip(log_g, log_o):
+        assert a["patches"] == b["patches"], (a, b)
+        assert {k: v for k, v in a["expand"].items() if k not in P.ExpandStats.WORK} == b["expand"]
+    compare(out_g, np.ones(len(out_g), np.int32), {}, out_o, np.ones(len(out_o), np.int32), {})
