@@ -1,20 +1,31 @@
 #!/usr/bin/env python3
-"""bench.py -- MI355X PMVS2 refine throughput (BASELINE.json metric), one JSON line on rank 0.
+"""bench.py -- MI355X PMVS2 dense-matching throughput (BASELINE.json metric), one JSON line on rank 0.
 
-Workload (BASELINE.json configs[1], "C2"): a synthetic 8-view 1920x1080 textured-sphere ring,
-level 1, csize 2, wsize 7, minImageNum 3, threshold 0.7; 100,000 seed-path candidates per GPU
-(CSeed::initialMatchSub shape: images = [most frontal view, next view], depth perturbed,
-normal tilted <= 10 deg).  One step = preProcess -> refinePatch (BOBYQA, <=1000 my_f evals)
--> postProcess over the whole batch on the device (candidates and results resident in HBM).
+Workload (default, BASELINE.json configs[2] "C3" -- the metric's "50-view 4K synthetic"): a
+synthetic 50-view 3840x2160 textured-sphere ring, level 0, csize 2, wsize 7, minImageNum 3,
+threshold 0.7.  Setup (untimed): render the views, build the scene on the device, refine 5000
+seed-path candidates into the seed model (the seed phase, SURVEY.md §8(f) f1, is not on this
+path).  One step = CFindMatch::run after the seeds: 3 x (CExpand::run -> COptim refine ->
+CFilter::run, updateThreshold) through pmvs_run_loop, with the model resident in HBM.
 
-value = refined (accepted) patches/s over all ranks; also reported: NCC evals/s.
-roofline: algorithmic bytes = 588 B x valid textures per my_f evaluation over
-the refine kernel's HIP-event time, against 8 TB/s HBM.
-cpu_baseline: the oracle (CPU restatement, std::thread pool) on a bounded sample on this host.
+value = refined patches/s: patches the expansion refined and committed to the model
+(preProcess -> refinePatch -> postProcess passed, expand.cpp:238) over all ranks / step time.
+Also: NCC evals/s (my_f + computeINCC evaluations), refined candidates/s.
+roofline: the loop's dominant kernel, refine_v2_kernel: algorithmic bytes = 588 B x valid
+textures per my_f evaluation over its HIP-event time, against 8 TB/s HBM.
+refine_c2: the refine kernel alone on configs[1] (8-view 1920x1080, level 1, 100k candidates).
+cpu_baseline: the oracle (CPU restatement, std::thread pool) on a bounded sample of the same
+scene's refine work (preProcess -> refinePatch -> postProcess, >= 80 % of the reference's CPU
+time) on this host.
 
-Multi-GPU (weak scaling): `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`;
-each rank owns one GPU and its own candidate batch; no data-path collective (the path shards
-by candidate); only barriers and the max-over-ranks time reduction.
+Multi-GPU (`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`), one
+process per GPU:
+  --mode cluster (default, weak scaling): each rank owns one CMVS-style cluster -- its own
+    50-view scene (rank-seeded texture) -- and runs the loop on it independently, as the
+    reference runs one pmvs2 per cluster option file (genOption.cpp:73-108); no data-path
+    collective, only barriers and the SUM / MAX reductions of the counters and the time.
+  --mode shard (strong scaling): all ranks run ONE scene; every expansion wave's refinements are
+    split over the ranks and all-gathered over RCCL (pmvs_scene_set_shard + DistExchange).
 """
 import argparse
 import json
@@ -30,49 +41,54 @@ sys.path.insert(0, os.path.join(ROOT, "cmvs-pmvs_amd"))
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 BYTES_PER_TEXTURE = 49 * 4 * 3  # wsize^2 samples x 4 texels x 3 B
+REFINE_KERNEL = "refine_v2_kernel<7,16,8>"
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--candidates", type=int, default=100000)
-    ap.add_argument("--views", type=int, default=8)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--level", type=int, default=1)
+    ap.add_argument("--mode", choices=("cluster", "shard"), default="cluster")
+    ap.add_argument("--views", type=int, default=50)
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--level", type=int, default=0)
+    ap.add_argument("--seeds", type=int, default=5000)
+    ap.add_argument("--wave", type=int, default=8192)
+    ap.add_argument("--min-candidates", type=int, default=16384)
+    ap.add_argument("--iterations", type=int, default=3)
+    ap.add_argument("--c2-candidates", type=int, default=100000)
+    ap.add_argument("--no-c2", action="store_true", help="skip the configs[1] refine-kernel side measurement")
+    ap.add_argument("--only-c2", action="store_true", help="only the configs[1] refine-kernel measurement (profiling)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-filter", action="store_true", help="skip the filter-pass side measurement")
     return ap.parse_args()
 
 
-def pmc_traffic(args):
-    """HBM bytes per refine launch from the committed rocprofv3 PMC summary (tools/gpu_round.sh +
-    tools/summarize_profiles.py; FETCH_SIZE x2 per MI355X_MICROARCH.md + WRITE_SIZE) when it was
-    measured on this same default workload; otherwise null."""
-    if (args.candidates, args.views, args.width, args.height, args.level) != (100000, 8, 1920, 1080, 1):
-        return None, None
+def pmc_traffic(workload):
+    """HBM bytes per refine-kernel launch from the newest committed rocprofv3 PMC summary of the
+    same workload (tools/gpu_round.sh + tools/summarize_profiles.py: FETCH_SIZE x2 per
+    MI355X_MICROARCH.md + WRITE_SIZE, separate --pmc passes); otherwise null."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
-    for f in reversed(files):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), reverse=True):
         d = json.load(open(f))
+        if d.get("workload") != workload:
+            continue
         for k, v in d.get("kernels", {}).items():
-            if "refine_v2_kernel" in k and k.endswith(os.environ.get("PMVS_REFINE_CONFIG_NAME", "<7, 16, 8>")):
-                return int(v["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT)
-    return None, None
+            if k.startswith("pmvsdev::refine_v2_kernel") or k.startswith("refine_v2_kernel"):
+                return int(v["hbm_bytes_per_launch"]), int(v.get("launches", 0)), os.path.relpath(f, ROOT)
+    return None, None, None
 
 
-def rank_candidate_seed(rank: int) -> int:
-    """Each rank refines its own candidate shard (weak scaling, no data-path exchange)."""
+def rank_seed(rank: int) -> int:
     return 0x5EED + 7919 * rank
 
 
 def reduce_over_ranks(dist, counts, elapsed, device):
-    """SUM the per-rank counters and MAX the per-rank timed-region length over all ranks (the
-    only collectives of the benchmark).  Works with nccl (RCCL) on GPUs and gloo on CPUs."""
+    """SUM the per-rank counters and MAX the per-rank timed-region length over all ranks.  Works
+    with nccl (RCCL) on GPUs and gloo on CPUs."""
     import torch
     totals = torch.tensor([float(c) for c in counts], dtype=torch.float64, device=device)
     tmax = torch.tensor([float(elapsed)], dtype=torch.float64, device=device)
@@ -80,6 +96,48 @@ def reduce_over_ranks(dist, counts, elapsed, device):
         dist.all_reduce(totals, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     return totals.tolist(), tmax.item()
+
+
+def refine_roofline(tex_valid, refine_ms, launches, traffic, traffic_launches, src):
+    s = refine_ms / 1e3
+    achieved = tex_valid * BYTES_PER_TEXTURE / s / 1e9 if s > 0 else 0.0
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": REFINE_KERNEL,
+            "launches": launches, "kernel_ms_avg": round(refine_ms / max(1, launches), 3),
+            "algorithmic_bytes_per_launch": int(tex_valid * BYTES_PER_TEXTURE / max(1, launches)),
+            "traffic_source": src, "traffic_launches": traffic_launches}
+
+
+def c2_refine(P, args, dev, rank):
+    """configs[1]: the refine kernel alone (preProcess -> refinePatch -> postProcess) on 100k
+    seed-path candidates of an 8-view 1920x1080 level-1 ring, candidates resident in HBM."""
+    import torch
+    inp, sp = P.synth_scene(8, 1920, 1080, level=1, supersample=2, nthreads=16)
+    scene = P.Scene(inp, device=dev.index or 0)
+    n = args.c2_candidates
+    cands = P.synth_candidates(sp, inp.projections, n, seed=rank_seed(rank))
+    d_in = torch.from_numpy(cands.view(np.uint8)).to(dev)
+    d_out = torch.empty(n * P.REFINED_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    scene.refine_batch_device(d_in.data_ptr(), n, d_out.data_ptr())
+    scene.sync()
+    stats = []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        scene.refine_batch_device(d_in.data_ptr(), n, d_out.data_ptr())
+        stats.append(scene.sync())
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    scene.close()
+    acc = sum(s["accepted"] for s in stats)
+    ev = sum(s["evals"] for s in stats)
+    tv = sum(s["tex_valid"] for s in stats)
+    rms = sum(s["refine_ms"] for s in stats)
+    tr, tl, src = pmc_traffic("c2")
+    return {"workload": "C2: 8-view 1920x1080 ring, level 1, 100000 seed candidates, refine kernel only",
+            "value": round(acc / el, 1), "unit": "refined patches/s", "ncc_evals_per_s": round(ev / el, 1),
+            "ms_per_step": round(el / 3 * 1e3, 3),
+            "roofline": refine_roofline(tv, rms, 3, tr, tl, src)}
 
 
 def main():
@@ -96,21 +154,34 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
     dev = torch.device("cuda", local)
+    shard = args.mode == "shard" and world > 1
+    if args.only_c2:
+        c2 = c2_refine(P, args, dev, rank)
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "refine_c2": c2}), flush=True)
+        return c2
 
-    # ---- scene (identical on every rank) and this rank's candidates
+    # ---- scene: one cluster per rank (cluster mode) or one shared scene (shard mode)
     t0 = time.time()
-    inp, sp = P.synth_scene(args.views, args.width, args.height, level=args.level, supersample=2, nthreads=16)
+    tex_seed = 0x504D5653 + (0 if (shard or world == 1) else 104729 * rank)
+    inp, sp = P.synth_scene(args.views, args.width, args.height, level=args.level, supersample=2, nthreads=16,
+                            seed=tex_seed)
     t_synth = time.time() - t0
+    t0 = time.time()
     scene = P.Scene(inp, device=local)
-    cands = P.synth_candidates(sp, inp.projections, args.candidates, seed=rank_candidate_seed(rank))
-    nbytes_in = cands.nbytes
-    d_in = torch.from_numpy(cands.view(np.uint8)).to(dev)
-    d_out = torch.empty(args.candidates * P.REFINED_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-    torch.cuda.synchronize()
+    cands = P.synth_candidates(sp, inp.projections, args.seeds, seed=rank_seed(0 if shard else rank))
+    res, _ = scene.refine_batch(cands)
+    seeds = P.patches_from_refined(res)
+    t_scene = time.time() - t0
+    ex = None
+    if shard:
+        ex = P.DistExchange(device=dev)
+        ex.attach(scene)
 
     def step():
-        scene.refine_batch_device(d_in.data_ptr(), args.candidates, d_out.data_ptr())
-        return scene.sync()
+        model, log = scene.run_loop(seeds, inp.threshold, iterations=args.iterations, wave=args.wave,
+                                    min_candidates=args.min_candidates)
+        return len(model), log
 
     for _ in range(args.warmup):
         step()
@@ -118,105 +189,90 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    stats = []
+    logs = []
     for _ in range(args.steps):
-        stats.append(step())
+        logs.append(step())
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
-    accepted = sum(s["accepted"] for s in stats)
-    evals = sum(s["evals"] for s in stats)
-    tex_valid = sum(s["tex_valid"] for s in stats)
-    kernel_ms = [s["refine_ms"] for s in stats]
-    stage_ms = {k: round(float(np.mean([s[k] for s in stats])), 3) for k in ("pre_ms", "refine_ms", "post_ms")}
-    prof = {k: sum(s[k] for s in stats) for k in ("opt_cycles", "objective_cycles", "rounds", "chunks")}
-    phase = np.sum([s["prof"] for s in stats], axis=0)
-    phase_names = ("refill", "step", "publish", "chunk_setup", "gather", "normalize", "dot", "reduce")
-    (accepted_all, evals_all, texv_all, cand_all), elapsed_max = reduce_over_ranks(
-        dist, [accepted, evals, tex_valid, args.candidates * args.steps], elapsed, dev)
+    def tot(key):
+        return sum(it["expand"][key] for _, log in logs for it in log)
+    added = tot("added")
+    own_added = added if (not shard or rank == 0) else 0  # shard mode: one shared model
+    refined, evals, tex_valid, refine_ms = tot("refined"), tot("evals"), tot("tex_valid"), tot("refine_ms")
+    expand_s = tot("wall_ms") / 1e3
+    filter_s = sum(it["filter"]["kernel_ms"] for _, log in logs for it in log) / 1e3
+    (added_all, refined_all, evals_all), elapsed_max = reduce_over_ranks(dist, [own_added, refined, evals], elapsed,
+                                                                         dev)
+    launches = tot("refine_launches")
+    traffic, traffic_launches, traffic_src = pmc_traffic("c3")
+    roof = refine_roofline(tex_valid, refine_ms, launches, traffic, traffic_launches, traffic_src)
 
-    # ---- roofline of the dominant kernel (refine_v2_kernel), per launch, HIP-event timed on the
-    # scene stream (events recorded right before and after that launch)
-    avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
-    bytes_per_launch = tex_valid / args.steps * BYTES_PER_TEXTURE
-    achieved = bytes_per_launch / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
-
-    # ---- side measurement: one CFilter::run pass (depth 1) over this rank's refined patches
-    filt = None
-    if not args.no_filter:
-        res = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=P.REFINED_DTYPE)
-        patches = P.patches_from_refined(res)
-        scene.set_thresholds(0.7, 0.4, 1)
-        t0 = time.perf_counter()
-        _, keep, fst = scene.filter_run(patches)
-        tf = time.perf_counter() - t0
-        scene.set_thresholds(0.7, 0.4, 0)
-        filt = {"patches": int(len(patches)), "kept": int(fst["kept"]), "device_ms": round(fst["kernel_ms"], 3),
-                "wall_ms": round(tf * 1e3, 3), "patches_per_s": round(len(patches) / (fst["kernel_ms"] / 1e3), 1),
-                "removed": [int(fst[k]) for k in ("removed_outside", "removed_exact", "removed_neighbor",
-                                                  "removed_groups")]}
-    traffic, traffic_src = pmc_traffic(args)
     result = None
+    c2 = None
+    if rank == 0 and not args.no_c2:
+        c2 = c2_refine(P, args, dev, rank)
     if rank == 0:
-        # ---- CPU baseline (oracle restatement on this host, bounded sample)
         cpu = None
         if not args.no_cpu_baseline:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import pyoracle as O
             o = O.OracleScene(inp)
             threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+            sample = P.synth_candidates(sp, inp.projections, 600000, seed=0xC0FFEE)
             done = acc_cpu = 0
-            chunk = 2000
-            t0 = time.perf_counter()
-            while time.perf_counter() - t0 < args.cpu_seconds and done < len(cands):
-                r, st = o.refine_batch(cands[done:done + chunk], nthreads=threads)
+            chunk = 1000
+            tc0 = time.perf_counter()
+            while time.perf_counter() - tc0 < args.cpu_seconds and done < len(sample):
+                r, st = o.refine_batch(sample[done:done + chunk], nthreads=threads)
                 done += len(r)
                 acc_cpu += st["accepted"]
-            tc = time.perf_counter() - t0
+            tc = time.perf_counter() - tc0
             o.close()
             cpu = {"value": round(acc_cpu / tc, 1), "unit": "refined patches/s", "cores": threads, "kind": "port",
-                   "sample": f"first {done} of the {args.candidates} rank-0 candidates, oracle/liboracle.so "
-                             f"(CPU restatement, std::thread pool), {tc:.1f} s"}
+                   "sample": f"{done} candidates of the rank-0 C3 scene through preProcess->refinePatch->"
+                             f"postProcess, oracle/liboracle.so (CPU restatement, std::thread pool), {tc:.1f} s"}
+        first = logs[0][1]
         result = {
             "metric": METRIC,
-            "value": round(accepted_all / elapsed_max, 1),
+            "value": round(added_all / elapsed_max, 1),
             "unit": "refined patches/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if shard else "weak",
             "vs_baseline": None,
             "dtype": "f32 (f64 optimizer)",
-            "data": "synthetic (textured-sphere ring rendered by pmvs_synth_ring; seeded candidates)",
+            "data": "synthetic (textured-sphere ring rendered by pmvs_synth_ring; seed model from refined "
+                    "synthetic seed candidates)",
             "config": {
-                "workload": f"C2: {args.views}-view {args.width}x{args.height} synthetic ring, level {args.level}, "
-                            f"{args.candidates} seed candidates per GPU, preProcess->refinePatch->postProcess",
-                "candidates_per_gpu": args.candidates, "views": args.views, "width": args.width,
-                "height": args.height, "level": args.level, "wsize": 7, "csize": 2, "minImageNum": 3,
-                "parallelism": f"candidate-sharded x{world}",
+                "workload": f"C3: {args.views}-view {args.width}x{args.height} synthetic ring, level {args.level}, "
+                            f"full expand->optim->filter loop ({args.iterations} iterations) from {args.seeds} "
+                            f"seed candidates" + (", one scene sharded over all GPUs" if shard else
+                                                  ", one cluster per GPU"),
+                "views": args.views, "width": args.width, "height": args.height, "level": args.level,
+                "seed_candidates": args.seeds, "seed_patches": int(len(seeds)), "wave": args.wave,
+                "min_candidates": args.min_candidates, "iterations": args.iterations, "wsize": 7, "csize": 2,
+                "minImageNum": 3, "threshold": 0.7,
+                "parallelism": f"{'wave-sharded' if shard else 'cluster-per-GPU'} x{world}",
             },
             "ncc_evals_per_s": round(evals_all / elapsed_max, 1),
-            "accepted_fraction": round(accepted_all / cand_all, 4),
-            "evals_per_candidate": round(evals_all / cand_all, 2),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "kernel": "refine_v2_kernel<7,16,8>", "kernel_ms_avg": round(avg_kernel_s * 1e3, 3),
-                         "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                         "traffic_source": traffic_src},
-            "stage_ms": stage_ms,
-            "filter_pass": filt,
+            "refined_candidates_per_s": round(refined_all / elapsed_max, 1),
+            "model_patches": logs[0][0],
+            "roofline": roof,
+            "stage_s_per_step": {"expand": round(expand_s / args.steps, 3), "filter_device": round(filter_s / args.steps, 3),
+                                 "refine_kernel": round(refine_ms / 1e3 / args.steps, 3)},
+            "iterations": [{"depth": it["depth"], "patches": it["patches"], "added": it["expand"]["added"],
+                            "candidates": it["expand"]["candidates"], "waves": it["expand"]["waves"],
+                            "expand_ms": round(it["expand"]["wall_ms"], 1),
+                            "filter_ms": round(it["filter"]["kernel_ms"], 1)} for it in first],
+            "refine_c2": c2,
             "cpu_baseline": cpu,
-            "setup_s": {"synth": round(t_synth, 2)},
-            "refine_profile": {"optimizer_cycle_frac": round(prof["opt_cycles"] / max(1, prof["opt_cycles"] + prof["objective_cycles"]), 4),
-                               "rounds": prof["rounds"], "chunks": prof["chunks"],
-                               "phase_frac": {k: round(float(v) / max(1.0, float(phase.sum())), 4) for k, v in zip(phase_names, phase)},
-                               "config": int(os.environ.get("PMVS_REFINE_CONFIG", "1608")),
-                               "waves_per_cu": int(os.environ.get("PMVS_REFINE_WAVES_PER_CU", "4"))},
-            "input_bytes_resident": nbytes_in,
+            "setup_s": {"synth": round(t_synth, 2), "scene_and_seeds": round(t_scene, 2)},
         }
         print(json.dumps(result), flush=True)
     scene.close()

@@ -758,7 +758,7 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
   // are reset per launch); the refine-kernel time of each launch is read at the next one, when
   // the host has synchronised in between.
   double refine_ms = 0.0;
-  int64_t refined = 0;
+  int64_t refined = 0, launches = 0;
   bool pending = false;
   auto take_time = [&]() {
     if (!pending) return;
@@ -773,6 +773,7 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
     hipError_t e = hipMemsetAsync(&sc->stats.p->queue, 0, 3 * sizeof(unsigned long long), sc->stream);
     if (e != hipSuccess) return e;
     refined += m;
+    ++launches;
     pending = true;
     return launch_refine(sc->ds, d_in, sc->jobs.p, d_out, m, sc->stats.p, sc->grid, sc->refine_grid, sc->tslots,
                          sc->stream, sc->kev);
@@ -808,6 +809,7 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
     stats->evals = (int64_t)ds.evals;
     stats->tex_valid = (int64_t)ds.tex_valid;
     stats->refine_ms = refine_ms;
+    stats->refine_launches = launches;
   }
   sc->last_refine = false;
   return PMVS_OK;

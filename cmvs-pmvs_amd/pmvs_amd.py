@@ -79,9 +79,10 @@ class FilterStats(C.Structure):
 class ExpandStats(C.Structure):
     _fields_ = [(k, C.c_int64) for k in ("parents", "candidates", "fail_prep", "fail_pre", "fail_post",
                                           "fail_commit", "added", "waves")] + [("wall_ms", C.c_double)] + \
-               [(k, C.c_int64) for k in ("refined", "evals", "tex_valid")] + [("refine_ms", C.c_double)]
+               [(k, C.c_int64) for k in ("refined", "evals", "tex_valid")] + [("refine_ms", C.c_double)] + \
+               [("refine_launches", C.c_int64)]
 
-    WORK = ("wall_ms", "refined", "evals", "tex_valid", "refine_ms")  # timing / per-rank work fields
+    WORK = ("wall_ms", "refined", "evals", "tex_valid", "refine_ms", "refine_launches")  # timing / per-rank work fields
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -557,8 +558,9 @@ def synth_candidates(p: SynthParams, proj: np.ndarray, n: int, seed: int = 0x5EE
 
 
 def synth_scene(num_views: int, width: int, height: int, level: int = 1, num_targets: Optional[int] = None,
-                supersample: int = 2, nthreads: int = 8, **opts) -> SceneInputs:
-    p = synth_params(num_views, width, height, num_targets=num_targets, supersample=supersample, level=level)
+                supersample: int = 2, nthreads: int = 8, seed: int = 0x504D5653, **opts) -> SceneInputs:
+    p = synth_params(num_views, width, height, num_targets=num_targets, supersample=supersample, level=level,
+                     seed=seed)
     rgb, proj = synth_ring(p, nthreads=nthreads)
     return SceneInputs(images=[rgb[i] for i in range(num_views)], projections=proj,
                        num_targets=p.num_targets, level=level, **opts), p

@@ -245,6 +245,7 @@ typedef struct pmvs_expand_stats {
    * refine-kernel time (HIP events) */
   int64_t refined, evals, tex_valid;
   double refine_ms;
+  int64_t refine_launches;
 } pmvs_expand_stats;
 pmvs_status pmvs_expand_run(pmvs_scene* scene, const pmvs_patch* patches, const int32_t* alive, int32_t n,
                             int32_t wave, int32_t min_candidates, int32_t count_threshold, int32_t flags, pmvs_patch* out, int32_t* alive_out,

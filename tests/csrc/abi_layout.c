@@ -28,7 +28,7 @@ int main(void) {
   O(pmvs_patch, grids); O(pmvs_patch, vimages); O(pmvs_patch, vgrids);
   S(pmvs_filter_stats); O(pmvs_filter_stats, kernel_ms);
   S(pmvs_expand_stats); O(pmvs_expand_stats, added); O(pmvs_expand_stats, wall_ms);
-  O(pmvs_expand_stats, refined); O(pmvs_expand_stats, tex_valid); O(pmvs_expand_stats, refine_ms);
+  O(pmvs_expand_stats, refined); O(pmvs_expand_stats, tex_valid); O(pmvs_expand_stats, refine_ms); O(pmvs_expand_stats, refine_launches);
   O(pmvs_patch, dflag);
   S(pmvs_loop_iter); O(pmvs_loop_iter, patches); O(pmvs_loop_iter, expand); O(pmvs_loop_iter, filter);
   S(pmvs_options); O(pmvs_options, threshold); O(pmvs_options, num_timages); O(pmvs_options, timages);

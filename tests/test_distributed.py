@@ -29,7 +29,7 @@ def _worker(rank, world, port, out):
     import pyoracle as O
     dist.init_process_group("gloo", rank=rank, world_size=world)
     inp, sp = P.synth_scene(4, 160, 120, level=1, supersample=1)
-    cands = P.synth_candidates(sp, inp.projections, 64, seed=bench.rank_candidate_seed(rank))
+    cands = P.synth_candidates(sp, inp.projections, 64, seed=bench.rank_seed(rank))
     o = O.OracleScene(inp)
     r, st = o.refine_batch(cands, nthreads=1)
     o.close()

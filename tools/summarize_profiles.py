@@ -35,27 +35,27 @@ def pmc(dirname, counter):
             for k, v in out.items()}
 
 
-def main(tag):
+def main(tag, workload="c3"):
     src = os.path.join(ROOT, "gpurun_out", tag)
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
     stats = glob.glob(os.path.join(src, "kt", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
-        shutil.copy(stats[0], os.path.join(dst, f"{tag}_kernel_stats.csv"))
+        shutil.copy(stats[0], os.path.join(dst, f"{tag.replace('/', '_')}_kernel_stats.csv"))
     if os.path.exists(os.path.join(src, "bench.json")):
-        shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, f"{tag}_bench.json"))
+        shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, f"{tag.replace('/', '_')}_bench.json"))
     fetch = pmc(os.path.join(src, "pmc_fetch"), "FETCH_SIZE")
     write = pmc(os.path.join(src, "pmc_write"), "WRITE_SIZE")
-    res = {"source": f"gpurun_out/{tag} (rocprofv3 --pmc, one bench step, C2 workload)",
-           "fetch_correction": 2.0, "kernels": {}}
+    res = {"source": f"gpurun_out/{tag} (rocprofv3 --pmc, one bench step, {workload} workload)",
+           "workload": workload, "fetch_correction": 2.0, "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         f = fetch.get(k, {}).get("bytes_per_launch", 0.0)
         w = write.get(k, {}).get("bytes_per_launch", 0.0)
-        res["kernels"][k] = {"fetch_bytes_raw": f, "fetch_bytes_corrected": 2.0 * f, "write_bytes": w,
-                             "hbm_bytes_per_launch": 2.0 * f + w}
-    json.dump(res, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
+        res["kernels"][k] = {"launches": fetch.get(k, write.get(k, {})).get("launches", 0), "fetch_bytes_raw": f,
+                             "fetch_bytes_corrected": 2.0 * f, "write_bytes": w, "hbm_bytes_per_launch": 2.0 * f + w}
+    json.dump(res, open(os.path.join(dst, f"{tag.replace('/', '_')}_pmc.json"), "w"), indent=1)
     print(json.dumps(res, indent=1)[:2000])
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "c3")
