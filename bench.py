@@ -55,8 +55,8 @@ def parse():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--level", type=int, default=0)
     ap.add_argument("--seeds", type=int, default=5000)
-    ap.add_argument("--wave", type=int, default=8192)
-    ap.add_argument("--min-candidates", type=int, default=16384)
+    ap.add_argument("--wave", type=int, default=32768)
+    ap.add_argument("--min-candidates", type=int, default=65536)
     ap.add_argument("--iterations", type=int, default=3)
     ap.add_argument("--c2-candidates", type=int, default=100000)
     ap.add_argument("--no-c2", action="store_true", help="skip the configs[1] refine-kernel side measurement")

@@ -28,6 +28,7 @@
 #include <cstddef>
 #include <cstdlib>
 #include <cstring>
+#include <sys/mman.h>
 #include <deque>
 #include <functional>
 #include <queue>
@@ -437,6 +438,7 @@ __global__ void exact_after_ref_kernel(DScene s, const pmvs_patch* __restrict__ 
 
 // --------------------------------------------------------------------------- filterNeighbor
 struct NbLds {
+  int sb[64], so[64], sl[64];  // gather_neighbors: per-slot list start, flattened offset, list kind
   int nb[NB_CAP];
   float fx[NB_CAP], fy[NB_CAP], fz[NB_CAP];
   float units[PMVS_MAX_IMAGES];
@@ -556,6 +558,41 @@ __device__ float compute_radius_wave(const DScene& s, NbLds& L, const pmvs_patch
 // CPatchOrganizerS::findNeighbors(patch, neighbors, lock, scale, margin, skipvis)
 // (patchOrganizerS.cpp:527-631) into L.nb[0..n), sorted by patch index and unique.  Returns n;
 // L.overflow is set when more than NB_CAP unique neighbours exist.
+__device__ __forceinline__ int wave_excl_scan_w(int v) {
+  const int lane = lane_id_w();
+  int x = v;
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  return x - v;
+}
+
+// Appends the hits of one 64-lane round in lane order (ballot), compacting the buffer (sort +
+// unique) when it nears capacity, as the reference's final sort/unique would (same set).
+__device__ __forceinline__ void nb_append(NbLds& L, bool hit, int j) {
+  const int lane = lane_id_w();
+  const unsigned long long mask = __ballot(hit);
+  const int before = __popcll(mask & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+  const int pos = L.cnt + before;
+  if (hit) {
+    if (pos < NB_CAP) L.nb[pos] = j;
+    else L.overflow = 1;
+  }
+  __syncthreads();
+  if (lane == 0) L.cnt += __popcll(mask);
+  __syncthreads();
+  const int cnt = uni(L.cnt);
+  if (cnt > NB_CAP - 64 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(cnt, NB_CAP), &L.cnt);
+}
+
+// CPatchOrganizerS::findNeighbors(patch, neighbors, lock, scale, margin, skipvis)
+// (patchOrganizerS.cpp:527-631) into L.nb[0..n), sorted by patch index and unique.  Returns n;
+// L.overflow is set when more than NB_CAP unique neighbours exist.
+// The (image list, dy, dx, pgrids/vpgrids) cells are visited 64 at a time, one per lane (their
+// list bounds load in parallel); the cells' entries are then flattened and tested 64 per round.
+// Expansion-time chain entries (FilterDev delta) are walked per lane.  The neighbour SET is the
+// reference's; the visiting order only matters for the buffer's compaction points.
 __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, const pmvs_patch& q, float scale,
                                 int margin, int skipvis) {
   const int lane = lane_id_w();
@@ -569,82 +606,83 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, c
   if (lane == 0) { L.cnt = 0; L.overflow = 0; }
   __syncthreads();
   const int nlists = skipvis ? ni : ni + uni(q.num_vimages);
-  for (int k = 0; k < nlists; ++k) {
-    const bool vis = k >= ni;
-    const int t = uni(vis ? q.vimages[k - ni] : q.images[k]);
-    if (s.tnum <= t) continue;
-    const int gx = uni(vis ? q.vgrids[k - ni][0] : q.grids[k][0]);
-    const int gy = uni(vis ? q.vgrids[k - ni][1] : q.grids[k][1]);
-    const int gw = gwidth(s, t), gh = gheight(s, t);
-    for (int dy = -margin; dy <= margin; ++dy) {
-      const int yt = gy + dy;
-      if (yt < 0 || gh <= yt) continue;
-      for (int dx = -margin; dx <= margin; ++dx) {
-        const int xt = gx + dx;
-        if (xt < 0 || gw <= xt) continue;
-        const long long c = F.tgoff[t] + (long long)yt * gw + xt;
-        for (int lst = 0; lst < 2; ++lst) {
+  const int side = 2 * margin + 1;
+  const int per_list = side * side * 2;
+  const int nslots = nlists * per_list;
+  for (int base = 0; base < nslots; base += 64) {
+    const int slot = base + lane;
+    int b = 0, e = 0, lst = 0, head = -1;
+    if (slot < nslots) {
+      const int k = slot / per_list;
+      int r = slot - k * per_list;
+      const int dyi = r / (2 * side);
+      r -= dyi * 2 * side;
+      const int dxi = r >> 1;
+      lst = r & 1;
+      const bool vis = k >= ni;
+      const int t = vis ? q.vimages[k - ni] : q.images[k];
+      if (t < s.tnum) {
+        const int gw = gwidth(s, t), gh = gheight(s, t);
+        const int yt = (vis ? q.vgrids[k - ni][1] : q.grids[k][1]) + dyi - margin;
+        const int xt = (vis ? q.vgrids[k - ni][0] : q.grids[k][0]) + dxi - margin;
+        if (0 <= yt && yt < gh && 0 <= xt && xt < gw) {
+          const long long c = F.tgoff[t] + (long long)yt * gw + xt;
           const int* off = lst ? F.vp_off : F.pg_off;
-          const int* items = lst ? F.vp_items : F.pg_items;
           const int lim = lst ? F.nvp : F.npg;
-          int b = uni(off[c]), e = uni(off[c + 1]);
+          b = off[c];
+          e = off[c + 1];
           if (b < 0 || e > lim || b > e) {
-            if (lane == 0) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 12 + lst); }
-            b = 0; e = 0;
+            atomicAdd(&F.err[0], 1);
+            atomicExch(&F.err[1], 12 + lst);
+            b = 0;
+            e = 0;
           }
-          for (int base = b; base < e; base += 64) {
-            const int idx = base + lane;
-            bool hit = false;
-            int j = 0;
-            if (idx < e) {
-              j = items[idx];
-              if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 14); j = 0; }
-              else hit = is_neighbor_h(q, F.P[j], unit, thr, radius, true) != 0;
-            }
-            const unsigned long long mask = __ballot(hit);
-            const int before = __popcll(mask & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
-            const int pos = L.cnt + before;
-            if (hit) {
-              if (pos < NB_CAP) L.nb[pos] = j;
-              else L.overflow = 1;
-            }
-            __syncthreads();
-            if (lane == 0) L.cnt += __popcll(mask);
-            __syncthreads();
-            // duplicates (one entry per image/cell registration) are compacted when the buffer
-            // fills; the reference sorts and uniques once at the end (same set)
-            const int cnt = uni(L.cnt);
-            if (cnt > NB_CAP - 64 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(cnt, NB_CAP), &L.cnt);
-          }
-          if (F.pg_dhead) {  // entries committed by earlier expansion waves: up to 64 per round
-            int ent = uni((lst ? F.vp_dhead : F.pg_dhead)[c]);
-            while (ent >= 0) {
-              int j = -1;
-              for (int w = 0; w < 64 && ent >= 0; ++w) {
-                const int it = uni(F.d_item[ent]);
-                if (lane == w) j = it;
-                ent = uni(F.d_next[ent]);
-              }
-              bool hit = false;
-              if (j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 15); j = -1; }
-              if (j >= 0) hit = is_neighbor_h(q, F.P[j], unit, thr, radius, true) != 0;
-              const unsigned long long mask = __ballot(hit);
-              const int before = __popcll(mask & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
-              const int pos = L.cnt + before;
-              if (hit) {
-                if (pos < NB_CAP) L.nb[pos] = j;
-                else L.overflow = 1;
-              }
-              __syncthreads();
-              if (lane == 0) L.cnt += __popcll(mask);
-              __syncthreads();
-              const int cnt = uni(L.cnt);
-              if (cnt > NB_CAP - 64 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(cnt, NB_CAP), &L.cnt);
-            }
-          }
+          if (F.pg_dhead) head = (lst ? F.vp_dhead : F.pg_dhead)[c];
         }
       }
     }
+    // the round's CSR entries, flattened in slot order
+    const int cntc = e - b;
+    const int offc = wave_excl_scan_w(cntc);
+    const int tot = uni(__shfl(offc + cntc, 63));
+    L.sb[lane] = b;
+    L.so[lane] = offc;
+    L.sl[lane] = lst;
+    __syncthreads();
+    for (int ib = 0; ib < tot; ib += 64) {
+      const int idx = ib + lane;
+      bool hit = false;
+      int j = 0;
+      if (idx < tot) {
+        int sidx = 0;
+        for (int step = 32; step >= 1; step >>= 1)
+          if (sidx + step < 64 && L.so[sidx + step] <= idx) sidx += step;
+        const int* items = L.sl[sidx] ? F.vp_items : F.pg_items;
+        j = items[L.sb[sidx] + idx - L.so[sidx]];
+        if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 14); j = 0; }
+        else hit = is_neighbor_h(q, F.P[j], unit, thr, radius, true) != 0;
+      }
+      nb_append(L, hit, j);
+    }
+    // entries committed by earlier expansion waves (short chains, walked per lane)
+    if (F.pg_dhead && __ballot(head >= 0) != 0ull) {
+      if (uni(L.cnt) > NB_CAP / 2 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(uni(L.cnt), NB_CAP), &L.cnt);
+      for (int ent = head; ent >= 0; ent = F.d_next[ent]) {
+        const int j = F.d_item[ent];
+        if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 15); continue; }
+        if (is_neighbor_h(q, F.P[j], unit, thr, radius, true)) {
+          const int pos = atomicAdd(&L.cnt, 1);
+          if (pos < NB_CAP) L.nb[pos] = j;
+          else L.overflow = 1;
+        }
+      }
+      __syncthreads();
+      if (lane == 0 && L.cnt > NB_CAP) L.cnt = NB_CAP;
+      __syncthreads();
+      const int cnt = uni(L.cnt);
+      if (cnt > NB_CAP - 64 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(cnt, NB_CAP), &L.cnt);
+    }
+    __syncthreads();
   }
   const int n = imin(uni(L.cnt), NB_CAP);
   return sort_unique_lds(L.nb, n, &L.cnt);
@@ -664,13 +702,15 @@ __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, d
   ydir[0] = z[1] * xdir[2] - z[2] * xdir[1];
   ydir[1] = z[2] * xdir[0] - z[0] * xdir[2];
   ydir[2] = z[0] * xdir[1] - z[1] * xdir[0];
+  for (int a = lane; a < n; a += 64) {  // the distances in parallel, their sum in order below
+    float d[4];
+    for (int k = 0; k < 4; ++k) d[k] = F.P[L.nb[a]].coord[k] - q.coord[k];
+    L.fx[a] = norm4(d);
+  }
+  __syncthreads();
   if (lane == 0) {
     float h = 0.0f;
-    for (int a = 0; a < n; ++a) {
-      float d[4];
-      for (int k = 0; k < 4; ++k) d[k] = F.P[L.nb[a]].coord[k] - q.coord[k];
-      h += norm4(d);
-    }
+    for (int a = 0; a < n; ++a) h += L.fx[a];
     L.f[1] = (double)__fdiv_rn(h, (float)n);
   }
   __syncthreads();
@@ -791,38 +831,49 @@ __global__ __launch_bounds__(64) void empty_blocks_kernel(DScene s, FilterDev F,
     const pmvs_patch& q = F.P[parents[k]];
     const float radius = compute_radius_wave(s, L, q);
     const int n = gather_neighbors(s, F, L, q, 4.0f, 1, 0);
+    if (lane == 0 && L.overflow) atomicAdd(overflow, 1);
+    float xdir[4] = {0, 0, 0, 0}, ydir[4] = {0, 0, 0, 0};
+    const float* z = q.normal;
+    if (fabs((double)z[0]) > 0.5) { xdir[0] = z[1]; xdir[1] = -z[0]; xdir[2] = 0; }
+    else if (fabs((double)z[1]) > 0.5) { xdir[1] = z[2]; xdir[2] = -z[1]; xdir[0] = 0; }
+    else { xdir[2] = z[0]; xdir[0] = -z[2]; xdir[1] = 0; }
+    unitize4(xdir);
+    ydir[0] = z[1] * xdir[2] - z[2] * xdir[1];
+    ydir[1] = z[2] * xdir[0] - z[0] * xdir[2];
+    ydir[2] = z[0] * xdir[1] - z[1] * xdir[0];
+    const float radiuslow = __fdiv_rn(radius, 6.0f), radiushigh = radius * 2.5f;
+    // fill[i] of the reference is a sum of non-negative terms compared with 0 (expand.cpp:160-176):
+    // it is > 0 iff some term is > 0 and none is NaN, so the neighbours are scanned lane-parallel
+    // and only those two facts per bin are reduced.
+    unsigned pos = 0u, nan = 0u;
+    for (int a = lane; a < n; a += 64) {
+      float d[4];
+      for (int c = 0; c < 4; ++c) d[c] = F.P[L.nb[a]].coord[c] - q.coord[c];
+      float f0 = dot4(d, xdir), f1 = dot4(d, ydir);
+      const float len = (float)sqrt((double)(f0 * f0 + f1 * f1));
+      if (len < radiuslow || radiushigh < len) continue;
+      f0 = __fdiv_rn(f0, len);
+      f1 = __fdiv_rn(f1, len);
+      float angle = (float)atan2((double)f1, (double)f0);
+      if (angle < 0.0) angle = (float)((double)angle + 2 * M_PI);
+      const float findex = (float)((double)angle / (2 * M_PI / 6));
+      const int lindex = (int)floor((double)findex);
+      const int hindex = lindex + 1;
+      const float t0 = (float)hindex - findex, t1 = findex - (float)lindex;
+      const int b0 = ((lindex % 6) + 6) % 6, b1 = ((hindex % 6) + 6) % 6;
+      if (t0 > 0.0f) pos |= 1u << b0;
+      if (t0 != t0) nan |= 1u << b0;
+      if (t1 > 0.0f) pos |= 1u << b1;
+      if (t1 != t1) nan |= 1u << b1;
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+      pos |= __shfl_xor(pos, d);
+      nan |= __shfl_xor(nan, d);
+    }
     if (lane == 0) {
-      if (L.overflow) atomicAdd(overflow, 1);
-      float xdir[4] = {0, 0, 0, 0}, ydir[4] = {0, 0, 0, 0};
-      const float* z = q.normal;
-      if (fabs((double)z[0]) > 0.5) { xdir[0] = z[1]; xdir[1] = -z[0]; xdir[2] = 0; }
-      else if (fabs((double)z[1]) > 0.5) { xdir[1] = z[2]; xdir[2] = -z[1]; xdir[0] = 0; }
-      else { xdir[2] = z[0]; xdir[0] = -z[2]; xdir[1] = 0; }
-      unitize4(xdir);
-      ydir[0] = z[1] * xdir[2] - z[2] * xdir[1];
-      ydir[1] = z[2] * xdir[0] - z[0] * xdir[2];
-      ydir[2] = z[0] * xdir[1] - z[1] * xdir[0];
-      float fill[6] = {0, 0, 0, 0, 0, 0};
-      const float radiuslow = __fdiv_rn(radius, 6.0f), radiushigh = radius * 2.5f;
-      for (int a = 0; a < n; ++a) {
-        float d[4];
-        for (int c = 0; c < 4; ++c) d[c] = F.P[L.nb[a]].coord[c] - q.coord[c];
-        float f0 = dot4(d, xdir), f1 = dot4(d, ydir);
-        const float len = (float)sqrt((double)(f0 * f0 + f1 * f1));
-        if (len < radiuslow || radiushigh < len) continue;
-        f0 = __fdiv_rn(f0, len);
-        f1 = __fdiv_rn(f1, len);
-        float angle = (float)atan2((double)f1, (double)f0);
-        if (angle < 0.0) angle = (float)((double)angle + 2 * M_PI);
-        const float findex = (float)((double)angle / (2 * M_PI / 6));
-        const int lindex = (int)floor((double)findex);
-        const int hindex = lindex + 1;
-        fill[lindex % 6] += (float)hindex - findex;
-        fill[hindex % 6] += findex - (float)lindex;
-      }
       for (int i = 0; i < 6; ++i) {
         int ok = 1;
-        if (0.0f < fill[i]) ok = 0;
+        if ((pos >> i & 1u) && !(nan >> i & 1u)) ok = 0;  // 0.0f < fill[i]
         if (q.dflag & (0x0001 << i)) ok = 0;
         cand_ok[6 * k + i] = ok;
         if (ok) {
@@ -1045,19 +1096,11 @@ struct DeltaLists {  // the per-cell chains of FilterDev (expansion), writable
   int* vp_head;
   int* item;
   int* next;
-  int* used;  // entries taken from the pool
-  int cap;
 };
-__device__ __forceinline__ void chain_push(const DeltaLists& D, int* head, long long cell, int p) {
-  const int e = atomicAdd(D.used, 1);
-  if (e >= D.cap) return;  // the host sizes the pool from the committed patches; never taken
-  D.item[e] = p;
-  D.next[e] = atomicExch(&head[cell], e);
-}
 
 __global__ void add_patches_kernel(DScene s, FilterDev F, int first, int count, int rank0, unsigned long long* __restrict__ preg,
                                    unsigned long long* __restrict__ vreg, int* __restrict__ order,
-                                   unsigned long long* __restrict__ dpkey, float* __restrict__ unit0, DeltaLists D) {
+                                   unsigned long long* __restrict__ dpkey, float* __restrict__ unit0) {
   const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= (long long)count * s.tnum) return;
   const int k = (int)(g / s.tnum), t = (int)(g - (long long)k * s.tnum);
@@ -1066,15 +1109,9 @@ __global__ void add_patches_kernel(DScene s, FilterDev F, int first, int count, 
   if (t == 0) {
     unsigned long long m = 0ull;
     for (int i = 0; i < q.num_images; ++i)
-      if (q.images[i] < s.tnum && in_grid(s, q.images[i], q.grids[i][0], q.grids[i][1])) {
-        m |= 1ull << i;
-        chain_push(D, D.pg_head, F.tgoff[q.images[i]] + (long long)q.grids[i][1] * gwidth(s, q.images[i]) + q.grids[i][0], p);
-      }
+      if (q.images[i] < s.tnum && in_grid(s, q.images[i], q.grids[i][0], q.grids[i][1])) m |= 1ull << i;
     preg[p] = m;
     vreg[p] = (q.num_vimages >= 64) ? ~0ull : ((1ull << q.num_vimages) - 1ull);
-    for (int i = 0; i < q.num_vimages; ++i)
-      if (in_grid(s, q.vimages[i], q.vgrids[i][0], q.vgrids[i][1]))
-        chain_push(D, D.vp_head, F.tgoff[q.vimages[i]] + (long long)q.vgrids[i][1] * gwidth(s, q.vimages[i]) + q.vgrids[i][0], p);
     order[rank0 + k] = p;
     unit0[p] = get_unit(s, s.views[q.images[0]], q.coord);
   }
@@ -1092,6 +1129,24 @@ __global__ void add_patches_kernel(DScene s, FilterDev F, int first, int count, 
       if (xs[i] < 0 || gw <= xs[i] || ys[j] < 0 || gh <= ys[j]) continue;
       atomicMin(&dpkey[F.tgoff[t] + (long long)ys[j] * gw + xs[i]], key);
     }
+}
+
+// addPatch's cell registrations of the committed patches into the per-cell chains (pgrids: the
+// in-grid target images; vpgrids: the vimages), one wavefront per patch, straight from its commit
+// record; entry slots eoff[k].. are assigned by the host (no shared allocation counter).
+__global__ __launch_bounds__(64) void register_kernel(DeltaLists D, const int* __restrict__ acc, const int* __restrict__ eoff,
+                                                      int nacc, int first, const int* __restrict__ rec, int rec_ints) {
+  const int k = blockIdx.x;
+  if (k >= nacc) return;
+  const int* r = rec + (size_t)acc[k] * rec_ints;
+  const int ni = r[3], nv = r[4];
+  for (int i = threadIdx.x; i < ni + nv; i += 64) {
+    const int e = eoff[k] + i;
+    const bool vis = i >= ni;
+    const int cell = vis ? r[5 + 2 * PMVS_MAX_IMAGES + (i - ni)] : r[5 + PMVS_MAX_IMAGES + i];
+    D.item[e] = first + k;
+    D.next[e] = atomicExch(&(vis ? D.vp_head : D.pg_head)[cell], e);
+  }
 }
 
 __global__ void flag_rank_kernel(pmvs_patch* __restrict__ P, const int* __restrict__ order, int na) {
@@ -1518,8 +1573,29 @@ __global__ void alive_reg_kernel(int n, const int* __restrict__ alive, unsigned 
   }
 }
 
+// Host mirror of one target cell during an expansion run.
+struct HostCell {
+  unsigned char count, occ;
+};
+static_assert(sizeof(HostCell) == 2, "HostCell layout");
+struct HostCells {  // 2 MB-aligned, transparent huge pages: the commit's accesses are random
+  HostCell* p = nullptr;
+  explicit HostCells(size_t n) {
+    const size_t bytes = ((n * sizeof(HostCell)) + (2u << 20) - 1) & ~((size_t)(2u << 20) - 1);
+    p = static_cast<HostCell*>(aligned_alloc(2u << 20, bytes ? bytes : (2u << 20)));
+    if (p) (void)madvise(p, bytes, MADV_HUGEPAGE);
+  }
+  ~HostCells() { free(p); }
+};
+
+// {count 0, occupied = pgrids holds a patch} per cell, for the host mirror.
+__global__ void cell_init_kernel(const int* __restrict__ pg_off, long long ncells, HostCell* __restrict__ out) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < ncells) out[c] = HostCell{0, (unsigned char)(pg_off[c + 1] > pg_off[c] ? 1 : 0)};
+}
+
 // CExpand::updateCounts results of one commit (host-computed): counts[cell] = value.
-__global__ void counts_scatter_kernel(const long long* __restrict__ cells, const unsigned char* __restrict__ vals, int n,
+__global__ void counts_scatter_kernel(const int* __restrict__ cells, const unsigned char* __restrict__ vals, int n,
                                       unsigned char* __restrict__ counts) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < n) counts[cells[k]] = vals[k];
@@ -1538,7 +1614,7 @@ static hipError_t grow(T*& p, size_t& cap, size_t need) {
 
 ExpandBuffers::~ExpandBuffers() {
   void* ps[] = {parents, cand_coord, cand_ok, cand, prep, status, slots, cand2, prep2, res, outp, ostatus, counts, alive,
-                pg_head, vp_head, d_item, d_next, pool_used, tcells, tvals, qtmp, crec, acc, dupd};
+                pg_head, vp_head, d_item, d_next, pool_used, tcells, tvals, qtmp, crec, acc, dupd, cellinit};
   for (void* p : ps)
     if (p) (void)hipFree(p);
 }
@@ -1621,8 +1697,6 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
   FCHK(grow(X.vp_head, X.cap_vphead, (size_t)ncells));
   FCHK(hipMemsetAsync(X.pg_head, 0xff, ncells * sizeof(int), st));
   FCHK(hipMemsetAsync(X.vp_head, 0xff, ncells * sizeof(int), st));
-  FCHK(grow(X.pool_used, X.cap_pused, 1));
-  FCHK(hipMemsetAsync(X.pool_used, 0, sizeof(int), st));
   size_t pool_need = 0;
   X.pool_host = 0;
   auto set_delta = [&]() {
@@ -1630,19 +1704,25 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
   };
   set_delta();
   // ---- host mirrors: pgrids occupancy per cell, counts (clearCounts), the queue
-  std::vector<int> occ(ncells + 1), order(c.nalive);
+  // per cell {count, occupied}: CExpand's _counts (unsigned char, clearCounts) and whether pgrids
+  // holds a patch, side by side so a commit touches one cache line per cell (huge pages)
+  HostCells cs((size_t)ncells);
+  if (!cs.p) return hipErrorOutOfMemory;
+  std::vector<int> order(c.nalive);
   std::vector<float> qtmp(c.nalive);
   FCHK(grow(X.qtmp, X.cap_qtmp, (size_t)std::max(1, c.nalive)));
+  FCHK(grow(X.cellinit, X.cap_cellinit, (size_t)ncells));
   if (c.nalive)
     hipLaunchKernelGGL(collect_flags_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, dP, B.order, c.nalive, X.qtmp);
-  FCHK(hipMemcpyAsync(occ.data(), B.pg_off, (ncells + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
+  hipLaunchKernelGGL(cell_init_kernel, dim3(nblk(ncells)), dim3(256), 0, st, B.pg_off, ncells,
+                     reinterpret_cast<HostCell*>(X.cellinit));
+  FCHK(hipMemcpyAsync(cs.p, X.cellinit, (size_t)ncells * sizeof(HostCell), hipMemcpyDeviceToHost, st));
   if (c.nalive) {
     FCHK(hipMemcpyAsync(order.data(), B.order, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
     FCHK(hipMemcpyAsync(qtmp.data(), X.qtmp, c.nalive * sizeof(float), hipMemcpyDeviceToHost, st));
   }
   FCHK(hipStreamSynchronize(st));
-  for (long long k = 0; k < ncells; ++k) occ[k] = occ[k + 1] - occ[k];
-  std::vector<unsigned char> counts(ncells, 0);
+  HostCell* const cell = cs.p;
   FCHK(grow(X.counts, X.cap_cnt, (size_t)ncells));
   FCHK(hipMemsetAsync(X.counts, 0, ncells, st));
   // The max-_tmp queue (P_compare; ties: earlier push first): the collected patches as a sorted
@@ -1664,10 +1744,11 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
   int rank_next = c.nalive;
   int nmodel = n0;
   const int G = std::max(1, sh.world), R = std::min(std::max(0, sh.rank), G - 1);
-  std::vector<long long> touched;
+  std::vector<int> touched;
   std::vector<unsigned char> tvals;
+  std::vector<int> seqk;  // the wave's slots with a refined record, in commit order (prefetch)
   std::vector<char> xsend, xrecv;
-  std::vector<int> rec, acc;
+  std::vector<int> rec, acc, eoff;
   std::vector<int2> dupd;
   T.mark(0);
   std::vector<int> okh;
@@ -1808,6 +1889,18 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
       touched.clear();
       acc.clear();
       dupd.clear();
+      seqk.clear();
+      for (int k = 0; k < np * 6; ++k)
+        if (status[k] == 0) seqk.push_back(slot2surv[k]);
+      size_t nextpf = 0;
+      auto prefetch = [&](size_t upto) {  // the cells of the records a few commits ahead
+        for (; nextpf < std::min(upto, seqk.size()); ++nextpf) {
+          const int* r = &rec[(size_t)seqk[nextpf] * kRecInts];
+          for (int i = 0; i < r[2]; ++i) __builtin_prefetch(&cell[r[5 + i]], 1);
+          for (int i = 0; i < r[4]; ++i) __builtin_prefetch(&cell[r[5 + 2 * PMVS_MAX_IMAGES + i]], 1);
+        }
+      };
+      size_t done = 0;
       for (int pi = 0; pi < np; ++pi) {
         int bits = 0;
         for (int dir = 0; dir < 6; ++dir) {
@@ -1815,6 +1908,7 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
           if (status[k] < 0) continue;
           int stc = status[k];  // 1 = prepare failed
           const int j = slot2surv[k];
+          if (stc == 0) prefetch(++done + 6);
           const int* r = (stc == 0) ? &rec[(size_t)j * kRecInts] : nullptr;
           if (stc == 0) stc = r[0];
           if (stc == 9) {
@@ -1825,8 +1919,8 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
             int full = 0, empty = 0;
             for (int i = 0; i < r[2]; ++i) {
               const int cidx = r[5 + i];
-              if (occ[cidx] > 0) { ++full; continue; }
-              if (cthr <= counts[cidx]) ++full;
+              if (cell[cidx].occ) { ++full; continue; }
+              if (cthr <= cell[cidx].count) ++full;
               else ++empty;
             }
             const bool fail = (s.depth <= 1) ? (empty < s.minImageNum && full != 0) : (empty < s.minImageNum - 1 && full != 0);
@@ -1840,7 +1934,7 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
           // CExpand::updateCounts (expand.cpp:325-406) + addPatch (pgrids registration)
           int full = 0, empty = 0;
           auto touch = [&](int cidx) {
-            unsigned char& cc = counts[cidx];
+            unsigned char& cc = cell[cidx].count;
             if (cthr <= cc) ++full;
             else ++empty;
             ++cc;
@@ -1848,7 +1942,7 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
           };
           for (int i = 0; i < r[3]; ++i) touch(r[5 + PMVS_MAX_IMAGES + i]);
           for (int i = 0; i < r[4]; ++i) touch(r[5 + 2 * PMVS_MAX_IMAGES + i]);
-          for (int i = 0; i < r[3]; ++i) occ[r[5 + PMVS_MAX_IMAGES + i]]++;
+          for (int i = 0; i < r[3]; ++i) cell[r[5 + PMVS_MAX_IMAGES + i]].occ = 1;
           pool_need += (size_t)r[3] + (size_t)r[4];
           if (nmodel + (int)acc.size() >= cap) return hipErrorOutOfMemory;
           const int newp = nmodel + (int)acc.size();
@@ -1864,10 +1958,10 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
       if (!touched.empty()) {
         const int nt = (int)touched.size();
         tvals.resize(nt);
-        for (int k = 0; k < nt; ++k) tvals[k] = counts[touched[k]];
+        for (int k = 0; k < nt; ++k) tvals[k] = cell[touched[k]].count;
         FCHK(grow(X.tcells, X.cap_tcells, (size_t)nt));
         FCHK(grow(X.tvals, X.cap_tvals, (size_t)nt));
-        FCHK(hipMemcpyAsync(X.tcells, touched.data(), nt * sizeof(long long), hipMemcpyHostToDevice, st));
+        FCHK(hipMemcpyAsync(X.tcells, touched.data(), nt * sizeof(int), hipMemcpyHostToDevice, st));
         FCHK(hipMemcpyAsync(X.tvals, tvals.data(), nt, hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(counts_scatter_kernel, dim3(nblk(nt)), dim3(256), 0, st, X.tcells, X.tvals, nt, X.counts);
       }
@@ -1894,14 +1988,25 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
           pcap = ncap;
           c.P = dP;
         }
-        FCHK(grow(X.acc, X.cap_acc, (size_t)added));
-        FCHK(hipMemcpyAsync(X.acc, acc.data(), added * sizeof(int), hipMemcpyHostToDevice, st));
+        // [acc | entry offsets] in one upload
+        eoff.resize(2 * (size_t)added);
+        size_t e0 = X.pool_host;
+        for (int q = 0; q < added; ++q) {
+          const int* r = &rec[(size_t)acc[q] * kRecInts];
+          eoff[q] = acc[q];
+          eoff[added + q] = (int)e0;
+          e0 += (size_t)r[3] + (size_t)r[4];
+        }
+        FCHK(grow(X.acc, X.cap_acc, 2 * (size_t)added));
+        FCHK(hipMemcpyAsync(X.acc, eoff.data(), 2 * (size_t)added * sizeof(int), hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(append_kernel, dim3(added), dim3(64), 0, st, dP, first, X.acc, added, X.outp);
         nmodel += added;
         c.n = nmodel;
-        DeltaLists D{X.pg_head, X.vp_head, X.d_item, X.d_next, X.pool_used, (int)std::min<size_t>(X.cap_item, INT32_MAX)};
+        DeltaLists D{X.pg_head, X.vp_head, X.d_item, X.d_next};
+        hipLaunchKernelGGL(register_kernel, dim3(added), dim3(64), 0, st, D, X.acc, X.acc + added, added, first, X.crec,
+                           kRecInts);
         hipLaunchKernelGGL(add_patches_kernel, dim3(nblk((long long)added * s.tnum)), dim3(256), 0, st, s, c.dev(), first,
-                           added, rank_next, B.preg, B.vreg, B.order, B.dpkey, B.unit0, D);
+                           added, rank_next, B.preg, B.vreg, B.order, B.dpkey, B.unit0);
         X.pool_host = pool_need;
         rank_next += added;
       }

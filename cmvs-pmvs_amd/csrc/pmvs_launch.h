@@ -53,7 +53,8 @@ struct ExpandBuffers {
   unsigned char* counts = nullptr;
   // registrations committed during the run: per-cell chain heads + entry pool (FilterDev delta)
   int *pg_head = nullptr, *vp_head = nullptr, *d_item = nullptr, *d_next = nullptr, *pool_used = nullptr;
-  long long* tcells = nullptr;  // cells whose counts a commit changed, and their values
+  int* tcells = nullptr;        // cells whose counts a commit changed, and their values
+  unsigned short* cellinit = nullptr;  // per-cell {count, occupied} staged for the host mirror
   float* qtmp = nullptr;        // _tmp of the collected patches (queue)
   int *crec = nullptr, *acc = nullptr;  // commit records; committed record indexes
   int2* dupd = nullptr;         // (parent, failed-direction bits) of a wave
@@ -62,7 +63,7 @@ struct ExpandBuffers {
   size_t cap_coord = 0, cap_ok = 0, cap_cand = 0, cap_prep = 0, cap_slots = 0, cap_prep2 = 0, cap_res = 0, cap_outp = 0,
          cap_ost = 0, cap_par = 0, cap_status = 0, cap_cand2 = 0, cap_alive = 0, cap_cnt = 0, cap_pghead = 0,
          cap_vphead = 0, cap_item = 0, cap_next = 0, cap_pused = 0, cap_tcells = 0, cap_tvals = 0,
-         cap_qtmp = 0, cap_crec = 0, cap_acc = 0, cap_dupd = 0;
+         cap_qtmp = 0, cap_crec = 0, cap_acc = 0, cap_dupd = 0, cap_cellinit = 0;
   std::vector<int> gw, gh;  // grid sizes of the target images
   ~ExpandBuffers();
 };
