@@ -132,3 +132,46 @@ def test_empty_and_invalid_batches(gpu_available):
     with pytest.raises(P.PmvsError):
         g.refine_batch(bad)
     g.close()
+
+
+@pytest.mark.parametrize("name", sorted(CONFIGS))
+def test_full_loop_matrix(gpu_available, oracle_mod, name):
+    """The whole expand/filter loop (pmvs_run_loop, CFindMatch::run after the seeds) under every
+    option configuration above -- masks, edges, bimages, visdata, timages subsets, sequence,
+    maxAngle, csize 1/4, wsize 5/9, levels 0-2, minImageNum 2/4 -- equals the oracle's loop
+    patch for patch (wave 128, min_candidates 256)."""
+    import pmvs_amd as P
+    inp, p = build(CONFIGS[name])
+    g = P.Scene(inp)
+    o = oracle_mod.OracleScene(inp)
+    cands = P.synth_candidates(p, inp.projections, 150, seed=21)
+    r, _ = g.refine_batch(cands)
+    seeds = P.patches_from_refined(r)
+    out_g, log_g = g.run_loop(seeds, inp.threshold, wave=128, min_candidates=256)
+    out_o, log_o = o.run_loop(seeds, inp.threshold, wave=128, min_candidates=256)
+    g.close()
+    o.close()
+    assert len(seeds) > 0 and len(out_o) > len(seeds)
+    for a, b in zip(log_g, log_o):
+        assert a["patches"] == b["patches"], (a, b)
+        assert {k: v for k, v in a["expand"].items() if k not in P.ExpandStats.WORK} == b["expand"]
+        assert [a["filter"][k] for k in ("removed_outside", "removed_exact", "removed_neighbor",
+                                         "removed_groups")] == b["filter"]
+    assert out_g.tobytes() == out_o.tobytes() or _same_patches(out_g, out_o)
+
+
+def _same_patches(a, b):
+    """Every defined field equal (image / vimage arrays compared up to their counts)."""
+    if len(a) != len(b):
+        return False
+    for f in ("coord", "normal", "ncc", "dscale", "ascale", "tmp", "timages", "flag", "fix", "num_images",
+              "num_vimages", "dflag"):
+        if bits(a[f]).tobytes() != bits(b[f]).tobytes() if a[f].dtype.kind == "f" else not np.array_equal(a[f], b[f]):
+            return False
+    for i in range(len(a)):
+        n, m = b["num_images"][i], b["num_vimages"][i]
+        if not (np.array_equal(a["images"][i][:n], b["images"][i][:n]) and np.array_equal(a["grids"][i][:n], b["grids"][i][:n])
+                and np.array_equal(a["vimages"][i][:m], b["vimages"][i][:m])
+                and np.array_equal(a["vgrids"][i][:m], b["vgrids"][i][:m])):
+            return False
+    return True
