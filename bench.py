@@ -41,7 +41,7 @@ sys.path.insert(0, os.path.join(ROOT, "cmvs-pmvs_amd"))
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 BYTES_PER_TEXTURE = 49 * 4 * 3  # wsize^2 samples x 4 texels x 3 B
-REFINE_KERNEL = "refine_v2_kernel<7,16,8>"
+REFINE_KERNEL = "refine_v2_kernel<7,24,8>"
 
 
 def parse():
@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--level", type=int, default=0)
     ap.add_argument("--seeds", type=int, default=5000)
     ap.add_argument("--wave", type=int, default=32768)
-    ap.add_argument("--min-candidates", type=int, default=65536)
+    ap.add_argument("--min-candidates", type=int, default=131072)
     ap.add_argument("--iterations", type=int, default=3)
     ap.add_argument("--c2-candidates", type=int, default=100000)
     ap.add_argument("--no-c2", action="store_true", help="skip the configs[1] refine-kernel side measurement")

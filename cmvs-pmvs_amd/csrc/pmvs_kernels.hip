@@ -1410,6 +1410,7 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
     case 1604: hipLaunchKernelGGL((refine_v2_kernel<WS, 16, 4>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     case 1608: hipLaunchKernelGGL((refine_v2_kernel<WS, 16, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     case 1616: hipLaunchKernelGGL((refine_v2_kernel<WS, 16, 16>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 2408: hipLaunchKernelGGL((refine_v2_kernel<WS, 24, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     case 3208: hipLaunchKernelGGL((refine_v2_kernel<WS, 32, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     case 4808: hipLaunchKernelGGL((refine_v2_kernel<WS, 48, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     default: hipLaunchKernelGGL((refine_v2_kernel<WS, 32, 16>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
