@@ -852,12 +852,22 @@ __device__ __forceinline__ int wave_excl_scan(int v) {
   return incl - v;
 }
 
+// Phase timers of the refine kernel (pmvs_stats.prof / cyc_opt / cyc_eval): diagnostic builds
+// only (-DBQ_PROFILE, libpmvs_amd_prof.so); the product build keeps the counters' registers free.
+#if defined(BQ_PROFILE)
+#define PROF_NOW() __builtin_amdgcn_s_memtime()
 #define PROF_MARK(slot)                                   \
   do {                                                    \
     const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
     prof[slot] += _t - tprev;                             \
     tprev = _t;                                           \
   } while (0)
+#else
+#define PROF_NOW() 0ull
+#define PROF_MARK(slot) \
+  do {                  \
+  } while (0)
+#endif
 
 template <int WS, int TSLOTS, int NC>
 __device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS, NC>& C, int njobs, unsigned long long* prof,
@@ -1040,7 +1050,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 4 ? 2 
   const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999};
   const double ub[3] = {HUGE_VAL, 23.99999, 23.99999};
   for (;;) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long t0 = PROF_NOW();
     tprev = t0;
     // (a) refill idle lanes from the queue (skipping candidates that failed preProcess)
     while (cand < 0 && !exhausted) {
@@ -1107,7 +1117,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 4 ? 2 
       }
     }
     const unsigned long long reqmask = __ballot(req);
-    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long t1 = PROF_NOW();
     prof[2] += t1 - tprev;
     tprev = t1;
     cyc_opt += t1 - t0;
@@ -1179,7 +1189,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 4 ? 2 
       }
       __syncthreads();
     }
-    cyc_eval += __builtin_amdgcn_s_memtime() - t1;
+    cyc_eval += PROF_NOW() - t1;
     // (e) consume results
     if (req) {
       if (need == 1) {
