@@ -877,8 +877,9 @@ __global__ __launch_bounds__(64) void empty_blocks_kernel(DScene s, FilterDev F,
         if (q.dflag & (0x0001 << i)) ok = 0;
         cand_ok[6 * k + i] = ok;
         if (ok) {
-          const double angle = 2 * M_PI * i / 6;
-          const double cr = cos(angle) * (double)radius, sr = sin(angle) * (double)radius;
+          // expand.cpp:176-177: the angle is stored as float, then cos/sin run in double.
+          const float angle = (float)(2 * M_PI * i / 6);
+          const double cr = cos((double)angle) * (double)radius, sr = sin((double)angle) * (double)radius;
           for (int c = 0; c < 4; ++c)
             cand_coord[4 * (6 * k + i) + c] = (q.coord[c] + (float)((double)xdir[c] * cr)) + (float)((double)ydir[c] * sr);
         }

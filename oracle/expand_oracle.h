@@ -82,6 +82,19 @@ static void model_add(Model& m, std::vector<FPatch>& P, int p) {
   update_depth_maps(m, P, p);
 }
 
+// The candidate centre of direction i (expand.cpp:176-177): `const float angle = 2*M_PI*i/dnum;`
+// then coord + cos(angle)*radius*xdir + sin(angle)*radius*ydir, where the float angle goes to the
+// double cos/sin (unqualified cos(float) resolves to ::cos(double) in that TU; probed), the
+// double scalar times a Vec4f rounds each component to float (vec4.hpp:177-184), and the two
+// Vec4f sums run left to right.
+static V4 candidate_coord(const V4& coord, const V4& xdir, const V4& ydir, float radius, int i, int dnum) {
+  const float angle = (float)(2 * M_PI * i / dnum);
+  const double cr = std::cos((double)angle) * (double)radius, sr = std::sin((double)angle) * (double)radius;
+  V4 c;
+  for (int k = 0; k < 4; ++k) c[k] = (coord[k] + (float)((double)xdir[k] * cr)) + (float)((double)ydir[k] * sr);
+  return c;
+}
+
 // CExpand::findEmptyBlocks (expand.cpp:95-180): free directions of a patch.
 static void find_empty_blocks(const Model& m, const std::vector<FPatch>& P, const FPatch& q, int dflag,
                               std::vector<std::pair<int, V4>>& out) {
@@ -112,11 +125,7 @@ static void find_empty_blocks(const Model& m, const std::vector<FPatch>& P, cons
   for (int i = 0; i < dnum; ++i) {
     if (0.0f < fill[i]) continue;
     if (dflag & (0x0001 << i)) continue;
-    const double angle = 2 * M_PI * i / dnum;
-    const double cr = std::cos(angle) * (double)radius, sr = std::sin(angle) * (double)radius;
-    V4 c;
-    for (int k = 0; k < 4; ++k) c[k] = (q.coord[k] + (float)((double)xdir[k] * cr)) + (float)((double)ydir[k] * sr);
-    out.push_back({i, c});
+    out.push_back({i, candidate_coord(q.coord, xdir, ydir, radius, i, dnum)});
   }
 }
 

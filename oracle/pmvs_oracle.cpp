@@ -984,6 +984,39 @@ void oracle_grab_tex(void* p, const pmvs_tex_query* q, int n, float* out, int* v
   }
 }
 
+// get_color at n (x, y) points of one view/level (pinned against the reference's inline
+// CImage::getColor through oracle/_ref ref_get_color): out 3 floats per point.
+void oracle_get_color(void* p, int view, int level, const float* xy, int n, float* out3) {
+  const OScene* s = static_cast<const OScene*>(p);
+  for (int i = 0; i < n; ++i) {
+    const V3 c = get_color(*s, view, xy[2 * i], xy[2 * i + 1], level);
+    out3[3 * i] = c[0]; out3[3 * i + 1] = c[1]; out3[3 * i + 2] = c[2];
+  }
+}
+
+// The organizer's depth (optical axis . coord) per point, as the filter oracle's depth_of.
+void oracle_depth(void* p, int view, const float* coords4, int n, float* out) {
+  const OScene* s = static_cast<const OScene*>(p);
+  for (int i = 0; i < n; ++i) {
+    V4 c = {{coords4[4 * i], coords4[4 * i + 1], coords4[4 * i + 2], coords4[4 * i + 3]}};
+    out[i] = dot4(s->views[view].oaxis, c);
+  }
+}
+
+// findEmptyBlocks' candidate centres for all 6 directions of (coord, normal, radius):
+// ortho() then candidate_coord(); out 24 floats per query.
+void oracle_expand_dirs(const float* coord4, const float* normal4, const float* radius, int n, float* out) {
+  for (int q = 0; q < n; ++q) {
+    V4 c, nn, xd, yd;
+    for (int k = 0; k < 4; ++k) { c[k] = coord4[4 * q + k]; nn[k] = normal4[4 * q + k]; }
+    ortho4(nn, xd, yd);
+    for (int i = 0; i < 6; ++i) {
+      const V4 r = candidate_coord(c, xd, yd, radius[q], i, 6);
+      for (int k = 0; k < 4; ++k) out[24 * q + 4 * i + k] = r[k];
+    }
+  }
+}
+
 // getPAxes for test queries: out 8 floats (pxaxis, pyaxis).
 void oracle_paxes(void* p, int view, const float* coord, const float* normal, float* out) {
   const OScene* s = static_cast<const OScene*>(p);

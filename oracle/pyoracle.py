@@ -41,6 +41,9 @@ def lib():
         L.oracle_camera.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
         L.oracle_project.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p]
         L.oracle_grab_tex.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        L.oracle_get_color.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p]
+        L.oracle_expand_dirs.argtypes = [C.c_void_p] * 3 + [C.c_int, C.c_void_p]
+        L.oracle_depth.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p]
         L.oracle_paxes.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.oracle_incc_eval.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         L.oracle_refine_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.POINTER(P.Stats)]
@@ -67,6 +70,9 @@ def ref_lib():
                                         C.c_void_p, C.c_int]
         R.ref_write_pset.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int]
         R.ref_ortho.argtypes = [C.c_void_p, C.c_void_p]
+        R.ref_get_color.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        R.ref_expand_dirs.argtypes = [C.c_void_p] * 3 + [C.c_int, C.c_void_p]
+        R.ref_camera_depth.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p]
         _ref = R
     return _ref
 
@@ -112,6 +118,18 @@ class OracleScene:
         coords = np.ascontiguousarray(coords, np.float32)
         out = np.zeros((len(coords), 3), np.float32)
         lib().oracle_project(self.h, view, level, _p(coords), len(coords), _p(out))
+        return out
+
+    def get_color(self, view, level, xy):
+        xy = np.ascontiguousarray(xy, np.float32)
+        out = np.zeros((len(xy), 3), np.float32)
+        lib().oracle_get_color(self.h, view, level, _p(xy), len(xy), _p(out))
+        return out
+
+    def depth(self, view, coords):
+        coords = np.ascontiguousarray(coords, np.float32)
+        out = np.zeros(len(coords), np.float32)
+        lib().oracle_depth(self.h, view, _p(coords), len(coords), _p(out))
         return out
 
     def paxes(self, view, coord, normal):

@@ -11,6 +11,9 @@
 // pins the oracle restatement and the product's host plumbing bit-for-bit on those pieces.
 // It is built only in the build container (where /root/reference exists) and is never
 // linked into the product.
+#define _USE_MATH_DEFINES
+#include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <fstream>
 #include <iomanip>
@@ -18,7 +21,11 @@
 #include <sstream>
 #include <string>
 
+#include <new>
+#include <vector>
+
 #include "image/camera.hpp"
+#include "image/image.hpp"
 #include "pmvs/option.hpp"
 #include "pmvs/patch.hpp"
 
@@ -34,9 +41,71 @@ struct CamProbe : public Image::CCamera {
     }
   }
 };
+// CImage's constructor and destructor live in image.cpp, which needs CImg.h (absent here), so
+// a CImage object cannot be constructed in this recipe.  CImage::getColor
+// (image.hpp:435-476, bilinear branch) and CImage::isSafe (image.hpp:165-178) are header-inline,
+// non-virtual, and read only _images / _widths / _heights.  ImgProbe names those protected
+// members; ref_get_color placement-constructs exactly those three vectors inside raw storage
+// of CImage's size and calls the reference's own inline functions on it (no stand-in header,
+// no restated code: the arithmetic executed is the unmodified header's).
+struct ImgProbe : public Image::CImage {
+  static auto images() { return &ImgProbe::_images; }
+  static auto widths() { return &ImgProbe::_widths; }
+  static auto heights() { return &ImgProbe::_heights; }
+};
+
+struct RawImage {
+  alignas(Image::CImage) unsigned char raw[sizeof(Image::CImage)];
+  Image::CImage* im() { return reinterpret_cast<Image::CImage*>(raw); }
+  RawImage(const unsigned char* rgb, int w, int h) {
+    using VU = std::vector<std::vector<unsigned char>>;
+    using VI = std::vector<int>;
+    new (&(im()->*ImgProbe::images())) VU(1, std::vector<unsigned char>(rgb, rgb + (size_t)3 * w * h));
+    new (&(im()->*ImgProbe::widths())) VI(1, w);
+    new (&(im()->*ImgProbe::heights())) VI(1, h);
+  }
+  ~RawImage() {
+    using VU = std::vector<std::vector<unsigned char>>;
+    using VI = std::vector<int>;
+    (im()->*ImgProbe::images()).~VU();
+    (im()->*ImgProbe::widths()).~VI();
+    (im()->*ImgProbe::heights()).~VI();
+  }
+};
 }  // namespace
 
 extern "C" {
+
+// CImage::getColor(fx, fy, level 0) of an RGB8 image (w x h, row-major, 3 B/pixel) at n
+// points xy[2*i]; out 3 floats per point.  safe[i] = CImage::isSafe(Vec3f(x, y, 1), 0).
+// getColor is only evaluated where isSafe holds (the reference never samples elsewhere:
+// grabSafe, optim.cpp:783-805, guards every grabTex).
+int ref_get_color(const unsigned char* rgb, int w, int h, const float* xy, int n, float* out3, int* safe) {
+  RawImage R(rgb, w, h);
+  const Image::CImage& im = *R.im();
+  for (int i = 0; i < n; ++i) {
+    const Vec3f ic(xy[2 * i], xy[2 * i + 1], 1.0f);
+    safe[i] = im.isSafe(ic, 0);
+    Vec3f c(0.0f, 0.0f, 0.0f);
+    if (safe[i]) c = im.getColor(xy[2 * i], xy[2 * i + 1], 0);
+    out3[3 * i] = c[0];
+    out3[3 * i + 1] = c[1];
+    out3[3 * i + 2] = c[2];
+  }
+  return 0;
+}
+
+// CCamera::computeDepth (camera.cpp:445-452), the depth the organizer's depth maps and
+// isVisible compare (CPhotoSetS::computeDepth): out 1 float per point.
+int ref_camera_depth(const char* txt, int max_level, const float* coords4, int n, float* out) {
+  Image::CCamera cam;
+  cam.init(txt, max_level);
+  for (int i = 0; i < n; ++i) {
+    const Vec4f c(coords4[4 * i], coords4[4 * i + 1], coords4[4 * i + 2], coords4[4 * i + 3]);
+    out[i] = cam.computeDepth(c);
+  }
+  return 0;
+}
 
 // out: [0..3] center, [4..7] oaxis, [8..16] x/y/z axes, [17..28] P at `level`.
 int ref_camera(const char* txt, int max_level, int level, float* out) {
@@ -134,6 +203,27 @@ int ref_write_pset(int n, const float* fin, char* out, int cap) {
   const int len = (int)s.size();
   if (len < cap) std::memcpy(out, s.data(), len + 1);
   return len;
+}
+
+// The candidate centres of CExpand::findEmptyBlocks (expand.cpp:114-115, 176-177), evaluated
+// in a TU with expand.cpp's own includes so the reference's overload resolution applies:
+// unqualified cos/sin on the float angle, TVec4 operator*(N, TVec4) (vec4.hpp:177) and
+// operator+ (vec4.hpp:149).  expand.cpp itself cannot be linked here (it needs COptim from
+// optim.cpp, i.e. nlopt); this evaluates its two lines with the reference's headers.
+void ref_expand_dirs(const float* coord4, const float* normal4, const float* radius_in, int n, float* out) {
+  const int dnum = 6;
+  for (int q = 0; q < n; ++q) {
+    const Vec4f coord(coord4[4 * q], coord4[4 * q + 1], coord4[4 * q + 2], coord4[4 * q + 3]);
+    const Vec4f normal(normal4[4 * q], normal4[4 * q + 1], normal4[4 * q + 2], normal4[4 * q + 3]);
+    const float radius = radius_in[q];
+    Vec4f xdir, ydir;
+    ortho(normal, xdir, ydir);
+    for (int i = 0; i < dnum; ++i) {
+      const float angle = 2 * M_PI * i / dnum;
+      Vec4f canCoord = coord + cos(angle) * radius * xdir + sin(angle) * radius * ydir;
+      for (int k = 0; k < 4; ++k) out[24 * q + 4 * i + k] = canCoord[k];
+    }
+  }
 }
 
 // Header-only numeric library: ortho (vec4.hpp:303-322) used by CExpand::findEmptyBlocks.

@@ -4,9 +4,12 @@
 Scenes are the deterministic synthetic rings of SURVEY.md §8(d) (pmvs_synth_ring, CPU code
 in libpmvs_amd.so; the images themselves are not stored, only their CRC32, since the
 renderer regenerates them bit-for-bit).  Expected outputs come from two sources:
-  * oracle/_ref (the reference's own camera.cpp compiled unmodified): per-view camera
-    centre / optical axis / axes / per-level projection, and CCamera::project of sample
-    points -- these vectors are REFERENCE outputs;
+  * oracle/_ref (the reference's own camera.cpp compiled unmodified, and its header-inline
+    CImage::getColor / isSafe): per-view camera centre / optical axis / axes / per-level
+    projection, CCamera::project and computeDepth of sample points, and bilinear getColor
+    samples on every pyramid level; the candidate centres of CExpand::findEmptyBlocks
+    (expand.cpp:176-177 evaluated with the reference headers, expand_dirs.npz) -- these
+    vectors are REFERENCE outputs;
   * oracle/liboracle.so (the CPU restatement, pinned on the pieces above): pyramid CRCs,
     grabTex textures, my_f values and full preProcess->refinePatch->postProcess records.
 Run from the repo root in the build container:  python tests/golden/make_golden.py
@@ -66,6 +69,70 @@ def ref_project(proj, max_level, level, pts):
     return out
 
 
+def ref_depth(proj, max_level, pts):
+    """CCamera::computeDepth (camera.cpp:445-452) per view and point."""
+    R = O.ref_lib()
+    out = np.zeros((len(proj), len(pts)), np.float32)
+    with tempfile.TemporaryDirectory() as d:
+        for v, pm in enumerate(proj):
+            path = os.path.join(d, "%08d.txt" % v)
+            write_contour(path, pm)
+            R.ref_camera_depth(path.encode(), max_level, pts.ctypes.data, len(pts), out[v].ctypes.data)
+    return out
+
+
+def color_points(rng, w, h, n):
+    """Sample positions inside CImage::isSafe (x in [0, w-2], y in [0, h-2]) incl. the corners,
+    integer positions and positions one float ulp below an integer."""
+    xy = np.stack([rng.uniform(0, w - 2, n), rng.uniform(0, h - 2, n)], 1).astype(np.float32)
+    xy[:8] = np.array([[0, 0], [w - 2, h - 2], [0, h - 2], [w - 2, 0], [1, 1], [w / 2, h / 2],
+                       [np.nextafter(np.float32(1), np.float32(0)), 2], [3.5, 2.25]], np.float32)
+    xy[8:40] = np.floor(xy[8:40])
+    xy[40:72] = np.nextafter(np.ceil(xy[40:72]), np.float32(0))
+    return xy
+
+
+def ref_colors(o, views, maxlv, n=512):
+    """CImage::getColor (image.hpp:435-476) of the reference header on the oracle's pyramid levels."""
+    R = O.ref_lib()
+    rng = np.random.default_rng(11)
+    xys, cols = [], []
+    for v in range(views):
+        for lv in range(maxlv):
+            img = np.ascontiguousarray(o.get_level(v, lv))
+            h, w = img.shape[:2]
+            xy = color_points(rng, w, h, n)
+            out = np.zeros((n, 3), np.float32)
+            safe = np.zeros(n, np.int32)
+            R.ref_get_color(img.ctypes.data, w, h, xy.ctypes.data, n, out.ctypes.data, safe.ctypes.data)
+            assert safe.all()
+            xys.append(xy)
+            cols.append(out)
+    return (np.stack(xys).reshape(views, maxlv, n, 2), np.stack(cols).reshape(views, maxlv, n, 3))
+
+
+def expand_dir_inputs(rng, n=2000):
+    """Parent (coord, normal, radius) triples for findEmptyBlocks' candidate centres: random and
+    axis-aligned normals (ortho's branches), radii from 1e-3 to 1."""
+    coord = np.concatenate([rng.normal(0, 1, (n, 3)), np.ones((n, 1))], 1).astype(np.float32)
+    nrm = rng.normal(0, 1, (n, 3))
+    nrm[:6] = np.array([[1, 0, 0], [0, 1, 0], [0, 0, 1], [-1, 0, 0], [0, -1, 0], [0, 0, -1]])
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    normal = np.concatenate([nrm, np.zeros((n, 1))], 1).astype(np.float32)
+    radius = np.exp(rng.uniform(np.log(1e-3), 0, n)).astype(np.float32)
+    return coord, normal, radius
+
+
+def make_expand_dirs():
+    R = O.ref_lib()
+    coord, normal, radius = expand_dir_inputs(np.random.default_rng(13))
+    out = np.zeros((len(coord), 6, 4), np.float32)
+    R.ref_expand_dirs(coord.ctypes.data, normal.ctypes.data, radius.ctypes.data, len(coord), out.ctypes.data)
+    path = os.path.join(HERE, "expand_dirs.npz")
+    np.savez_compressed(path, coord=coord, normal=normal, radius=radius, ref_coords=out)
+    print(f"{path}: {os.path.getsize(path)} B")
+
+
 def make(name, views, width, height, level, csize, ntex, neval, nref):
     inp, p = P.synth_scene(views, width, height, level=level, csize=csize, supersample=2)
     o = O.OracleScene(inp)
@@ -82,6 +149,8 @@ def make(name, views, width, height, level, csize, ntex, neval, nref):
     pts[140:150, :3] *= 50.0  # far and behind-camera points
     g["proj_points"] = pts
     g["ref_project"] = ref_project(inp.projections, maxlv, level, pts)
+    g["ref_depth"] = ref_depth(inp.projections, maxlv, pts)
+    g["color_xy"], g["ref_color"] = ref_colors(o, views, maxlv)
 
     tc = P.synth_candidates(p, inp.projections, ntex, seed=101)
     tq = pmvs_cases.tex_queries(o, views, tc)
@@ -107,5 +176,6 @@ def make(name, views, width, height, level, csize, ntex, neval, nref):
 
 if __name__ == "__main__":
     O.build()
+    make_expand_dirs()
     for k, v in SCENES.items():
         make(k, *v)

@@ -62,3 +62,17 @@ def test_loop_oracle(seeds):
     assert log[0]["expand"]["added"] > 5 * len(pa)
     assert len(model) == log[-1]["patches"] > len(pa)
     assert all(x["expand"]["parents"] > 0 for x in log)
+
+
+def test_candidate_centres_match_reference(oracle_mod):
+    """findEmptyBlocks' candidate centres (expand.cpp:176-177: float angle, double cos/sin,
+    Vec4f scaling) from the oracle == the same two reference lines evaluated with the
+    reference's own headers in oracle/_ref (tests/golden/expand_dirs.npz), bit for bit.  The
+    earlier double-angle restatement differed on ~22 % of these centres."""
+    import os
+    import numpy as np
+    g = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "expand_dirs.npz")))
+    out = np.zeros_like(g["ref_coords"])
+    oracle_mod.lib().oracle_expand_dirs(g["coord"].ctypes.data, g["normal"].ctypes.data, g["radius"].ctypes.data,
+                                        len(g["coord"]), out.ctypes.data)
+    assert out.view(np.uint32).tobytes() == g["ref_coords"].view(np.uint32).tobytes()
