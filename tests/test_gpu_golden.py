@@ -11,7 +11,9 @@ import pytest
 from pmvs_cases import bits
 
 pytestmark = pytest.mark.gpu
-GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+# scene goldens (c1, ring8); expand_dirs.npz holds scene-free candidate-centre vectors
+GOLDEN = sorted(p for p in glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz"))
+                if not os.path.basename(p).startswith("expand_dirs"))
 
 
 @pytest.fixture(scope="module", params=GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
