@@ -255,11 +255,37 @@ struct QCmp {
 // their free directions found against the same start-of-wave model) while it holds fewer than
 // `min_cands` candidate directions: late passes, where most parents are already surrounded, then
 // batch enough refinements per wave.  min_cands = 0 (or wave = 1) keeps plain waves.
+// nthreads > 1 runs findEmptyBlocks, the candidate preparation and the refinements of one wave
+// on a std::thread pool (one scratch context per thread, the reference's threading model,
+// expand.cpp:41-52); they only read the start-of-wave model, so the result is identical for every
+// thread count.  max_waves > 0 stops after that many waves (bounded CPU-baseline samples).
+template <class F>
+static void parallel_for(int nthreads, size_t n, F&& f) {
+  if (nthreads <= 1 || n < 2) {
+    for (size_t i = 0; i < n; ++i) f(0, i);
+    return;
+  }
+  std::atomic<size_t> next(0);
+  auto work = [&](int tid) {
+    for (;;) {
+      const size_t i = next.fetch_add(1);
+      if (i >= n) break;
+      f(tid, i);
+    }
+  };
+  std::vector<std::thread> th;
+  const int T = (int)std::min<size_t>((size_t)nthreads, n);
+  for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& t : th) t.join();
+}
+
 static void expand_run(const OScene& s, std::vector<FPatch>& P, std::vector<int>& alive, int wave, int cthr, int flags,
-                       ExpandStats& st, int min_cands = 0) {
+                       ExpandStats& st, int min_cands = 0, int nthreads = 1, int64_t max_waves = 0) {
   Model m(s);
-  OCtx ctx;
-  init_ctx(s, ctx);
+  nthreads = std::max(1, nthreads);
+  std::vector<OCtx> ctxs(nthreads);
+  for (auto& c : ctxs) init_ctx(s, c);
   model_load(m, P, alive, (flags & 1) == 0);
   for (int p : m.o.ppatches) P[p].flag = 0;  // clearFlags
   std::priority_queue<QItem, std::vector<QItem>, QCmp> queue;
@@ -272,7 +298,7 @@ static void expand_run(const OScene& s, std::vector<FPatch>& P, std::vector<int>
           queue.push({P[p].tmp, seq++, p});
         }
   const int W = std::max(1, wave);
-  while (!queue.empty()) {
+  while (!queue.empty() && (max_waves <= 0 || st.waves < max_waves)) {
     st.waves++;
     // Every parent's free directions are found against the model at the start of the wave
     // (expand.cpp:92-93); wave = 1 then prepares, refines and commits them one after the other
@@ -286,10 +312,12 @@ static void expand_run(const OScene& s, std::vector<FPatch>& P, std::vector<int>
         chunk.push_back(queue.top().p);
         queue.pop();
       }
-      for (int par : chunk) {
-        std::vector<std::pair<int, V4>> d;
-        find_empty_blocks(m, P, P[par], P[par].dflag, d);
-        for (auto& x : d) {
+      std::vector<std::vector<std::pair<int, V4>>> found(chunk.size());
+      parallel_for(W > 1 ? nthreads : 1, chunk.size(),
+                   [&](int, size_t k) { find_empty_blocks(m, P, P[chunk[k]], P[chunk[k]].dflag, found[k]); });
+      for (size_t k = 0; k < chunk.size(); ++k) {
+        const int par = chunk[k];
+        for (auto& x : found[k]) {
           Cand c;
           c.parent = par;
           c.dir = x.first;
@@ -301,13 +329,16 @@ static void expand_run(const OScene& s, std::vector<FPatch>& P, std::vector<int>
     } while (W > 1 && (int64_t)dirs.size() < min_cands && !queue.empty());
     st.parents += (int64_t)parents.size();
     auto batch = [&](size_t b, size_t e, bool recheck) {
-      for (size_t i = b; i < e; ++i) {
-        Cand& c = dirs[i];
+      const int T = e - b > 1 ? nthreads : 1;
+      parallel_for(T, e - b, [&](int, size_t k) {
+        Cand& c = dirs[b + k];
         c.status = prepare_candidate(m, P[c.parent], c.coord, cthr, s.depth, c.prep, c.edge_images) ? 1 : 0;
-      }
+      });
       st.candidates += (int64_t)(e - b);
-      for (size_t i = b; i < e; ++i)
-        if (dirs[i].status == 0) dirs[i].status = refine_candidate(m, P, ctx, dirs[i].prep, dirs[i].edge_images, dirs[i].out);
+      parallel_for(T, e - b, [&](int tid, size_t k) {
+        Cand& c = dirs[b + k];
+        if (c.status == 0) c.status = refine_candidate(m, P, ctxs[tid], c.prep, c.edge_images, c.out);
+      });
       for (size_t i = b; i < e; ++i) {
         Cand& c = dirs[i];
         int status = c.status;

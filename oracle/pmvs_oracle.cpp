@@ -1186,13 +1186,14 @@ static void from_fpatch(const FPatch& q, pmvs_patch& a) {
 // patch count or -1 when cap is too small.  stats: parents, candidates, fail_prep, fail_pre,
 // fail_post, fail_commit, added, waves.
 int oracle_expand_run(void* h, const pmvs_patch* patches, const int* alive, int n, int wave, int cthr, int flags,
-                      int min_cands, pmvs_patch* out, int* alive_out, int cap, int64_t* stats) {
+                      int min_cands, pmvs_patch* out, int* alive_out, int cap, int64_t* stats, int nthreads,
+                      int64_t max_waves) {
   const OScene& s = *static_cast<const OScene*>(h);
   std::vector<FPatch> P(n);
   std::vector<int> al(alive, alive + n);
   for (int i = 0; i < n; ++i) to_fpatch(patches[i], P[i]);
   ExpandStats st;
-  expand_run(s, P, al, wave, cthr, flags, st, min_cands);
+  expand_run(s, P, al, wave, cthr, flags, st, min_cands, nthreads, max_waves);
   if ((int)P.size() > cap) return -1;
   for (size_t i = 0; i < P.size(); ++i) {
     from_fpatch(P[i], out[i]);

@@ -49,7 +49,7 @@ def lib():
         L.oracle_refine_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.POINTER(P.Stats)]
         L.oracle_filter_run.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         L.oracle_expand_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
-                                        C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+                                        C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int64]
         L.oracle_bobyqa_test.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_int, C.POINTER(C.c_int)]
         _lib = L
@@ -161,7 +161,8 @@ class OracleScene:
         lib().oracle_filter_run(self.h, _p(pa), len(pa), _p(keep), _p(counts))
         return pa, keep, counts
 
-    def expand_run(self, patches, alive=None, wave=1, count_threshold=4, cap=None, after_seeds=False, min_candidates=0):
+    def expand_run(self, patches, alive=None, wave=1, count_threshold=4, cap=None, after_seeds=False, min_candidates=0,
+                   nthreads=1, max_waves=0):
         """One CExpand::run; returns (patches_out, alive_out, stats dict)."""
         pa = np.ascontiguousarray(patches, P.PATCH_DTYPE)
         al = np.ones(len(pa), np.int32) if alive is None else np.ascontiguousarray(alive, np.int32)
@@ -171,13 +172,14 @@ class OracleScene:
         st = np.zeros(8, np.int64)
         m = lib().oracle_expand_run(self.h, _p(pa), _p(al), len(pa), wave, count_threshold, int(after_seeds),
                                     int(min_candidates), _p(out), _p(alo), cap,
-                                    _p(st))
+                                    _p(st), int(nthreads), int(max_waves))
         if m < 0:
             raise RuntimeError("expand_run: capacity too small")
         keys = ("parents", "candidates", "fail_prep", "fail_pre", "fail_post", "fail_commit", "added", "waves")
         return out[:m].copy(), alo[:m].copy(), dict(zip(keys, st.tolist()))
 
-    def run_loop(self, seeds, threshold, iterations=3, wave=4096, cap=None, after_seeds=True, min_candidates=0):
+    def run_loop(self, seeds, threshold, iterations=3, wave=4096, cap=None, after_seeds=True, min_candidates=0,
+                 nthreads=1):
         """findMatch.cpp:196-217 after the seed phase, restated: returns (patches, per-iteration counts)."""
         ncc = np.float32(threshold)
         before = np.float32(ncc - np.float32(0.3))  # findMatch.cpp:104
@@ -186,7 +188,8 @@ class OracleScene:
         for t in range(iterations):
             self.set_thresholds(float(ncc), float(before), depth)
             model, _, st_e = self.expand_run(model, wave=wave, count_threshold=cthr, cap=cap,
-                                             after_seeds=after_seeds and t == 0, min_candidates=min_candidates)
+                                             after_seeds=after_seeds and t == 0, min_candidates=min_candidates,
+                                             nthreads=nthreads)
             model, keep, counts = self.filter_run(model)
             model = model[keep == 1]
             log.append({"depth": depth, "expand": st_e, "filter": counts.tolist(), "patches": len(model)})
