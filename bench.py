@@ -14,9 +14,14 @@ Also: NCC evals/s (my_f + computeINCC evaluations), refined candidates/s.
 roofline: the loop's dominant kernel, refine_v2_kernel: algorithmic bytes = 588 B x valid
 textures per my_f evaluation over its HIP-event time, against 8 TB/s HBM.
 refine_c2: the refine kernel alone on configs[1] (8-view 1920x1080, level 1, 100k candidates).
-cpu_baseline: the oracle (CPU restatement, std::thread pool) on a bounded sample of the same
-scene's refine work (preProcess -> refinePatch -> postProcess, >= 80 % of the reference's CPU
-time) on this host.
+cpu_baseline: the same metric on the host CPU -- the oracle (CPU restatement) runs the first
+expansion of the same rank-0 C3 scene from the same seeds with the same wave schedule
+(findEmptyBlocks, preparation and the refinements of a wave on a std::thread pool over every CPU
+this process may use, commit serial as in the product), bounded to its first --cpu-waves waves;
+value = patches committed / wall time of those waves.  A refine-only rate over synthetic seed
+candidates is reported beside it (refine_only).
+checks: size-independent properties of the C3 model (identical model from every repetition,
+finite geometry, unit normals, image-list invariants, the synthetic sphere's surface residual).
 
 Multi-GPU (`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`), one
 process per GPU:
@@ -61,8 +66,9 @@ def parse():
     ap.add_argument("--c2-candidates", type=int, default=100000)
     ap.add_argument("--no-c2", action="store_true", help="skip the configs[1] refine-kernel side measurement")
     ap.add_argument("--only-c2", action="store_true", help="only the configs[1] refine-kernel measurement (profiling)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="refine-only CPU sample time budget")
+    ap.add_argument("--cpu-waves", type=int, default=2, help="expansion waves in the CPU loop sample")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
@@ -80,6 +86,96 @@ def pmc_traffic(workload):
             if k.startswith("pmvsdev::refine_v2_kernel") or k.startswith("refine_v2_kernel"):
                 return int(v["hbm_bytes_per_launch"]), int(v.get("launches", 0)), os.path.relpath(f, ROOT)
     return None, None, None
+
+
+def host_cpus():
+    """CPUs this process may use: the affinity mask, further limited by a cgroup v2 CPU quota
+    (cpu.max) when one is set; with the machine's logical CPU count and model for the record."""
+    import math
+    logical = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = logical
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    usable = affinity if quota is None else max(1, min(affinity, math.ceil(quota)))
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"usable": usable, "logical": logical, "affinity": affinity, "cgroup_quota_cpus": quota, "model": model}
+
+
+def cpu_loop_baseline(P, inp, sp, seeds, args):
+    """Loop-level CPU baseline (see the module docstring): refined patches committed per second by
+    the oracle's threaded expansion on the C3 scene, first --cpu-waves waves of iteration 1."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+    cpus = host_cpus()
+    threads = args.cpu_threads or cpus["usable"]
+    o = O.OracleScene(inp)
+    ncc = np.float32(inp.threshold)
+    o.set_thresholds(float(ncc), float(np.float32(ncc - np.float32(0.3))), 1)
+    _, _, st = o.expand_run(seeds, wave=args.wave, count_threshold=4, cap=max(1 << 20, 64 * len(seeds)),
+                            after_seeds=True, min_candidates=args.min_candidates, nthreads=threads,
+                            max_waves=args.cpu_waves)
+    loop_s = o.last_wave_s
+    # refine-only side figure: preProcess -> refinePatch -> postProcess on seed-path candidates
+    sample = P.synth_candidates(sp, inp.projections, 400000, seed=0xC0FFEE)
+    done = acc = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds and done < len(sample):
+        r, rs = o.refine_batch(sample[done:done + 2000], nthreads=threads)
+        done += len(r)
+        acc += rs["accepted"]
+    tr = time.perf_counter() - t0
+    o.close()
+    return {"value": round(float(st["added"]) / loop_s, 1), "unit": "refined patches/s", "cores": threads,
+            "kind": "port",
+            "sample": f"first {st['waves']} expansion waves (wave {args.wave}, min_candidates {args.min_candidates}) "
+                      f"of iteration 1 on the rank-0 C3 scene from its {len(seeds)} seeds: {st['parents']} parents, "
+                      f"{st['candidates']} candidates, {st['added']} patches committed in {loop_s:.2f} s; "
+                      f"oracle/liboracle.so (CPU restatement), {threads} threads",
+            "host": cpus,
+            "refine_only": {"value": round(acc / tr, 1), "unit": "refined patches/s",
+                            "sample": f"{done} seed-path candidates, preProcess->refinePatch->postProcess, {tr:.1f} s"}}
+
+
+def model_checks(model, inp, hashes):
+    """Size-independent properties of a C3 loop result (the model is too large for the oracle)."""
+    import pmvs_amd as P
+    n = len(model)
+    coord = model["coord"][:, :3].astype(np.float64)
+    normal = model["normal"][:, :3].astype(np.float64)
+    ni = model["num_images"]
+    tnum = inp.num_targets
+    radius = np.linalg.norm(coord, axis=1)  # synthetic scene: the unit sphere
+    checks = {
+        "model_identical_across_steps": len(set(hashes)) == 1,
+        "model_hash": hashes[0] if hashes else None,
+        "finite": bool(np.isfinite(model["coord"]).all() and np.isfinite(model["normal"]).all()),
+        "unit_normals": bool(np.all(np.abs(np.linalg.norm(normal, axis=1) - 1.0) < 1e-3)),
+        "min_images_ok": bool(np.all(ni >= inp.min_image_num)),
+        "reference_is_target": bool(np.all(model["images"][:, 0] < tnum)),
+        "images_unique": bool(all(len(set(model["images"][i, :ni[i]].tolist())) == ni[i]
+                                  for i in range(0, n, max(1, n // 20000)))),
+        "sphere_residual_mean": float(np.mean(np.abs(radius - 1.0))),
+        "sphere_residual_p99": float(np.percentile(np.abs(radius - 1.0), 99)),
+        "ncc_min": float(model["ncc"].min()) if n else None,
+    }
+    checks["ok"] = all(checks[k] for k in ("model_identical_across_steps", "finite", "unit_normals",
+                                           "min_images_ok", "reference_is_target", "images_unique"))
+    return checks
 
 
 def rank_seed(rank: int) -> int:
@@ -179,23 +275,29 @@ def main():
         ex.attach(scene)
 
     def step():
-        model, log = scene.run_loop(seeds, inp.threshold, iterations=args.iterations, wave=args.wave,
-                                    min_candidates=args.min_candidates)
-        return len(model), log
+        return scene.run_loop(seeds, inp.threshold, iterations=args.iterations, wave=args.wave,
+                              min_candidates=args.min_candidates)
 
+    import hashlib
+    hashes = []
     for _ in range(args.warmup):
-        step()
+        model, _ = step()
+        hashes.append(hashlib.sha1(model.view(np.uint8)).hexdigest())
+        del model
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     logs = []
+    last = None
     for _ in range(args.steps):
-        logs.append(step())
+        last, log = step()
+        logs.append((len(last), log))
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    hashes.append(hashlib.sha1(last.view(np.uint8)).hexdigest())  # after the timed region
 
     def tot(key):
         return sum(it["expand"][key] for _, log in logs for it in log)
@@ -215,25 +317,11 @@ def main():
     if rank == 0 and not args.no_c2:
         c2 = c2_refine(P, args, dev, rank)
     if rank == 0:
+        checks = model_checks(last, inp, hashes)
+        del last
         cpu = None
         if not args.no_cpu_baseline:
-            sys.path.insert(0, os.path.join(ROOT, "oracle"))
-            import pyoracle as O
-            o = O.OracleScene(inp)
-            threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-            sample = P.synth_candidates(sp, inp.projections, 600000, seed=0xC0FFEE)
-            done = acc_cpu = 0
-            chunk = 1000
-            tc0 = time.perf_counter()
-            while time.perf_counter() - tc0 < args.cpu_seconds and done < len(sample):
-                r, st = o.refine_batch(sample[done:done + chunk], nthreads=threads)
-                done += len(r)
-                acc_cpu += st["accepted"]
-            tc = time.perf_counter() - tc0
-            o.close()
-            cpu = {"value": round(acc_cpu / tc, 1), "unit": "refined patches/s", "cores": threads, "kind": "port",
-                   "sample": f"{done} candidates of the rank-0 C3 scene through preProcess->refinePatch->"
-                             f"postProcess, oracle/liboracle.so (CPU restatement, std::thread pool), {tc:.1f} s"}
+            cpu = cpu_loop_baseline(P, inp, sp, seeds, args)
         first = logs[0][1]
         result = {
             "metric": METRIC,
@@ -272,9 +360,12 @@ def main():
                             "filter_ms": round(it["filter"]["kernel_ms"], 1)} for it in first],
             "refine_c2": c2,
             "cpu_baseline": cpu,
+            "checks": checks,
             "setup_s": {"synth": round(t_synth, 2), "scene_and_seeds": round(t_scene, 2)},
         }
         print(json.dumps(result), flush=True)
+        if not checks["ok"]:
+            print(f"bench.py: C3 model checks failed: {checks}", file=sys.stderr, flush=True)
     scene.close()
     if dist:
         dist.barrier()

@@ -22,6 +22,7 @@ namespace oracle {
 struct ExpandStats {
   int64_t parents = 0, candidates = 0, fail_prep = 0, fail_pre = 0, fail_post = 0, fail_commit = 0, added = 0,
           waves = 0;
+  int64_t wave_ns = 0;  // wall time of the waves (after the model load and queue setup)
 };
 
 struct Model {
@@ -259,27 +260,6 @@ struct QCmp {
 // on a std::thread pool (one scratch context per thread, the reference's threading model,
 // expand.cpp:41-52); they only read the start-of-wave model, so the result is identical for every
 // thread count.  max_waves > 0 stops after that many waves (bounded CPU-baseline samples).
-template <class F>
-static void parallel_for(int nthreads, size_t n, F&& f) {
-  if (nthreads <= 1 || n < 2) {
-    for (size_t i = 0; i < n; ++i) f(0, i);
-    return;
-  }
-  std::atomic<size_t> next(0);
-  auto work = [&](int tid) {
-    for (;;) {
-      const size_t i = next.fetch_add(1);
-      if (i >= n) break;
-      f(tid, i);
-    }
-  };
-  std::vector<std::thread> th;
-  const int T = (int)std::min<size_t>((size_t)nthreads, n);
-  for (int t = 1; t < T; ++t) th.emplace_back(work, t);
-  work(0);
-  for (auto& t : th) t.join();
-}
-
 static void expand_run(const OScene& s, std::vector<FPatch>& P, std::vector<int>& alive, int wave, int cthr, int flags,
                        ExpandStats& st, int min_cands = 0, int nthreads = 1, int64_t max_waves = 0) {
   Model m(s);
@@ -298,6 +278,7 @@ static void expand_run(const OScene& s, std::vector<FPatch>& P, std::vector<int>
           queue.push({P[p].tmp, seq++, p});
         }
   const int W = std::max(1, wave);
+  const auto t_waves = std::chrono::steady_clock::now();
   while (!queue.empty() && (max_waves <= 0 || st.waves < max_waves)) {
     st.waves++;
     // Every parent's free directions are found against the model at the start of the wave
@@ -369,6 +350,7 @@ static void expand_run(const OScene& s, std::vector<FPatch>& P, std::vector<int>
     else
       batch(0, dirs.size(), true);
   }
+  st.wave_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_waves).count();
 }
 
 }  // namespace oracle

@@ -156,6 +156,31 @@ static void set_vimages_vgrids(const Organizer& o, const std::vector<FPatch>& P,
   }
 }
 
+// Thread pool for the per-patch stages (the reference runs them on _CPU threads, filter.cpp:
+// filterOutsideThread / filterExactThread / filterNeighborThread / setVImagesVGrids threads).  Each
+// task writes only its own slot, so results do not depend on the thread count.
+static int g_threads = 1;
+template <class F>
+static void parallel_for(int nthreads, size_t n, F&& f) {
+  if (nthreads <= 1 || n < 2) {
+    for (size_t i = 0; i < n; ++i) f(0, i);
+    return;
+  }
+  std::atomic<size_t> next(0);
+  auto work = [&](int tid) {
+    for (;;) {
+      const size_t i = next.fetch_add(1);
+      if (i >= n) break;
+      f(tid, i);
+    }
+  };
+  std::vector<std::thread> th;
+  const int T = (int)std::min<size_t>((size_t)nthreads, n);
+  for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& t : th) t.join();
+}
+
 // CFilter::setDepthMapsVGridsVPGridsAddPatchV (filter.cpp:727-770).
 static void set_dm_vgrids(Organizer& o, std::vector<FPatch>& P, int additive) {
   collect_patches(o, P, 0);
@@ -167,7 +192,7 @@ static void set_dm_vgrids(Organizer& o, std::vector<FPatch>& P, int additive) {
       P[p].vimages.clear();
       P[p].vgrids.clear();
     }
-  for (int p : o.ppatches) set_vimages_vgrids(o, P, P[p]);
+  parallel_for(g_threads, o.ppatches.size(), [&](int, size_t k) { set_vimages_vgrids(o, P, P[o.ppatches[k]]); });
   for (int t = 0; t < o.s.tnum; ++t)  // addPatchVThread: first matching entry only
     for (int p : o.ppatches) {
       const FPatch& q = P[p];
@@ -234,7 +259,7 @@ static float compute_gain(const Organizer& o, const std::vector<FPatch>& P, cons
 static int filter_outside(Organizer& o, std::vector<FPatch>& P) {
   collect_patches(o, P, 1);
   std::vector<float> gains(o.ppatches.size());
-  for (size_t k = 0; k < o.ppatches.size(); ++k) gains[k] = compute_gain(o, P, P[o.ppatches[k]]);
+  parallel_for(g_threads, o.ppatches.size(), [&](int, size_t k) { gains[k] = compute_gain(o, P, P[o.ppatches[k]]); });
   int count = 0;
   for (size_t k = 0; k < o.ppatches.size(); ++k)
     if (gains[k] < 0.0) {
@@ -245,13 +270,16 @@ static int filter_outside(Organizer& o, std::vector<FPatch>& P) {
 }
 
 // CFilter::filterExact (filter.cpp:203-356), neighbourThreshold1 = 1.0.
-static int filter_exact(Organizer& o, std::vector<FPatch>& P, OCtx& ctx) {
+static int filter_exact(Organizer& o, std::vector<FPatch>& P, std::vector<OCtx>& ctxs) {
   const OScene& s = o.s;
   collect_patches(o, P, 0);
   const int psize = (int)o.ppatches.size();
   std::vector<std::vector<int>> newimages(psize), removeimages(psize);
   std::vector<std::vector<std::pair<int, int>>> newgrids(psize), removegrids(psize);
-  for (int t = 0; t < s.tnum; ++t) {
+  // per target image (in parallel): (patch id, x, y, safe) in cell order; merged in image order
+  std::vector<std::vector<std::array<int, 4>>> found(s.tnum);
+  parallel_for(g_threads, (size_t)s.tnum, [&](int, size_t tt) {
+    const int t = (int)tt;
     const int w = s.gwidths[t], h = s.gheights[t];
     int index = -1;
     for (int y = 0; y < h; ++y)
@@ -266,16 +294,20 @@ static int filter_exact(Organizer& o, std::vector<FPatch>& P, OCtx& ctx) {
           else if (x < w - 1 && is_visible(o, P, q, t, x + 1, y, 1.0f)) safe = 1;
           else if (0 < y && is_visible(o, P, q, t, x, y - 1, 1.0f)) safe = 1;
           else if (y < h - 1 && is_visible(o, P, q, t, x, y + 1, 1.0f)) safe = 1;
-          if (safe) {
-            newimages[q.id].push_back(t);
-            newgrids[q.id].push_back({x, y});
-          } else {
-            removeimages[q.id].push_back(t);
-            removegrids[q.id].push_back({x, y});
-          }
+          found[t].push_back({{q.id, x, y, safe}});
         }
       }
-  }
+  });
+  for (int t = 0; t < s.tnum; ++t)
+    for (const auto& f : found[t]) {
+      if (f[3]) {
+        newimages[f[0]].push_back(t);
+        newgrids[f[0]].push_back({f[1], f[2]});
+      } else {
+        removeimages[f[0]].push_back(t);
+        removegrids[f[0]].push_back({f[1], f[2]});
+      }
+    }
   for (int k = 0; k < psize; ++k) {
     const int p = o.ppatches[k];
     if (P[p].fix) continue;
@@ -284,11 +316,11 @@ static int filter_exact(Organizer& o, std::vector<FPatch>& P, OCtx& ctx) {
       erase_from(o.pgrids[t][o.cell(t, removegrids[k][i].first, removegrids[k][i].second)], p);
     }
   }
-  int count = 0;
-  for (int k = 0; k < psize; ++k) {
+  parallel_for(g_threads, (size_t)psize, [&](int tid, size_t kk) {
+    const int k = (int)kk;
     const int p = o.ppatches[k];
     FPatch& q = P[p];
-    if (q.fix) continue;
+    if (q.fix) return;
     q.timages = (int)newimages[k].size();
     for (size_t i = 0; i < q.images.size(); ++i)
       if (s.tnum <= q.images[i]) {
@@ -301,12 +333,18 @@ static int filter_exact(Organizer& o, std::vector<FPatch>& P, OCtx& ctx) {
       OPatch op;
       op.coord = q.coord; op.normal = q.normal; op.images = q.images; op.grids = q.grids;
       op.dscale = q.dscale; op.ascale = q.ascale; op.ncc = q.ncc;
-      set_ref_image(s, ctx, op);
+      set_ref_image(s, ctxs[tid], op);
       q.images = op.images;
       OPatch g = op;
       set_grids(s, g);
       q.grids = g.grids;
     }
+  });
+  int count = 0;
+  for (int k = 0; k < psize; ++k) {
+    const int p = o.ppatches[k];
+    FPatch& q = P[p];
+    if (q.fix) continue;
     if ((int)q.images.size() < s.minImageNum) {
       remove_patch(o, P, p);
       count++;
@@ -457,13 +495,13 @@ static int filter_quad(const OScene& s, const std::vector<FPatch>& P, const FPat
 static int filter_neighbor(Organizer& o, std::vector<FPatch>& P) {
   collect_patches(o, P, 1);
   std::vector<int> rejects(o.ppatches.size(), 0);
-  for (size_t k = 0; k < o.ppatches.size(); ++k) {
+  parallel_for(g_threads, o.ppatches.size(), [&](int, size_t k) {
     const FPatch& q = P[o.ppatches[k]];
     std::vector<int> nb;
     find_neighbors(o, P, q, nb, 4.0f, 2, 1);
     if ((int)nb.size() < 6) rejects[k] = 1;
     else if (filter_quad(o.s, P, q, nb)) rejects[k] = 1;
-  }
+  });
   int count = 0;
   for (size_t k = 0; k < o.ppatches.size(); ++k)
     if (rejects[k]) {
@@ -531,13 +569,13 @@ static int filter_small_groups(Organizer& o, std::vector<FPatch>& P) {
 // CFilter::run (filter.cpp:13-27).  counts[0..3] = removed by outside/exact/neighbor/groups.
 static void filter_run(const OScene& s, std::vector<FPatch>& P, std::vector<int>& keep, int counts[4]) {
   Organizer o(s);
-  OCtx ctx;
-  init_ctx(s, ctx);
+  std::vector<OCtx> ctxs(std::max(1, g_threads));
+  for (auto& c : ctxs) init_ctx(s, c);
   for (int p = 0; p < (int)P.size(); ++p) add_patch_p(o, P, p);
   set_dm_vgrids(o, P, 0);
   counts[0] = filter_outside(o, P);
   set_dm_vgrids(o, P, 1);
-  counts[1] = filter_exact(o, P, ctx);
+  counts[1] = filter_exact(o, P, ctxs);
   set_dm_vgrids(o, P, 1);
   counts[2] = filter_neighbor(o, P);
   set_dm_vgrids(o, P, 1);

@@ -17,6 +17,7 @@
 // Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use this file.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <climits>
 #include <cmath>
 #include <cstdint>
@@ -1111,6 +1112,10 @@ int oracle_bobyqa_test(int kind, const double* x0, int maxeval, double* xout, do
 }
 
 // One CFilter::run pass (filter_oracle.h).  counts[4]: removed by outside/exact/neighbor/groups.
+// Thread count of the filter's per-patch stages (filter_oracle.h g_threads); results are
+// independent of it.
+void oracle_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
+
 void oracle_filter_run(void* h, pmvs_patch* patches, int n, int* keep, int* counts) {
   const OScene& s = *static_cast<const OScene*>(h);
   std::vector<FPatch> P(n);
@@ -1184,7 +1189,7 @@ static void from_fpatch(const FPatch& q, pmvs_patch& a) {
 // One CExpand::run (expand_oracle.h) on the model (patches[i], alive[i]).  Writes the updated
 // model (old patches first, new ones appended) to out/alive_out (capacity cap); returns the new
 // patch count or -1 when cap is too small.  stats: parents, candidates, fail_prep, fail_pre,
-// fail_post, fail_commit, added, waves.
+// fail_post, fail_commit, added, waves, wave_ns (9 entries).
 int oracle_expand_run(void* h, const pmvs_patch* patches, const int* alive, int n, int wave, int cthr, int flags,
                       int min_cands, pmvs_patch* out, int* alive_out, int cap, int64_t* stats, int nthreads,
                       int64_t max_waves) {
@@ -1199,9 +1204,9 @@ int oracle_expand_run(void* h, const pmvs_patch* patches, const int* alive, int 
     from_fpatch(P[i], out[i]);
     alive_out[i] = al[i];
   }
-  const int64_t v[8] = {st.parents, st.candidates, st.fail_prep, st.fail_pre, st.fail_post, st.fail_commit, st.added,
-                        st.waves};
-  for (int k = 0; k < 8; ++k) stats[k] = v[k];
+  const int64_t v[9] = {st.parents, st.candidates, st.fail_prep, st.fail_pre, st.fail_post, st.fail_commit, st.added,
+                        st.waves, st.wave_ns};
+  for (int k = 0; k < 9; ++k) stats[k] = v[k];
   return (int)P.size();
 }
 

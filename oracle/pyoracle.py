@@ -43,6 +43,7 @@ def lib():
         L.oracle_grab_tex.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         L.oracle_get_color.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p]
         L.oracle_expand_dirs.argtypes = [C.c_void_p] * 3 + [C.c_int, C.c_void_p]
+        L.oracle_set_threads.argtypes = [C.c_int]
         L.oracle_depth.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p]
         L.oracle_paxes.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.oracle_incc_eval.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
@@ -169,20 +170,23 @@ class OracleScene:
         cap = cap or max(4 * len(pa), 1024)
         out = np.zeros(cap, P.PATCH_DTYPE)
         alo = np.zeros(cap, np.int32)
-        st = np.zeros(8, np.int64)
+        st = np.zeros(9, np.int64)
         m = lib().oracle_expand_run(self.h, _p(pa), _p(al), len(pa), wave, count_threshold, int(after_seeds),
                                     int(min_candidates), _p(out), _p(alo), cap,
                                     _p(st), int(nthreads), int(max_waves))
         if m < 0:
             raise RuntimeError("expand_run: capacity too small")
         keys = ("parents", "candidates", "fail_prep", "fail_pre", "fail_post", "fail_commit", "added", "waves")
-        return out[:m].copy(), alo[:m].copy(), dict(zip(keys, st.tolist()))
+        stats = dict(zip(keys, st.tolist()))
+        self.last_wave_s = st[8] / 1e9  # wall time of the waves (not part of the parity dict)
+        return out[:m].copy(), alo[:m].copy(), stats
 
     def run_loop(self, seeds, threshold, iterations=3, wave=4096, cap=None, after_seeds=True, min_candidates=0,
                  nthreads=1):
         """findMatch.cpp:196-217 after the seed phase, restated: returns (patches, per-iteration counts)."""
         ncc = np.float32(threshold)
         before = np.float32(ncc - np.float32(0.3))  # findMatch.cpp:104
+        lib().oracle_set_threads(int(nthreads))
         cthr, depth, model, log = 4, 1, np.ascontiguousarray(seeds, P.PATCH_DTYPE), []
         cap = cap or max(64 * len(model), 1 << 16)
         for t in range(iterations):
