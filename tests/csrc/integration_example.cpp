@@ -1,35 +1,19 @@
-# INTEGRATION — dropping the MI355X dense-matching core into the reference
+// tests/csrc/integration_example.cpp -- TEST INFRASTRUCTURE: the reference-side binding that
+// INTEGRATION.md shows, as one translation unit.  tests/test_integration_doc.py checks that every
+// ```cpp block of INTEGRATION.md occurs in this file and, where /root/reference exists (the build
+// container), compiles it with -fsyntax-only against the reference's own headers and
+// include/pmvs_amd.h -- so the documented binding type-checks against both sides of the boundary.
+#include <algorithm>
+#include <iostream>
+#include <memory>
+#include <vector>
 
-The reference runs the hot path per patch, per thread, through `COptim`:
+#include "pmvs/findMatch.hpp"
+#include "pmvs_amd.h"
 
-```text
-// seed.cpp:387-414 (CSeed::initialMatchSub) and expand.cpp:225-237 (CExpand::expandSub)
-if (_fm._optim.preProcess(patch, id, 1)) { ++_fcounts0[id]; return 1; }
-_fm._optim.refinePatch(patch, id, 100);
-if (_fm._optim.postProcess(patch, id, 1)) { ++_fcounts1[id]; return 1; }
-++_pcounts[id];
-```
+namespace pmvs_integration {
 
-With `libpmvs_amd.so` these per-patch calls become batched calls:
-
-- The **seed** call site runs at depth 0. Its postProcess needs no organizer state, so a batch of
-  seed candidates maps to `pmvs_refine_batch` (§2).
-- The **expansion** call site runs at depth ≥ 1. Its postProcess reads the organizer
-  (`setVImagesVGrids`, and `check()` at depth ≥ 2), and its candidates come from the organizer
-  (`findEmptyBlocks`, `checkCounts`). A whole `CExpand::run` therefore maps to
-  `pmvs_expand_run` (§3). `pmvs_refine_batch` rejects depth ≥ 1 with `PMVS_EUNSUPPORTED`.
-- `pmvs_run_loop` replaces the three expand/filter iterations of `CFindMatch::run` (§4).
-- The standalone executable `pmvs2` (§5) replaces `pmvs.cpp` as a whole.
-
-A maintainer adds `include/pmvs_amd.h`, links `-lpmvs_amd`, and adds the functions below.
-Every C++ block here is taken verbatim from `tests/csrc/integration_example.cpp`.
-`tests/test_integration_doc.py` checks that the blocks occur in that file. Where the reference
-sources exist, it also compiles the file with `-fsyntax-only` against the reference's own headers
-(`include/pmvs/findMatch.hpp` …) and `include/pmvs_amd.h`.
-
-## 1. Scene setup (once, after `CFindMatch::init`, findMatch.cpp:30-107)
-
-```cpp
+// ---- §1 scene setup
 pmvs_scene* make_scene(PMVS3::CFindMatch& fm, int device) {
   const int n = fm.NumImages();                // targets first, then other images
   std::vector<pmvs_view_desc> views(n);
@@ -64,19 +48,9 @@ pmvs_scene* make_scene(PMVS3::CFindMatch& fm, int device) {
   }
   return s;
 }
-```
 
-Wherever `CFindMatch::updateThreshold` runs (findMatch.cpp:23-28), call
-`pmvs_set_thresholds(s, fm._nccThreshold, fm._nccThresholdBefore, fm._depth)`.
-`pmvs_expand_run` callers must do this; `pmvs_run_loop` sets the thresholds itself.
-
-## 2. Seed call site: batched preProcess → refinePatch → postProcess (depth 0)
-
-`CSeed::initialMatch` (seed.cpp:133-204) tries a feature's candidates one after the other.
-The batched form collects them, refines them in one call, and replays the serial decisions on
-the results. Each result depends only on the candidate and the scene, never on the model.
-
-```cpp
+// ---- §2 seed call site (CSeed::initialMatchSub, seed.cpp:387-414), depth 0
+// status[i]: 0 accepted, 1 rejected by preProcess (_fcounts0), 2 rejected by postProcess (_fcounts1)
 int refine_seed_candidates(pmvs_scene* scene, std::vector<Patch::CPatch>& batch, std::vector<int>& status) {
   std::vector<pmvs_candidate> in(batch.size());
   for (size_t i = 0; i < batch.size(); ++i) {
@@ -107,14 +81,36 @@ int refine_seed_candidates(pmvs_scene* scene, std::vector<Patch::CPatch>& batch,
   }
   return 0;
 }
-```
 
-A candidate whose image list exceeds `PMVS_MAX_IMAGES` (128) gets `PMVS_FAIL_OVERFLOW`.
-The reference has no such limit, so this outcome has no reference counterpart.
+// ---- §3 expansion call site: one CExpand::run (expand.cpp:17-72, whose expandSub at
+// expand.cpp:200-266 needs the organizer at depth >= 1) becomes one pmvs_expand_run
+static void to_pmvs(const Patch::CPatch& p, pmvs_patch& a) {
+  a = pmvs_patch{};
+  for (int k = 0; k < 4; ++k) { a.coord[k] = p._coord[k]; a.normal[k] = p._normal[k]; }
+  a.ncc = p._ncc;  a.dscale = p._dscale;  a.ascale = p._ascale;  a.tmp = p._tmp;
+  a.timages = p._timages;  a.flag = p._flag;  a.fix = p._fix;  a.dflag = p._dflag;
+  a.num_images = (int)std::min<size_t>(p._images.size(), PMVS_MAX_IMAGES);
+  for (int k = 0; k < a.num_images; ++k) {
+    a.images[k] = p._images[k];  a.grids[k][0] = p._grids[k][0];  a.grids[k][1] = p._grids[k][1];
+  }
+  a.num_vimages = (int)std::min<size_t>(p._vimages.size(), PMVS_MAX_IMAGES);
+  for (int k = 0; k < a.num_vimages; ++k) {
+    a.vimages[k] = p._vimages[k];  a.vgrids[k][0] = p._vgrids[k][0];  a.vgrids[k][1] = p._vgrids[k][1];
+  }
+}
 
-## 3. Expansion call site: one `CExpand::run` on the device
+static void from_pmvs(const pmvs_patch& a, Patch::CPatch& p) {
+  for (int k = 0; k < 4; ++k) { p._coord[k] = a.coord[k]; p._normal[k] = a.normal[k]; }
+  p._ncc = a.ncc;  p._dscale = a.dscale;  p._ascale = a.ascale;  p._tmp = a.tmp;
+  p._timages = a.timages;  p._flag = a.flag;  p._fix = (char)a.fix;  p._dflag = (unsigned char)a.dflag;
+  p._images.assign(a.images, a.images + a.num_images);
+  p._grids.clear();
+  for (int k = 0; k < a.num_images; ++k) p._grids.push_back(TVec2<int>(a.grids[k][0], a.grids[k][1]));
+  p._vimages.assign(a.vimages, a.vimages + a.num_vimages);
+  p._vgrids.clear();
+  for (int k = 0; k < a.num_vimages; ++k) p._vgrids.push_back(TVec2<int>(a.vgrids[k][0], a.vgrids[k][1]));
+}
 
-```cpp
 int expand_on_device(PMVS3::CFindMatch& fm, pmvs_scene* scene, bool after_seeds) {
   fm._pos.collectPatches();                    // the model = _ppatches (patchOrganizerS.cpp:228-248)
   const int n = (int)fm._pos._ppatches.size();
@@ -144,16 +140,8 @@ int expand_on_device(PMVS3::CFindMatch& fm, pmvs_scene* scene, bool after_seeds)
   }
   return 0;
 }
-```
 
-`to_pmvs` / `from_pmvs` copy the `CPatch` fields into and out of `pmvs_patch`; they are in the
-same file. `wave = 1, min_candidates = 0` gives the reference's single-thread schedule exactly.
-Any other wave size is deterministic but is a different valid schedule. DESIGN.md §4 describes it
-and §6 measures how far it moves the output.
-
-## 4. The whole loop (replaces findMatch.cpp:196-217 after the seed phase)
-
-```cpp
+// ---- §4 the whole loop (findMatch.cpp:196-217 after the seed phase)
 int run_loop_on_device(PMVS3::CFindMatch& fm, pmvs_scene* scene, std::vector<pmvs_patch>& model) {
   fm._pos.collectPatches();
   std::vector<pmvs_patch> seeds(fm._pos._ppatches.size());
@@ -169,32 +157,5 @@ int run_loop_on_device(PMVS3::CFindMatch& fm, pmvs_scene* scene, std::vector<pmv
   model.resize(n);
   return pmvs_loop_fetch(scene, model.data(), n) == PMVS_OK ? 0 : 1;
 }
-```
 
-The model is then written with `pmvs_write_patches` / `pmvs_write_pset` / `pmvs_write_ply`, or
-rebuilt into `fm._pos`.
-
-Multi-GPU:
-- `pmvs_scene_set_shard(scene, rank, world, allgather_fn, ctx)` before the call makes it
-  collective. Every rank passes the same seeds.
-- `allgather_fn` is any all-gather of host buffers: MPI, RCCL through a staging buffer, or the
-  library's `pmvs_thread_allgather` for several scenes in one process.
-
-## 5. Python / ctypes binding (what `cmvs-pmvs_amd/pmvs_amd.py` already does)
-
-```python
-import ctypes as C, numpy as np
-import pmvs_amd as P                      # record dtypes with the exact C layouts
-lib = P.load_library()                    # raises if libpmvs_amd.so is not built (no fallback)
-inp, params = P.synth_scene(8, 1920, 1080, level=1)
-scene = P.Scene(inp, device=0)            # pmvs_scene_create
-cands = P.synth_candidates(params, inp.projections, 100000)
-out, stats = scene.refine_batch(cands)    # pmvs_refine_batch -> numpy REFINED_DTYPE records
-```
-
-- The loop is `scene.run_loop(seeds, threshold, wave=32768, min_candidates=131072)`
-  (`pmvs_run_loop`).
-- `P.DistExchange().attach(scene)` shards it over torch.distributed ranks.
-- Device-resident batches (inputs already in HBM, e.g. torch tensors) use
-  `scene.refine_batch_device(d_in_ptr, n, d_out_ptr)` + `scene.sync()`. This is what `bench.py`
-  times.
+}  // namespace pmvs_integration

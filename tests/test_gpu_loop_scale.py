@@ -19,13 +19,13 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 PROD = dict(wave=32768, min_candidates=131072)
-# Schedule-gap tolerances: relative patch-count difference, cell-coverage Jaccard,
-# symmetric Chamfer distance in units of the mean patch dscale... see _gap().
-TOL_COUNT = 0.03
-TOL_JACCARD = 0.93
-TOL_CHAMFER_UNITS = 1.0
-TOL_NCC_MEAN = 0.01
-TOL_NCC_HIST_L1 = 0.06
+# Schedule-gap tolerances (DESIGN.md §6 records the measured values):
+TOL_COUNT = 0.04          # |patches_prod / patches_ref - 1|
+TOL_WITHIN1 = 0.99        # covered target cells lying within one cell of the other run's coverage
+TOL_COVERAGE = 0.04       # max over target images of the relative difference in covered cells
+TOL_CHAMFER_UNITS = 1.0   # symmetric Chamfer distance / mean patch dscale
+TOL_NCC_MEAN = 0.01       # |mean ncc difference|
+TOL_NCC_HIST_L1 = 0.06    # L1 distance of the 20-bin ncc histograms
 
 
 def _threads():
@@ -70,12 +70,33 @@ def test_loop_50_views_matches_oracle(gpu_available, oracle_mod):
     assert out_g.tobytes() == out_o.tobytes() or _same_patches(out_g, out_o)
 
 
-def _cells(inp, model, csize=2):
-    """Occupied (reference image, cell) pairs: images[0] and grids[0] of every patch."""
-    t = model["images"][:, 0].astype(np.int64)
-    gx = model["grids"][:, 0, 0].astype(np.int64)
-    gy = model["grids"][:, 0, 1].astype(np.int64)
+def _cells(inp, model):
+    """Covered target cells: every (target image, cell) some patch is registered in -- the
+    CPatchOrganizerS::_pgrids entries the expansion tries to fill (patchOrganizerS.cpp:308-330)."""
+    ni = model["num_images"]
+    k = np.arange(model["images"].shape[1])[None, :]
+    sel = (k < ni[:, None]) & (model["images"] < inp.num_targets)
+    t = model["images"][sel].astype(np.int64)
+    gx = model["grids"][..., 0][sel].astype(np.int64)
+    gy = model["grids"][..., 1][sel].astype(np.int64)
     return set(((t << 40) | (gy << 20) | gx).tolist())
+
+
+def _dilate(cells):
+    """The cell set grown by one cell in x and y (keys as in _cells)."""
+    out = set()
+    for c in cells:
+        for dy in (-1, 0, 1):
+            for dx in (-1, 0, 1):
+                out.add(c + (dy << 20) + dx)
+    return out
+
+
+def _per_image_coverage(inp, cells):
+    cov = np.zeros(inp.num_targets, np.int64)
+    for c in cells:
+        cov[c >> 40] += 1
+    return cov
 
 
 def _chamfer(a, b):
@@ -92,10 +113,16 @@ def _gap(inp, ref, prod):
     h = np.linspace(0.0, 1.0, 21)
     hr = np.histogram(ref["ncc"], h)[0] / len(ref)
     hp = np.histogram(prod["ncc"], h)[0] / len(prod)
+    dr, dp = _dilate(cr), _dilate(cp)
+    covr, covp = _per_image_coverage(inp, cr), _per_image_coverage(inp, cp)
     return {
         "patches_ref": len(ref), "patches_prod": len(prod),
         "count_rel": abs(len(prod) / len(ref) - 1.0),
+        "cells_ref": len(cr), "cells_prod": len(cp),
         "cell_jaccard": len(cr & cp) / len(cr | cp),
+        # each covered cell of one run lies within one cell of a covered cell of the other
+        "cell_within1": min(len(cp & dr) / len(cp), len(cr & dp) / len(cr)),
+        "coverage_rel_max": float(np.max(np.abs(covp - covr) / np.maximum(covr, 1))),
         "chamfer_units": _chamfer(ref["coord"][:, :3], prod["coord"][:, :3]) / unit,
         "ncc_mean_diff": abs(float(np.mean(prod["ncc"])) - float(np.mean(ref["ncc"]))),
         "ncc_hist_l1": float(np.abs(hr - hp).sum()),
@@ -119,7 +146,8 @@ def test_schedule_gap_vs_single_thread(gpu_available, views, w, h, nseeds):
     gap = _gap(inp, ref, prod)
     print(f"schedule gap {views}v {w}x{h}: {gap}")
     assert gap["count_rel"] <= TOL_COUNT, gap
-    assert gap["cell_jaccard"] >= TOL_JACCARD, gap
+    assert gap["cell_within1"] >= TOL_WITHIN1, gap
+    assert gap["coverage_rel_max"] <= TOL_COVERAGE, gap
     assert gap["chamfer_units"] <= TOL_CHAMFER_UNITS, gap
     assert gap["ncc_mean_diff"] <= TOL_NCC_MEAN, gap
     assert gap["ncc_hist_l1"] <= TOL_NCC_HIST_L1, gap
