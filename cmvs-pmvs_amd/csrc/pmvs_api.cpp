@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/pmvs_amd.h"
+#include "pmvs_features.h"
 #include "pmvs_launch.h"
 
 using namespace pmvsdev;
@@ -195,6 +196,7 @@ struct pmvs_scene {
   int xkept = -1, lkept = -1;   // models kept on the device for pmvs_expand_fetch / pmvs_loop_fetch
   std::vector<int> xalive;
   DBuf<pmvs_patch> fpatches2;   // compaction target of pmvs_run_loop
+  FeatBuffers feat;             // feature-detection scratch (pmvs_detect_features)
   // staging for host-pointer calls
   DBuf<pmvs_candidate> cand;
   DBuf<pmvs_refined> res;
@@ -466,6 +468,99 @@ pmvs_status pmvs_scene_get_level(pmvs_scene* sc, int32_t view, int32_t level, ui
   if (e == hipSuccess) e = hipStreamSynchronize(sc->stream);
   (void)hipFree(tmp);
   if (e != hipSuccess) return fail(PMVS_EDEVICE, "get_level: %s", hipGetErrorString(e));
+  return PMVS_OK;
+}
+
+// ---- feature detection (CDetectFeatures::run, detectFeatures.cpp:47-124)
+namespace {
+
+// CDetector::setGaussI (detector.cpp:29-49): float weights, exp() of a float argument evaluated
+// by the double C exp (unqualified exp(float) in that TU; probed), float normalisation.
+FeatFilter gauss_i(float sigma) {
+  FeatFilter f{};
+  const int m = (int)std::ceil((double)(2 * sigma));
+  f.n = 2 * m + 1;
+  float denom = 0.0f;
+  for (int x = 0; x < f.n; ++x) {
+    const int xt = x - m;
+    const float arg = (float)(-(xt * xt)) / (2 * sigma * sigma);
+    const float d = (float)std::exp((double)arg);
+    f.w[x] = d;
+    denom += d;
+  }
+  for (int x = 0; x < f.n; ++x) f.w[x] /= denom;
+  return f;
+}
+
+// The result multisets of one detector (harris.cpp:251-261 / dog.cpp:192-202) read from the
+// largest element (detectFeatures.cpp:84-88, 103-107): blocks are inserted in raster order, each
+// block's points in ascending order, so equal responses come out in reverse insertion order.
+void order_points(const FeatPoint* pts, const int* cnt, int nb, int type, std::vector<pmvs_point>& out) {
+  struct Item { float r; int64_t seq; float x, y; };
+  std::vector<Item> v;
+  int64_t seq = 0;
+  for (int b = 0; b < nb; ++b)
+    for (int k = 0; k < cnt[b]; ++k) {
+      const FeatPoint& p = pts[4 * b + k];
+      v.push_back({p.response, seq++, p.x, p.y});
+    }
+  std::sort(v.begin(), v.end(), [](const Item& a, const Item& b) {
+    if (a.r != b.r) return a.r > b.r;
+    return a.seq > b.seq;
+  });
+  for (const Item& it : v) out.push_back(pmvs_point{it.x, it.y, it.r, type});
+}
+
+}  // namespace
+
+pmvs_status pmvs_detect_features(pmvs_scene* sc, int32_t view, int32_t fcsize, pmvs_point* out, int32_t cap,
+                                 int32_t* n_out) {
+  if (!sc || !n_out || (cap > 0 && !out)) return fail(PMVS_EINVAL, "null argument");
+  if (view < 0 || view >= sc->ds.num) return fail(PMVS_EINVAL, "view %d", view);
+  if (fcsize < 1) return fail(PMVS_EINVAL, "fcsize %d", fcsize);
+  HIPCHK(hipSetDevice(sc->device));
+  const int level = sc->ds.level;
+  const DView& v = sc->hviews[view];
+  FeatJob j{};
+  j.W = v.w[level];
+  j.H = v.h[level];
+  j.pyr = sc->pyr.p + v.pyr_off[level];
+  j.mask = v.mask_off[level] >= 0 ? sc->masks.p + v.mask_off[level] : nullptr;
+  j.edge = v.edge_off[level] >= 0 ? sc->edges.p + v.edge_off[level] : nullptr;
+  // CHarris::run: gridsize = gspeedup * 2 (harris.cpp:216-221), gspeedup = fcsize (16 in findMatch.cpp:81)
+  j.gsize = fcsize * 2;
+  j.bw = (j.W + j.gsize - 1) / j.gsize;
+  j.bh = (j.H + j.gsize - 1) / j.gsize;
+  const float sigma = 4.0f;  // detectFeatures.cpp:73
+  j.harris_margin = ((2 * (int)std::ceil((double)(2 * sigma)) + 1)) / 2;  // (int)_gaussD.size() / 2
+  j.dfilter.n = 3;
+  j.dfilter.w[0] = -0.5f; j.dfilter.w[1] = 0.0f; j.dfilter.w[2] = 0.5f;  // harris.cpp:151
+  j.ifilter.n = 3;
+  j.ifilter.w[0] = j.ifilter.w[1] = j.ifilter.w[2] = (float)(1.0 / 3.0);  // harris.cpp:153
+  j.gaussI = gauss_i(sigma);
+  // CDifferenceOfGaussians::run (dog.cpp:130-160), firstScale 1, lastScale 3 (detectFeatures.cpp:75-76)
+  const float first = 1.0f, last = 3.0f;
+  const float step = (float)std::pow(2.0, 0.5);  // pow(2.0f, 1 / 2.0f): the double C pow
+  const int steps = std::max(4, (int)std::ceil(std::log((double)(last / first)) / std::log((double)step)));
+  if (steps != 4) return fail(PMVS_EUNSUPPORTED, "DoG with %d steps", steps);
+  const float scales[5] = {first, first * step, first * step * step, (float)(first * std::pow((double)step, 3.0)),
+                           (float)(first * std::pow((double)step, 4.0))};
+  for (int k = 0; k < 5; ++k) j.dog_gauss[k] = gauss_i(scales[k]);
+  for (int k = 0; k < 2; ++k) j.dog_margin[k] = (int)std::ceil((double)(2 * scales[3 + k]));
+  for (const FeatFilter* f : {&j.gaussI, &j.dog_gauss[4]})
+    if (f->n > 32) return fail(PMVS_EUNSUPPORTED, "filter with %d taps", f->n);
+  HIPCHK(detect_features(j, sc->feat, sc->stream));
+  const int nb = j.bw * j.bh;
+  std::vector<FeatPoint> pts((size_t)nb * 8);
+  std::vector<int> cnt((size_t)nb * 2);
+  HIPCHK(hipMemcpyAsync(pts.data(), sc->feat.pts, pts.size() * sizeof(FeatPoint), hipMemcpyDeviceToHost, sc->stream));
+  HIPCHK(hipMemcpyAsync(cnt.data(), sc->feat.cnt, cnt.size() * sizeof(int), hipMemcpyDeviceToHost, sc->stream));
+  HIPCHK(hipStreamSynchronize(sc->stream));
+  std::vector<pmvs_point> all;
+  order_points(pts.data(), cnt.data(), nb, 0, all);
+  order_points(pts.data() + 4 * (size_t)nb, cnt.data() + nb, nb, 1, all);
+  *n_out = (int32_t)all.size();
+  if (out) std::memcpy(out, all.data(), std::min<size_t>(all.size(), (size_t)std::max(cap, 0)) * sizeof(pmvs_point));
   return PMVS_OK;
 }
 

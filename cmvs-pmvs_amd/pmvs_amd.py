@@ -38,6 +38,7 @@ PATCH_DTYPE = np.dtype(
      ("tmp", "<f4"), ("timages", "<i4"), ("flag", "<i4"), ("fix", "<i4"), ("num_images", "<i4"),
      ("num_vimages", "<i4"), ("dflag", "<i4"), ("images", "<i4", MAX_IMAGES), ("grids", "<i4", (MAX_IMAGES, 2)),
      ("vimages", "<i4", MAX_IMAGES), ("vgrids", "<i4", (MAX_IMAGES, 2))], align=True)
+POINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("response", "<f4"), ("type", "<i4")])  # pmvs_point
 TEX_QUERY_DTYPE = np.dtype(
     [("coord", "<f4", 4), ("pxaxis", "<f4", 4), ("pyaxis", "<f4", 4), ("normal", "<f4", 4),
      ("view", "<i4"), ("normalize", "<i4")], align=True)
@@ -119,7 +120,7 @@ EXPORTS = ["pmvs_last_error", "pmvs_device_count", "pmvs_scene_create", "pmvs_sc
            "pmvs_ppm_load", "pmvs_options_load", "pmvs_options_free", "pmvs_write_patches", "pmvs_write_pset",
            "pmvs_write_ply", "pmvs_patch_colors", "pmvs_filter_run",
            "pmvs_expand_run", "pmvs_expand_fetch", "pmvs_run_loop", "pmvs_loop_fetch", "pmvs_scene_set_shard", "pmvs_thread_exchange_create",
-           "pmvs_thread_exchange_ctx", "pmvs_thread_allgather", "pmvs_thread_exchange_destroy"]
+           "pmvs_thread_exchange_ctx", "pmvs_thread_allgather", "pmvs_thread_exchange_destroy", "pmvs_detect_features"]
 
 # int fn(void* ctx, const void* send, int64_t bytes, void* recv): all-gather (pmvs_allgather_fn)
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p)
@@ -144,6 +145,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.pmvs_scene_get_level.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p,
                                          C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     lib.pmvs_grab_tex.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+    lib.pmvs_detect_features.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
+                                         C.POINTER(C.c_int32)]
     lib.pmvs_incc_eval.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(Stats)]
     lib.pmvs_refine_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(Stats)]
     lib.pmvs_refine_batch_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
@@ -321,6 +324,15 @@ class Scene:
         _check(self.lib.pmvs_scene_get_level(self.handle, view, level, None, C.byref(w), C.byref(h)))
         out = np.empty((h.value, w.value, 3), np.uint8)
         _check(self.lib.pmvs_scene_get_level(self.handle, view, level, _ptr(out), C.byref(w), C.byref(h)))
+        return out
+
+    def detect_features(self, view: int, fcsize: int = 16) -> np.ndarray:
+        """CDetectFeatures::run for one view on the device (pmvs_detect_features): POINT_DTYPE
+        records, Harris then DoG, each by decreasing response (the reference's order)."""
+        n = C.c_int32(0)
+        _check(self.lib.pmvs_detect_features(self.handle, view, fcsize, None, 0, C.byref(n)))
+        out = np.zeros(n.value, POINT_DTYPE)
+        _check(self.lib.pmvs_detect_features(self.handle, view, fcsize, _ptr(out), n.value, C.byref(n)))
         return out
 
     def grab_tex(self, q: np.ndarray):

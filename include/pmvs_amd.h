@@ -164,6 +164,23 @@ pmvs_status pmvs_set_thresholds(pmvs_scene* scene, float ncc, float ncc_before, 
 pmvs_status pmvs_scene_get_level(pmvs_scene* scene, int32_t view, int32_t level, uint8_t* out,
                                  int32_t* width, int32_t* height);
 
+/* A feature point (PMVS3::CPoint, point.hpp): image coordinates at the option level, detector
+ * response, type 0 = Harris, 1 = DoG. */
+typedef struct pmvs_point {
+  float x, y, response;
+  int32_t type;
+} pmvs_point;
+
+/* PMVS3::CDetectFeatures::run for one view (detectFeatures.cpp:47-124; the caller is
+ * CFindMatch::init, findMatch.cpp:79-82 with fcsize 16): CHarris (sigma 4) then
+ * CDifferenceOfGaussians (scales 1..3) on the view's pyramid at the scene level with its mask and
+ * edge images, at most 4 points per 2*fcsize block, computed on the device.  Points come in the
+ * reference's order: Harris points by decreasing response, then DoG points by decreasing response
+ * (each detector's std::multiset read from its end).  *n_out = the number of points; at most cap
+ * are written (call with cap = 0 to size the array). */
+pmvs_status pmvs_detect_features(pmvs_scene* scene, int32_t view, int32_t fcsize, pmvs_point* out, int32_t cap,
+                                 int32_t* n_out);
+
 /* Batched COptim::grabTex + normalize: out_tex is n * 3*wsize*wsize floats, out_valid n ints
  * (1 = texture grabbed, 0 = grabTex returned 1 / empty texture). */
 pmvs_status pmvs_grab_tex(pmvs_scene* scene, const pmvs_tex_query* q, int32_t n, float* out_tex,

@@ -73,9 +73,30 @@ def ref_lib():
         R.ref_ortho.argtypes = [C.c_void_p, C.c_void_p]
         R.ref_get_color.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         R.ref_expand_dirs.argtypes = [C.c_void_p] * 3 + [C.c_int, C.c_void_p]
+        R.ref_detect_features.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                          C.c_int]
         R.ref_camera_depth.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p]
         _ref = R
     return _ref
+
+
+def ref_detect_features(rgb, mask=None, edge=None, fcsize=16):
+    """The reference's own CHarris + CDifferenceOfGaussians (oracle/_ref) on an RGB8 image:
+    float32 [n, 4] = (x, y, response, type) in detectFeatures.cpp order; None if _ref is absent."""
+    R = ref_lib()
+    if R is None:
+        return None
+    rgb = np.ascontiguousarray(rgb, np.uint8)
+    h, w = rgb.shape[:2]
+    m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+    e = None if edge is None else np.ascontiguousarray(edge, np.uint8)
+    cap = 1 << 16
+    while True:
+        out = np.zeros((cap, 4), np.float32)
+        n = R.ref_detect_features(_p(rgb), _p(m), _p(e), w, h, fcsize, _p(out), cap)
+        if n <= cap:
+            return out[:n]
+        cap = n
 
 
 def _p(a):

@@ -6,6 +6,7 @@
 //                                             optical centre/axis, camera axes)
 //   /root/reference/source/pmvs/option.cpp   (SOption: pmvs2 option-file parsing, vis.dat)
 //   /root/reference/source/pmvs/patch.cpp    (CPatch text serialisation, operator<< / >>)
+//   /root/reference/source/pmvs/{harris,dog,detector,point}.cpp  (the feature detectors)
 // plus the header-only numeric library (include/numeric/*.hpp) and the inline
 // CCamera::project (include/image/camera.hpp:89-108).  The resulting oracle/_ref/libpmvs_ref.so
 // pins the oracle restatement and the product's host plumbing bit-for-bit on those pieces.
@@ -24,8 +25,12 @@
 #include <new>
 #include <vector>
 
+#include <set>
+
 #include "image/camera.hpp"
 #include "image/image.hpp"
+#include "pmvs/dog.hpp"
+#include "pmvs/harris.hpp"
 #include "pmvs/option.hpp"
 #include "pmvs/patch.hpp"
 
@@ -224,6 +229,39 @@ void ref_expand_dirs(const float* coord4, const float* normal4, const float* rad
       for (int k = 0; k < 4; ++k) out[24 * q + 4 * i + k] = canCoord[k];
     }
   }
+}
+
+// The two detectors of CDetectFeatures::runThread (detectFeatures.cpp:77-108) -- the
+// reference's own CHarris::run (sigma 4) and CDifferenceOfGaussians::run (scales 1, 3) from
+// harris.cpp / dog.cpp / detector.cpp / point.cpp, compiled unmodified -- on one RGB8 image with
+// optional mask / edge bytes, each result multiset read from its end as detectFeatures.cpp does.
+// out: 4 floats per point (x, y, response, type); returns the point count (<= cap written).
+int ref_detect_features(const unsigned char* rgb, const unsigned char* mask, const unsigned char* edge, int w, int h,
+                        int fcsize, float* out, int cap) {
+  const std::vector<unsigned char> image(rgb, rgb + (size_t)3 * w * h);
+  std::vector<unsigned char> m, e;
+  if (mask) m.assign(mask, mask + (size_t)w * h);
+  if (edge) e.assign(edge, edge + (size_t)w * h);
+  std::vector<PMVS3::CPoint> pts;
+  {
+    PMVS3::CHarris harris;
+    std::multiset<PMVS3::CPoint> result;
+    harris.run(image, m, e, w, h, fcsize, 4.0f, result);
+    for (auto it = result.rbegin(); it != result.rend(); ++it) pts.push_back(*it);
+  }
+  {
+    PMVS3::CDifferenceOfGaussians dog;
+    std::multiset<PMVS3::CPoint> result;
+    dog.run(image, m, e, w, h, fcsize, 1.0f, 3.0f, result);
+    for (auto it = result.rbegin(); it != result.rend(); ++it) pts.push_back(*it);
+  }
+  for (int i = 0; i < (int)pts.size() && i < cap; ++i) {
+    out[4 * i] = pts[i]._icoord[0];
+    out[4 * i + 1] = pts[i]._icoord[1];
+    out[4 * i + 2] = pts[i]._response;
+    out[4 * i + 3] = (float)pts[i]._type;
+  }
+  return (int)pts.size();
 }
 
 // Header-only numeric library: ortho (vec4.hpp:303-322) used by CExpand::findEmptyBlocks.

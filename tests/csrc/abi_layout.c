@@ -33,6 +33,7 @@ int main(void) {
   S(pmvs_loop_iter); O(pmvs_loop_iter, patches); O(pmvs_loop_iter, expand); O(pmvs_loop_iter, filter);
   S(pmvs_options); O(pmvs_options, threshold); O(pmvs_options, num_timages); O(pmvs_options, timages);
   O(pmvs_options, visdata2);
+  S(pmvs_point); O(pmvs_point, response); O(pmvs_point, type);
   S(pmvs_synth_params); O(pmvs_synth_params, seed); O(pmvs_synth_params, arc_step_deg);
   return 0;
 }

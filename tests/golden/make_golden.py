@@ -8,7 +8,8 @@ renderer regenerates them bit-for-bit).  Expected outputs come from two sources:
     CImage::getColor / isSafe): per-view camera centre / optical axis / axes / per-level
     projection, CCamera::project and computeDepth of sample points, and bilinear getColor
     samples on every pyramid level; the candidate centres of CExpand::findEmptyBlocks
-    (expand.cpp:176-177 evaluated with the reference headers, expand_dirs.npz) -- these
+    (expand.cpp:176-177 evaluated with the reference headers, expand_dirs.npz); the Harris and
+    DoG feature points of every golden view (harris.cpp / dog.cpp, features.npz) -- these
     vectors are REFERENCE outputs;
   * oracle/liboracle.so (the CPU restatement, pinned on the pieces above): pyramid CRCs,
     grabTex textures, my_f values and full preProcess->refinePatch->postProcess records.
@@ -133,6 +134,26 @@ def make_expand_dirs():
     print(f"{path}: {os.path.getsize(path)} B")
 
 
+def make_features():
+    """CDetectFeatures' two detectors (harris.cpp / dog.cpp compiled unmodified in oracle/_ref) on
+    every view of the scene goldens at their option level: REFERENCE outputs (features.npz)."""
+    g = {}
+    for name, (views, width, height, level, csize, *_rest) in SCENES.items():
+        inp, p = P.synth_scene(views, width, height, level=level, csize=csize, supersample=2)
+        o = O.OracleScene(inp)
+        pts, off = [], [0]
+        for v in range(views):
+            f = O.ref_detect_features(o.get_level(v, level), fcsize=16)
+            pts.append(f)
+            off.append(off[-1] + len(f))
+        o.close()
+        g[f"{name}_points"] = np.concatenate(pts).astype(np.float32)
+        g[f"{name}_offsets"] = np.array(off, np.int64)
+    path = os.path.join(HERE, "features.npz")
+    np.savez_compressed(path, **g)
+    print(f"{path}: {os.path.getsize(path)} B, " + ", ".join(f"{k} {len(v)}" for k, v in g.items() if k.endswith("points")))
+
+
 def make(name, views, width, height, level, csize, ntex, neval, nref):
     inp, p = P.synth_scene(views, width, height, level=level, csize=csize, supersample=2)
     o = O.OracleScene(inp)
@@ -177,5 +198,6 @@ def make(name, views, width, height, level, csize, ntex, neval, nref):
 if __name__ == "__main__":
     O.build()
     make_expand_dirs()
+    make_features()
     for k, v in SCENES.items():
         make(k, *v)

@@ -48,7 +48,7 @@ def test_python_mirror_layout_matches_c(tmp_path):
     import pmvs_amd as P
     np_types = {"pmvs_candidate": P.CANDIDATE_DTYPE, "pmvs_refined": P.REFINED_DTYPE,
                 "pmvs_eval_query": P.EVAL_QUERY_DTYPE, "pmvs_tex_query": P.TEX_QUERY_DTYPE,
-                "pmvs_patch": P.PATCH_DTYPE}
+                "pmvs_patch": P.PATCH_DTYPE, "pmvs_point": P.POINT_DTYPE}
     for name, dt in np_types.items():
         assert dt.itemsize == c[name + ".sizeof"], name
         for f in dt.names:
