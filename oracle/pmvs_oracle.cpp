@@ -855,6 +855,7 @@ static void init_ctx(const OScene& s, OCtx& c) {
 
 #include "filter_oracle.h"
 #include "expand_oracle.h"
+#include "seed_oracle.h"
 
 using namespace oracle;
 
@@ -1208,6 +1209,97 @@ int oracle_expand_run(void* h, const pmvs_patch* patches, const int* alive, int 
                         st.waves, st.wave_ns};
   for (int k = 0; k < 9; ++k) stats[k] = v[k];
   return (int)P.size();
+}
+
+
+// ---- seed phase (seed_oracle.h)
+static std::vector<std::vector<SeedPoint>> split_points(const OScene& s, const pmvs_point* pts, const int* npts) {
+  std::vector<std::vector<SeedPoint>> v(s.num);
+  size_t k = 0;
+  for (int i = 0; i < s.num; ++i)
+    for (int q = 0; q < npts[i]; ++q, ++k) v[i].push_back({pts[k].x, pts[k].y, pts[k].response, pts[k].type});
+  return v;
+}
+
+// CSeed::run (CPU 1) from the feature points of every view (pts: npts[0] points of view 0, then
+// view 1, ...).  Writes the seed patches in addPatch order; returns their number, or -1 when cap
+// is too small.  stats: trial, pass, fail0 (preProcess), fail1 (postProcess).
+int oracle_seed_run(void* h, const pmvs_point* pts, const int* npts, pmvs_patch* out, int cap, int64_t* stats) {
+  const OScene& s = *static_cast<const OScene*>(h);
+  std::vector<pmvs_patch> seeds;
+  int64_t st[4];
+  seed_run(s, split_points(s, pts, npts), seeds, st);
+  for (int k = 0; k < 4; ++k) stats[k] = st[k];
+  if ((int)seeds.size() > cap) return -1;
+  std::memcpy(out, seeds.data(), seeds.size() * sizeof(pmvs_patch));
+  return (int)seeds.size();
+}
+
+// Diagnostics for the parity tests: collectImages of every view (tau entries max, -1 padded),
+// the seed job order, and the sorted candidate list of one feature point against the empty
+// model (view, point, cell, coord[4], response per entry; returns the count, -1 if cap is short).
+void oracle_seed_images(void* h, int* out_images, int* out_order) {
+  const OScene& s = *static_cast<const OScene*>(h);
+  std::vector<std::vector<float>> dist;
+  set_distances(s, dist);
+  std::vector<int> idx;
+  for (int i = 0; i < s.num; ++i) {
+    collect_images(s, dist, i, idx);
+    for (int k = 0; k < s.tau; ++k) out_images[i * s.tau + k] = k < (int)idx.size() ? idx[k] : -1;
+  }
+  const std::vector<int> order = seed_order(s.tnum);
+  for (int i = 0; i < s.tnum; ++i) out_order[i] = order[i];
+}
+
+int oracle_seed_candidates(void* h, const pmvs_point* pts, const int* npts, int index, int point, int* out_int,
+                           float* out_f, int cap) {
+  const OScene& s = *static_cast<const OScene*>(h);
+  SeedState st(s);
+  st.pts = split_points(s, pts, npts);
+  st.cells.resize(s.num);
+  for (int i = 0; i < s.num; ++i) {
+    st.cells[i].assign((size_t)s.gwidths[i] * s.gheights[i], std::vector<int>());
+    for (int q = 0; q < (int)st.pts[i].size(); ++q) {
+      const int ix = ((int)std::floor(st.pts[i][q].x + 0.5f)) / s.csize;
+      const int iy = ((int)std::floor(st.pts[i][q].y + 0.5f)) / s.csize;
+      st.cells[i][iy * s.gwidths[i] + ix].push_back(q);
+    }
+  }
+  st.counts.resize(s.tnum);
+  st.occupied.resize(s.tnum);
+  for (int t = 0; t < s.tnum; ++t) {
+    st.counts[t].assign((size_t)s.gwidths[t] * s.gheights[t], 0);
+    st.occupied[t].assign((size_t)s.gwidths[t] * s.gheights[t], 0);
+  }
+  set_distances(s, st.dist);
+  std::vector<int> idx;
+  collect_images(s, st.dist, index, idx);
+  std::vector<SeedCand> vcp;
+  collect_candidates(st, index, idx, st.pts[index][point], vcp);
+  if ((int)vcp.size() > cap) return -1;
+  for (size_t k = 0; k < vcp.size(); ++k) {
+    out_int[3 * k] = vcp[k].view; out_int[3 * k + 1] = vcp[k].point; out_int[3 * k + 2] = vcp[k].cell;
+    for (int c = 0; c < 4; ++c) out_f[5 * k + c] = vcp[k].coord[c];
+    out_f[5 * k + 4] = vcp[k].response;
+  }
+  return (int)vcp.size();
+}
+
+// Image::setF / computeEPD / CSeed::unproject on explicit inputs (pinned against the reference
+// headers by tests/test_seed_pinning.py).
+void oracle_seed_geometry(void* h, int i0, int i1, const float* xy0, const float* xy1, int n, double* F9, float* epd,
+                          float* coords4) {
+  const OScene& s = *static_cast<const OScene*>(h);
+  double F[3][3];
+  set_f(s, i0, i1, F);
+  for (int i = 0; i < 9; ++i) F9[i] = F[i / 3][i % 3];
+  for (int k = 0; k < n; ++k) {
+    const double p0[3] = {xy0[2 * k], xy0[2 * k + 1], 1.0}, p1[3] = {xy1[2 * k], xy1[2 * k + 1], 1.0};
+    epd[k] = compute_epd(F, p0, p1);
+    const SeedPoint a{xy0[2 * k], xy0[2 * k + 1], 0.0f, 0}, b{xy1[2 * k], xy1[2 * k + 1], 0.0f, 0};
+    const V4 c = unproject(s, i0, i1, a, b);
+    for (int j = 0; j < 4; ++j) coords4[4 * k + j] = c[j];
+  }
 }
 
 }  // extern "C"
