@@ -197,6 +197,10 @@ struct pmvs_scene {
   std::vector<int> xalive;
   DBuf<pmvs_patch> fpatches2;   // compaction target of pmvs_run_loop
   FeatBuffers feat;             // feature-detection scratch (pmvs_detect_features)
+  // host copies the seed phase's control logic reads (canAdd masks, collectImages inputs)
+  std::vector<std::vector<uint8_t>> hmask_level;  // per view, the binary mask at the scene level (empty = none)
+  std::vector<int> hvis_off, hvis;
+  int sequence = -1;
   // staging for host-pointer calls
   DBuf<pmvs_candidate> cand;
   DBuf<pmvs_refined> res;
@@ -352,6 +356,7 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
       for (size_t k = 0; k < pyr[0].size(); ++k)
         pyr[0][k] = isMask ? ((127 < (int)m0[k]) ? 255 : 0) : ((1 < m0[k]) ? 255 : 0);  // image.cpp:159-180
       build_binary(pyr, v.w, v.h, maxLevel);
+      if (isMask) sc->hmask_level[i] = pyr[d->level];
       for (int l = 0; l < maxLevel; ++l) {
         (isMask ? v.mask_off[l] : v.edge_off[l]) = (long long)all.size();
         all.insert(all.end(), pyr[l].begin(), pyr[l].end());
@@ -362,6 +367,7 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
       return fail(PMVS_EDEVICE, "mask/edge copy");
     return PMVS_OK;
   };
+  sc->hmask_level.assign(num, std::vector<uint8_t>());
   pmvs_status st = upload_binary(anyMask, true, sc->masks);
   if (st == PMVS_OK) st = upload_binary(anyEdge, false, sc->edges);
   if (st != PMVS_OK) return bail(st);
@@ -369,6 +375,9 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
   // ---- tables
   std::vector<int> voff(d->visdata2_offsets, d->visdata2_offsets + num + 1);
   const int nvis = voff[num];
+  sc->hvis_off = voff;
+  sc->hvis.assign(d->visdata2, d->visdata2 + nvis);
+  sc->sequence = d->sequence;
   for (int k = 0; k < nvis; ++k)
     if (d->visdata2[k] < 0 || d->visdata2[k] >= num) return bail(fail(PMVS_EINVAL, "visdata2[%d] = %d", k, d->visdata2[k]));
   for (int k = 0; k < d->num_bindexes; ++k)
@@ -561,6 +570,57 @@ pmvs_status pmvs_detect_features(pmvs_scene* sc, int32_t view, int32_t fcsize, p
   order_points(pts.data() + 4 * (size_t)nb, cnt.data() + nb, nb, 1, all);
   *n_out = (int32_t)all.size();
   if (out) std::memcpy(out, all.data(), std::min<size_t>(all.size(), (size_t)std::max(cap, 0)) * sizeof(pmvs_point));
+  return PMVS_OK;
+}
+
+pmvs_status pmvs_seed_run(pmvs_scene* sc, const pmvs_point* points, const int32_t* num_points, int32_t batch,
+                          pmvs_patch* out, int32_t cap, int32_t* n_out, pmvs_seed_stats* stats) {
+  if (!sc || !num_points || !n_out || cap < 0 || (cap > 0 && !out)) return fail(PMVS_EINVAL, "null argument");
+  if (sc->ds.depth != 0) return fail(PMVS_EINVAL, "the seed phase runs at depth 0 (scene depth %d)", sc->ds.depth);
+  long long np = 0;
+  for (int i = 0; i < sc->ds.num; ++i) {
+    if (num_points[i] < 0) return fail(PMVS_EINVAL, "num_points[%d] = %d", i, num_points[i]);
+    np += num_points[i];
+  }
+  if (np > 0 && !points) return fail(PMVS_EINVAL, "null points");
+  for (long long k = 0; k < np; ++k)
+    if (!(points[k].x >= 0.0f && points[k].y >= 0.0f)) return fail(PMVS_EINVAL, "point %lld outside the image", k);
+  *n_out = 0;
+  if (stats) std::memset(stats, 0, sizeof(*stats));
+  HIPCHK(hipSetDevice(sc->device));
+  SeedInput in;
+  in.points = points;
+  in.npts = num_points;
+  in.vis_off = sc->hvis_off.data();
+  in.vis = sc->hvis.data();
+  in.sequence = sc->sequence;
+  in.angle0 = (float)(60.0f * M_PI / 180.0f);  // findMatch.cpp:92
+  for (int i = 0; i < sc->ds.num; ++i) in.mask_level.push_back(sc->hmask_level[i].empty() ? nullptr : sc->hmask_level[i].data());
+  in.batch = batch > 0 ? batch : 16384;
+  in.per_cell = 4;
+  if (const char* e = getenv("PMVS_SEED_PER_CELL")) in.per_cell = std::max(1, atoi(e));
+  HIPCHK(hipMemsetAsync(sc->stats.p, 0, sizeof(DevStats), sc->stream));
+  RefineFn refine = [&](const pmvs_candidate* d_in, int m, pmvs_refined* d_out) -> hipError_t {
+    if (ensure(sc->jobs, m)) return hipErrorOutOfMemory;
+    hipError_t e = hipMemsetAsync(&sc->stats.p->queue, 0, 3 * sizeof(unsigned long long), sc->stream);
+    if (e != hipSuccess) return e;
+    return launch_refine(sc->ds, d_in, sc->jobs.p, d_out, m, sc->stats.p, sc->grid, sc->refine_grid, sc->tslots,
+                         sc->stream, sc->kev);
+  };
+  SeedOutput so;
+  const hipError_t e = seed_pass(sc->ds, sc->hviews, in, sc->stream, refine, so);
+  if (e == hipErrorOutOfMemory) return fail(PMVS_ENOMEM, "seed phase: device memory");
+  HIPCHK(e);
+  sc->last_refine = false;
+  const int ns = (int)so.seeds.size();
+  *n_out = ns;
+  if (stats) {
+    stats->trial = so.stats[0]; stats->pass = so.stats[1]; stats->fail0 = so.stats[2]; stats->fail1 = so.stats[3];
+    stats->refined = so.stats[4]; stats->rounds = so.stats[5]; stats->candidates = so.stats[6];
+    stats->wall_ms = so.wall_ms; stats->gen_ms = so.gen_ms; stats->refine_ms = so.refine_ms;
+  }
+  if (ns > cap) return fail(PMVS_EINVAL, "seed phase: %d seeds, capacity %d", ns, cap);
+  if (ns) std::memcpy(out, so.seeds.data(), (size_t)ns * sizeof(pmvs_patch));
   return PMVS_OK;
 }
 

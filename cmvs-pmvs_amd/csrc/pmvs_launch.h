@@ -83,4 +83,23 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
 hipError_t compact_model(FilterBuffers& B, const pmvs_patch* src, int n, const int* keep, pmvs_patch* dst, int* nkept,
                          hipStream_t st);
 hipError_t fill_int(int* a, int n, int v, hipStream_t st);
+
+// ---- seed phase (pmvs_seed.hip)
+struct SeedInput {
+  const pmvs_point* points;  // every view's feature points, view 0 first
+  const int* npts;           // per view
+  const int* vis_off;        // visdata2 CSR (host)
+  const int* vis;
+  int sequence;
+  float angle0;              // _angleThreshold0
+  std::vector<const uint8_t*> mask_level;  // per view: binary mask at the scene level (host), or null
+  int batch, per_cell;       // speculative refine batch size / unknown candidates requested per cell
+};
+struct SeedOutput {
+  std::vector<pmvs_patch> seeds;  // addPatch order
+  long long stats[8];             // trial, pass, fail0, fail1, refined, rounds, candidates
+  double gen_ms = 0, refine_ms = 0, wall_ms = 0;
+};
+hipError_t seed_pass(const DScene& s, const std::vector<DView>& hv, const SeedInput& in, hipStream_t st,
+                     const RefineFn& refine, SeedOutput& out);
 }  // namespace pmvsdev

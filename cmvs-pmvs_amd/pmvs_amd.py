@@ -97,6 +97,16 @@ class LoopIter(C.Structure):
                 "patches": self.patches}
 
 
+class SeedStats(C.Structure):
+    _fields_ = [(k, C.c_int64) for k in ("trial", "pass_", "fail0", "fail1", "refined", "rounds", "candidates",
+                                          "reserved")] + [(k, C.c_double) for k in ("wall_ms", "gen_ms", "refine_ms")]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+        d["pass"] = d.pop("pass_")
+        return d
+
+
 class Options(C.Structure):
     _fields_ = [(k, C.c_int32) for k in ("level", "csize", "wsize", "min_image_num", "cpu", "use_bound",
                                           "use_vis_data", "sequence", "tflag", "oflag")] + \
@@ -120,7 +130,8 @@ EXPORTS = ["pmvs_last_error", "pmvs_device_count", "pmvs_scene_create", "pmvs_sc
            "pmvs_ppm_load", "pmvs_options_load", "pmvs_options_free", "pmvs_write_patches", "pmvs_write_pset",
            "pmvs_write_ply", "pmvs_patch_colors", "pmvs_filter_run",
            "pmvs_expand_run", "pmvs_expand_fetch", "pmvs_run_loop", "pmvs_loop_fetch", "pmvs_scene_set_shard", "pmvs_thread_exchange_create",
-           "pmvs_thread_exchange_ctx", "pmvs_thread_allgather", "pmvs_thread_exchange_destroy", "pmvs_detect_features"]
+           "pmvs_thread_exchange_ctx", "pmvs_thread_allgather", "pmvs_thread_exchange_destroy", "pmvs_detect_features",
+           "pmvs_seed_run"]
 
 # int fn(void* ctx, const void* send, int64_t bytes, void* recv): all-gather (pmvs_allgather_fn)
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p)
@@ -147,6 +158,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.pmvs_grab_tex.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
     lib.pmvs_detect_features.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
                                          C.POINTER(C.c_int32)]
+    lib.pmvs_seed_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
+                                  C.POINTER(C.c_int32), C.POINTER(SeedStats)]
     lib.pmvs_incc_eval.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(Stats)]
     lib.pmvs_refine_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(Stats)]
     lib.pmvs_refine_batch_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
@@ -335,6 +348,18 @@ class Scene:
         _check(self.lib.pmvs_detect_features(self.handle, view, fcsize, _ptr(out), n.value, C.byref(n)))
         return out
 
+    def seed_run(self, points, batch: int = 0, cap=None):
+        """CSeed::run on the device (pmvs_seed_run) from per-view feature points (POINT_DTYPE arrays,
+        or float [n, 4] = x, y, response, type): (seed patches in addPatch order, stats)."""
+        flat, npts = points_flat(points)
+        cap = int(cap or max(1024, int(npts.sum())))
+        out = np.zeros(cap, PATCH_DTYPE)
+        n = C.c_int32(0)
+        st = SeedStats()
+        _check(self.lib.pmvs_seed_run(self.handle, _ptr(flat), _ptr(npts), int(batch), _ptr(out), cap, C.byref(n),
+                                      C.byref(st)))
+        return out[:n.value].copy(), st.as_dict()
+
     def grab_tex(self, q: np.ndarray):
         q = np.ascontiguousarray(q, TEX_QUERY_DTYPE)
         n = len(q)
@@ -444,6 +469,22 @@ class Scene:
         st = Stats()
         _check(self.lib.pmvs_scene_sync(self.handle, C.byref(st)))
         return st.as_dict()
+
+
+def points_flat(points):
+    """Per-view feature points -> (flat POINT_DTYPE array, per-view counts)."""
+    parts = []
+    for pv in points:
+        if isinstance(pv, np.ndarray) and pv.dtype == POINT_DTYPE:
+            parts.append(pv)
+            continue
+        a = np.asarray(pv, np.float32).reshape(-1, 4)
+        r = np.zeros(len(a), POINT_DTYPE)
+        r["x"], r["y"], r["response"], r["type"] = a[:, 0], a[:, 1], a[:, 2], a[:, 3].astype(np.int32)
+        parts.append(r)
+    npts = np.array([len(p) for p in parts], np.int32)
+    flat = np.concatenate(parts) if parts and npts.sum() else np.zeros(1, POINT_DTYPE)
+    return np.ascontiguousarray(flat), npts
 
 
 def selftest_math(op: int, x: np.ndarray, device: int = 0) -> np.ndarray:

@@ -287,6 +287,26 @@ pmvs_status pmvs_run_loop(pmvs_scene* scene, const pmvs_patch* seeds, int32_t n,
                           int32_t wave, int32_t min_candidates, int32_t flags, int32_t cap, int32_t* n_out, pmvs_loop_iter* iters);
 pmvs_status pmvs_loop_fetch(pmvs_scene* scene, pmvs_patch* out, int32_t n);
 
+/* The seed phase, PMVS3::CSeed::init + run (seed.cpp:11-107) at CPU 1: target images in the
+ * reference's std::shuffle(mt19937(42)) order, cells in raster order, the feature points of every
+ * view (points: num_points[0] of view 0, then view 1, ..., as pmvs_detect_features returns them)
+ * matched along epipolar lines on the device, and the candidates of a point refined in order of
+ * _response (the reference sorts them by heap address, seed.cpp:322: documented deviation) until
+ * two succeed (preProcess -> refinePatch -> postProcess, seed.cpp:387-414).  Refinement is batched
+ * and speculative; the result equals the sequential one for any batch size.  Runs at depth 0 with
+ * the scene's current thresholds (CFindMatch::init values).  Writes the seed patches in addPatch
+ * order (at most cap; *n_out = their number) -- the `seeds` input of pmvs_run_loop. */
+typedef struct pmvs_seed_stats {
+  int64_t trial, pass, fail0, fail1; /* initialMatchSub calls and outcomes (seed.cpp:94-100) */
+  int64_t refined;                   /* candidates refined on the device (incl. speculative ones) */
+  int64_t rounds;                    /* refine launches */
+  int64_t candidates;                /* epipolar candidates collected */
+  int64_t reserved;
+  double wall_ms, gen_ms, refine_ms; /* whole call, candidate generation, refine batches (wall) */
+} pmvs_seed_stats;
+pmvs_status pmvs_seed_run(pmvs_scene* scene, const pmvs_point* points, const int32_t* num_points, int32_t batch,
+                          pmvs_patch* out, int32_t cap, int32_t* n_out, pmvs_seed_stats* stats);
+
 /* Multi-GPU sharding of the expansion: one scene per GPU/rank, all holding the
  * same model.  Each wave's candidates are split into contiguous rank ranges for the refine and
  * the per-candidate results are all-gathered through `fn` before the (replicated) commit.

@@ -51,6 +51,12 @@ def lib():
         L.oracle_filter_run.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         L.oracle_expand_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                         C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int64]
+        L.oracle_seed_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+        L.oracle_seed_images.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_seed_candidates.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                             C.c_void_p, C.c_int]
+        L.oracle_seed_geometry.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
+                                           C.c_void_p, C.c_void_p]
         L.oracle_bobyqa_test.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_int, C.POINTER(C.c_int)]
         _lib = L
@@ -75,6 +81,8 @@ def ref_lib():
         R.ref_expand_dirs.argtypes = [C.c_void_p] * 3 + [C.c_int, C.c_void_p]
         R.ref_detect_features.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                           C.c_int]
+        R.ref_seed_geometry.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
+                                        C.c_void_p, C.c_void_p, C.c_void_p]
         R.ref_camera_depth.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p]
         _ref = R
     return _ref
@@ -222,6 +230,57 @@ class OracleScene:
             before = np.float32(before - np.float32(0.05))
             cthr, depth = 2, depth + 1
         return model, log
+
+    @staticmethod
+    def _points(points):
+        """points: list (one per view) of float32 [n, 4] = (x, y, response, type)."""
+        npts = np.array([len(p) for p in points], np.int32)
+        flat = np.zeros(int(npts.sum()), P.POINT_DTYPE)
+        k = 0
+        for pv in points:
+            pv = np.asarray(pv, np.float32).reshape(-1, 4)
+            flat["x"][k:k + len(pv)] = pv[:, 0]
+            flat["y"][k:k + len(pv)] = pv[:, 1]
+            flat["response"][k:k + len(pv)] = pv[:, 2]
+            flat["type"][k:k + len(pv)] = pv[:, 3].astype(np.int32)
+            k += len(pv)
+        return flat, npts
+
+    def seed_run(self, points, cap=None):
+        """CSeed::run (CPU 1, _response-ordered candidates): (seed patches in addPatch order, stats)."""
+        flat, npts = self._points(points)
+        cap = cap or max(1024, int(npts.sum()))
+        out = np.zeros(cap, P.PATCH_DTYPE)
+        st = np.zeros(4, np.int64)
+        m = lib().oracle_seed_run(self.h, _p(flat), _p(npts), _p(out), cap, _p(st))
+        if m < 0:
+            raise RuntimeError("seed_run: capacity too small")
+        return out[:m].copy(), dict(zip(("trial", "pass", "fail0", "fail1"), st.tolist()))
+
+    def seed_images(self, num_views, num_targets, tau):
+        imgs = np.zeros((num_views, tau), np.int32)
+        order = np.zeros(num_targets, np.int32)
+        lib().oracle_seed_images(self.h, _p(imgs), _p(order))
+        return imgs, order
+
+    def seed_candidates(self, points, index, point, cap=1 << 16):
+        flat, npts = self._points(points)
+        oi = np.zeros((cap, 3), np.int32)
+        of = np.zeros((cap, 5), np.float32)
+        m = lib().oracle_seed_candidates(self.h, _p(flat), _p(npts), index, point, _p(oi), _p(of), cap)
+        if m < 0:
+            raise RuntimeError("seed_candidates: capacity too small")
+        return oi[:m].copy(), of[:m].copy()
+
+    def seed_geometry(self, i0, i1, xy0, xy1):
+        xy0 = np.ascontiguousarray(xy0, np.float32)
+        xy1 = np.ascontiguousarray(xy1, np.float32)
+        n = len(xy0)
+        F = np.zeros(9, np.float64)
+        epd = np.zeros(n, np.float32)
+        co = np.zeros((n, 4), np.float32)
+        lib().oracle_seed_geometry(self.h, i0, i1, _p(xy0), _p(xy1), n, _p(F), _p(epd), _p(co))
+        return F.reshape(3, 3), epd, co
 
     def refine_batch(self, cands, nthreads=1):
         cands = np.ascontiguousarray(cands, P.CANDIDATE_DTYPE)

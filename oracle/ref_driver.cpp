@@ -28,6 +28,8 @@
 #include <set>
 
 #include "image/camera.hpp"
+#include "numeric/mat3.hpp"
+#include "numeric/mat4.hpp"
 #include "image/image.hpp"
 #include "pmvs/dog.hpp"
 #include "pmvs/harris.hpp"
@@ -272,5 +274,55 @@ void ref_ortho(const float* z, float* out) {
     out[i] = x[i];
     out[4 + i] = y[i];
   }
+}
+
+// Seed-phase geometry on the reference's own CCamera (camera.cpp) and header templates:
+// Image::setF<double> and Image::computeEPD<double> (camera.hpp:119-151) are called as they are;
+// the triangulation of CSeed::unproject (seed.cpp:340-384, a CSeed member that cannot be
+// instantiated without CFindMatch) is evaluated with the reference's TMat4/TMat3/TVec types and
+// operators (transpose, Mat4 * Mat4, Mat4 * Vec4, invert(Mat3), Mat3 * Vec3), so the operation
+// order is the headers'.  out: F9 (row-major), epd[n], coords4[4n].
+int ref_seed_geometry(const char* txt0, const char* txt1, int max_level, int level, const float* xy0, const float* xy1,
+                      int n, double* F9, float* epd, float* coords4) {
+  Image::CCamera c0, c1;
+  c0.init(txt0, max_level);
+  c1.init(txt1, max_level);
+  Mat3 F;
+  Image::setF(c0, c1, F, level);
+  for (int i = 0; i < 9; ++i) F9[i] = F[i / 3][i % 3];
+  const std::vector<Vec4f> P0 = c0.ProjectionMatrix()[level];
+  const std::vector<Vec4f> P1 = c1.ProjectionMatrix()[level];
+  for (int k = 0; k < n; ++k) {
+    const Vec3f a(xy0[2 * k], xy0[2 * k + 1], 1.0f), b(xy1[2 * k], xy1[2 * k + 1], 1.0f);
+    const Vec3 p0(a[0], a[1], a[2]), p1(b[0], b[1], b[2]);
+    epd[k] = Image::computeEPD(F, p0, p1);
+    Mat4 A;
+    for (int j = 0; j < 3; ++j) {
+      A[0][j] = P0[0][j] - a[0] * P0[2][j];
+      A[1][j] = P0[1][j] - a[1] * P0[2][j];
+      A[2][j] = P1[0][j] - b[0] * P1[2][j];
+      A[3][j] = P1[1][j] - b[1] * P1[2][j];
+    }
+    Vec4 bb;
+    bb[0] = a[0] * P0[2][3] - P0[0][3];
+    bb[1] = a[1] * P0[2][3] - P0[1][3];
+    bb[2] = b[0] * P1[2][3] - P1[0][3];
+    bb[3] = b[1] * P1[2][3] - P1[1][3];
+    const Mat4 AT = transpose(A);
+    const Mat4 ATA = AT * A;
+    const Vec4 ATb = AT * bb;
+    Mat3 M3;
+    Vec3 r3;
+    for (int y = 0; y < 3; ++y) {
+      for (int x = 0; x < 3; ++x) M3[y][x] = ATA[y][x];
+      r3[y] = ATb[y];
+    }
+    Mat3 iM3;
+    invert(iM3, M3);
+    const Vec3 ans = iM3 * r3;
+    for (int y = 0; y < 3; ++y) coords4[4 * k + y] = ans[y];
+    coords4[4 * k + 3] = 1.0f;
+  }
+  return 0;
 }
 }

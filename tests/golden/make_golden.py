@@ -9,10 +9,12 @@ renderer regenerates them bit-for-bit).  Expected outputs come from two sources:
     projection, CCamera::project and computeDepth of sample points, and bilinear getColor
     samples on every pyramid level; the candidate centres of CExpand::findEmptyBlocks
     (expand.cpp:176-177 evaluated with the reference headers, expand_dirs.npz); the Harris and
-    DoG feature points of every golden view (harris.cpp / dog.cpp, features.npz) -- these
-    vectors are REFERENCE outputs;
+    DoG feature points of every golden view (harris.cpp / dog.cpp, features.npz); the seed
+    phase's setF / computeEPD / triangulation of feature pairs (seeds.npz) -- these vectors are
+    REFERENCE outputs;
   * oracle/liboracle.so (the CPU restatement, pinned on the pieces above): pyramid CRCs,
-    grabTex textures, my_f values and full preProcess->refinePatch->postProcess records.
+    grabTex textures, my_f values, full preProcess->refinePatch->postProcess records and the
+    seed phase's seed patches (seeds.npz).
 Run from the repo root in the build container:  python tests/golden/make_golden.py
 """
 import os
@@ -154,6 +156,60 @@ def make_features():
     print(f"{path}: {os.path.getsize(path)} B, " + ", ".join(f"{k} {len(v)}" for k, v in g.items() if k.endswith("points")))
 
 
+def ref_seed_geometry(proj, max_level, level, i0, i1, xy0, xy1):
+    """Image::setF / computeEPD and the CSeed::unproject triangulation evaluated with the
+    reference's CCamera (camera.cpp) and numeric headers (oracle/_ref ref_seed_geometry)."""
+    R = O.ref_lib()
+    n = len(xy0)
+    F = np.zeros(9, np.float64)
+    epd = np.zeros(n, np.float32)
+    co = np.zeros((n, 4), np.float32)
+    with tempfile.TemporaryDirectory() as d:
+        p0, p1 = os.path.join(d, "a.txt"), os.path.join(d, "b.txt")
+        write_contour(p0, proj[i0])
+        write_contour(p1, proj[i1])
+        R.ref_seed_geometry(p0.encode(), p1.encode(), max_level, level, xy0.ctypes.data, xy1.ctypes.data, n,
+                            F.ctypes.data, epd.ctypes.data, co.ctypes.data)
+    return F.reshape(3, 3), epd, co
+
+
+def make_seeds():
+    """Seed phase vectors (seeds.npz): per golden scene, setF / computeEPD / triangulation of feature
+    point pairs from the REFERENCE (oracle/_ref), and the oracle's CSeed::run result (seed patches
+    in addPatch order + trial/pass/fail counts) on the reference-detected features (regression)."""
+    feats = dict(np.load(os.path.join(HERE, "features.npz")))
+    g = {}
+    rng = np.random.default_rng(17)
+    for name, (views, width, height, level, csize, *_rest) in SCENES.items():
+        inp, p = P.synth_scene(views, width, height, level=level, csize=csize, supersample=2)
+        off = feats[f"{name}_offsets"]
+        pts = [feats[f"{name}_points"][off[v]:off[v + 1]] for v in range(views)]
+        pairs = [(0, 1), (1, 0), (0, views - 1), (views - 1, 1)]
+        F_all, epd_all, co_all, xy_all = [], [], [], []
+        for i0, i1 in pairs:
+            a = pts[i0][:, :2]
+            b = pts[i1][rng.integers(0, len(pts[i1]), len(a)), :2]
+            xy0 = np.ascontiguousarray(a, np.float32)
+            xy1 = np.ascontiguousarray(b, np.float32)
+            F, epd, co = ref_seed_geometry(inp.projections, level + 3, level, i0, i1, xy0, xy1)
+            F_all.append(F); epd_all.append(epd); co_all.append(co); xy_all.append(np.stack([xy0, xy1], 1))
+        g[f"{name}_pairs"] = np.array(pairs, np.int32)
+        g[f"{name}_ref_F"] = np.stack(F_all)
+        g[f"{name}_xy"] = np.concatenate(xy_all)
+        g[f"{name}_pair_len"] = np.array([len(e) for e in epd_all], np.int64)
+        g[f"{name}_ref_epd"] = np.concatenate(epd_all)
+        g[f"{name}_ref_coords"] = np.concatenate(co_all)
+        o = O.OracleScene(inp)
+        seeds, st = o.seed_run(pts)
+        o.close()
+        g[f"{name}_seeds"] = seeds
+        g[f"{name}_seed_stats"] = np.array([st[k] for k in ("trial", "pass", "fail0", "fail1")], np.int64)
+        print(f"{name}: {len(seeds)} seeds, {st}")
+    path = os.path.join(HERE, "seeds.npz")
+    np.savez_compressed(path, **g)
+    print(f"{path}: {os.path.getsize(path)} B")
+
+
 def make(name, views, width, height, level, csize, ntex, neval, nref):
     inp, p = P.synth_scene(views, width, height, level=level, csize=csize, supersample=2)
     o = O.OracleScene(inp)
@@ -199,5 +255,6 @@ if __name__ == "__main__":
     O.build()
     make_expand_dirs()
     make_features()
+    make_seeds()
     for k, v in SCENES.items():
         make(k, *v)

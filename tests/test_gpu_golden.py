@@ -13,7 +13,7 @@ from pmvs_cases import bits
 pytestmark = pytest.mark.gpu
 # scene goldens (c1, ring8); expand_dirs.npz / features.npz hold other reference vectors
 GOLDEN = sorted(p for p in glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz"))
-                if not os.path.basename(p).startswith(("expand_dirs", "features")))
+                if not os.path.basename(p).startswith(("expand_dirs", "features", "seeds")))
 
 
 @pytest.fixture(scope="module", params=GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
