@@ -233,18 +233,8 @@ class OracleScene:
 
     @staticmethod
     def _points(points):
-        """points: list (one per view) of float32 [n, 4] = (x, y, response, type)."""
-        npts = np.array([len(p) for p in points], np.int32)
-        flat = np.zeros(int(npts.sum()), P.POINT_DTYPE)
-        k = 0
-        for pv in points:
-            pv = np.asarray(pv, np.float32).reshape(-1, 4)
-            flat["x"][k:k + len(pv)] = pv[:, 0]
-            flat["y"][k:k + len(pv)] = pv[:, 1]
-            flat["response"][k:k + len(pv)] = pv[:, 2]
-            flat["type"][k:k + len(pv)] = pv[:, 3].astype(np.int32)
-            k += len(pv)
-        return flat, npts
+        """points: list (one per view) of POINT_DTYPE arrays or float32 [n, 4] = (x, y, response, type)."""
+        return P.points_flat(points)
 
     def seed_run(self, points, cap=None):
         """CSeed::run (CPU 1, _response-ordered candidates): (seed patches in addPatch order, stats)."""
