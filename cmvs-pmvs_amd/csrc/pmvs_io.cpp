@@ -5,6 +5,9 @@
 //
 // Each function restates the reference routine it replaces, with the same tokenisation and
 // arithmetic, but reports errors through pmvs_status instead of exit(1).
+#include <dlfcn.h>
+#include <setjmp.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
@@ -19,6 +22,14 @@
 #include <vector>
 
 #include "../../include/pmvs_amd.h"
+
+// libjpeg's API types (the image's libjpeg 9 headers); the library itself is loaded at run time
+// (dlopen), so the product has no link-time JPEG dependency and reports PMVS_EUNSUPPORTED for
+// .jpg inputs where libjpeg is absent.
+#if __has_include("/opt/conda/include/jpeglib.h")
+#include "/opt/conda/include/jpeglib.h"
+#define PMVS_HAVE_JPEG_HEADERS 1
+#endif
 
 pmvs_status pmvs_io_fail(pmvs_status st, const char* fmt, ...);  // pmvs_api.cpp
 
@@ -187,6 +198,215 @@ pmvs_status pmvs_ppm_load(const char* path, int32_t* width, int32_t* height, uin
     }
   }
   std::fclose(f);
+  return PMVS_OK;
+}
+
+// ------------------------------------------------------------------ JPEG (dlopen'ed libjpeg)
+#ifdef PMVS_HAVE_JPEG_HEADERS
+namespace {
+struct JpegApi {
+  void* h = nullptr;
+  struct jpeg_error_mgr* (*std_error)(struct jpeg_error_mgr*);
+  void (*create)(j_decompress_ptr, int, size_t);
+  void (*stdio_src)(j_decompress_ptr, FILE*);
+  int (*read_header)(j_decompress_ptr, boolean);
+  boolean (*start)(j_decompress_ptr);
+  JDIMENSION (*read_scanlines)(j_decompress_ptr, JSAMPARRAY, JDIMENSION);
+  boolean (*finish)(j_decompress_ptr);
+  void (*destroy)(j_decompress_ptr);
+  bool load() {
+    if (h) return true;
+    for (const char* name : {"libjpeg.so.9", "/opt/conda/lib/libjpeg.so.9", "libjpeg.so"}) {
+      h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+      if (h) break;
+    }
+    if (!h) return false;
+    std_error = (decltype(std_error))dlsym(h, "jpeg_std_error");
+    create = (decltype(create))dlsym(h, "jpeg_CreateDecompress");
+    stdio_src = (decltype(stdio_src))dlsym(h, "jpeg_stdio_src");
+    read_header = (decltype(read_header))dlsym(h, "jpeg_read_header");
+    start = (decltype(start))dlsym(h, "jpeg_start_decompress");
+    read_scanlines = (decltype(read_scanlines))dlsym(h, "jpeg_read_scanlines");
+    finish = (decltype(finish))dlsym(h, "jpeg_finish_decompress");
+    destroy = (decltype(destroy))dlsym(h, "jpeg_destroy_decompress");
+    return std_error && create && stdio_src && read_header && start && read_scanlines && finish && destroy;
+  }
+};
+JpegApi g_jpeg;
+struct JpegErr {
+  struct jpeg_error_mgr pub;
+  jmp_buf jb;
+};
+void jpeg_err_exit(j_common_ptr c) { longjmp(reinterpret_cast<JpegErr*>(c->err)->jb, 1); }
+
+// CImg::load_jpeg (cimg_use_jpeg) as CImage::readAnyImage uses it (image.cpp:473-506): libjpeg
+// defaults (islow IDCT, fancy upsampling), 3-component output copied in (x, y, c) order.
+pmvs_status jpeg_load(const char* path, int32_t* width, int32_t* height, uint8_t* rgb) {
+  if (!g_jpeg.load()) return pmvs_io_fail(PMVS_EUNSUPPORTED, "%s: libjpeg (libjpeg.so.9) is not available", path);
+  FILE* f = std::fopen(path, "rb");
+  if (!f) return pmvs_io_fail(PMVS_EINVAL, "cannot open image %s", path);
+  struct jpeg_decompress_struct ci;
+  JpegErr err;
+  ci.err = g_jpeg.std_error(&err.pub);
+  err.pub.error_exit = jpeg_err_exit;
+  std::vector<uint8_t> row;
+  if (setjmp(err.jb)) {
+    g_jpeg.destroy(&ci);
+    std::fclose(f);
+    return pmvs_io_fail(PMVS_EINVAL, "%s: corrupt JPEG", path);
+  }
+  g_jpeg.create(&ci, JPEG_LIB_VERSION, sizeof(ci));
+  g_jpeg.stdio_src(&ci, f);
+  g_jpeg.read_header(&ci, TRUE);
+  g_jpeg.start(&ci);
+  const int nc = ci.output_components;
+  if (nc < 3) {
+    g_jpeg.destroy(&ci);
+    std::fclose(f);
+    // the reference prints "Unsufficient components (not a color image)" and leaves the image empty
+    return pmvs_io_fail(PMVS_EUNSUPPORTED, "%s: %d components (not a color image)", path, nc);
+  }
+  *width = (int32_t)ci.output_width;
+  *height = (int32_t)ci.output_height;
+  if (rgb) {
+    row.resize((size_t)ci.output_width * nc);
+    JSAMPROW rp = row.data();
+    for (uint32_t y = 0; y < ci.output_height; ++y) {
+      g_jpeg.read_scanlines(&ci, &rp, 1);
+      uint8_t* o = rgb + (size_t)y * ci.output_width * 3;
+      for (uint32_t x = 0; x < ci.output_width; ++x)
+        for (int c = 0; c < 3; ++c) o[3 * x + c] = row[(size_t)x * nc + c];
+    }
+    g_jpeg.finish(&ci);
+  }
+  g_jpeg.destroy(&ci);
+  std::fclose(f);
+  return PMVS_OK;
+}
+}  // namespace
+#endif
+
+static bool has_suffix(const std::string& s, const char* suf) {
+  const size_t n = std::strlen(suf);
+  return s.size() >= n && s.compare(s.size() - n, n, suf) == 0;
+}
+
+// CImage::readAnyImage (image.cpp:473-506): the colour image of a view, by extension (.ppm / .jpg).
+pmvs_status pmvs_image_load(const char* path, int32_t* width, int32_t* height, uint8_t* rgb) {
+  if (!path || !width || !height) return pmvs_io_fail(PMVS_EINVAL, "null argument");
+  const std::string p(path);
+  if (has_suffix(p, ".ppm")) return pmvs_ppm_load(path, width, height, rgb);
+  if (has_suffix(p, ".jpg") || has_suffix(p, ".jpeg") || has_suffix(p, ".JPG")) {
+#ifdef PMVS_HAVE_JPEG_HEADERS
+    return jpeg_load(path, width, height, rgb);
+#else
+    return pmvs_io_fail(PMVS_EUNSUPPORTED, "%s: built without JPEG support", path);
+#endif
+  }
+  return pmvs_io_fail(PMVS_EUNSUPPORTED, "%s: unsupported image format (ppm, jpg)", path);
+}
+
+// CImage::readPGMImage (image.cpp:622-670, binary P5) / readPBMImage (image.cpp:508-560, P4: bit 1
+// -> 0, bit 0 -> 255), as the mask and edge readers of CImage::alloc (image.cpp:143-180).  The
+// raw bytes are returned; the 127 / 1 thresholds are applied by pmvs_scene_create.
+pmvs_status pmvs_pnm_mask_load(const char* path, int32_t* width, int32_t* height, uint8_t* out) {
+  if (!path || !width || !height) return pmvs_io_fail(PMVS_EINVAL, "null argument");
+  const std::string p(path);
+  const bool pgm = has_suffix(p, "pgm"), pbm = has_suffix(p, "pbm");
+  if (!pgm && !pbm) return pmvs_io_fail(PMVS_EUNSUPPORTED, "%s: masks/edges are .pgm or .pbm", path);
+  std::ifstream ifstr(path, std::ios::binary);
+  if (!ifstr.is_open()) return pmvs_io_fail(PMVS_EINVAL, "cannot open %s", path);
+  std::string header;
+  unsigned char uc;
+  ifstr >> header;
+  ifstr.read((char*)&uc, 1);
+  if (header != (pgm ? "P5" : "P4")) return pmvs_io_fail(PMVS_EUNSUPPORTED, "%s: only binary %s", path, pgm ? "pgm" : "pbm");
+  while (true) {
+    ifstr.read((char*)&uc, 1);
+    ifstr.putback(uc);
+    if (uc == '#') {
+      char buffer[1024];
+      ifstr.getline(buffer, 1024);
+    } else {
+      break;
+    }
+  }
+  int w = 0, h = 0, maxv = 0;
+  ifstr >> w >> h;
+  if (pgm) ifstr >> maxv;
+  ifstr.read((char*)&uc, 1);
+  if (!ifstr || w <= 0 || h <= 0) return pmvs_io_fail(PMVS_EINVAL, "%s: bad header", path);
+  *width = w;
+  *height = h;
+  if (!out) return PMVS_OK;
+  const size_t n = (size_t)w * h;
+  if (pgm) {
+    ifstr.read((char*)out, (std::streamsize)n);
+    if ((size_t)ifstr.gcount() != n) return pmvs_io_fail(PMVS_EINVAL, "%s: truncated", path);
+  } else {
+    // bit stream over the whole image (no per-row padding), as the reference reads it
+    size_t bcount = n;
+    if (bcount % 8 != 0) bcount++;
+    size_t count = 0;
+    for (size_t i = 0; i < bcount && count < n; ++i) {
+      ifstr.read((char*)&uc, 1);
+      for (int j = 0; j < 8 && count < n; ++j, ++count) {
+        out[count] = (uc >> 7) ? 0 : 255;
+        uc <<= 1;
+      }
+    }
+  }
+  return PMVS_OK;
+}
+
+// CImage::setEdge (image.cpp:407-460, option setEdge != 0): squared RGB central differences,
+// separable Gaussian filterG (sigma 3, image.cpp:1013-1056, border renormalised), threshold.
+pmvs_status pmvs_set_edge(const uint8_t* rgb, int32_t width, int32_t height, float threshold, uint8_t* edge_out) {
+  if (!rgb || !edge_out || width < 1 || height < 1) return pmvs_io_fail(PMVS_EINVAL, "invalid argument");
+  const int W = width, H = height;
+  std::vector<float> a((size_t)W * H, 0.0f), b((size_t)W * H, 0.0f);
+  for (int y = 1; y < H - 1; ++y)
+    for (int x = 1; x < W - 1; ++x) {
+      const int index = 3 * (y * W + x);
+      const int r = index + 3, l = index - 3, t = index - 3 * W, bo = index + 3 * W;
+      float& v = a[(size_t)y * W + x];
+      for (int i = 0; i < 3; ++i) {
+        const int i0 = std::abs(rgb[r + i] - rgb[l + i]);
+        v += i0 * i0;
+        const int i1 = std::abs(rgb[bo + i] - rgb[t + i]);
+        v += i1 * i1;
+      }
+    }
+  const float sigma = 3.f;
+  const float sigma2 = 2.f * sigma * sigma;
+  const int margin = (int)std::floor(2 * sigma);
+  std::vector<float> filter(2 * margin + 1);
+  for (int i = -margin; i <= margin; ++i) filter[i + margin] = (float)std::exp((double)(-i * i / sigma2));
+  // vertical into b, horizontal back into a
+  for (int y = 0; y < H; ++y)
+    for (int x = 0; x < W; ++x) {
+      float acc = 0.0f, denom = 0.0f;
+      for (int j = -margin; j <= margin; ++j) {
+        const int yt = y + j;
+        if (yt < 0 || H <= yt) continue;
+        acc += filter[j + margin] * a[(size_t)yt * W + x];
+        denom += filter[j + margin];
+      }
+      b[(size_t)y * W + x] = acc / denom;
+    }
+  for (int y = 0; y < H; ++y)
+    for (int x = 0; x < W; ++x) {
+      float acc = 0.0f, denom = 0.0f;
+      for (int i = -margin; i <= margin; ++i) {
+        const int xt = x + i;
+        if (xt < 0 || W <= xt) continue;
+        acc += filter[i + margin] * b[(size_t)y * W + xt];
+        denom += filter[i + margin];
+      }
+      a[(size_t)y * W + x] = acc / denom;
+    }
+  const float nt = threshold * threshold * (2 * margin + 1) * (2 * margin + 1) / 3.0f;
+  for (size_t k = 0; k < (size_t)W * H; ++k) edge_out[k] = (nt < a[k]) ? 255 : 0;
   return PMVS_OK;
 }
 

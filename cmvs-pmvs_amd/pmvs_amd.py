@@ -131,7 +131,7 @@ EXPORTS = ["pmvs_last_error", "pmvs_device_count", "pmvs_scene_create", "pmvs_sc
            "pmvs_write_ply", "pmvs_patch_colors", "pmvs_filter_run",
            "pmvs_expand_run", "pmvs_expand_fetch", "pmvs_run_loop", "pmvs_loop_fetch", "pmvs_scene_set_shard", "pmvs_thread_exchange_create",
            "pmvs_thread_exchange_ctx", "pmvs_thread_allgather", "pmvs_thread_exchange_destroy", "pmvs_detect_features",
-           "pmvs_seed_run"]
+           "pmvs_seed_run", "pmvs_image_load", "pmvs_pnm_mask_load", "pmvs_set_edge"]
 
 # int fn(void* ctx, const void* send, int64_t bytes, void* recv): all-gather (pmvs_allgather_fn)
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p)
@@ -171,6 +171,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
                                          C.c_void_p, C.POINTER(C.c_double)]
     lib.pmvs_selftest_math.argtypes = [C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32]
     lib.pmvs_camera_load.argtypes = [C.c_char_p, C.c_void_p]
+    lib.pmvs_image_load.argtypes = [C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_void_p]
+    lib.pmvs_pnm_mask_load.argtypes = [C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_void_p]
+    lib.pmvs_set_edge.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_float, C.c_void_p]
     lib.pmvs_ppm_load.argtypes = [C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_void_p]
     lib.pmvs_options_load.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.POINTER(Options))]
     lib.pmvs_options_free.argtypes = [C.POINTER(Options)]
@@ -517,6 +520,34 @@ def ppm_load(path: str) -> np.ndarray:
     img = np.zeros((h.value, w.value, 3), np.uint8)
     _check(lib.pmvs_ppm_load(path.encode(), C.byref(w), C.byref(h), _ptr(img)))
     return img
+
+
+def image_load(path: str) -> np.ndarray:
+    """CImage::readAnyImage: PPM or JPEG -> uint8 [H, W, 3] (pmvs_image_load)."""
+    lib = load_library()
+    w, h = C.c_int32(), C.c_int32()
+    _check(lib.pmvs_image_load(path.encode(), C.byref(w), C.byref(h), None))
+    img = np.zeros((h.value, w.value, 3), np.uint8)
+    _check(lib.pmvs_image_load(path.encode(), C.byref(w), C.byref(h), _ptr(img)))
+    return img
+
+
+def mask_load(path: str) -> np.ndarray:
+    """Binary PGM (P5) / PBM (P4) mask or edge image -> uint8 [H, W] (pmvs_pnm_mask_load)."""
+    lib = load_library()
+    w, h = C.c_int32(), C.c_int32()
+    _check(lib.pmvs_pnm_mask_load(path.encode(), C.byref(w), C.byref(h), None))
+    m = np.zeros((h.value, w.value), np.uint8)
+    _check(lib.pmvs_pnm_mask_load(path.encode(), C.byref(w), C.byref(h), _ptr(m)))
+    return m
+
+
+def set_edge(rgb: np.ndarray, threshold: float) -> np.ndarray:
+    """CImage::setEdge (option setEdge): edge map of a level-0 image (pmvs_set_edge)."""
+    rgb = np.ascontiguousarray(rgb, np.uint8)
+    out = np.zeros(rgb.shape[:2], np.uint8)
+    _check(load_library().pmvs_set_edge(_ptr(rgb), rgb.shape[1], rgb.shape[0], float(threshold), _ptr(out)))
+    return out
 
 
 def options_load(prefix: str, option_file: str) -> dict:

@@ -336,6 +336,18 @@ pmvs_status pmvs_camera_load(const char* txt_path, float projection[12]);
  * rgb may be NULL to query the size; otherwise width*height*3 bytes are written. */
 pmvs_status pmvs_ppm_load(const char* path, int32_t* width, int32_t* height, uint8_t* rgb);
 
+/* CImage::readAnyImage (image.cpp:473-506) by extension: binary PPM, or JPEG decoded with the
+ * image's libjpeg (loaded at run time, as CImg's cimg_use_jpeg path).  rgb may be NULL (size query). */
+pmvs_status pmvs_image_load(const char* path, int32_t* width, int32_t* height, uint8_t* rgb);
+
+/* CImage::readPGMImage / readPBMImage (image.cpp:508-670): binary P5 / P4 mask or edge image, raw
+ * bytes (P4 bits: 1 -> 0, 0 -> 255).  out may be NULL (size query). */
+pmvs_status pmvs_pnm_mask_load(const char* path, int32_t* width, int32_t* height, uint8_t* out);
+
+/* CImage::setEdge (image.cpp:407-460): the edge map the option `setEdge threshold` derives from the
+ * level-0 image (width*height bytes, 0/255). */
+pmvs_status pmvs_set_edge(const uint8_t* rgb, int32_t width, int32_t height, float threshold, uint8_t* edge_out);
+
 /* PMVS3::SOption (option.cpp:10-307): option file keys and defaults, timages/oimages
  * (enumeration, -1 range, -2 from vis.dat, -3 none), useVisData (vis.dat), useBound
  * (bimages.dat).  Image lists are image NUMBERS; visdata2 is CSR over view indexes

@@ -1,0 +1,139 @@
+"""CPU tests of the pmvs2 / genOption executables and the image-input surface (SURVEY.md §8(b)
+external boundary, §8(f) f3/f4):
+  * genOption (cmvs-pmvs_amd/genOption) against the reference's own genOption.cpp compiled
+    unmodified into oracle/_ref: identical option files and pmvs.sh for the same ske.dat;
+  * JPEG input against libjpeg 9's own djpeg (the image's /opt/conda/bin/djpeg, libjpeg defaults
+    = CImg's load_jpeg path of CImage::readAnyImage);
+  * P5 / P4 mask readers and CImage::setEdge (numpy restatement in the same float order);
+  * pmvs2 usage / error exits (no GPU needed)."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "cmvs-pmvs_amd")
+REF_GENOPTION = os.path.join(ROOT, "oracle", "_ref", "genOption")
+
+
+def write_ske(path, clusters, inum=40):
+    with open(path, "w") as f:
+        f.write(f"SKE\n{inum} {len(clusters)}\n")
+        for t, o in clusters:
+            f.write(f"{len(t)} {len(o)}\n" + " ".join(map(str, t)) + "\n" + " ".join(map(str, o)) + "\n")
+
+
+@pytest.mark.parametrize("args", [[], ["2"], ["0", "1", "0.55", "9", "2", "16"]])
+def test_genoption_matches_reference(product_lib, tmp_path, args):
+    if not os.path.exists(REF_GENOPTION):
+        pytest.skip("oracle/_ref/genOption not built (reference absent)")
+    clusters = [(list(range(0, 12)), [12, 13, 14]), (list(range(12, 25)), [3, 4]), ([30], [])]
+    outs = []
+    for tool in (os.path.join(PKG, "genOption"), REF_GENOPTION):
+        d = tmp_path / os.path.basename(os.path.dirname(tool))
+        d.mkdir()
+        write_ske(d / "ske.dat", clusters)
+        subprocess.run([tool, str(d) + "/"] + args, check=True)
+        outs.append({f: (d / f).read_bytes() for f in sorted(os.listdir(d)) if f != "ske.dat"})
+    assert outs[0] == outs[1]
+    assert len(outs[0]) == len(clusters) + 1
+
+
+def test_genoption_gpu_script(product_lib, tmp_path):
+    write_ske(tmp_path / "ske.dat", [([0, 1], [2]), ([2, 3], []), ([4], [5]), ([6], [])])
+    subprocess.run([os.path.join(PKG, "genOption"), str(tmp_path) + "/", "--gpus", "2"], check=True)
+    s = (tmp_path / "pmvs_gpus.sh").read_text()
+    assert "PMVS_DEVICE=0 pmvs2 pmvs/ option-0000 && PMVS_DEVICE=0 pmvs2 pmvs/ option-0002" in s
+    assert "PMVS_DEVICE=1 pmvs2 pmvs/ option-0001 && PMVS_DEVICE=1 pmvs2 pmvs/ option-0003" in s
+    assert (tmp_path / "option-0003").exists() and (tmp_path / "pmvs.sh").exists()
+
+
+def test_jpeg_matches_libjpeg(product_lib, tmp_path):
+    import pmvs_amd as P
+    cjpeg, djpeg = shutil.which("cjpeg") or "/opt/conda/bin/cjpeg", shutil.which("djpeg") or "/opt/conda/bin/djpeg"
+    if not (os.path.exists(cjpeg) and os.path.exists(djpeg)):
+        pytest.skip("libjpeg tools absent")
+    rng = np.random.default_rng(3)
+    img = (rng.random((61, 83, 3)) * 255).astype(np.uint8)
+    img[20:40, 10:50] = [200, 30, 90]
+    ppm = tmp_path / "a.ppm"
+    ppm.write_bytes(b"P6\n83 61\n255\n" + img.tobytes())
+    jpg = tmp_path / "a.jpg"
+    with open(jpg, "wb") as f:
+        subprocess.run([cjpeg, "-quality", "85", str(ppm)], stdout=f, check=True)
+    ref = subprocess.run([djpeg, "-pnm", str(jpg)], stdout=subprocess.PIPE, check=True).stdout
+    ref_px = np.frombuffer(ref[-83 * 61 * 3:], np.uint8).reshape(61, 83, 3)
+    got = P.image_load(str(jpg))
+    assert got.shape == (61, 83, 3)
+    assert np.array_equal(got, ref_px)
+    assert np.array_equal(P.image_load(str(ppm)), img)
+
+
+def test_mask_readers(product_lib, tmp_path):
+    import pmvs_amd as P
+    m = (np.arange(7 * 5) % 3 == 0).astype(np.uint8) * 200
+    (tmp_path / "m.pgm").write_bytes(b"P5\n# c\n7 5\n255\n" + m.tobytes())
+    assert np.array_equal(P.mask_load(str(tmp_path / "m.pgm")), m.reshape(5, 7))
+    bits = (np.arange(7 * 5) % 4 == 1).astype(np.uint8)  # 1 = black (outside)
+    packed = np.packbits(np.concatenate([bits, np.zeros(5, np.uint8)]))
+    (tmp_path / "m.pbm").write_bytes(b"P4\n7 5\n" + packed.tobytes())
+    assert np.array_equal(P.mask_load(str(tmp_path / "m.pbm")), np.where(bits == 1, 0, 255).astype(np.uint8).reshape(5, 7))
+
+
+def test_set_edge_restatement(product_lib):
+    """CImage::setEdge (image.cpp:407-460) restated in numpy with the same float32 operation order."""
+    import pmvs_amd as P
+    rng = np.random.default_rng(9)
+    img = np.repeat(np.repeat((np.arange(52) * 2 + 20).astype(np.uint8)[None, :, None], 40, 0), 3, 2)
+    img = (img + (rng.random(img.shape) * 6).astype(np.uint8)).astype(np.uint8)
+    img[:, 26:] += 90
+    H, W = img.shape[:2]
+    a = np.zeros((H, W), np.float32)
+    im = img.astype(np.int32)
+    for i in range(3):
+        d0 = np.abs(im[1:-1, 2:, i] - im[1:-1, :-2, i])
+        d1 = np.abs(im[2:, 1:-1, i] - im[:-2, 1:-1, i])
+        a[1:-1, 1:-1] += (d0 * d0).astype(np.float32)
+        a[1:-1, 1:-1] += (d1 * d1).astype(np.float32)
+    sigma2 = np.float32(18.0)
+    flt = np.array([np.float32(np.exp(np.float64(np.float32(-i * i) / sigma2))) for i in range(-6, 7)], np.float32)
+
+    def smooth(x, axis):
+        out = np.zeros_like(x)
+        n = x.shape[axis]
+        for idx in range(n):
+            acc = np.zeros(x.shape[1 - axis], np.float32)
+            den = np.float32(0)
+            for j in range(-6, 7):
+                t = idx + j
+                if t < 0 or t >= n:
+                    continue
+                acc = acc + flt[j + 6] * (x[t] if axis == 0 else x[:, t])
+                den = np.float32(den + flt[j + 6])
+            if axis == 0:
+                out[idx] = acc / den
+            else:
+                out[:, idx] = acc / den
+        return out
+
+    s = smooth(smooth(a, 0), 1)
+    thr = np.float32(5.0)
+    nt = np.float32(np.float32(np.float32(thr * thr) * np.float32(13)) * np.float32(13)) / np.float32(3.0)
+    want = np.where(nt < s, 255, 0).astype(np.uint8)
+    got = P.set_edge(img, 5.0)
+    assert np.array_equal(got, want)
+    assert 0 < (got == 255).sum() < got.size
+
+
+def test_pmvs2_usage(product_lib):
+    r = subprocess.run([os.path.join(PKG, "pmvs2")], capture_output=True, text=True)
+    assert r.returncode == 1
+    assert "prefix option_file [Optional export]" in r.stderr and "PATCH PSET" in r.stderr
+
+
+def test_pmvs2_missing_option_file(product_lib, tmp_path):
+    r = subprocess.run([os.path.join(PKG, "pmvs2"), str(tmp_path) + "/", "nope"], capture_output=True, text=True)
+    assert r.returncode == 1
+    assert "pmvs2: option file" in r.stderr
