@@ -34,6 +34,7 @@ int main(void) {
   S(pmvs_options); O(pmvs_options, threshold); O(pmvs_options, num_timages); O(pmvs_options, timages);
   O(pmvs_options, visdata2);
   S(pmvs_point); O(pmvs_point, response); O(pmvs_point, type);
+  S(pmvs_seed_stats); O(pmvs_seed_stats, refined); O(pmvs_seed_stats, wall_ms); O(pmvs_seed_stats, refine_ms);
   S(pmvs_synth_params); O(pmvs_synth_params, seed); O(pmvs_synth_params, arc_step_deg);
   return 0;
 }

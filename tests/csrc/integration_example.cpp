@@ -111,6 +111,31 @@ static void from_pmvs(const pmvs_patch& a, Patch::CPatch& p) {
   for (int k = 0; k < a.num_vimages; ++k) p._vgrids.push_back(TVec2<int>(a.vgrids[k][0], a.vgrids[k][1]));
 }
 
+// ---- §2b the whole seed phase: CSeed::run (seed.cpp:40-107) on the device, from the points
+// CDetectFeatures produced (or pmvs_detect_features); the seeds are added as CSeed does
+int seeds_on_device(PMVS3::CFindMatch& fm, pmvs_scene* scene, const std::vector<std::vector<PMVS3::CPoint>>& points) {
+  std::vector<pmvs_point> flat;
+  std::vector<int32_t> counts;
+  for (const auto& view : points) {            // one entry per image index, detector order
+    counts.push_back((int32_t)view.size());
+    for (const PMVS3::CPoint& p : view) flat.push_back({p._icoord[0], p._icoord[1], p._response, p._type});
+  }
+  std::vector<pmvs_patch> seeds(std::max<size_t>(flat.size(), 1024));
+  int32_t n = 0;
+  pmvs_seed_stats st{};
+  if (pmvs_seed_run(scene, flat.data(), counts.data(), /*batch*/ 0, seeds.data(), (int32_t)seeds.size(), &n,
+                    &st) != PMVS_OK) {
+    std::cerr << "pmvs_seed_run: " << pmvs_last_error() << std::endl;
+    return 1;
+  }
+  for (int i = 0; i < n; ++i) {                // addPatch order of the reference's CPU 1 run
+    Patch::PPatch pp(new Patch::CPatch());
+    from_pmvs(seeds[i], *pp);
+    fm._pos.addPatch(pp);
+  }
+  return 0;
+}
+
 int expand_on_device(PMVS3::CFindMatch& fm, pmvs_scene* scene, bool after_seeds) {
   fm._pos.collectPatches();                    // the model = _ppatches (patchOrganizerS.cpp:228-248)
   const int n = (int)fm._pos._ppatches.size();

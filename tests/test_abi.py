@@ -57,7 +57,8 @@ def test_python_mirror_layout_matches_c(tmp_path):
                 assert dt.fields[f][1] == c[key], key
     ct_types = {"pmvs_view_desc": P.ViewDesc, "pmvs_scene_desc": P.SceneDesc, "pmvs_stats": P.Stats,
                 "pmvs_synth_params": P.SynthParams, "pmvs_filter_stats": P.FilterStats, "pmvs_options": P.Options,
-                "pmvs_expand_stats": P.ExpandStats, "pmvs_loop_iter": P.LoopIter}
+                "pmvs_expand_stats": P.ExpandStats, "pmvs_loop_iter": P.LoopIter,
+                "pmvs_seed_stats": P.SeedStats}
     for name, T in ct_types.items():
         assert C.sizeof(T) == c[name + ".sizeof"], name
         for f, _ in T._fields_:
