@@ -14,7 +14,7 @@
 //     strict "depth < dtmp" over collect order.
 // Kernels are one thread per patch (gains, vimages, visibility, small-group edges), one thread
 // per cell entry (filterExact), one wavefront per patch (filterNeighbor: neighbour gather,
-// sort/unique in LDS, Householder least squares in double), and the setRefImage of filterExact
+// sort/unique in LDS, Cmylapack::lls with Eigen's JacobiSVD algorithm in double), and the setRefImage of filterExact
 // reuses the refine path's wavefront kernel (pmvs_kernels.hip).  The connected-component labels of
 // filterSmallGroups are a breadth-first search over the device-computed, ordered edge lists on the
 // host (the reference's label assignment is an order-dependent BFS; its cost is O(edges)).
@@ -443,58 +443,245 @@ struct NbLds {
   float fx[NB_CAP], fy[NB_CAP], fz[NB_CAP];
   float units[PMVS_MAX_IMAGES];
   int cnt, overflow;
-  double R[5][5], xs[5], f[5];
+  double f[5];
+  double nu[5], nd[5], tau[5], den;  // lls5_wave: column norms (updated / direct), Householder taus
+  int perm[5], big;
   float x[5];
 };
 
-// Householder least squares (the oracle's lls5, same operation order), rows in global scratch.
+// Cmylapack::lls (mylapack.cpp:102-149, Eigen JacobiSVD(ThinU | ThinV).solve) with Eigen's algorithm,
+// the same operation order as the oracle's lls5 (oracle/filter_oracle.h): column-pivoting
+// Householder QR of the scaled n x 5 system (rows in global scratch; per-column sums by one lane
+// each, in row order; elementwise updates spread over the lanes), then two-sided Jacobi, sorting
+// and the rank-thresholded minimum-norm solve on the 5 x 5 factor by lane 0.
+__device__ __forceinline__ double dmaxd(double a, double b) { return (a < b) ? b : a; }  // std::max
 __device__ void lls5_wave(NbLds& L, double* M, double* r, int n) {
+  constexpr int N = 5;
+  const double eps = 2.220446049250313e-16, dmin = 2.2250738585072014e-308;
   const int lane = lane_id_w();
-  for (int k = 0; k < 5; ++k) {
-    if (lane == 0) {
-      double nrm = 0.0;
-      for (int i = k; i < n; ++i) nrm += M[(size_t)i * 5 + k] * M[(size_t)i * 5 + k];
-      nrm = sqrt(nrm);
-      const double akk = M[(size_t)k * 5 + k];
-      const double alpha = (akk > 0.0) ? -nrm : nrm;
-      M[(size_t)k * 5 + k] = akk - alpha;
-      double vnorm2 = 0.0;
-      for (int i = k; i < n; ++i) vnorm2 += M[(size_t)i * 5 + k] * M[(size_t)i * 5 + k];
-      L.R[k][k] = alpha;
-      L.f[0] = vnorm2;
-    }
+  auto bar = []() {
+    __threadfence_block();
     __syncthreads();
-    const double vnorm2 = L.f[0];
-    if (vnorm2 > 0.0) {
-      // columns j > k and the right-hand side: one lane each, sequential dot over rows
-      const int j = k + 1 + lane;
-      if (lane < 5 - k) {
-        double dotv = 0.0;
-        if (j < 5) {
-          for (int i = k; i < n; ++i) dotv += M[(size_t)i * 5 + k] * M[(size_t)i * 5 + j];
-          const double fj = 2.0 * dotv / vnorm2;
-          for (int i = k; i < n; ++i) M[(size_t)i * 5 + j] -= fj * M[(size_t)i * 5 + k];
-        } else {
-          for (int i = k; i < n; ++i) dotv += M[(size_t)i * 5 + k] * r[i];
-          const double fb = 2.0 * dotv / vnorm2;
-          for (int i = k; i < n; ++i) r[i] -= fb * M[(size_t)i * 5 + k];
+  };
+  // scale = max |a_ij| (exact in any order)
+  double mx = 0.0;
+  for (int u = lane; u < n * N; u += 64) mx = dmaxd(mx, fabs(M[u]));
+  for (int d = 32; d >= 1; d >>= 1) mx = dmaxd(mx, __shfl_xor(mx, d));
+  if (!isfinite(mx)) {
+    if (lane == 0)
+      for (int k = 0; k < N; ++k) L.x[k] = 0.0f;
+    bar();
+    return;
+  }
+  const double scale = (mx == 0.0) ? 1.0 : mx;
+  for (int u = lane; u < n * N; u += 64) M[u] = M[u] / scale;
+  bar();
+  // column norms (one lane per column, rows in order)
+  if (lane < N) {
+    double sq = 0.0;
+    for (int i = 0; i < n; ++i) sq += M[(size_t)i * N + lane] * M[(size_t)i * N + lane];
+    L.nu[lane] = L.nd[lane] = sqrt(sq);
+    L.perm[lane] = lane;
+  }
+  bar();
+  const double downdate = sqrt(eps);
+  for (int k = 0; k < N; ++k) {
+    if (lane == 0) {
+      int big = k;
+      for (int j = k + 1; j < N; ++j)
+        if (L.nu[j] > L.nu[big]) big = j;
+      L.big = big;
+      if (big != k) {
+        double t = L.nu[k]; L.nu[k] = L.nu[big]; L.nu[big] = t;
+        t = L.nd[k]; L.nd[k] = L.nd[big]; L.nd[big] = t;
+        const int pk = L.perm[k]; L.perm[k] = L.perm[big]; L.perm[big] = pk;
+      }
+    }
+    bar();
+    const int big = L.big;
+    if (big != k)
+      for (int i = lane; i < n; i += 64) {
+        const double t = M[(size_t)i * N + k];
+        M[(size_t)i * N + k] = M[(size_t)i * N + big];
+        M[(size_t)i * N + big] = t;
+      }
+    bar();
+    if (lane == 0) {  // makeHouseholderInPlace
+      double tail = 0.0;
+      for (int i = k + 1; i < n; ++i) tail += M[(size_t)i * N + k] * M[(size_t)i * N + k];
+      const double c0 = M[(size_t)k * N + k];
+      double beta, tau, den = 0.0;
+      if (tail <= dmin) {
+        tau = 0.0;
+        beta = c0;
+      } else {
+        beta = sqrt(c0 * c0 + tail);
+        if (c0 >= 0.0) beta = -beta;
+        den = c0 - beta;
+        tau = (beta - c0) / beta;
+      }
+      L.tau[k] = tau;
+      L.den = den;
+      M[(size_t)k * N + k] = beta;
+    }
+    bar();
+    const double tauk = L.tau[k], den = L.den;
+    for (int i = k + 1 + lane; i < n; i += 64) M[(size_t)i * N + k] = (tauk == 0.0) ? 0.0 : M[(size_t)i * N + k] / den;
+    bar();
+    if (tauk != 0.0 && lane > k && lane < N) {  // applyHouseholderOnTheLeft, column j = lane
+      const int j = lane;
+      double t = 0.0;
+      for (int i = k + 1; i < n; ++i) t += M[(size_t)i * N + k] * M[(size_t)i * N + j];
+      t += M[(size_t)k * N + j];
+      M[(size_t)k * N + j] -= tauk * t;
+      for (int i = k + 1; i < n; ++i) M[(size_t)i * N + j] -= (tauk * M[(size_t)i * N + k]) * t;
+    }
+    bar();
+    if (lane > k && lane < N && L.nu[lane] != 0.0) {  // norm downdating (LAPACK xGEQPF)
+      const int j = lane;
+      double t = fabs(M[(size_t)k * N + j]) / L.nu[j];
+      t = (1.0 + t) * (1.0 - t);
+      if (t < 0.0) t = 0.0;
+      const double q = L.nu[j] / L.nd[j];
+      const double t2 = t * (q * q);
+      if (t2 <= downdate) {
+        double sq = 0.0;
+        for (int i = k + 1; i < n; ++i) sq += M[(size_t)i * N + j] * M[(size_t)i * N + j];
+        L.nd[j] = L.nu[j] = sqrt(sq);
+      } else {
+        L.nu[j] *= sqrt(t);
+      }
+    }
+    bar();
+  }
+  // Q^T b
+  for (int k = 0; k < N; ++k) {
+    const double tauk = L.tau[k];
+    if (tauk == 0.0) continue;
+    if (lane == 0) {
+      double t = 0.0;
+      for (int i = k + 1; i < n; ++i) t += M[(size_t)i * N + k] * r[i];
+      t += r[k];
+      L.den = t;
+    }
+    bar();
+    const double t = L.den;
+    if (lane == 0) r[k] -= tauk * t;
+    for (int i = k + 1 + lane; i < n; i += 64) r[i] -= (tauk * M[(size_t)i * N + k]) * t;
+    bar();
+  }
+  if (lane == 0) {
+    double W[N][N], U[N][N], V[N][N];
+    for (int i = 0; i < N; ++i)
+      for (int j = 0; j < N; ++j) {
+        W[i][j] = (j >= i) ? M[(size_t)i * N + j] : 0.0;
+        U[i][j] = V[i][j] = (i == j) ? 1.0 : 0.0;
+      }
+    double maxd = 0.0;
+    for (int i = 0; i < N; ++i) maxd = dmaxd(maxd, fabs(W[i][i]));
+    bool finished = false;
+    for (int sweep = 0; !finished && sweep < 100; ++sweep) {
+      finished = true;
+      for (int p = 1; p < N; ++p)
+        for (int q = 0; q < p; ++q) {
+          const double thr = dmaxd(dmin, 2.0 * eps * maxd);
+          if (!(fabs(W[p][q]) > thr || fabs(W[q][p]) > thr)) continue;
+          finished = false;
+          double m00 = W[p][p], m01 = W[p][q], m10 = W[q][p], m11 = W[q][q];
+          const double t = m00 + m11, d = m10 - m01;
+          double c1 = 1.0, s1 = 0.0;
+          if (!(fabs(d) < dmin)) {
+            const double u = t / d;
+            const double tmp = sqrt(1.0 + u * u);
+            s1 = 1.0 / tmp;
+            c1 = u / tmp;
+          }
+          {
+            const double a0 = m00, a1 = m01, b0 = m10, b1 = m11;
+            m00 = c1 * a0 + s1 * b0; m01 = c1 * a1 + s1 * b1;
+            m10 = -s1 * a0 + c1 * b0; m11 = -s1 * a1 + c1 * b1;
+          }
+          double cr = 1.0, sr = 0.0;
+          const double deno = 2.0 * fabs(m01);
+          if (!(deno < dmin)) {
+            const double tau_ = (m00 - m11) / deno;
+            const double w = sqrt(tau_ * tau_ + 1.0);
+            const double tt = (tau_ > 0.0) ? 1.0 / (tau_ + w) : 1.0 / (tau_ - w);
+            const double sign_t = tt > 0.0 ? 1.0 : -1.0;
+            const double nn = 1.0 / sqrt(tt * tt + 1.0);
+            sr = -sign_t * (m01 / fabs(m01)) * fabs(tt) * nn;
+            cr = nn;
+          }
+          const double cl = c1 * cr - s1 * (-sr);
+          const double sl = c1 * (-sr) + s1 * cr;
+          for (int j = 0; j < N; ++j) {  // W rows p, q by j_left
+            const double xp = W[p][j], xq = W[q][j];
+            W[p][j] = cl * xp + sl * xq;
+            W[q][j] = -sl * xp + cl * xq;
+          }
+          for (int i = 0; i < N; ++i) {  // U columns p, q by j_left^T
+            const double xp = U[i][p], xq = U[i][q];
+            U[i][p] = cl * xp - (-sl) * xq;
+            U[i][q] = (-sl) * xp + cl * xq;
+          }
+          for (int i = 0; i < N; ++i) {  // W columns p, q by j_right
+            const double xp = W[i][p], xq = W[i][q];
+            W[i][p] = cr * xp - sr * xq;
+            W[i][q] = sr * xp + cr * xq;
+          }
+          for (int i = 0; i < N; ++i) {  // V columns p, q by j_right
+            const double xp = V[i][p], xq = V[i][q];
+            V[i][p] = cr * xp - sr * xq;
+            V[i][q] = sr * xp + cr * xq;
+          }
+          maxd = dmaxd(maxd, dmaxd(fabs(W[p][p]), fabs(W[q][q])));
+        }
+    }
+    double sv[N];
+    for (int i = 0; i < N; ++i) {
+      sv[i] = fabs(W[i][i]);
+      if (W[i][i] < 0.0)
+        for (int k = 0; k < N; ++k) U[k][i] = -U[k][i];
+    }
+    for (int i = 0; i < N; ++i) sv[i] *= scale;
+    int nonzero = N;
+    for (int i = 0; i < N; ++i) {
+      int pos = i;
+      for (int j = i + 1; j < N; ++j)
+        if (sv[j] > sv[pos]) pos = j;
+      if (sv[pos] == 0.0) {
+        nonzero = i;
+        break;
+      }
+      if (pos != i) {
+        double t = sv[i]; sv[i] = sv[pos]; sv[pos] = t;
+        for (int k = 0; k < N; ++k) {
+          t = U[k][i]; U[k][i] = U[k][pos]; U[k][pos] = t;
+          t = V[k][i]; V[k][i] = V[k][pos]; V[k][pos] = t;
         }
       }
     }
-    __syncthreads();
-    if (lane == 0)
-      for (int jj = k + 1; jj < 5; ++jj) L.R[k][jj] = M[(size_t)k * 5 + jj];
-    __syncthreads();
-  }
-  if (lane == 0) {
-    for (int k = 4; k >= 0; --k) {
-      double v = r[k];
-      for (int j = k + 1; j < 5; ++j) v -= L.R[k][j] * L.xs[j];
-      L.xs[k] = (L.R[k][k] != 0.0) ? v / L.R[k][k] : 0.0;
+    int rank = 0;
+    if (nonzero > 0) {
+      const double pre = dmaxd(sv[0] * (N * eps), dmin);
+      int i = nonzero - 1;
+      while (i >= 0 && sv[i] < pre) --i;
+      rank = i + 1;
     }
-    for (int k = 0; k < 5; ++k) L.x[k] = (float)L.xs[k];
+    double y[N], z[N];
+    for (int i = 0; i < rank; ++i) {
+      double t = 0.0;
+      for (int k = 0; k < N; ++k) t += U[k][i] * r[k];
+      y[i] = t / sv[i];
+    }
+    for (int k = 0; k < N; ++k) {
+      double t = 0.0;
+      for (int i = 0; i < rank; ++i) t += V[k][i] * y[i];
+      z[k] = t;
+    }
+    for (int k = 0; k < N; ++k) L.x[L.perm[k]] = (float)z[k];
   }
-  __syncthreads();
+  bar();
 }
 
 // Sort a[0..n) ascending (bitonic over the next power of two, padded with INT_MAX) and drop

@@ -17,8 +17,9 @@
 // on pointer order (findNeighbors sorts neighbours by address, which feeds the float sums and
 // the least-squares fit of filterQuad).  Here insertion order = patch array index, and
 // neighbour lists are sorted by array index.  Cmylapack::lls (Eigen JacobiSVD, absent from the
-// image) is replaced by a Householder-QR least-squares solve in double: filterQuad decisions
-// are therefore "parity unpinned" against the reference binary.
+// image) is restated with Eigen's algorithm (column-pivoting QR preconditioner, two-sided Jacobi,
+// rank-thresholded minimum-norm solve; lls5 below): filterQuad decisions are "parity unpinned"
+// against the reference binary (Eigen's vectorised reductions sum in another order).
 #pragma once
 
 #include <array>
@@ -414,48 +415,218 @@ static void ortho4(const V4& z, V4& x, V4& y) {
   y[2] = z[0] * x[1] - z[1] * x[0];
 }
 
-// Least squares min ||A x - b|| for an n x 5 system in double by Householder QR
-// (replaces Cmylapack::lls = Eigen JacobiSVD solve, mylapack.cpp:102-149; parity unpinned).
+// Cmylapack::lls (mylapack.cpp:102-149): x = A.jacobiSvd(ComputeThinU | ComputeThinV).solve(b) in
+// double for an n x 5 system (n >= 6), restated with Eigen 3.3's JacobiSVD algorithm (Eigen is absent
+// from the image; parity unpinned against it):
+//   1. scale = max|a_ij| (1 if 0); the scaled matrix is reduced by a column-pivoting Householder
+//      QR (ColPivHouseholderQRPreconditioner: pivot = largest updated column norm, LAPACK xGEQPF
+//      norm downdating, makeHouseholder: beta = -sign(c0) |x|, tau = (beta - c0) / beta,
+//      essential = tail / (c0 - beta));
+//   2. two-sided Jacobi sweeps on the 5 x 5 R (pairs p > q, threshold max(DBL_MIN, 2 eps max|diag|),
+//      real_2x2_jacobi_svd + makeJacobi rotations, left rotations accumulated into U, right into V);
+//   3. singular values |diag| * scale (U column negated for a negative diagonal), sorted descending;
+//   4. solve with rank = #{s_i >= max(s_0 * 5 eps, DBL_MIN)}: x = V_r diag(1/s_r) U_r^T b -- the
+//      minimum-norm least-squares solution on rank-deficient neighbourhoods.
+// Sums run in index order; U^T b is formed as (Q^T b)[0..4] rotated by the accumulated 5 x 5 U.
 static void lls5(const std::vector<std::array<float, 5>>& A, const std::vector<float>& b, float x[5]) {
   const int n = (int)A.size();
-  std::vector<double> M((size_t)n * 5), r(n);
+  constexpr int N = 5;
+  const double eps = 2.220446049250313e-16, dmin = 2.2250738585072014e-308;
+  std::vector<double> M((size_t)n * N), r(n);
+  double scale = 0.0;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < N; ++j) scale = std::max(scale, std::fabs((double)A[i][j]));
+  if (!std::isfinite(scale)) {  // Eigen reports InvalidInput; the solve then returns garbage: zeros here
+    for (int k = 0; k < N; ++k) x[k] = 0.0f;
+    return;
+  }
+  if (scale == 0.0) scale = 1.0;
   for (int i = 0; i < n; ++i) {
-    for (int j = 0; j < 5; ++j) M[(size_t)i * 5 + j] = A[i][j];
+    for (int j = 0; j < N; ++j) M[(size_t)i * N + j] = (double)A[i][j] / scale;
     r[i] = b[i];
   }
-  double R[5][5] = {{0}};
-  for (int k = 0; k < 5; ++k) {
-    double nrm = 0.0;
-    for (int i = k; i < n; ++i) nrm += M[(size_t)i * 5 + k] * M[(size_t)i * 5 + k];
-    nrm = std::sqrt(nrm);
-    const double akk = M[(size_t)k * 5 + k];
-    const double alpha = (akk > 0.0) ? -nrm : nrm;
-    // v = a_k - alpha e_k (stored in column k, rows k..n-1)
-    M[(size_t)k * 5 + k] = akk - alpha;
-    double vnorm2 = 0.0;
-    for (int i = k; i < n; ++i) vnorm2 += M[(size_t)i * 5 + k] * M[(size_t)i * 5 + k];
-    if (vnorm2 > 0.0) {
-      for (int j = k + 1; j < 5; ++j) {
-        double dotv = 0.0;
-        for (int i = k; i < n; ++i) dotv += M[(size_t)i * 5 + k] * M[(size_t)i * 5 + j];
-        const double f = 2.0 * dotv / vnorm2;
-        for (int i = k; i < n; ++i) M[(size_t)i * 5 + j] -= f * M[(size_t)i * 5 + k];
-      }
-      double dotb = 0.0;
-      for (int i = k; i < n; ++i) dotb += M[(size_t)i * 5 + k] * r[i];
-      const double f = 2.0 * dotb / vnorm2;
-      for (int i = k; i < n; ++i) r[i] -= f * M[(size_t)i * 5 + k];
+  auto at = [&](int i, int j) -> double& { return M[(size_t)i * N + j]; };
+  // ---- 1. column-pivoting Householder QR
+  int perm[N];
+  double nu[N], nd[N], tau[N];
+  for (int j = 0; j < N; ++j) {
+    perm[j] = j;
+    double sq = 0.0;
+    for (int i = 0; i < n; ++i) sq += at(i, j) * at(i, j);
+    nd[j] = nu[j] = std::sqrt(sq);
+  }
+  const double downdate = std::sqrt(eps);
+  for (int k = 0; k < N; ++k) {
+    int big = k;
+    for (int j = k + 1; j < N; ++j)
+      if (nu[j] > nu[big]) big = j;
+    if (big != k) {
+      for (int i = 0; i < n; ++i) std::swap(at(i, k), at(i, big));
+      std::swap(nu[k], nu[big]);
+      std::swap(nd[k], nd[big]);
+      std::swap(perm[k], perm[big]);
     }
-    R[k][k] = alpha;
-    for (int j = k + 1; j < 5; ++j) R[k][j] = M[(size_t)k * 5 + j];
+    double tail = 0.0;
+    for (int i = k + 1; i < n; ++i) tail += at(i, k) * at(i, k);
+    const double c0 = at(k, k);
+    double beta;
+    if (tail <= dmin) {
+      tau[k] = 0.0;
+      beta = c0;
+      for (int i = k + 1; i < n; ++i) at(i, k) = 0.0;
+    } else {
+      beta = std::sqrt(c0 * c0 + tail);
+      if (c0 >= 0.0) beta = -beta;
+      const double den = c0 - beta;
+      for (int i = k + 1; i < n; ++i) at(i, k) = at(i, k) / den;
+      tau[k] = (beta - c0) / beta;
+    }
+    at(k, k) = beta;
+    if (tau[k] != 0.0)
+      for (int j = k + 1; j < N; ++j) {
+        double t = 0.0;
+        for (int i = k + 1; i < n; ++i) t += at(i, k) * at(i, j);
+        t += at(k, j);
+        at(k, j) -= tau[k] * t;
+        for (int i = k + 1; i < n; ++i) at(i, j) -= (tau[k] * at(i, k)) * t;
+      }
+    for (int j = k + 1; j < N; ++j) {
+      if (nu[j] == 0.0) continue;
+      double t = std::fabs(at(k, j)) / nu[j];
+      t = (1.0 + t) * (1.0 - t);
+      if (t < 0.0) t = 0.0;
+      const double q = nu[j] / nd[j];
+      const double t2 = t * (q * q);
+      if (t2 <= downdate) {
+        double sq = 0.0;
+        for (int i = k + 1; i < n; ++i) sq += at(i, j) * at(i, j);
+        nd[j] = nu[j] = std::sqrt(sq);
+      } else {
+        nu[j] *= std::sqrt(t);
+      }
+    }
   }
-  double xs[5];
-  for (int k = 4; k >= 0; --k) {
-    double v = r[k];
-    for (int j = k + 1; j < 5; ++j) v -= R[k][j] * xs[j];
-    xs[k] = (R[k][k] != 0.0) ? v / R[k][k] : 0.0;
+  // Q^T b (H_0 first)
+  for (int k = 0; k < N; ++k) {
+    if (tau[k] == 0.0) continue;
+    double t = 0.0;
+    for (int i = k + 1; i < n; ++i) t += at(i, k) * r[i];
+    t += r[k];
+    r[k] -= tau[k] * t;
+    for (int i = k + 1; i < n; ++i) r[i] -= (tau[k] * at(i, k)) * t;
   }
-  for (int k = 0; k < 5; ++k) x[k] = (float)xs[k];
+  // ---- 2. two-sided Jacobi on R
+  double W[N][N], U[N][N], V[N][N];
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) {
+      W[i][j] = (j >= i) ? at(i, j) : 0.0;
+      U[i][j] = V[i][j] = (i == j) ? 1.0 : 0.0;
+    }
+  double maxd = 0.0;
+  for (int i = 0; i < N; ++i) maxd = std::max(maxd, std::fabs(W[i][i]));
+  auto rot_left = [&](double (*X)[N], int p, int q, double c, double s_) {  // rows p, q
+    for (int j = 0; j < N; ++j) {
+      const double xp = X[p][j], xq = X[q][j];
+      X[p][j] = c * xp + s_ * xq;
+      X[q][j] = -s_ * xp + c * xq;
+    }
+  };
+  auto rot_right = [&](double (*X)[N], int p, int q, double c, double s_) {  // columns p, q by (c, s)^T
+    for (int i = 0; i < N; ++i) {
+      const double xp = X[i][p], xq = X[i][q];
+      X[i][p] = c * xp - s_ * xq;
+      X[i][q] = s_ * xp + c * xq;
+    }
+  };
+  bool finished = false;
+  for (int sweep = 0; !finished && sweep < 100; ++sweep) {
+    finished = true;
+    for (int p = 1; p < N; ++p)
+      for (int q = 0; q < p; ++q) {
+        const double thr = std::max(dmin, 2.0 * eps * maxd);
+        if (!(std::fabs(W[p][q]) > thr || std::fabs(W[q][p]) > thr)) continue;
+        finished = false;
+        // real_2x2_jacobi_svd on [[W_pp, W_pq], [W_qp, W_qq]]
+        double m00 = W[p][p], m01 = W[p][q], m10 = W[q][p], m11 = W[q][q];
+        const double t = m00 + m11, d = m10 - m01;
+        double c1 = 1.0, s1 = 0.0;
+        if (!(std::fabs(d) < dmin)) {
+          const double u = t / d;
+          const double tmp = std::sqrt(1.0 + u * u);
+          s1 = 1.0 / tmp;
+          c1 = u / tmp;
+        }
+        {  // m.applyOnTheLeft(0, 1, rot1)
+          const double a0 = m00, a1 = m01, b0 = m10, b1 = m11;
+          m00 = c1 * a0 + s1 * b0; m01 = c1 * a1 + s1 * b1;
+          m10 = -s1 * a0 + c1 * b0; m11 = -s1 * a1 + c1 * b1;
+        }
+        double cr = 1.0, sr = 0.0;  // makeJacobi(m00, m01, m11)
+        const double deno = 2.0 * std::fabs(m01);
+        if (!(deno < dmin)) {
+          const double tau_ = (m00 - m11) / deno;
+          const double w = std::sqrt(tau_ * tau_ + 1.0);
+          const double tt = (tau_ > 0.0) ? 1.0 / (tau_ + w) : 1.0 / (tau_ - w);
+          const double sign_t = tt > 0.0 ? 1.0 : -1.0;
+          const double nn = 1.0 / std::sqrt(tt * tt + 1.0);
+          sr = -sign_t * (m01 / std::fabs(m01)) * std::fabs(tt) * nn;
+          cr = nn;
+        }
+        // j_left = rot1 * j_right^T, with j_right^T = (cr, -sr)
+        const double cl = c1 * cr - s1 * (-sr);
+        const double sl = c1 * (-sr) + s1 * cr;
+        rot_left(W, p, q, cl, sl);
+        rot_right(U, p, q, cl, -sl);  // U.applyOnTheRight(p, q, j_left^T)
+        rot_right(W, p, q, cr, sr);
+        rot_right(V, p, q, cr, sr);
+        maxd = std::max(maxd, std::max(std::fabs(W[p][p]), std::fabs(W[q][q])));
+      }
+  }
+  // ---- 3. singular values, signs, scale; 4. sort descending
+  double sv[N];
+  for (int i = 0; i < N; ++i) {
+    sv[i] = std::fabs(W[i][i]);
+    if (W[i][i] < 0.0)
+      for (int k = 0; k < N; ++k) U[k][i] = -U[k][i];
+  }
+  for (int i = 0; i < N; ++i) sv[i] *= scale;
+  int nonzero = N;
+  for (int i = 0; i < N; ++i) {
+    int pos = i;
+    for (int j = i + 1; j < N; ++j)
+      if (sv[j] > sv[pos]) pos = j;
+    if (sv[pos] == 0.0) {
+      nonzero = i;
+      break;
+    }
+    if (pos != i) {
+      std::swap(sv[i], sv[pos]);
+      for (int k = 0; k < N; ++k) {
+        std::swap(U[k][i], U[k][pos]);
+        std::swap(V[k][i], V[k][pos]);
+      }
+    }
+  }
+  int rank = 0;
+  if (nonzero > 0) {
+    const double pre = std::max(sv[0] * (N * eps), dmin);
+    int i = nonzero - 1;
+    while (i >= 0 && sv[i] < pre) --i;
+    rank = i + 1;
+  }
+  // ---- 5. x = P V_r diag(1/s_r) U_r^T (Q^T b)[0..4]
+  double y[N], z[N];
+  for (int i = 0; i < rank; ++i) {
+    double t = 0.0;
+    for (int k = 0; k < N; ++k) t += U[k][i] * r[k];
+    y[i] = t / sv[i];
+  }
+  for (int k = 0; k < N; ++k) {
+    double t = 0.0;
+    for (int i = 0; i < rank; ++i) t += V[k][i] * y[i];
+    z[k] = t;
+  }
+  for (int k = 0; k < N; ++k) x[perm[k]] = (float)z[k];
 }
 
 // CFilter::filterQuad (filter.cpp:387-446).

@@ -1302,4 +1302,14 @@ void oracle_seed_geometry(void* h, int i0, int i1, const float* xy0, const float
   }
 }
 
+
+// Cmylapack::lls restated (filter_oracle.h lls5) on an n x 5 float system, for tests/test_lls.py.
+void oracle_lls5(const float* A, const float* b, int n, float* x) {
+  std::vector<std::array<float, 5>> a(n);
+  std::vector<float> bb(b, b + n);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < 5; ++j) a[i][j] = A[5 * i + j];
+  lls5(a, bb, x);
+}
+
 }  // extern "C"

@@ -57,6 +57,7 @@ def lib():
                                              C.c_void_p, C.c_int]
         L.oracle_seed_geometry.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
                                            C.c_void_p, C.c_void_p]
+        L.oracle_lls5.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
         L.oracle_bobyqa_test.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_int, C.POINTER(C.c_int)]
         _lib = L
@@ -278,6 +279,15 @@ class OracleScene:
         st = P.Stats()
         lib().oracle_refine_batch(self.h, _p(cands), len(cands), _p(out), nthreads, C.byref(st))
         return out, st.as_dict()
+
+
+def lls5(A, b):
+    """Cmylapack::lls restated (Eigen JacobiSVD semantics): float32 x[5] for an n x 5 system."""
+    A = np.ascontiguousarray(A, np.float32).reshape(-1, 5)
+    b = np.ascontiguousarray(b, np.float32)
+    x = np.zeros(5, np.float32)
+    lib().oracle_lls5(_p(A), _p(b), len(A), _p(x))
+    return x
 
 
 def bobyqa_test(kind, x0, maxeval=1000, maxrec=2000):
