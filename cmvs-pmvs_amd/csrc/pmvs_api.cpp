@@ -149,6 +149,18 @@ void build_binary(std::vector<uint8_t>* pyr, const int* w, const int* h, int max
   }
 }
 
+// PMVS_POISON_ALLOC=<byte>: fill new device allocations with that byte (uninitialised-read hunting).
+inline void poison_alloc(void* p, size_t bytes) {
+  static const int v = [] {
+    const char* e = getenv("PMVS_POISON_ALLOC");
+    return e ? atoi(e) : -1;
+  }();
+  if (v >= 0 && p && bytes) {
+    (void)hipMemset(p, v & 0xff, bytes);
+    (void)hipDeviceSynchronize();
+  }
+}
+
 template <class T>
 struct DBuf {
   T* p = nullptr;
@@ -157,7 +169,9 @@ struct DBuf {
     release();
     n = count;
     if (count == 0) return hipSuccess;
-    return hipMalloc((void**)&p, count * sizeof(T));
+    const hipError_t e = hipMalloc((void**)&p, count * sizeof(T));
+    if (e == hipSuccess) poison_alloc(p, count * sizeof(T));
+    return e;
   }
   void release() {
     if (p) (void)hipFree(p);
@@ -237,7 +251,9 @@ int grow_alive(pmvs_scene* sc, int n) {
   if (X.alive) (void)hipFree(X.alive);
   X.alive = nullptr;
   X.cap_alive = (size_t)n;
-  return hipMalloc((void**)&X.alive, (size_t)n * sizeof(int)) == hipSuccess ? 0 : 1;
+  if (hipMalloc((void**)&X.alive, (size_t)n * sizeof(int)) != hipSuccess) return 1;
+  poison_alloc(X.alive, (size_t)n * sizeof(int));
+  return 0;
 }
 }  // namespace
 
@@ -763,6 +779,16 @@ pmvs_status pmvs_selftest_math(int32_t device, int32_t op, const double* in, dou
   (void)hipFree(di);
   if (dout) (void)hipFree(dout);
   if (e != hipSuccess) return fail(PMVS_EDEVICE, "math selftest: %s", hipGetErrorString(e));
+  return PMVS_OK;
+}
+
+pmvs_status pmvs_selftest_lls(int32_t device, const float* A, const float* b, const int32_t* offsets, int32_t nsys,
+                              float* x) {
+  if (!A || !b || !offsets || !x || nsys <= 0) return fail(PMVS_EINVAL, "null argument");
+  for (int k = 0; k < nsys; ++k)
+    if (offsets[k + 1] - offsets[k] < 5) return fail(PMVS_EINVAL, "system %d has fewer than 5 rows", k);
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(lls_selftest(A, b, offsets, nsys, offsets[nsys], x));
   return PMVS_OK;
 }
 

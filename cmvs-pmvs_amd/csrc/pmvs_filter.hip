@@ -40,6 +40,19 @@
 
 namespace pmvsdev {
 
+// Debug builds of the tests: PMVS_POISON_ALLOC=<byte> fills every new device allocation with that
+// byte, so a read of memory no kernel wrote shows up as a result change (tests/test_gpu_poison.py).
+inline void poison_alloc(void* p, size_t bytes) {
+  static const int v = [] {
+    const char* e = getenv("PMVS_POISON_ALLOC");
+    return e ? atoi(e) : -1;
+  }();
+  if (v >= 0 && p && bytes) {
+    (void)hipMemset(p, v & 0xff, bytes);
+    (void)hipDeviceSynchronize();
+  }
+}
+
 constexpr int NB_CAP = 1024;  // neighbours per patch in filterNeighbor (overflow is reported)
 __device__ __forceinline__ int lane_id_w() { return threadIdx.x & 63; }
 // Wave-uniform copies (SGPR) of values that are uniform by construction but loaded from memory:
@@ -1363,7 +1376,9 @@ template <class T>
 static hipError_t dalloc(T*& p, size_t n) {
   if (p) (void)hipFree(p);
   p = nullptr;
-  return hipMalloc((void**)&p, (n ? n : 1) * sizeof(T));
+  const hipError_t e = hipMalloc((void**)&p, (n ? n : 1) * sizeof(T));
+  if (e == hipSuccess) poison_alloc(p, (n ? n : 1) * sizeof(T));
+  return e;
 }
 
 FilterBuffers::~FilterBuffers() {
@@ -1795,7 +1810,9 @@ static hipError_t grow(T*& p, size_t& cap, size_t need) {
   if (p) (void)hipFree(p);
   p = nullptr;
   cap = need;
-  return hipMalloc((void**)&p, (need ? need : 1) * sizeof(T));
+  const hipError_t e = hipMalloc((void**)&p, (need ? need : 1) * sizeof(T));
+  if (e == hipSuccess) poison_alloc(p, (need ? need : 1) * sizeof(T));
+  return e;
 }
 
 }  // namespace
@@ -1814,6 +1831,7 @@ static hipError_t grow_keep(T*& p, size_t& cap, size_t need, size_t used, hipStr
   const size_t ncap = std::max(need, cap * 2 + 1024);
   T* q = nullptr;
   FCHK(hipMalloc((void**)&q, ncap * sizeof(T)));
+  poison_alloc(q, ncap * sizeof(T));
   if (p && used) FCHK(hipMemcpyAsync(q, p, used * sizeof(T), hipMemcpyDeviceToDevice, st));
   FCHK(hipStreamSynchronize(st));
   if (p) (void)hipFree(p);
@@ -2210,6 +2228,48 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
   }
   *n_out = nmodel;
   return hipGetLastError();
+}
+
+// Self-test of lls5_wave (tests/test_gpu_lls.py): one workgroup per n x 5 system.
+__global__ __launch_bounds__(64) void lls_selftest_kernel(const float* __restrict__ A, const float* __restrict__ b,
+                                                          const int* __restrict__ off, int nsys, double* __restrict__ scratch,
+                                                          float* __restrict__ x) {
+  __shared__ NbLds L;
+  const int sys = blockIdx.x;
+  if (sys >= nsys) return;
+  const int o = off[sys], n = off[sys + 1] - off[sys];
+  double* M = scratch + (size_t)o * 6;
+  double* r = M + (size_t)n * 5;
+  for (int i = threadIdx.x; i < n; i += 64) {
+    for (int j = 0; j < 5; ++j) M[(size_t)i * 5 + j] = (double)A[(size_t)(o + i) * 5 + j];
+    r[i] = (double)b[o + i];
+  }
+  __threadfence_block();
+  __syncthreads();
+  lls5_wave(L, M, r, n);
+  if (threadIdx.x < 5) x[(size_t)sys * 5 + threadIdx.x] = L.x[threadIdx.x];
+}
+
+hipError_t lls_selftest(const float* A, const float* b, const int* off, int nsys, int total, float* x) {
+  float *dA = nullptr, *db = nullptr, *dx = nullptr;
+  int* doff = nullptr;
+  double* scr = nullptr;
+  hipError_t e = hipMalloc((void**)&dA, (size_t)total * 5 * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc((void**)&db, (size_t)total * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc((void**)&dx, (size_t)nsys * 5 * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc((void**)&doff, (size_t)(nsys + 1) * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc((void**)&scr, (size_t)total * 6 * sizeof(double));
+  if (e == hipSuccess) e = hipMemcpy(dA, A, (size_t)total * 5 * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(db, b, (size_t)total * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(doff, off, (size_t)(nsys + 1) * sizeof(int), hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(lls_selftest_kernel, dim3(nsys), dim3(64), 0, nullptr, dA, db, doff, nsys, scr, dx);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(x, dx, (size_t)nsys * 5 * sizeof(float), hipMemcpyDeviceToHost);
+  for (void* p : {(void*)dA, (void*)db, (void*)dx, (void*)doff, (void*)scr})
+    if (p) (void)hipFree(p);
+  return e;
 }
 
 // ============================================================================ loop helpers

@@ -83,6 +83,7 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
 hipError_t compact_model(FilterBuffers& B, const pmvs_patch* src, int n, const int* keep, pmvs_patch* dst, int* nkept,
                          hipStream_t st);
 hipError_t fill_int(int* a, int n, int v, hipStream_t st);
+hipError_t lls_selftest(const float* A, const float* b, const int* off, int nsys, int total, float* x);
 
 // ---- seed phase (pmvs_seed.hip)
 struct SeedInput {

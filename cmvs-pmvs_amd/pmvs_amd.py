@@ -131,7 +131,7 @@ EXPORTS = ["pmvs_last_error", "pmvs_device_count", "pmvs_scene_create", "pmvs_sc
            "pmvs_write_ply", "pmvs_patch_colors", "pmvs_filter_run",
            "pmvs_expand_run", "pmvs_expand_fetch", "pmvs_run_loop", "pmvs_loop_fetch", "pmvs_scene_set_shard", "pmvs_thread_exchange_create",
            "pmvs_thread_exchange_ctx", "pmvs_thread_allgather", "pmvs_thread_exchange_destroy", "pmvs_detect_features",
-           "pmvs_seed_run", "pmvs_image_load", "pmvs_pnm_mask_load", "pmvs_set_edge"]
+           "pmvs_seed_run", "pmvs_selftest_lls", "pmvs_image_load", "pmvs_pnm_mask_load", "pmvs_set_edge"]
 
 # int fn(void* ctx, const void* send, int64_t bytes, void* recv): all-gather (pmvs_allgather_fn)
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p)
@@ -169,6 +169,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
                                           C.c_float, C.c_float, C.c_void_p]
     lib.pmvs_selftest_bobyqa.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_int32,
                                          C.c_void_p, C.POINTER(C.c_double)]
+    lib.pmvs_selftest_lls.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
     lib.pmvs_selftest_math.argtypes = [C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32]
     lib.pmvs_camera_load.argtypes = [C.c_char_p, C.c_void_p]
     lib.pmvs_image_load.argtypes = [C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_void_p]
@@ -495,6 +496,17 @@ def selftest_math(op: int, x: np.ndarray, device: int = 0) -> np.ndarray:
     out = np.zeros_like(x)
     _check(load_library().pmvs_selftest_math(device, op, _ptr(x), _ptr(out), len(x)))
     return out
+
+
+def selftest_lls(systems, device: int = 0) -> np.ndarray:
+    """Device lls (filterQuad's least squares) on a list of (A [n, 5], b [n]) systems: x [k, 5]."""
+    A = np.ascontiguousarray(np.concatenate([np.asarray(a, np.float32).reshape(-1, 5) for a, _ in systems]))
+    b = np.ascontiguousarray(np.concatenate([np.asarray(v, np.float32).reshape(-1) for _, v in systems]))
+    off = np.zeros(len(systems) + 1, np.int32)
+    off[1:] = np.cumsum([len(v) for _, v in systems])
+    x = np.zeros((len(systems), 5), np.float32)
+    _check(load_library().pmvs_selftest_lls(device, _ptr(A), _ptr(b), _ptr(off), len(systems), _ptr(x)))
+    return x
 
 
 def selftest_bobyqa(kind: int, x0: np.ndarray, mode: int = 0, maxeval: int = 1000, device: int = 0):

@@ -208,6 +208,12 @@ pmvs_status pmvs_scene_sync(pmvs_scene* scene, pmvs_stats* stats);
  * 5 atan, 6 log, 7 f32 sqrt, 8 f32 divide in[i]/in[i+1], 9 floor) on n doubles. */
 pmvs_status pmvs_selftest_math(int32_t device, int32_t op, const double* in, double* out, int32_t n);
 
+/* Self-test: the device Cmylapack::lls (filterQuad's least squares, Eigen JacobiSVD semantics) on
+ * nsys n_k x 5 systems: rows offsets[k] .. offsets[k+1]-1 of A (5 floats per row) and b; x: 5 floats
+ * per system. */
+pmvs_status pmvs_selftest_lls(int32_t device, const float* A, const float* b, const int32_t* offsets, int32_t nsys,
+                              float* x);
+
 /* Self-test: device BOBYQA on analytic objective `kind` (0 quadratic, 1 Rosenbrock-3, 2 bound
  * active) from n start points x0 (3 doubles each).  mode 0 = one problem per lane, 1 = one per
  * wavefront.  out: 6 doubles per problem (x[3], minf, nevals, result code); *ms kernel time. */
