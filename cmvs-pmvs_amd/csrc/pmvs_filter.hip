@@ -1817,11 +1817,13 @@ static hipError_t grow(T*& p, size_t& cap, size_t need) {
 
 }  // namespace
 
+void delete_commit_work(CommitWork* w);  // after CommitWork's definition
 ExpandBuffers::~ExpandBuffers() {
   void* ps[] = {parents, cand_coord, cand_ok, cand, prep, status, slots, cand2, prep2, res, outp, ostatus, counts, alive,
-                pg_head, vp_head, d_item, d_next, pool_used, tcells, tvals, qtmp, crec, acc, dupd, cellinit};
+                pg_head, vp_head, d_item, d_next, pool_used, tcells, tvals, qtmp, crec, acc, dupd, cellinit, occ};
   for (void* p : ps)
     if (p) (void)hipFree(p);
+  delete_commit_work(cm);
 }
 
 // Grows a device array keeping its contents (the delta-chain entry pool).
@@ -1838,6 +1840,367 @@ static hipError_t grow_keep(T*& p, size_t& cap, size_t need, size_t used, hipStr
   p = q;
   cap = ncap;
   return hipSuccess;
+}
+
+// ============================================================================ device commit
+// CExpand's commit of a wave (expand.cpp:225-266 addPatch + checkCounts, :309-406 updateCounts) in
+// (parent priority, direction) order k = 6 * parent + direction, on the device.  The decision of
+// candidate k depends on the counts / occupancy of its cells as left by every earlier candidate
+// that touches one of them; candidates that share no cell with an undecided earlier candidate
+// are decided in the same round.  Every access (prep cells read by checkCounts, image / vimage
+// cells written by updateCounts and addPatch) is sorted by (cell, k); a round marks, per cell,
+// the first undecided candidate, and decides every candidate that is first in all of its cells
+// (so each cell has one writer per round and plain stores suffice).  The result is the
+// sequential commit exactly, in as many rounds as the longest chain of cell-sharing candidates.
+struct CommitWork {
+  int *stc = nullptr, *nacc = nullptr, *aoff = nullptr, *vals = nullptr, *vals2 = nullptr, *pos = nullptr,
+      *head = nullptr, *segid = nullptr, *seghead = nullptr, *segptr = nullptr, *segfirst = nullptr,
+      *slot2 = nullptr, *flag = nullptr, *scan = nullptr, *ctr = nullptr, *pbits = nullptr;
+  unsigned long long *keys = nullptr, *keys2 = nullptr;
+  unsigned char* dec = nullptr;
+  int2* push = nullptr;
+  void* temp = nullptr;
+  size_t cap_k = 0, cap_a = 0, temp_bytes = 0;
+  ~CommitWork() {
+    void* ps[] = {stc, nacc, aoff, vals, vals2, pos, head, segid, seghead, segptr, segfirst, slot2, flag, scan, ctr,
+                  pbits, keys, keys2, dec, push, temp};
+    for (void* p : ps)
+      if (p) (void)hipFree(p);
+  }
+};
+
+void delete_commit_work(CommitWork* w) { delete w; }
+
+// occupancy per target cell after the model load: pgrids holds a patch
+__global__ void occ_init_kernel(const int* __restrict__ pg_off, long long ncells, unsigned char* __restrict__ occ) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < ncells) occ[c] = pg_off[c + 1] > pg_off[c] ? 1 : 0;
+}
+
+// per k: outcome so far (-1 no candidate, 1 prepare failed, 2 / 3 refine failed, 9 invalid record,
+// 0 refined: to be decided) and its number of cell accesses
+__global__ void cm_stage_kernel(const int* __restrict__ status, const int* __restrict__ slot2, const int* __restrict__ rec,
+                                int nk, int* __restrict__ stc, int* __restrict__ nacc, unsigned char* __restrict__ dec,
+                                int* __restrict__ nlive) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nk) return;
+  int st = status[k], a = 0;
+  unsigned char d = 1;
+  if (st < 0) {
+    st = -1;
+  } else if (st == 0) {
+    const int* r = rec + (size_t)slot2[k] * kRecInts;
+    st = r[0];
+    if (st == 0) {
+      a = r[2] + r[3] + r[4];
+      d = 0;
+      atomicAdd(nlive, 1);
+    }
+  }
+  stc[k] = st;
+  nacc[k] = a;
+  dec[k] = d;
+}
+
+__global__ void cm_emit_kernel(const int* __restrict__ stc, const int* __restrict__ slot2, const int* __restrict__ rec,
+                               const int* __restrict__ aoff, int nk, unsigned long long* __restrict__ keys,
+                               int* __restrict__ vals) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nk || stc[k] != 0) return;
+  const int* r = rec + (size_t)slot2[k] * kRecInts;
+  int o = aoff[k];
+  auto emit = [&](int cell) {
+    keys[o] = ((unsigned long long)(unsigned int)cell << 32) | (unsigned int)k;
+    vals[o] = o;
+    ++o;
+  };
+  for (int i = 0; i < r[2]; ++i) emit(r[5 + i]);
+  for (int i = 0; i < r[3]; ++i) emit(r[5 + PMVS_MAX_IMAGES + i]);
+  for (int i = 0; i < r[4]; ++i) emit(r[5 + 2 * PMVS_MAX_IMAGES + i]);
+}
+
+__global__ void cm_head_kernel(const unsigned long long* __restrict__ keys, const int* __restrict__ vals, int na,
+                               int* __restrict__ head, int* __restrict__ pos) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= na) return;
+  head[p] = (p == 0 || (keys[p] >> 32) != (keys[p - 1] >> 32)) ? 1 : 0;
+  pos[vals[p]] = p;
+}
+
+// segid = inclusive scan of head - 1; seghead[segment] = its first position, seghead[nseg] = na
+__global__ void cm_seg_kernel(const int* __restrict__ head, int* __restrict__ segid, int na, int* __restrict__ seghead,
+                              int* __restrict__ segptr) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= na) return;
+  const int s = segid[p] - 1;
+  segid[p] = s;
+  if (head[p]) {
+    seghead[s] = p;
+    segptr[s] = p;
+  }
+  if (p == na - 1) seghead[s + 1] = na;
+}
+
+__global__ void cm_first_kernel(const unsigned long long* __restrict__ keys, const unsigned char* __restrict__ dec,
+                                const int* __restrict__ seghead, int nseg, int* __restrict__ segptr,
+                                int* __restrict__ segfirst) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nseg) return;
+  int p = segptr[s];
+  const int end = seghead[s + 1];
+  while (p < end && dec[(int)(keys[p] & 0xffffffffull)]) ++p;
+  segptr[s] = p;
+  segfirst[s] = (p < end) ? (int)(keys[p] & 0xffffffffull) : -1;
+}
+
+// Decides every undecided candidate that is the first undecided one in all of its cells.
+// ctr: [0] decided this call, [1] fail_commit, [2] invalid.
+__global__ void cm_decide_kernel(DScene s, int nk, const int* __restrict__ slot2, const int* __restrict__ rec,
+                                 const int* __restrict__ aoff, const int* __restrict__ nacc, const int* __restrict__ pos,
+                                 const int* __restrict__ segid, const int* __restrict__ segfirst,
+                                 unsigned char* __restrict__ dec, int* __restrict__ stc, int* __restrict__ flag,
+                                 unsigned char* __restrict__ counts, unsigned char* __restrict__ occ, int cthr, int check,
+                                 int* __restrict__ ctr) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nk || dec[k]) return;
+  for (int e = aoff[k], ee = aoff[k] + nacc[k]; e < ee; ++e)
+    if (segfirst[segid[pos[e]]] != k) return;
+  const int* r = rec + (size_t)slot2[k] * kRecInts;
+  int st = 0;
+  if (check) {  // checkCounts with the committed state (expand.cpp:309-322)
+    int full = 0, empty = 0;
+    for (int i = 0; i < r[2]; ++i) {
+      const int c = r[5 + i];
+      if (occ[c]) { ++full; continue; }
+      if (cthr <= counts[c]) ++full;
+      else ++empty;
+    }
+    const bool fail = (s.depth <= 1) ? (empty < s.minImageNum && full != 0) : (empty < s.minImageNum - 1 && full != 0);
+    if (fail) st = 4;
+  }
+  if (st == 0) {  // updateCounts (expand.cpp:325-406) + addPatch's pgrids registration
+    int full = 0, empty = 0;
+    auto touch = [&](int c) {
+      const unsigned char cc = counts[c];
+      if (cthr <= cc) ++full;
+      else ++empty;
+      counts[c] = (unsigned char)(cc + 1);
+    };
+    for (int i = 0; i < r[3]; ++i) touch(r[5 + PMVS_MAX_IMAGES + i]);
+    for (int i = 0; i < r[4]; ++i) touch(r[5 + 2 * PMVS_MAX_IMAGES + i]);
+    for (int i = 0; i < r[3]; ++i) occ[r[5 + PMVS_MAX_IMAGES + i]] = 1;
+    flag[k] = (empty != 0) ? 3 : 1;  // bit 0 accepted, bit 1 pushed on the queue
+  } else {
+    stc[k] = st;
+    flag[k] = 0;
+    atomicAdd(&ctr[1], 1);
+  }
+  dec[k] = 1;
+  atomicAdd(&ctr[0], 1);
+}
+
+// flags of the non-refined candidates (0) and the outcome counters: ctr[3] fail_prep, [4] fail_pre,
+// [5] fail_post, [2] invalid records
+__global__ void cm_noref_kernel(const int* __restrict__ stc, int nk, int* __restrict__ flag, int* __restrict__ ctr) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nk) return;
+  const int st = stc[k];
+  if (st != 0) flag[k] = 0;
+  if (st == 1) atomicAdd(&ctr[3], 1);
+  else if (st == 2) atomicAdd(&ctr[4], 1);
+  else if (st == 3) atomicAdd(&ctr[5], 1);
+  else if (st != 0 && st != -1 && st != 4) atomicAdd(&ctr[2], 1);
+}
+
+// acc list [slot | entry offset] of the accepted candidates in k order, their pushes, and each
+// parent's failed-direction bits (applied to _dflag when apply_dflag, else kept for the host)
+__global__ void cm_accept_scan_kernel(const int* __restrict__ flag, int nk, int* __restrict__ a, int* __restrict__ b,
+                                      int* __restrict__ c, const int* __restrict__ slot2, const int* __restrict__ rec) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nk) return;
+  const int f = flag[k];
+  a[k] = f & 1;               // accepted
+  b[k] = (f >> 1) & 1;        // pushed
+  if (f & 1) {
+    const int* r = rec + (size_t)slot2[k] * kRecInts;
+    c[k] = r[3] + r[4];       // registration entries
+  } else {
+    c[k] = 0;
+  }
+}
+
+__global__ void cm_write_kernel(const int* __restrict__ flag, int nk, const int* __restrict__ qa, const int* __restrict__ qb,
+                                const int* __restrict__ qc, const int* __restrict__ slot2, const int* __restrict__ rec,
+                                int nacc, int pool0, int first, int* __restrict__ acc, int2* __restrict__ push) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nk) return;
+  const int f = flag[k];
+  if (!(f & 1)) return;
+  const int q = qa[k];
+  acc[q] = slot2[k];
+  acc[nacc + q] = pool0 + qc[k];
+  if (f & 2) {
+    const int* r = rec + (size_t)slot2[k] * kRecInts;
+    push[qb[k]] = make_int2(r[1], first + q);
+  }
+}
+
+// _dflag |= failed directions (stc > 0) of each parent of the wave
+__global__ void cm_bits_kernel(const int* __restrict__ stc, int np, int* __restrict__ bits) {
+  const int pi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pi >= np) return;
+  int b = 0;
+  for (int d = 0; d < 6; ++d)
+    if (stc[6 * pi + d] > 0) b |= 1 << d;
+  bits[pi] = b;
+}
+__global__ void cm_dflag_kernel(pmvs_patch* __restrict__ P, const int* __restrict__ parents, const int* __restrict__ bits,
+                                int np) {
+  const int pi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pi < np && bits[pi]) P[parents[pi]].dflag |= bits[pi];
+}
+
+template <class T>
+static hipError_t cm_grow(T*& p, size_t n) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  const hipError_t e = hipMalloc((void**)&p, (n ? n : 1) * sizeof(T));
+  if (e == hipSuccess) poison_alloc(p, (n ? n : 1) * sizeof(T));
+  return e;
+}
+
+struct CommitOut {
+  int nacc = 0, pbits = 0;
+  long long entries = 0, fail[4] = {0, 0, 0, 0};  // fail_prep, fail_pre, fail_post, fail_commit
+  std::vector<int2> push;                          // (tmp bits, new patch index) in commit order
+};
+
+// One wave's commit on the device (see CommitWork).  slot2h[k]: survivor slot of candidate k
+// (status[k] == 0).  Writes X.acc = [slot of accepted q | pool0 + entry offset], applies the
+// failed-direction bits to _dflag (apply_dflag) or returns them (wave = 1: one parent).
+static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t st, int np, const std::vector<int>& slot2h,
+                                int cthr, bool check, int first, long long pool0, bool apply_dflag, pmvs_patch* dP,
+                                CommitOut& out) {
+  if (!X.cm) X.cm = new CommitWork();
+  CommitWork& W = *X.cm;
+  const int nk = np * 6;
+  if ((size_t)nk + 1 > W.cap_k) {
+    const size_t c = std::max((size_t)nk + 1, 2 * W.cap_k);
+    FCHK(cm_grow(W.stc, c)); FCHK(cm_grow(W.nacc, c)); FCHK(cm_grow(W.aoff, c)); FCHK(cm_grow(W.slot2, c));
+    FCHK(cm_grow(W.flag, c)); FCHK(cm_grow(W.scan, 6 * c)); FCHK(cm_grow(W.dec, c)); FCHK(cm_grow(W.pbits, c));
+    FCHK(cm_grow(W.push, c));
+    W.cap_k = c;
+  }
+  if (!W.ctr) FCHK(cm_grow(W.ctr, 8));
+  FCHK(hipMemcpyAsync(W.slot2, slot2h.data(), (size_t)nk * sizeof(int), hipMemcpyHostToDevice, st));
+  FCHK(hipMemsetAsync(W.ctr, 0, 8 * sizeof(int), st));
+  hipLaunchKernelGGL(cm_stage_kernel, dim3(nblk(nk)), dim3(256), 0, st, X.status, W.slot2, X.crec, nk, W.stc, W.nacc,
+                     W.dec, W.ctr + 6);
+  FCHK(hipMemsetAsync(W.nacc + nk, 0, sizeof(int), st));
+  auto temp_need = [&](size_t bytes) -> hipError_t {
+    if (bytes <= W.temp_bytes && W.temp) return hipSuccess;
+    W.temp_bytes = std::max(bytes, 2 * W.temp_bytes);
+    return cm_grow(reinterpret_cast<char*&>(W.temp), W.temp_bytes);
+  };
+  size_t tb = 0;
+  FCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, W.nacc, W.aoff, nk + 1, st));
+  FCHK(temp_need(tb));
+  tb = W.temp_bytes;
+  FCHK(hipcub::DeviceScan::ExclusiveSum(W.temp, tb, W.nacc, W.aoff, nk + 1, st));
+  int hv[2] = {0, 0};
+  FCHK(hipMemcpyAsync(&hv[0], W.aoff + nk, sizeof(int), hipMemcpyDeviceToHost, st));
+  FCHK(hipMemcpyAsync(&hv[1], W.ctr + 6, sizeof(int), hipMemcpyDeviceToHost, st));
+  FCHK(hipStreamSynchronize(st));
+  const int na = hv[0], nlive = hv[1];
+  int nseg = 0;
+  if (na > 0) {
+    if ((size_t)na + 1 > W.cap_a) {
+      const size_t c = std::max((size_t)na + 1, 2 * W.cap_a);
+      FCHK(cm_grow(W.keys, c)); FCHK(cm_grow(W.keys2, c)); FCHK(cm_grow(W.vals, c)); FCHK(cm_grow(W.vals2, c));
+      FCHK(cm_grow(W.pos, c)); FCHK(cm_grow(W.head, c)); FCHK(cm_grow(W.segid, c)); FCHK(cm_grow(W.seghead, c));
+      FCHK(cm_grow(W.segptr, c)); FCHK(cm_grow(W.segfirst, c));
+      W.cap_a = c;
+    }
+    hipLaunchKernelGGL(cm_emit_kernel, dim3(nblk(nk)), dim3(256), 0, st, W.stc, W.slot2, X.crec, W.aoff, nk, W.keys,
+                       W.vals);
+    tb = 0;
+    FCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, W.keys, W.keys2, W.vals, W.vals2, na, 0, 64, st));
+    size_t tb2 = 0;
+    FCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb2, W.head, W.segid, na, st));
+    FCHK(temp_need(std::max(tb, tb2)));
+    tb = W.temp_bytes;
+    FCHK(hipcub::DeviceRadixSort::SortPairs(W.temp, tb, W.keys, W.keys2, W.vals, W.vals2, na, 0, 64, st));
+    hipLaunchKernelGGL(cm_head_kernel, dim3(nblk(na)), dim3(256), 0, st, W.keys2, W.vals2, na, W.head, W.pos);
+    tb = W.temp_bytes;
+    FCHK(hipcub::DeviceScan::InclusiveSum(W.temp, tb, W.head, W.segid, na, st));
+    FCHK(hipMemcpyAsync(&nseg, W.segid + na - 1, sizeof(int), hipMemcpyDeviceToHost, st));
+    FCHK(hipStreamSynchronize(st));
+    hipLaunchKernelGGL(cm_seg_kernel, dim3(nblk(na)), dim3(256), 0, st, W.head, W.segid, na, W.seghead, W.segptr);
+  }
+  // rounds: every round decides at least the lowest undecided candidate
+  int decided = 0;
+  for (int round = 0; decided < nlive; ) {
+    for (int r = 0; r < 4; ++r, ++round) {
+      if (nseg > 0)
+        hipLaunchKernelGGL(cm_first_kernel, dim3(nblk(nseg)), dim3(256), 0, st, W.keys2, W.dec, W.seghead, nseg, W.segptr,
+                           W.segfirst);
+      hipLaunchKernelGGL(cm_decide_kernel, dim3(nblk(nk)), dim3(256), 0, st, s, nk, W.slot2, X.crec, W.aoff, W.nacc, W.pos,
+                         W.segid, W.segfirst, W.dec, W.stc, W.flag, X.counts, X.occ, cthr, check ? 1 : 0, W.ctr);
+    }
+    FCHK(hipMemcpyAsync(&decided, W.ctr, sizeof(int), hipMemcpyDeviceToHost, st));
+    FCHK(hipStreamSynchronize(st));
+    if (round > 4 * (nlive + 2)) return hipErrorIllegalState;  // cannot happen (progress every round)
+  }
+  hipLaunchKernelGGL(cm_noref_kernel, dim3(nblk(nk)), dim3(256), 0, st, W.stc, nk, W.flag, W.ctr);
+  // accepted / pushed / entries in k order
+  int* qa = W.scan;
+  int* qb = W.scan + (nk + 1);
+  int* qc = W.scan + 2 * (size_t)(nk + 1);
+  int* ia = W.scan + 3 * (size_t)(nk + 1);
+  int* ib = W.scan + 4 * (size_t)(nk + 1);
+  int* ic = W.scan + 5 * (size_t)(nk + 1);
+  hipLaunchKernelGGL(cm_accept_scan_kernel, dim3(nblk(nk)), dim3(256), 0, st, W.flag, nk, ia, ib, ic, W.slot2, X.crec);
+  FCHK(hipMemsetAsync(ia + nk, 0, sizeof(int), st));
+  FCHK(hipMemsetAsync(ib + nk, 0, sizeof(int), st));
+  FCHK(hipMemsetAsync(ic + nk, 0, sizeof(int), st));
+  tb = 0;
+  FCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ia, qa, nk + 1, st));
+  FCHK(temp_need(tb));
+  for (int t = 0; t < 3; ++t) {
+    tb = W.temp_bytes;
+    FCHK(hipcub::DeviceScan::ExclusiveSum(W.temp, tb, t == 0 ? ia : t == 1 ? ib : ic, t == 0 ? qa : t == 1 ? qb : qc,
+                                          nk + 1, st));
+  }
+  int tot[3], ctr[8];
+  FCHK(hipMemcpyAsync(&tot[0], qa + nk, sizeof(int), hipMemcpyDeviceToHost, st));
+  FCHK(hipMemcpyAsync(&tot[1], qb + nk, sizeof(int), hipMemcpyDeviceToHost, st));
+  FCHK(hipMemcpyAsync(&tot[2], qc + nk, sizeof(int), hipMemcpyDeviceToHost, st));
+  FCHK(hipMemcpyAsync(ctr, W.ctr, 8 * sizeof(int), hipMemcpyDeviceToHost, st));
+  FCHK(hipStreamSynchronize(st));
+  if (ctr[2] != 0) {
+    fprintf(stderr, "expand: %d refined records are not valid patches\n", ctr[2]);
+    return hipErrorIllegalState;
+  }
+  out.nacc = tot[0];
+  out.entries = tot[2];
+  out.fail[0] = ctr[3]; out.fail[1] = ctr[4]; out.fail[2] = ctr[5]; out.fail[3] = ctr[1];
+  if (out.nacc > 0) {
+    FCHK(grow(X.acc, X.cap_acc, 2 * (size_t)out.nacc));
+    hipLaunchKernelGGL(cm_write_kernel, dim3(nblk(nk)), dim3(256), 0, st, W.flag, nk, qa, qb, qc, W.slot2, X.crec, out.nacc,
+                       (int)pool0, first, X.acc, W.push);
+  }
+  out.push.resize(tot[1]);
+  if (tot[1] > 0)
+    FCHK(hipMemcpyAsync(out.push.data(), W.push, (size_t)tot[1] * sizeof(int2), hipMemcpyDeviceToHost, st));
+  hipLaunchKernelGGL(cm_bits_kernel, dim3(nblk(np)), dim3(256), 0, st, W.stc, np, W.pbits);
+  out.pbits = 0;
+  if (apply_dflag) {
+    hipLaunchKernelGGL(cm_dflag_kernel, dim3(nblk(np)), dim3(256), 0, st, dP, X.parents, W.pbits, np);
+  } else {
+    FCHK(hipMemcpyAsync(&out.pbits, W.pbits, sizeof(int), hipMemcpyDeviceToHost, st));
+  }
+  FCHK(hipStreamSynchronize(st));
+  return hipGetLastError();
 }
 
 // PMVS_EXPAND_PROFILE=1: host wall time per expansion phase (synchronising at phase ends), to stderr.
@@ -1909,28 +2272,22 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
     c.pg_dhead = X.pg_head; c.vp_dhead = X.vp_head; c.d_item = X.d_item; c.d_next = X.d_next;
   };
   set_delta();
-  // ---- host mirrors: pgrids occupancy per cell, counts (clearCounts), the queue
-  // per cell {count, occupied}: CExpand's _counts (unsigned char, clearCounts) and whether pgrids
-  // holds a patch, side by side so a commit touches one cache line per cell (huge pages)
-  HostCells cs((size_t)ncells);
-  if (!cs.p) return hipErrorOutOfMemory;
+  // ---- device state of the commit: CExpand's _counts (unsigned char, clearCounts) and whether
+  // pgrids holds a patch, per target cell; the host keeps only the queue
   std::vector<int> order(c.nalive);
   std::vector<float> qtmp(c.nalive);
   FCHK(grow(X.qtmp, X.cap_qtmp, (size_t)std::max(1, c.nalive)));
-  FCHK(grow(X.cellinit, X.cap_cellinit, (size_t)ncells));
+  FCHK(grow(X.occ, X.cap_occ, (size_t)ncells));
   if (c.nalive)
     hipLaunchKernelGGL(collect_flags_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, dP, B.order, c.nalive, X.qtmp);
-  hipLaunchKernelGGL(cell_init_kernel, dim3(nblk(ncells)), dim3(256), 0, st, B.pg_off, ncells,
-                     reinterpret_cast<HostCell*>(X.cellinit));
-  FCHK(hipMemcpyAsync(cs.p, X.cellinit, (size_t)ncells * sizeof(HostCell), hipMemcpyDeviceToHost, st));
+  hipLaunchKernelGGL(occ_init_kernel, dim3(nblk(ncells)), dim3(256), 0, st, B.pg_off, ncells, X.occ);
   if (c.nalive) {
     FCHK(hipMemcpyAsync(order.data(), B.order, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
     FCHK(hipMemcpyAsync(qtmp.data(), X.qtmp, c.nalive * sizeof(float), hipMemcpyDeviceToHost, st));
   }
-  FCHK(hipStreamSynchronize(st));
-  HostCell* const cell = cs.p;
   FCHK(grow(X.counts, X.cap_cnt, (size_t)ncells));
   FCHK(hipMemsetAsync(X.counts, 0, ncells, st));
+  FCHK(hipStreamSynchronize(st));
   // The max-_tmp queue (P_compare; ties: earlier push first): the collected patches as a sorted
   // run, the patches pushed during the run in a heap, popped by merging the two.
   std::vector<QItem> initial(c.nalive);
@@ -1950,12 +2307,8 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
   int rank_next = c.nalive;
   int nmodel = n0;
   const int G = std::max(1, sh.world), R = std::min(std::max(0, sh.rank), G - 1);
-  std::vector<int> touched;
-  std::vector<unsigned char> tvals;
-  std::vector<int> seqk;  // the wave's slots with a refined record, in commit order (prefetch)
   std::vector<char> xsend, xrecv;
-  std::vector<int> rec, acc, eoff;
-  std::vector<int2> dupd;
+  CommitOut co;
   T.mark(0);
   std::vector<int> okh;
   while (!q_empty()) {
@@ -2086,99 +2439,20 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
         FCHK(grow(X.crec, X.cap_crec, (size_t)m * kRecInts));
         hipLaunchKernelGGL(commit_rec_kernel, dim3(nblk(m)), dim3(256), 0, st, s, B.tgoff, X.outp, X.ostatus, X.prep2, m,
                            X.crec);
-        rec.resize((size_t)m * kRecInts);
-        FCHK(hipMemcpyAsync(rec.data(), X.crec, (size_t)m * kRecInts * sizeof(int), hipMemcpyDeviceToHost, st));
-        FCHK(hipStreamSynchronize(st));
       }
       T.mark(6);
-      // ---- commit in (parent priority, direction) order
-      touched.clear();
-      acc.clear();
-      dupd.clear();
-      seqk.clear();
-      for (int k = 0; k < np * 6; ++k)
-        if (status[k] == 0) seqk.push_back(slot2surv[k]);
-      size_t nextpf = 0;
-      auto prefetch = [&](size_t upto) {  // the cells of the records a few commits ahead
-        for (; nextpf < std::min(upto, seqk.size()); ++nextpf) {
-          const int* r = &rec[(size_t)seqk[nextpf] * kRecInts];
-          for (int i = 0; i < r[2]; ++i) __builtin_prefetch(&cell[r[5 + i]], 1);
-          for (int i = 0; i < r[4]; ++i) __builtin_prefetch(&cell[r[5 + 2 * PMVS_MAX_IMAGES + i]], 1);
-        }
-      };
-      size_t done = 0;
-      for (int pi = 0; pi < np; ++pi) {
-        int bits = 0;
-        for (int dir = 0; dir < 6; ++dir) {
-          const int k = 6 * pi + dir;
-          if (status[k] < 0) continue;
-          int stc = status[k];  // 1 = prepare failed
-          const int j = slot2surv[k];
-          if (stc == 0) prefetch(++done + 6);
-          const int* r = (stc == 0) ? &rec[(size_t)j * kRecInts] : nullptr;
-          if (stc == 0) stc = r[0];
-          if (stc == 9) {
-            fprintf(stderr, "expand: refined record %d of %d is not a valid patch\n", j, m);
-            return hipErrorIllegalState;
-          }
-          if (stc == 0 && only < 0) {  // checkCounts again with the committed state
-            int full = 0, empty = 0;
-            for (int i = 0; i < r[2]; ++i) {
-              const int cidx = r[5 + i];
-              if (cell[cidx].occ) { ++full; continue; }
-              if (cthr <= cell[cidx].count) ++full;
-              else ++empty;
-            }
-            const bool fail = (s.depth <= 1) ? (empty < s.minImageNum && full != 0) : (empty < s.minImageNum - 1 && full != 0);
-            if (fail) stc = 4;
-          }
-          if (stc != 0) {
-            bits |= 0x0001 << dir;
-            stats[1 + std::min(stc, 4)]++;  // 2 fail_prep, 3 fail_pre, 4 fail_post, 5 fail_commit
-            continue;
-          }
-          // CExpand::updateCounts (expand.cpp:325-406) + addPatch (pgrids registration)
-          int full = 0, empty = 0;
-          auto touch = [&](int cidx) {
-            unsigned char& cc = cell[cidx].count;
-            if (cthr <= cc) ++full;
-            else ++empty;
-            ++cc;
-            touched.push_back(cidx);
-          };
-          for (int i = 0; i < r[3]; ++i) touch(r[5 + PMVS_MAX_IMAGES + i]);
-          for (int i = 0; i < r[4]; ++i) touch(r[5 + 2 * PMVS_MAX_IMAGES + i]);
-          for (int i = 0; i < r[3]; ++i) cell[r[5 + PMVS_MAX_IMAGES + i]].occ = 1;
-          pool_need += (size_t)r[3] + (size_t)r[4];
-          if (nmodel + (int)acc.size() >= cap) return hipErrorOutOfMemory;
-          const int newp = nmodel + (int)acc.size();
-          acc.push_back(j);
-          stats[6]++;
-          if (empty != 0) queue.push({__int_as_float_h(r[1]), seq++, newp});
-        }
-        if (W == 1) pbits |= bits;
-        else if (bits) dupd.push_back(make_int2(parents[pi], bits));
-      }
+      // ---- commit in (parent priority, direction) order, on the device (device_commit)
+      const int first = nmodel;
+      FCHK(device_commit(s, X, st, np, slot2surv, cthr, only < 0, first, (long long)X.pool_host, W > 1, dP, co));
+      for (int q = 0; q < 4; ++q) stats[2 + q] += co.fail[q];
+      if (W == 1) pbits |= co.pbits;
+      const int added = co.nacc;
+      if (added > 0 && nmodel + added > cap) return hipErrorOutOfMemory;
+      stats[6] += added;
+      for (const int2& u : co.push) queue.push({__int_as_float_h(u.x), seq++, u.y});
       T.mark(7);
-      // device counts: the cells this commit touched (final values)
-      if (!touched.empty()) {
-        const int nt = (int)touched.size();
-        tvals.resize(nt);
-        for (int k = 0; k < nt; ++k) tvals[k] = cell[touched[k]].count;
-        FCHK(grow(X.tcells, X.cap_tcells, (size_t)nt));
-        FCHK(grow(X.tvals, X.cap_tvals, (size_t)nt));
-        FCHK(hipMemcpyAsync(X.tcells, touched.data(), nt * sizeof(int), hipMemcpyHostToDevice, st));
-        FCHK(hipMemcpyAsync(X.tvals, tvals.data(), nt, hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(counts_scatter_kernel, dim3(nblk(nt)), dim3(256), 0, st, X.tcells, X.tvals, nt, X.counts);
-      }
-      if (!dupd.empty()) {
-        FCHK(grow(X.dupd, X.cap_dupd, dupd.size()));
-        FCHK(hipMemcpyAsync(X.dupd, dupd.data(), dupd.size() * sizeof(int2), hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(dflag_kernel, dim3(nblk((long long)dupd.size())), dim3(256), 0, st, dP, X.dupd, (int)dupd.size());
-      }
-      const int added = (int)acc.size();
       if (added > 0) {
-        const int first = nmodel;
+        pool_need = X.pool_host + (size_t)co.entries;
         FCHK(grow_keep(X.d_item, X.cap_item, pool_need, X.pool_host, st));
         FCHK(grow_keep(X.d_next, X.cap_next, pool_need, X.pool_host, st));
         set_delta();
@@ -2194,17 +2468,6 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
           pcap = ncap;
           c.P = dP;
         }
-        // [acc | entry offsets] in one upload
-        eoff.resize(2 * (size_t)added);
-        size_t e0 = X.pool_host;
-        for (int q = 0; q < added; ++q) {
-          const int* r = &rec[(size_t)acc[q] * kRecInts];
-          eoff[q] = acc[q];
-          eoff[added + q] = (int)e0;
-          e0 += (size_t)r[3] + (size_t)r[4];
-        }
-        FCHK(grow(X.acc, X.cap_acc, 2 * (size_t)added));
-        FCHK(hipMemcpyAsync(X.acc, eoff.data(), 2 * (size_t)added * sizeof(int), hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(append_kernel, dim3(added), dim3(64), 0, st, dP, first, X.acc, added, X.outp);
         nmodel += added;
         c.n = nmodel;

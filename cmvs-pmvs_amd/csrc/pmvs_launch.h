@@ -44,7 +44,11 @@ hipError_t launch_filter_refimage(const DScene& s, pmvs_patch* P, const int* lis
 
 // ---- expansion run (pmvs_filter.hip)
 constexpr int kMaxWave = 65536;  // parents per expansion wave (device slot arrays are sized by it)
+struct CommitWork;  // device commit scratch (pmvs_filter.hip)
 struct ExpandBuffers {
+  CommitWork* cm = nullptr;
+  unsigned char* occ = nullptr;  // per target cell: pgrids holds a patch (device commit)
+  size_t cap_occ = 0;
   int *parents = nullptr, *cand_ok = nullptr, *status = nullptr, *slots = nullptr, *ostatus = nullptr, *alive = nullptr;
   float* cand_coord = nullptr;
   pmvs_candidate *cand = nullptr, *cand2 = nullptr;
