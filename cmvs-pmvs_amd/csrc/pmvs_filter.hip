@@ -2060,6 +2060,77 @@ __global__ void cm_dflag_kernel(pmvs_patch* __restrict__ P, const int* __restric
   if (pi < np && bits[pi]) P[parents[pi]].dflag |= bits[pi];
 }
 
+// Small waves (the reference's wave = 1 schedule: one parent, <= 6 candidates per batch): the same
+// commit by one lane in k order, with one small read-back.  out = [nacc, npush, entries, fail_prep,
+// fail_pre, fail_post, fail_commit, invalid, bits of parent 0, pushes (tmp bits, new index) x nk].
+constexpr int kSerialCommit = 64;
+__global__ void cm_serial_kernel(DScene s, const int* __restrict__ status, const int* __restrict__ slot2,
+                                 const int* __restrict__ rec, int nk, int np, unsigned char* __restrict__ counts,
+                                 unsigned char* __restrict__ occ, int cthr, int check, int first, int pool0,
+                                 int* __restrict__ acc, int* __restrict__ out, const int* __restrict__ parents,
+                                 pmvs_patch* __restrict__ P, int apply_dflag) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int accs[kSerialCommit], ents[kSerialCommit];
+  int nacc = 0, npush = 0, entries = 0, f[5] = {0, 0, 0, 0, 0};
+  int bits[kSerialCommit / 6 + 1];
+  for (int pi = 0; pi < np; ++pi) bits[pi] = 0;
+  for (int k = 0; k < nk; ++k) {
+    int st = status[k];
+    if (st < 0) continue;
+    const int* r = nullptr;
+    if (st == 0) {
+      r = rec + (size_t)slot2[k] * kRecInts;
+      st = r[0];
+    }
+    if (st == 0 && check) {
+      int full = 0, empty = 0;
+      for (int i = 0; i < r[2]; ++i) {
+        const int c = r[5 + i];
+        if (occ[c]) { ++full; continue; }
+        if (cthr <= counts[c]) ++full;
+        else ++empty;
+      }
+      const bool fail = (s.depth <= 1) ? (empty < s.minImageNum && full != 0) : (empty < s.minImageNum - 1 && full != 0);
+      if (fail) st = 4;
+    }
+    if (st != 0) {
+      bits[k / 6] |= 1 << (k % 6);
+      if (st >= 1 && st <= 4) f[st - 1]++;
+      else f[4]++;
+      continue;
+    }
+    int full = 0, empty = 0;
+    auto touch = [&](int c) {
+      const unsigned char cc = counts[c];
+      if (cthr <= cc) ++full;
+      else ++empty;
+      counts[c] = (unsigned char)(cc + 1);
+    };
+    for (int i = 0; i < r[3]; ++i) touch(r[5 + PMVS_MAX_IMAGES + i]);
+    for (int i = 0; i < r[4]; ++i) touch(r[5 + 2 * PMVS_MAX_IMAGES + i]);
+    for (int i = 0; i < r[3]; ++i) occ[r[5 + PMVS_MAX_IMAGES + i]] = 1;
+    accs[nacc] = slot2[k];
+    ents[nacc] = entries;
+    entries += r[3] + r[4];
+    if (empty != 0) {
+      out[9 + 2 * npush] = r[1];
+      out[9 + 2 * npush + 1] = first + nacc;
+      ++npush;
+    }
+    ++nacc;
+  }
+  for (int q = 0; q < nacc; ++q) {
+    acc[q] = accs[q];
+    acc[nacc + q] = pool0 + ents[q];
+  }
+  out[0] = nacc; out[1] = npush; out[2] = entries;
+  out[3] = f[0]; out[4] = f[1]; out[5] = f[2]; out[6] = f[3]; out[7] = f[4];
+  out[8] = bits[0];
+  if (apply_dflag)
+    for (int pi = 0; pi < np; ++pi)
+      if (bits[pi]) P[parents[pi]].dflag |= bits[pi];
+}
+
 template <class T>
 static hipError_t cm_grow(T*& p, size_t n) {
   if (p) (void)hipFree(p);
@@ -2091,8 +2162,27 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
     FCHK(cm_grow(W.push, c));
     W.cap_k = c;
   }
-  if (!W.ctr) FCHK(cm_grow(W.ctr, 8));
+  if (!W.ctr) FCHK(cm_grow(W.ctr, 9 + 2 * kSerialCommit));
   FCHK(hipMemcpyAsync(W.slot2, slot2h.data(), (size_t)nk * sizeof(int), hipMemcpyHostToDevice, st));
+  if (nk <= kSerialCommit) {
+    FCHK(grow(X.acc, X.cap_acc, 2 * (size_t)nk));
+    hipLaunchKernelGGL(cm_serial_kernel, dim3(1), dim3(64), 0, st, s, X.status, W.slot2, X.crec, nk, np, X.counts, X.occ,
+                       cthr, check ? 1 : 0, first, (int)pool0, X.acc, W.ctr, X.parents, dP, apply_dflag ? 1 : 0);
+    int h[9 + 2 * kSerialCommit];
+    FCHK(hipMemcpyAsync(h, W.ctr, sizeof(h), hipMemcpyDeviceToHost, st));
+    FCHK(hipStreamSynchronize(st));
+    if (h[7] != 0) {
+      fprintf(stderr, "expand: %d refined records are not valid patches\n", h[7]);
+      return hipErrorIllegalState;
+    }
+    out.nacc = h[0];
+    out.entries = h[2];
+    for (int q = 0; q < 4; ++q) out.fail[q] = h[3 + q];
+    out.pbits = apply_dflag ? 0 : h[8];
+    out.push.resize(h[1]);
+    for (int q = 0; q < h[1]; ++q) out.push[q] = make_int2(h[9 + 2 * q], h[9 + 2 * q + 1]);
+    return hipGetLastError();
+  }
   FCHK(hipMemsetAsync(W.ctr, 0, 8 * sizeof(int), st));
   hipLaunchKernelGGL(cm_stage_kernel, dim3(nblk(nk)), dim3(256), 0, st, X.status, W.slot2, X.crec, nk, W.stc, W.nacc,
                      W.dec, W.ctr + 6);
