@@ -130,8 +130,8 @@ def _gap(inp, ref, prod):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("views,w,h,nseeds", [(10, 400, 300, 150), (50, 480, 270, 300)],
-                         ids=["10v_400x300", "50v_480x270"])
+@pytest.mark.parametrize("views,w,h,nseeds", [(10, 400, 300, 150), (50, 320, 180, 300)],
+                         ids=["10v_400x300", "50v_320x180"])
 def test_schedule_gap_vs_single_thread(gpu_available, views, w, h, nseeds):
     import pmvs_amd as P
     inp, p, cands = _scene(views, w, h, nseeds)
