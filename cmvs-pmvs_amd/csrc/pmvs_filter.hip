@@ -460,6 +460,7 @@ struct NbLds {
   double nu[5], nd[5], tau[5], den;  // lls5_wave: column norms (updated / direct), Householder taus
   int perm[5], big;
   float x[5];
+  double jw[5][5], ju[5][5], jv[5][5], sv[5], jy[5];  // lls5_wave's Jacobi stage (lane 0)
 };
 
 // Cmylapack::lls (mylapack.cpp:102-149, Eigen JacobiSVD(ThinU | ThinV).solve) with Eigen's algorithm,
@@ -467,8 +468,132 @@ struct NbLds {
 // Householder QR of the scaled n x 5 system (rows in global scratch; per-column sums by one lane
 // each, in row order; elementwise updates spread over the lanes), then two-sided Jacobi, sorting
 // and the rank-thresholded minimum-norm solve on the 5 x 5 factor by lane 0.
+typedef __attribute__((address_space(3))) double lds_f64;
 __device__ __forceinline__ double dmaxd(double a, double b) { return (a < b) ? b : a; }  // std::max
-__device__ void lls5_wave(NbLds& L, double* M, double* r, int n) {
+// lls5_wave's 5 x 5 stage on lane 0 (two-sided Jacobi, signs, sort, rank-thresholded solve).
+__device__ __attribute__((noinline)) void lls5_jacobi(NbLds& L, const double* M, const double* r, double scale) {
+  constexpr int N = 5;
+  const double eps = 2.220446049250313e-16, dmin = 2.2250738585072014e-308;
+    // L lives in LDS in every caller: LDS-typed pointers give 32-bit addresses with immediate offsets
+    // (generic 64-bit addresses of the unrolled 5 x 5 loops were hoisted into ~200 registers, which
+    // capped the occupancy of the calling neighbour walks; one lane runs this stage)
+    lds_f64* W = (lds_f64*)&L.jw[0][0];
+    lds_f64* U = (lds_f64*)&L.ju[0][0];
+    lds_f64* V = (lds_f64*)&L.jv[0][0];
+    for (int i = 0; i < N; ++i)
+      for (int j = 0; j < N; ++j) {
+        W[i * N + j] = (j >= i) ? M[(size_t)i * N + j] : 0.0;
+        U[i * N + j] = V[i * N + j] = (i == j) ? 1.0 : 0.0;
+      }
+    double maxd = 0.0;
+    for (int i = 0; i < N; ++i) maxd = dmaxd(maxd, fabs(W[(i) * N + (i)]));
+    bool finished = false;
+    for (int sweep = 0; !finished && sweep < 100; ++sweep) {
+      finished = true;
+#pragma nounroll
+      for (int p = 1; p < N; ++p)
+#pragma nounroll
+        for (int q = 0; q < p; ++q) {
+          const double thr = dmaxd(dmin, 2.0 * eps * maxd);
+          if (!(fabs(W[(p) * N + (q)]) > thr || fabs(W[(q) * N + (p)]) > thr)) continue;
+          finished = false;
+          double m00 = W[(p) * N + (p)], m01 = W[(p) * N + (q)], m10 = W[(q) * N + (p)], m11 = W[(q) * N + (q)];
+          const double t = m00 + m11, d = m10 - m01;
+          double c1 = 1.0, s1 = 0.0;
+          if (!(fabs(d) < dmin)) {
+            const double u = t / d;
+            const double tmp = sqrt(1.0 + u * u);
+            s1 = 1.0 / tmp;
+            c1 = u / tmp;
+          }
+          {
+            const double a0 = m00, a1 = m01, b0 = m10, b1 = m11;
+            m00 = c1 * a0 + s1 * b0; m01 = c1 * a1 + s1 * b1;
+            m10 = -s1 * a0 + c1 * b0; m11 = -s1 * a1 + c1 * b1;
+          }
+          double cr = 1.0, sr = 0.0;
+          const double deno = 2.0 * fabs(m01);
+          if (!(deno < dmin)) {
+            const double tau_ = (m00 - m11) / deno;
+            const double w = sqrt(tau_ * tau_ + 1.0);
+            const double tt = (tau_ > 0.0) ? 1.0 / (tau_ + w) : 1.0 / (tau_ - w);
+            const double sign_t = tt > 0.0 ? 1.0 : -1.0;
+            const double nn = 1.0 / sqrt(tt * tt + 1.0);
+            sr = -sign_t * (m01 / fabs(m01)) * fabs(tt) * nn;
+            cr = nn;
+          }
+          const double cl = c1 * cr - s1 * (-sr);
+          const double sl = c1 * (-sr) + s1 * cr;
+          for (int j = 0; j < N; ++j) {  // W rows p, q by j_left
+            const double xp = W[(p) * N + (j)], xq = W[(q) * N + (j)];
+            W[(p) * N + (j)] = cl * xp + sl * xq;
+            W[(q) * N + (j)] = -sl * xp + cl * xq;
+          }
+          for (int i = 0; i < N; ++i) {  // U columns p, q by j_left^T
+            const double xp = U[(i) * N + (p)], xq = U[(i) * N + (q)];
+            U[(i) * N + (p)] = cl * xp - (-sl) * xq;
+            U[(i) * N + (q)] = (-sl) * xp + cl * xq;
+          }
+          for (int i = 0; i < N; ++i) {  // W columns p, q by j_right
+            const double xp = W[(i) * N + (p)], xq = W[(i) * N + (q)];
+            W[(i) * N + (p)] = cr * xp - sr * xq;
+            W[(i) * N + (q)] = sr * xp + cr * xq;
+          }
+          for (int i = 0; i < N; ++i) {  // V columns p, q by j_right
+            const double xp = V[(i) * N + (p)], xq = V[(i) * N + (q)];
+            V[(i) * N + (p)] = cr * xp - sr * xq;
+            V[(i) * N + (q)] = sr * xp + cr * xq;
+          }
+          maxd = dmaxd(maxd, dmaxd(fabs(W[(p) * N + (p)]), fabs(W[(q) * N + (q)])));
+        }
+    }
+    lds_f64* sv = (lds_f64*)L.sv;
+    for (int i = 0; i < N; ++i) {
+      sv[i] = fabs(W[(i) * N + (i)]);
+      if (W[(i) * N + (i)] < 0.0)
+        for (int k = 0; k < N; ++k) U[(k) * N + (i)] = -U[(k) * N + (i)];
+    }
+    for (int i = 0; i < N; ++i) sv[i] *= scale;
+    int nonzero = N;
+    for (int i = 0; i < N; ++i) {
+      int pos = i;
+      for (int j = i + 1; j < N; ++j)
+        if (sv[j] > sv[pos]) pos = j;
+      if (sv[pos] == 0.0) {
+        nonzero = i;
+        break;
+      }
+      if (pos != i) {
+        double t = sv[i]; sv[i] = sv[pos]; sv[pos] = t;
+        for (int k = 0; k < N; ++k) {
+          t = U[(k) * N + (i)]; U[(k) * N + (i)] = U[(k) * N + (pos)]; U[(k) * N + (pos)] = t;
+          t = V[(k) * N + (i)]; V[(k) * N + (i)] = V[(k) * N + (pos)]; V[(k) * N + (pos)] = t;
+        }
+      }
+    }
+    int rank = 0;
+    if (nonzero > 0) {
+      const double pre = dmaxd(sv[0] * (N * eps), dmin);
+      int i = nonzero - 1;
+      while (i >= 0 && sv[i] < pre) --i;
+      rank = i + 1;
+    }
+    lds_f64* y = (lds_f64*)L.jy;
+    for (int i = 0; i < rank; ++i) {
+      double t = 0.0;
+      for (int k = 0; k < N; ++k) t += U[(k) * N + (i)] * r[k];
+      y[i] = t / sv[i];
+    }
+    for (int k = 0; k < N; ++k) {
+      double t = 0.0;
+      for (int i = 0; i < rank; ++i) t += V[(k) * N + (i)] * y[i];
+      L.x[L.perm[k]] = (float)t;
+    }
+}
+
+// Out of line: its registers do not add to the latency-bound neighbour walks of the callers (whose
+// occupancy is register-limited); M / r rows in global scratch, the 5 x 5 stage in NbLds.
+__device__ __attribute__((noinline)) void lls5_wave(NbLds& L, double* M, double* r, int n) {
   constexpr int N = 5;
   const double eps = 2.220446049250313e-16, dmin = 2.2250738585072014e-308;
   const int lane = lane_id_w();
@@ -583,117 +708,7 @@ __device__ void lls5_wave(NbLds& L, double* M, double* r, int n) {
     for (int i = k + 1 + lane; i < n; i += 64) r[i] -= (tauk * M[(size_t)i * N + k]) * t;
     bar();
   }
-  if (lane == 0) {
-    double W[N][N], U[N][N], V[N][N];
-    for (int i = 0; i < N; ++i)
-      for (int j = 0; j < N; ++j) {
-        W[i][j] = (j >= i) ? M[(size_t)i * N + j] : 0.0;
-        U[i][j] = V[i][j] = (i == j) ? 1.0 : 0.0;
-      }
-    double maxd = 0.0;
-    for (int i = 0; i < N; ++i) maxd = dmaxd(maxd, fabs(W[i][i]));
-    bool finished = false;
-    for (int sweep = 0; !finished && sweep < 100; ++sweep) {
-      finished = true;
-      for (int p = 1; p < N; ++p)
-        for (int q = 0; q < p; ++q) {
-          const double thr = dmaxd(dmin, 2.0 * eps * maxd);
-          if (!(fabs(W[p][q]) > thr || fabs(W[q][p]) > thr)) continue;
-          finished = false;
-          double m00 = W[p][p], m01 = W[p][q], m10 = W[q][p], m11 = W[q][q];
-          const double t = m00 + m11, d = m10 - m01;
-          double c1 = 1.0, s1 = 0.0;
-          if (!(fabs(d) < dmin)) {
-            const double u = t / d;
-            const double tmp = sqrt(1.0 + u * u);
-            s1 = 1.0 / tmp;
-            c1 = u / tmp;
-          }
-          {
-            const double a0 = m00, a1 = m01, b0 = m10, b1 = m11;
-            m00 = c1 * a0 + s1 * b0; m01 = c1 * a1 + s1 * b1;
-            m10 = -s1 * a0 + c1 * b0; m11 = -s1 * a1 + c1 * b1;
-          }
-          double cr = 1.0, sr = 0.0;
-          const double deno = 2.0 * fabs(m01);
-          if (!(deno < dmin)) {
-            const double tau_ = (m00 - m11) / deno;
-            const double w = sqrt(tau_ * tau_ + 1.0);
-            const double tt = (tau_ > 0.0) ? 1.0 / (tau_ + w) : 1.0 / (tau_ - w);
-            const double sign_t = tt > 0.0 ? 1.0 : -1.0;
-            const double nn = 1.0 / sqrt(tt * tt + 1.0);
-            sr = -sign_t * (m01 / fabs(m01)) * fabs(tt) * nn;
-            cr = nn;
-          }
-          const double cl = c1 * cr - s1 * (-sr);
-          const double sl = c1 * (-sr) + s1 * cr;
-          for (int j = 0; j < N; ++j) {  // W rows p, q by j_left
-            const double xp = W[p][j], xq = W[q][j];
-            W[p][j] = cl * xp + sl * xq;
-            W[q][j] = -sl * xp + cl * xq;
-          }
-          for (int i = 0; i < N; ++i) {  // U columns p, q by j_left^T
-            const double xp = U[i][p], xq = U[i][q];
-            U[i][p] = cl * xp - (-sl) * xq;
-            U[i][q] = (-sl) * xp + cl * xq;
-          }
-          for (int i = 0; i < N; ++i) {  // W columns p, q by j_right
-            const double xp = W[i][p], xq = W[i][q];
-            W[i][p] = cr * xp - sr * xq;
-            W[i][q] = sr * xp + cr * xq;
-          }
-          for (int i = 0; i < N; ++i) {  // V columns p, q by j_right
-            const double xp = V[i][p], xq = V[i][q];
-            V[i][p] = cr * xp - sr * xq;
-            V[i][q] = sr * xp + cr * xq;
-          }
-          maxd = dmaxd(maxd, dmaxd(fabs(W[p][p]), fabs(W[q][q])));
-        }
-    }
-    double sv[N];
-    for (int i = 0; i < N; ++i) {
-      sv[i] = fabs(W[i][i]);
-      if (W[i][i] < 0.0)
-        for (int k = 0; k < N; ++k) U[k][i] = -U[k][i];
-    }
-    for (int i = 0; i < N; ++i) sv[i] *= scale;
-    int nonzero = N;
-    for (int i = 0; i < N; ++i) {
-      int pos = i;
-      for (int j = i + 1; j < N; ++j)
-        if (sv[j] > sv[pos]) pos = j;
-      if (sv[pos] == 0.0) {
-        nonzero = i;
-        break;
-      }
-      if (pos != i) {
-        double t = sv[i]; sv[i] = sv[pos]; sv[pos] = t;
-        for (int k = 0; k < N; ++k) {
-          t = U[k][i]; U[k][i] = U[k][pos]; U[k][pos] = t;
-          t = V[k][i]; V[k][i] = V[k][pos]; V[k][pos] = t;
-        }
-      }
-    }
-    int rank = 0;
-    if (nonzero > 0) {
-      const double pre = dmaxd(sv[0] * (N * eps), dmin);
-      int i = nonzero - 1;
-      while (i >= 0 && sv[i] < pre) --i;
-      rank = i + 1;
-    }
-    double y[N], z[N];
-    for (int i = 0; i < rank; ++i) {
-      double t = 0.0;
-      for (int k = 0; k < N; ++k) t += U[k][i] * r[k];
-      y[i] = t / sv[i];
-    }
-    for (int k = 0; k < N; ++k) {
-      double t = 0.0;
-      for (int i = 0; i < rank; ++i) t += V[k][i] * y[i];
-      z[k] = t;
-    }
-    for (int k = 0; k < N; ++k) L.x[L.perm[k]] = (float)z[k];
-  }
+  if (lane == 0) lls5_jacobi(L, M, r, scale);
   bar();
 }
 
