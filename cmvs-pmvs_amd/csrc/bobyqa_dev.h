@@ -19,6 +19,21 @@
 #else
 #define BQ_HD inline
 #endif
+// The optimizer's state lives in LDS on the device (one BqState per chain, RefLds::bq).  Its big
+// routines are called out of line with LDS-typed pointers (BQ_AS): 32-bit ds addressing with
+// immediate offsets, and a register peak of the routine itself rather than of the whole inlined
+// kernel (the inlined optimizer hoisted state into ~470 VGPR+AGPR and capped the refine kernel at
+// one wavefront per SIMD).  Host builds (tests/csrc/bq_host.cpp) see plain pointers.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define BQ_AS __attribute__((address_space(3)))
+#else
+#define BQ_AS
+#endif
+#if defined(__HIPCC__) && !defined(BQ_INLINE)
+#define BQ_NI __host__ __device__ inline __attribute__((noinline))
+#else
+#define BQ_NI BQ_HD
+#endif
 
 #include <math.h>
 
@@ -83,10 +98,10 @@ struct BqState {
 };
 
 // ---------------------------------------------------------------- TRSBOX
-BQ_HD void bq_trsbox(const double (*xpt)[BQN + 1], const double* xopt, const double* gopt,
-                     const double* hq, const double* pq, const double* sl, const double* su,
-                     double delta, double* xnew, double* d, double* gnew, double* dsq_out,
-                     double* crvmin_out) {
+BQ_NI void bq_trsbox(const BQ_AS double (*xpt)[BQN + 1], const BQ_AS double* xopt, const BQ_AS double* gopt,
+                     const BQ_AS double* hq, const BQ_AS double* pq, const BQ_AS double* sl, const BQ_AS double* su,
+                     double delta, BQ_AS double* xnew, BQ_AS double* d, BQ_AS double* gnew, BQ_AS double* dsq_out,
+                     BQ_AS double* crvmin_out) {
   const double half = 0.5, one = 1.0, onemin = -1.0, zero = 0.0;
   double xbdi[BQN + 1], s[BQN + 1], hs[BQN + 1], hred[BQN + 1];
   int iterc = 0, nact = 0, itermax = 0, itcsav = 0, iact = 0, isav = 0, iu = 0;
@@ -348,10 +363,10 @@ L210: {
 }
 
 // ---------------------------------------------------------------- ALTMOV
-BQ_HD void bq_altmov(const double (*xpt)[BQN + 1], const double* xopt, const double (*bmat)[BQN + 1],
-                     const double (*zmat)[BQNPTM + 1], const double* sl, const double* su, int kopt,
-                     int knew, double adelt, double* xnew, double* xalt, double* alpha,
-                     double* cauchy) {
+BQ_NI void bq_altmov(const BQ_AS double (*xpt)[BQN + 1], const BQ_AS double* xopt, const BQ_AS double (*bmat)[BQN + 1],
+                     const BQ_AS double (*zmat)[BQNPTM + 1], const BQ_AS double* sl, const BQ_AS double* su, int kopt,
+                     int knew, double adelt, BQ_AS double* xnew, BQ_AS double* xalt, BQ_AS double* alpha,
+                     BQ_AS double* cauchy) {
   const double half = 0.5, one = 1.0, zero = 0.0;
   const double cnst = one + sqrt(2.0);
   double glag[BQN + 1], hcol[BQNPT + 1], w[2 * BQN + 1];
@@ -554,8 +569,8 @@ L120:
 }
 
 // ---------------------------------------------------------------- UPDATE
-BQ_HD void bq_update(double (*bmat)[BQN + 1], double (*zmat)[BQNPTM + 1], double* vlag, double beta,
-                     double denom, int knew, double* w) {
+BQ_NI void bq_update(BQ_AS double (*bmat)[BQN + 1], BQ_AS double (*zmat)[BQNPTM + 1], BQ_AS double* vlag, double beta,
+                     double denom, int knew, BQ_AS double* w) {
   const double one = 1.0, zero = 0.0;
   double ztest = zero, temp, tempa, tempb, alpha, tau;
   for (int k = 1; k <= BQNPT; ++k)
@@ -612,7 +627,7 @@ BQ_HD double bq_default_step(double x, double lb, double ub) {
 
 // Initialise: the nlopt_optimize -> bobyqa() wrapper up to the call of BOBYQB.
 // Returns 0 (then call bq_step with any f) or a negative NLopt error code.
-BQ_HD int bq_begin(BqState& st, const double* x0, const double* lb, const double* ub,
+BQ_HD int bq_begin(BQ_AS BqState& st, const double* x0, const double* lb, const double* ub,
                    double xtol_rel, int maxeval) {
   double dxs[BQN];
   for (int i = 0; i < BQN; ++i) dxs[i] = bq_default_step(x0[i], lb[i], ub[i]);
@@ -682,14 +697,14 @@ BQ_HD int bq_begin(BqState& st, const double* x0, const double* lb, const double
 
 // Advance the optimizer.  fin is the objective value requested by the previous call (ignored
 // on the first call).  Returns BQ_NEED_F with st.xeval set, or BQ_DONE with st.rc/st.xout.
-BQ_HD int bq_step_impl(BqState& st, double fin);
-BQ_HD int bq_step(BqState& st, double fin) {
+BQ_NI int bq_step_impl(BQ_AS BqState& st, double fin);
+BQ_HD int bq_step(BQ_AS BqState& st, double fin) {
   BQ_PT(t_all);
   const int r = bq_step_impl(st, fin);
   BQ_PA(3, t_all);
   return r;
 }
-BQ_HD int bq_step_impl(BqState& st, double fin) {
+BQ_NI int bq_step_impl(BQ_AS BqState& st, double fin) {
   const double half = 0.5, one = 1.0, ten = 10.0, tenth = 0.1, two = 2.0, zero = 0.0;
   double temp, sum, suma, sumb, bsum, dx, delsq, scaden, biglsq, hdiag, den, errbig, frhosq,
       bdtol, bdtest, curv, fracsq, sumpq, sumz, sumw, densav, pqold, gqsq, gisq, dist;

@@ -1032,12 +1032,24 @@ __device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS, NC>& C, int njobs
   PROF_MARK(6);
 }
 
+// Wavefronts per SIMD the refine kernel's register budget is sized for: 2 (<= 256 VGPR+AGPR).  The
+// out-of-line BOBYQA routines get the budget of their most permissive caller, so the self-test
+// kernels that call them use the same value.  Measured on C2 (tools/sweep_variants.sh,
+// profiles/r02g_sweeps.txt): 2 waves of 4 chains with 12 texture slots (19 KB LDS, 8 per CU)
+// beat 1 wave of 8 chains with the 512-register inlined optimizer by 17 %; 3 or 4 waves per SIMD
+// (168 / 128 registers) spill and lose 40-50 %.
+#ifndef REFINE_WPE
+#define REFINE_WPE(NC) 2
+#endif
+#ifndef BQ_CALLER_WPE
+#define BQ_CALLER_WPE 2
+#endif
 template <int WS, int TSLOTS, int NC>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC <= 4 ? 2 : 1))) void refine_v2_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(REFINE_WPE(NC)))) void refine_v2_kernel(
     DScene s, RefineJob* __restrict__ jobs, int n, DevStats* st) {
   __shared__ RefLds<WS, TSLOTS, NC> C;
   const int lane = lane_id();
-  BqState& bq = C.bq[lane < NC ? lane : 0];
+  BQ_AS BqState& bq = *(BQ_AS BqState*)&C.bq[lane < NC ? lane : 0];
   RefineSetup R;
   int cand = -1, need = 0, evals = 0, size = 0, nimg = 0, rc = 0;
   bool exhausted = lane >= NC;  // lanes >= NC only help evaluate
@@ -1412,18 +1424,21 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
   (void)hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL((pre_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_in, d_jobs, n, d_st);
   (void)hipEventRecord(ev[1], stream);
+  // a request's textures must fit one chunk (TSLOTS >= tau, tau <= PMVS_MAX_TAU = 16): smaller
+  // chunk configs are only valid for small tau, otherwise the default 24-slot kernel runs
+  if (tslots / 100 < s.tau) {
+    tslots = 2408;
+    refine_grid = refine_grid / 2 > 0 ? refine_grid / 2 : 1;  // 39 KB LDS: 4 resident per CU
+  }
   const int nc = tslots % 100;
   const int rg = refine_grid < (n + nc - 1) / nc ? refine_grid : (n + nc - 1) / nc;
   // tslots = texture slots per objective chunk * 100 + optimizer chains per wavefront
   switch (tslots) {
     case 804: hipLaunchKernelGGL((refine_v2_kernel<WS, 8, 4>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
-    case 1604: hipLaunchKernelGGL((refine_v2_kernel<WS, 16, 4>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 808: hipLaunchKernelGGL((refine_v2_kernel<WS, 8, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     case 1608: hipLaunchKernelGGL((refine_v2_kernel<WS, 16, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
-    case 1616: hipLaunchKernelGGL((refine_v2_kernel<WS, 16, 16>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     case 2408: hipLaunchKernelGGL((refine_v2_kernel<WS, 24, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
-    case 3208: hipLaunchKernelGGL((refine_v2_kernel<WS, 32, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
-    case 4808: hipLaunchKernelGGL((refine_v2_kernel<WS, 48, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
-    default: hipLaunchKernelGGL((refine_v2_kernel<WS, 32, 16>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    default: hipLaunchKernelGGL((refine_v2_kernel<WS, 12, 4>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
   }
   (void)hipEventRecord(ev[2], stream);
   hipLaunchKernelGGL((post_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_jobs, d_out, n, d_st);
@@ -1608,7 +1623,7 @@ hipError_t launch_math_selftest(int op, const double* d_in, double* d_out, int n
 // ==================================================================== BOBYQA self-test
 // Runs the device BOBYQA on analytic test objectives (same as oracle_bobyqa_test) so its
 // trajectories can be checked against the CPU oracle and its cost measured.
-//   mode 0: one problem per LANE, state in private memory (scratch)
+//   mode 0: one problem per LANE, 64 per workgroup (state in LDS, as in the refine kernel)
 //   mode 1: one problem per WAVE, lane 0 steps the state held in LDS (the v1 refine layout)
 namespace pmvsdev {
 __device__ __forceinline__ double bq_test_f(int kind, const double* v) {
@@ -1620,32 +1635,15 @@ __device__ __forceinline__ double bq_test_f(int kind, const double* v) {
   return (v[0] - 1) * (v[0] - 1) + (v[1] - 40) * (v[1] - 40) + (v[2] + 50) * (v[2] + 50);
 }
 
-__global__ void bobyqa_lane_kernel(int kind, const double* __restrict__ x0, int n, int maxeval, double* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  BqState st;
-  const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999}, ub[3] = {HUGE_VAL, 23.99999, 23.99999};
-  double x[3] = {x0[3 * i], x0[3 * i + 1], x0[3 * i + 2]};
-  bq_begin(st, x, lb, ub, 1e-7, maxeval);
-  double f = 0.0;
-  while (bq_step(st, f) == BQ_NEED_F) f = bq_test_f(kind, st.xeval);
-  out[6 * i + 0] = st.xout[0];
-  out[6 * i + 1] = st.xout[1];
-  out[6 * i + 2] = st.xout[2];
-  out[6 * i + 3] = st.minf;
-  out[6 * i + 4] = (double)st.nevals;
-  out[6 * i + 5] = (double)st.rc;
-}
-
 // Lane-per-problem with the BOBYQA state resident in LDS (C problems per 64-lane workgroup).
 template <int C>
-__global__ __launch_bounds__(64) void bobyqa_lds_kernel(int kind, const double* __restrict__ x0, int n, int maxeval,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BQ_CALLER_WPE))) void bobyqa_lds_kernel(int kind, const double* __restrict__ x0, int n, int maxeval,
                                                         double* __restrict__ out) {
   __shared__ BqState sts[C];
   const int lane = threadIdx.x;
   const int i = blockIdx.x * C + lane;
   if (lane >= C || i >= n) return;
-  BqState& st = sts[lane];
+  BQ_AS BqState& st = *(BQ_AS BqState*)&sts[lane];
   const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999}, ub[3] = {HUGE_VAL, 23.99999, 23.99999};
   double x[3] = {x0[3 * i], x0[3 * i + 1], x0[3 * i + 2]};
   bq_begin(st, x, lb, ub, 1e-7, maxeval);
@@ -1659,9 +1657,10 @@ __global__ __launch_bounds__(64) void bobyqa_lds_kernel(int kind, const double* 
   out[6 * i + 5] = (double)st.rc;
 }
 
-__global__ __launch_bounds__(64) void bobyqa_wave_kernel(int kind, const double* __restrict__ x0, int n, int maxeval,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BQ_CALLER_WPE))) void bobyqa_wave_kernel(int kind, const double* __restrict__ x0, int n, int maxeval,
                                                          double* __restrict__ out) {
-  __shared__ BqState st;
+  __shared__ BqState st_;
+  BQ_AS BqState& st = *(BQ_AS BqState*)&st_;
   __shared__ int stepv;
   __shared__ double fres;
   const int i = blockIdx.x;
@@ -1698,7 +1697,7 @@ hipError_t launch_bobyqa_selftest(int mode, int kind, const double* d_x0, int n,
                                   hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   if (mode == 0)
-    hipLaunchKernelGGL(bobyqa_lane_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, kind, d_x0, n, maxeval, d_out);
+    hipLaunchKernelGGL((bobyqa_lds_kernel<64>), dim3((n + 63) / 64), dim3(64), 0, stream, kind, d_x0, n, maxeval, d_out);
   else if (mode == 1)
     hipLaunchKernelGGL(bobyqa_wave_kernel, dim3(n), dim3(64), 0, stream, kind, d_x0, n, maxeval, d_out);
   else if (mode == 2)
