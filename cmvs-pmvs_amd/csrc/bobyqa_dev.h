@@ -11,7 +11,8 @@
 // (PRELIM, the main loop's label 360 and RESCUE) and resume.  One lane owns a BqState while
 // the whole wavefront evaluates the objective (cmvs-pmvs_amd/csrc/pmvs_kernels.hip).  The
 // arithmetic is Powell's, operation for operation; parity against the CPU oracle
-// (oracle/bobyqa_oracle.h) is tested trajectory-for-trajectory in tests/test_bobyqa.py.
+// (oracle/bobyqa_oracle.h) is tested trajectory-for-trajectory in tests/test_gpu_bobyqa.py (device)
+// and tests/test_bobyqa_host.py (this header compiled for the host).
 #pragma once
 
 #if defined(__HIPCC__)

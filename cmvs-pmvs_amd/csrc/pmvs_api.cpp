@@ -279,6 +279,15 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
   const int tau = std::min(d->min_image_num * 2, d->num_views);
   if (tau > PMVS_MAX_TAU) return fail(PMVS_EUNSUPPORTED, "tau = min(2*minImageNum, num) = %d > %d", tau, PMVS_MAX_TAU);
   if (!d->views || !d->visdata2_offsets) return fail(PMVS_EINVAL, "views / visdata2 missing");
+  {  // the organizer and commit records index target cells (pgrids) with 32-bit ints
+    long long cells = 0;
+    for (int t = 0; t < d->num_targets; ++t) {
+      long long w = d->views[t].width, h = d->views[t].height;
+      for (int l = 0; l < d->level; ++l) { w /= 2; h /= 2; }
+      cells += ((w + d->csize - 1) / d->csize) * ((h + d->csize - 1) / d->csize);
+    }
+    if (cells > INT_MAX) return fail(PMVS_EUNSUPPORTED, "%lld target cells at level %d exceed 2^31 - 1", cells, d->level);
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(PMVS_EDEVICE, "no HIP device available");
   if (device < 0 || device >= ndev) return fail(PMVS_EINVAL, "device %d of %d", device, ndev);

@@ -54,6 +54,13 @@ inline void poison_alloc(void* p, size_t bytes) {
 }
 
 constexpr int NB_CAP = 1024;  // neighbours per patch in filterNeighbor (overflow is reported)
+// Global scratch per persistent workgroup of the neighbour walks (doubles): the lls rows M
+// (5 NB_CAP), its right-hand side r (NB_CAP), then the filterQuad coordinates fx, fy, fz as floats
+// (1.5 NB_CAP).  Kept out of LDS so NbLds stays ~8 KB (occupancy of the latency-bound walks).
+constexpr int NB_SCR = NB_CAP * 8;
+// Persistent workgroups per CU-grid unit for the NbLds kernels (neighbor_kernel, depth_post_kernel,
+// empty_blocks_kernel): twice the organizer grid, since ~8 KB of LDS and <= 107 VGPRs leave room.
+constexpr int NB_GRID_MULT = 2;
 __device__ __forceinline__ int lane_id_w() { return threadIdx.x & 63; }
 // Wave-uniform copies (SGPR) of values that are uniform by construction but loaded from memory:
 // every branch or loop around a barrier is driven by one of these, never by a VGPR value.
@@ -453,7 +460,7 @@ __global__ void exact_after_ref_kernel(DScene s, const pmvs_patch* __restrict__ 
 struct NbLds {
   int sb[64], so[64], sl[64];  // gather_neighbors: per-slot list start, flattened offset, list kind
   int nb[NB_CAP];
-  float fx[NB_CAP], fy[NB_CAP], fz[NB_CAP];
+  float seq[NB_CAP];  // values summed in the reference's order by one lane (filterQuad)
   float units[PMVS_MAX_IMAGES];
   int cnt, overflow;
   double f[5];
@@ -917,15 +924,18 @@ __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, d
   ydir[0] = z[1] * xdir[2] - z[2] * xdir[1];
   ydir[1] = z[2] * xdir[0] - z[0] * xdir[2];
   ydir[2] = z[0] * xdir[1] - z[1] * xdir[0];
+  float* gx = reinterpret_cast<float*>(r + NB_CAP);  // fx, fy, fz in the workgroup's global scratch
+  float* gy = gx + NB_CAP;
+  float* gz = gy + NB_CAP;
   for (int a = lane; a < n; a += 64) {  // the distances in parallel, their sum in order below
     float d[4];
     for (int k = 0; k < 4; ++k) d[k] = F.P[L.nb[a]].coord[k] - q.coord[k];
-    L.fx[a] = norm4(d);
+    L.seq[a] = norm4(d);
   }
   __syncthreads();
   if (lane == 0) {
     float h = 0.0f;
-    for (int a = 0; a < n; ++a) h += L.fx[a];
+    for (int a = 0; a < n; ++a) h += L.seq[a];
     L.f[1] = (double)__fdiv_rn(h, (float)n);
   }
   __syncthreads();
@@ -934,7 +944,7 @@ __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, d
     float d[4];
     for (int k = 0; k < 4; ++k) d[k] = F.P[L.nb[a]].coord[k] - q.coord[k];
     const float fx = __fdiv_rn(dot4(d, xdir), h), fy = __fdiv_rn(dot4(d, ydir), h), fz = dot4(d, q.normal);
-    L.fx[a] = fx; L.fy[a] = fy; L.fz[a] = fz;
+    gx[a] = fx; gy[a] = fy; gz[a] = fz;
     M[(size_t)a * 5 + 0] = (double)(fx * fx);
     M[(size_t)a * 5 + 1] = (double)(fy * fy);
     M[(size_t)a * 5 + 2] = (double)(fx * fy);
@@ -945,17 +955,19 @@ __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, d
   __threadfence_block();
   __syncthreads();
   lls5_wave(L, M, r, n);
+  for (int a = lane; a < n; a += 64) {  // the residuals in parallel (each lane its own rows)
+    const float fx = gx[a], fy = gy[a];
+    L.seq[a] = L.x[0] * (fx * fx) + L.x[1] * (fy * fy) + L.x[2] * (fx * fy) + L.x[3] * fx + L.x[4] * fy - gz[a];
+  }
+  __syncthreads();
   if (lane == 0) {
     const int inum = imin(s.tau, q.num_images);
     float u2 = 0.0f;
     for (int k = 0; k < inum; ++k) u2 += get_unit(s, s.views[q.images[k]], q.coord);
     u2 = __fdiv_rn(u2, (float)inum);
     float residual = 0.0f;
-    for (int a = 0; a < n; ++a) {
-      const float fx = L.fx[a], fy = L.fy[a];
-      const float res = L.x[0] * (fx * fx) + L.x[1] * (fy * fy) + L.x[2] * (fx * fy) + L.x[3] * fx + L.x[4] * fy - L.fz[a];
-      residual = (float)((double)residual + fabs((double)res) / (double)u2);  // float += double
-    }
+    for (int a = 0; a < n; ++a)  // in the reference's order
+      residual = (float)((double)residual + fabs((double)L.seq[a]) / (double)u2);  // float += double
     residual = __fdiv_rn(residual, (float)(n - 5));
     L.cnt = (residual < s.quad ? 0 : 1);
   }
@@ -970,7 +982,7 @@ __global__ __launch_bounds__(64) void neighbor_kernel(DScene s, FilterDev F, dou
                                                       int* __restrict__ queue, int* __restrict__ dbg_counts) {
   __shared__ NbLds L;
   const int lane = threadIdx.x;
-  double* M = scratch + (size_t)blockIdx.x * NB_CAP * 6;
+  double* M = scratch + (size_t)blockIdx.x * NB_SCR;
   double* r = M + (size_t)NB_CAP * 5;
   for (;;) {
     int i = 0;
@@ -1187,7 +1199,7 @@ __global__ __launch_bounds__(64) void depth_post_kernel(DScene s, FilterDev F, c
   __shared__ NbLds L;
   __shared__ pmvs_patch Q;  // the patch is built in LDS and stored once (no global read-back)
   const int lane = threadIdx.x;
-  double* M = scratch + (size_t)blockIdx.x * NB_CAP * 6;
+  double* M = scratch + (size_t)blockIdx.x * NB_SCR;
   double* r = M + (size_t)NB_CAP * 5;
   for (;;) {
     int k = 0;
@@ -1416,7 +1428,7 @@ hipError_t FilterBuffers::reserve(int n_, long long ncells_, int tnum_, int grid
   FCHK(dalloc(pg_items, ne)); FCHK(dalloc(vp_items, ne)); FCHK(dalloc(dpkey, cap_cells));
   FCHK(dalloc(order, cap_n)); FCHK(dalloc(rank, cap_n)); FCHK(dalloc(unit0, cap_n)); FCHK(dalloc(flags, cap_n));
   FCHK(dalloc(safe, cap_n)); FCHK(dalloc(need, cap_n)); FCHK(dalloc(list, cap_n));
-  FCHK(dalloc(scratch, (size_t)cap_grid * NB_CAP * 6)); FCHK(dalloc(counters, 8));
+  FCHK(dalloc(scratch, (size_t)cap_grid * NB_SCR)); FCHK(dalloc(counters, 8));
   FCHK(dalloc(edge_off, cap_n + 1));
   size_t t1 = 0, t2 = 0;
   FCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, t1, keys, keys2, (int)ne));
@@ -1535,7 +1547,7 @@ static hipError_t apply_flags(Ctx& c, int* removed) {
 hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n, long long ncells, const long long* h_tgoff,
                        int grid, hipStream_t st, int counts[4], int* overflow, int* keep_dev) {
   dbg(st, "start");
-  FCHK(B.reserve(n, ncells, s.tnum, grid));
+  FCHK(B.reserve(n, ncells, s.tnum, grid * NB_GRID_MULT));
   dbg(st, "reserve");
   FCHK(hipMemcpyAsync(B.tgoff, h_tgoff, (s.tnum + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
   Ctx c{s, B, dP, n, ncells, grid, st};
@@ -1581,7 +1593,7 @@ hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n,
   FCHK(hipMemsetAsync(B.flags, 0, n * sizeof(int), st));
   FCHK(hipMemsetAsync(B.counters + 3, 0, 5 * sizeof(int), st));
   if (c.nalive)
-    hipLaunchKernelGGL(neighbor_kernel, dim3(std::min(grid, c.nalive)), dim3(64), 0, st, s, c.dev(), B.scratch, B.flags,
+    hipLaunchKernelGGL(neighbor_kernel, dim3(std::min(grid * NB_GRID_MULT, c.nalive)), dim3(64), 0, st, s, c.dev(), B.scratch, B.flags,
                        B.counters + 3, B.counters + 4, getenv("PMVS_FILTER_DEBUG") ? B.need : nullptr);
   dbg(st, "neighbor kernel");
   if (getenv("PMVS_FILTER_DEBUG")) {
@@ -2342,17 +2354,30 @@ struct PhaseTimer {
 // depth >= 1 postProcess of a wave's candidates is split into contiguous rank ranges, and the
 // refined records are all-gathered (sh.exchange) before the identical commit -- so the model is
 // bit-identical to the one-rank run with the same wave.
-hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs_patch*& dP, size_t& dP_cap, int n0,
-                       const int* d_alive, int cap, long long ncells, const long long* h_tgoff, int wave, int cthr,
-                       int flags, int grid, hipStream_t st, const RefineFn& refine, const Shard& sh, long long stats[8],
-                       int* n_out, int min_cands) {
+// Sharded error protocol: every rank makes the same sequence of exchanges.  Each refine batch
+// all-gathers a 2-int header {error, overflow} before its payload; a rank that fails anywhere
+// else (allocation, a device error between exchanges) leaves the pass and makes one terminal
+// header exchange with its error (expand_pass), which its peers receive in place of their next
+// batch header or of their own terminal exchange -- so all ranks return the error together
+// instead of blocking in the next all-gather.  `agreed` = the pass ended on a header every rank saw.
+// Test hook (tests/test_gpu_expand.py): PMVS_TEST_SHARD_FAIL="rank:wave:b|a" fails that rank at the
+// given wave before its batch exchange (b) or right after it (a).
+static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs_patch*& dP, size_t& dP_cap,
+                                   int n0, const int* d_alive, int cap, long long ncells, const long long* h_tgoff,
+                                   int wave, int cthr, int flags, int grid, hipStream_t st, const RefineFn& refine,
+                                   const Shard& sh, long long stats[8], int* n_out, int min_cands, bool& agreed) {
+  agreed = false;
+  int inj_rank = -1, inj_wave = -1;
+  char inj_where = 0;
+  if (const char* e = getenv("PMVS_TEST_SHARD_FAIL")) (void)sscanf(e, "%d:%d:%c", &inj_rank, &inj_wave, &inj_where);
+  const bool inject = sh.world > 1 && inj_rank == sh.rank;
   for (int k = 0; k < 8; ++k) stats[k] = 0;
   *n_out = n0;
   PhaseTimer T(st);
   const int W = std::max(1, std::min(wave, kMaxWave));
   // device patch capacity: the model plus a few waves, doubled when the commits need more
   size_t pcap = std::min<size_t>((size_t)cap, (size_t)n0 + 12 * (size_t)W + 1024);
-  FCHK(B.reserve((int)pcap, ncells, s.tnum, grid));
+  FCHK(B.reserve((int)pcap, ncells, s.tnum, grid * NB_GRID_MULT));
   pcap = std::min<size_t>((size_t)B.cap_n, (size_t)cap);
   FCHK(grow_keep(dP, dP_cap, pcap, (size_t)n0, st));
   FCHK(hipMemcpyAsync(B.tgoff, h_tgoff, (s.tnum + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
@@ -2418,6 +2443,7 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
   std::vector<int> okh;
   while (!q_empty()) {
     stats[7]++;
+    if (inject && inj_where == 'b' && stats[7] == inj_wave) return hipErrorOutOfMemory;
     // A wave: chunks of W parents (queue order) until it holds min_cands candidate directions
     // (findEmptyBlocks against the start-of-wave model; min_cands = 0 or W = 1: one chunk).
     std::vector<int> parents;
@@ -2433,7 +2459,7 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
       FCHK(grow_keep(X.cand_ok, X.cap_ok, parents.size() * 6, (size_t)off * 6, st));
       FCHK(hipMemcpyAsync(X.parents + off, parents.data() + off, nc * sizeof(int), hipMemcpyHostToDevice, st));
       FCHK(hipMemsetAsync(B.counters + 3, 0, 5 * sizeof(int), st));
-      hipLaunchKernelGGL(empty_blocks_kernel, dim3(std::min(grid, nc)), dim3(64), 0, st, s, c.dev(), X.parents + off, nc,
+      hipLaunchKernelGGL(empty_blocks_kernel, dim3(std::min(grid * NB_GRID_MULT, nc)), dim3(64), 0, st, s, c.dev(), X.parents + off, nc,
                          X.cand_coord + (size_t)off * 24, X.cand_ok + (size_t)off * 6, B.counters + 4, B.counters + 3);
       if (W > 1 && min_cands > 0) {
         okh.resize((size_t)nc * 6);
@@ -2496,7 +2522,7 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
             FCHK(refine(X.cand2 + lo, mine, X.res + lo));
             T.mark(4);
             FCHK(hipMemsetAsync(B.counters + 4, 0, sizeof(int), st));
-            hipLaunchKernelGGL(depth_post_kernel, dim3(std::min(grid, mine)), dim3(64), 0, st, s, c.dev(), X.res + lo, mine,
+            hipLaunchKernelGGL(depth_post_kernel, dim3(std::min(grid * NB_GRID_MULT, mine)), dim3(64), 0, st, s, c.dev(), X.res + lo, mine,
                                X.outp + lo, X.ostatus + lo, B.scratch, B.counters + 4, B.counters + 3);
             FCHK(hipPeekAtLastError());
           }
@@ -2506,37 +2532,40 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
       hipError_t lerr = local();
       T.mark(5);
       if (G > 1) {
-        // all-gather of [error, overflow, status[chunk], patch[chunk]] per rank; the other ranks'
-        // ranges are then uploaded so every rank holds all m refined records
-        const size_t bytes = 2 * sizeof(int) + (size_t)chunk * (sizeof(int) + sizeof(pmvs_patch));
+        // all-gather of the header {error, overflow}, then (every rank ok) of [status[chunk],
+        // patch[chunk]] per rank; the other ranks' ranges are uploaded so every rank holds all m
+        // refined records
+        const size_t bytes = (size_t)chunk * (sizeof(int) + sizeof(pmvs_patch));
         xsend.assign(bytes, 0);
         xrecv.assign(bytes * G, 0);
-        int hdr[2] = {(int)lerr, ovf};
-        std::memcpy(xsend.data(), hdr, sizeof(hdr));
         if (lerr == hipSuccess && mine > 0) {
-          lerr = hipMemcpyAsync(xsend.data() + 2 * sizeof(int), X.ostatus + lo, mine * sizeof(int), hipMemcpyDeviceToHost, st);
+          lerr = hipMemcpyAsync(xsend.data(), X.ostatus + lo, mine * sizeof(int), hipMemcpyDeviceToHost, st);
           if (lerr == hipSuccess)
-            lerr = hipMemcpyAsync(xsend.data() + 2 * sizeof(int) + (size_t)chunk * sizeof(int), X.outp + lo,
-                                  (size_t)mine * sizeof(pmvs_patch), hipMemcpyDeviceToHost, st);
+            lerr = hipMemcpyAsync(xsend.data() + (size_t)chunk * sizeof(int), X.outp + lo, (size_t)mine * sizeof(pmvs_patch),
+                                  hipMemcpyDeviceToHost, st);
           if (lerr == hipSuccess) lerr = hipStreamSynchronize(st);
-          hdr[0] = (int)lerr;
-          std::memcpy(xsend.data(), hdr, sizeof(hdr));
         }
-        if (sh.exchange(xsend.data(), bytes, xrecv.data()) != 0) return hipErrorUnknown;
+        int hdr[2] = {(int)lerr, ovf};
+        std::vector<int> hall(2 * (size_t)G, 0);
+        agreed = true;  // from here on every return is seen by all ranks
+        if (sh.exchange(hdr, sizeof(hdr), hall.data()) != 0) return hipErrorUnknown;
         for (int r = 0; r < G; ++r) {
-          const char* b = xrecv.data() + (size_t)r * bytes;
-          std::memcpy(hdr, b, sizeof(hdr));
-          if (hdr[0] != 0 && lerr == hipSuccess) lerr = hipErrorUnknown;  // another rank failed
-          ovf |= hdr[1];
+          if (hall[2 * r] != 0 && lerr == hipSuccess) lerr = hipErrorUnknown;  // another rank failed
+          ovf |= hall[2 * r + 1];
         }
-        for (int r = 0; r < G && lerr == hipSuccess && !ovf; ++r) {
+        FCHK(lerr);
+        if (ovf) return hipErrorOutOfMemory;  // more than NB_CAP neighbours (reported by the API)
+        if (sh.exchange(xsend.data(), bytes, xrecv.data()) != 0) return hipErrorUnknown;
+        agreed = false;
+        for (int r = 0; r < G; ++r) {
           const char* b = xrecv.data() + (size_t)r * bytes;
           const int rlo = std::min(m, r * chunk), rhi = std::min(m, rlo + chunk);
           if (r == R || rhi <= rlo) continue;
-          FCHK(hipMemcpyAsync(X.ostatus + rlo, b + 2 * sizeof(int), (rhi - rlo) * sizeof(int), hipMemcpyHostToDevice, st));
-          FCHK(hipMemcpyAsync(X.outp + rlo, b + 2 * sizeof(int) + (size_t)chunk * sizeof(int),
-                              (size_t)(rhi - rlo) * sizeof(pmvs_patch), hipMemcpyHostToDevice, st));
+          FCHK(hipMemcpyAsync(X.ostatus + rlo, b, (rhi - rlo) * sizeof(int), hipMemcpyHostToDevice, st));
+          FCHK(hipMemcpyAsync(X.outp + rlo, b + (size_t)chunk * sizeof(int), (size_t)(rhi - rlo) * sizeof(pmvs_patch),
+                              hipMemcpyHostToDevice, st));
         }
+        if (inject && inj_where == 'a' && stats[7] == inj_wave) return hipErrorOutOfMemory;
       }
       FCHK(lerr);
       if (ovf) return hipErrorOutOfMemory;  // more than NB_CAP neighbours (reported by the API)
@@ -2596,6 +2625,24 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
   }
   *n_out = nmodel;
   return hipGetLastError();
+}
+
+hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs_patch*& dP, size_t& dP_cap, int n0,
+                       const int* d_alive, int cap, long long ncells, const long long* h_tgoff, int wave, int cthr,
+                       int flags, int grid, hipStream_t st, const RefineFn& refine, const Shard& sh, long long stats[8],
+                       int* n_out, int min_cands) {
+  bool agreed = false;
+  hipError_t e = expand_pass_impl(s, B, X, dP, dP_cap, n0, d_alive, cap, ncells, h_tgoff, wave, cthr, flags, grid, st,
+                                  refine, sh, stats, n_out, min_cands, agreed);
+  if (sh.world > 1 && !agreed) {  // terminal header: a local failure reaches the peers, or theirs reach us
+    const int G = sh.world;
+    int hdr[2] = {(int)e, 0};
+    std::vector<int> hall(2 * (size_t)G, 0);
+    if (sh.exchange(hdr, sizeof(hdr), hall.data()) != 0) return e != hipSuccess ? e : hipErrorUnknown;
+    for (int r = 0; r < G; ++r)
+      if (hall[2 * r] != 0 && e == hipSuccess) e = hipErrorUnknown;  // a peer failed
+  }
+  return e;
 }
 
 // Self-test of lls5_wave (tests/test_gpu_lls.py): one workgroup per n x 5 system.

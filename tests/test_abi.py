@@ -86,3 +86,22 @@ def test_invalid_arguments_rejected(product_lib):
     assert lib.pmvs_scene_create(None, 0, C.byref(h)) != 0
     assert lib.pmvs_last_error()
     assert lib.pmvs_refine_batch(None, None, 0, None, None) != 0
+
+
+def test_cell_index_range_rejected(product_lib):
+    """Target cells are indexed with 32-bit ints (pgrids, commit records): a scene whose target
+    cells at its level exceed 2^31 - 1 (64 targets of 8192x4320 at csize 1) is rejected as
+    PMVS_EUNSUPPORTED before anything is allocated (advice r01, low)."""
+    import pmvs_amd as P
+    lib = product_lib
+    nv = 64
+    views = (P.ViewDesc * nv)()
+    for v in views:
+        v.width, v.height = 8192, 4320
+    off = (C.c_int32 * (nv + 1))()
+    d = P.SceneDesc(num_views=nv, num_targets=nv, level=0, csize=1, wsize=7, min_image_num=3, threshold=0.7,
+                    max_angle=10.0, quad_threshold=2.0, sequence=-1, visdata2_offsets=C.cast(off, C.c_void_p),
+                    views=views)
+    h = C.c_void_p()
+    assert lib.pmvs_scene_create(C.byref(d), 0, C.byref(h)) == 4  # PMVS_EUNSUPPORTED
+    assert b"target cells" in lib.pmvs_last_error()

@@ -132,7 +132,7 @@ def test_expand_device_growth_small_waves(gpu_available, oracle_mod):
     compare(out_g, al_g, st_g, out_o, al_o, st_o)
 
 
-def run_sharded(P, inp, model, world, fn, **kw):
+def run_sharded(P, inp, model, world, fn, expect_errors=False, **kw):
     """`world` scenes on GPU 0, one per thread, sharing one in-process all-gather (the same
     protocol bench.py runs with one process per GPU over RCCL)."""
     import threading
@@ -140,23 +140,27 @@ def run_sharded(P, inp, model, world, fn, **kw):
     scenes = [P.Scene(inp) for _ in range(world)]
     for r, sc in enumerate(scenes):
         sc.set_shard(r, world, *ex.endpoint(r))
-    res, errs = [None] * world, []
+    res, errs = [None] * world, [None] * world
 
     def work(r):
         try:
             res[r] = fn(scenes[r], model, **kw)
         except Exception as e:  # noqa: BLE001
-            errs.append(e)
+            errs[r] = e
 
-    th = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    th = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(world)]
     for t in th:
         t.start()
     for t in th:
-        t.join(timeout=300)
+        t.join(timeout=120)
+    hung = [r for r, t in enumerate(th) if t.is_alive()]
+    assert not hung, f"ranks {hung} still blocked (exchange deadlock)"
     for sc in scenes:
         sc.close()
     ex.close()
-    assert not errs, errs
+    if expect_errors:
+        return errs
+    assert not any(errs), errs
     return res
 
 
@@ -183,6 +187,26 @@ def test_sharded_expand_matches_single_rank(gpu_available, world, wave):
     assert sum(r[2]["refined"] for r in res) == st_ref["refined"]
     assert sum(r[2]["evals"] for r in res) == st_ref["evals"]
     assert all(r[2]["refined"] > 0 for r in res)
+
+
+@pytest.mark.parametrize("where", ["b", "a"])
+def test_sharded_expand_rank_failure_fails_all_ranks(gpu_available, monkeypatch, where):
+    """A failure on ONE rank of a sharded expansion (advice r01: an allocation failure between
+    exchanges used to leave the peers blocked in the next all-gather) makes every rank return an
+    error: injected on rank 1 at wave 2 before its batch exchange (b) or right after it (a)."""
+    import pmvs_amd as P
+    inp, p = P.synth_scene(6, 480, 360, level=1, supersample=2)
+    g = P.Scene(inp)
+    pa = seed_model(P, g, inp, p, 300, 3)
+    g.close()
+
+    def fn(sc, model, **kw):
+        sc.set_thresholds(inp.threshold, inp.threshold - 0.3, 2)
+        return sc.expand_run(model, **kw)
+
+    monkeypatch.setenv("PMVS_TEST_SHARD_FAIL", f"1:2:{where}")
+    errs = run_sharded(P, inp, pa, 2, fn, expect_errors=True, wave=64)
+    assert all(isinstance(e, P.PmvsError) for e in errs), errs
 
 
 def test_sharded_full_loop_matches_single_rank(gpu_available):
