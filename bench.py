@@ -46,7 +46,7 @@ sys.path.insert(0, os.path.join(ROOT, "cmvs-pmvs_amd"))
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 BYTES_PER_TEXTURE = 49 * 4 * 3  # wsize^2 samples x 4 texels x 3 B
-_RCFG = int(os.environ.get("PMVS_REFINE_CONFIG", "1204"))  # texture slots * 100 + chains per wavefront
+_RCFG = int(os.environ.get("PMVS_REFINE_CONFIG", "1206"))  # texture slots * 100 + chains per wavefront
 REFINE_KERNEL = f"refine_v2_kernel<7,{_RCFG // 100},{_RCFG % 100}>"
 
 

@@ -73,17 +73,19 @@ BQ_HD double bq_min(double a, double b) { return (a <= b) ? a : b; }  // NLopt M
 BQ_HD double bq_max(double a, double b) { return (a >= b) ? a : b; }  // NLopt MAX2
 
 struct BqState {
-  // problem (rescaled space, 1-based)
-  double x[BQN + 1], xl[BQN + 1], xu[BQN + 1], s[BQN];
+  // Powell's 1-based arrays stored without their unused row/column 0 (2216 -> 1736 bytes: the
+  // state of a chain lives in LDS); bq_begin / bq_step_impl address them through 1-based aliases
+  // (BQ_ALIASES).
+  // problem (rescaled space)
+  double x_[BQN], xl_[BQN], xu_[BQN], s[BQN];
   double rhobeg, rhoend;
   int maxeval, nevals;
   // BOBYQB arrays
-  double xbase[BQN + 1], xpt[BQNPT + 1][BQN + 1], fval[BQNPT + 1], xopt[BQN + 1], gopt[BQN + 1],
-      hq[BQNH + 1], pq[BQNPT + 1], bmat[BQNDIM + 1][BQN + 1], zmat[BQNPT + 1][BQNPTM + 1],
-      sl[BQN + 1], su[BQN + 1], xnew[BQN + 1], xalt[BQN + 1], d[BQN + 1], vlag[BQNDIM + 1],
-      w[BQNDIM + BQNPT + 1];
-  double gnew[BQN + 1];  // TRSBOX's GNEW (Powell's W(1..N) after TRSBOX)
-  double ptsaux[3][BQN + 1], ptsid[BQNPT + 1];
+  double xbase_[BQN], xpt_[BQNPT][BQN], fval_[BQNPT], xopt_[BQN], gopt_[BQN], hq_[BQNH], pq_[BQNPT],
+      bmat_[BQNDIM][BQN], zmat_[BQNPT][BQNPTM], sl_[BQN], su_[BQN], xnew_[BQN], xalt_[BQN], d_[BQN],
+      vlag_[BQNDIM], w_[BQNDIM + BQNPT];
+  double gnew_[BQN];  // TRSBOX's GNEW (Powell's W(1..N) after TRSBOX)
+  double ptsaux_[2][BQN], ptsid_[BQNPT];
   // BOBYQB scalars
   double f, fbeg, fsave, xoptsq, rho, delta, diffa, diffb, diffc, dnorm, distsq, dsq, crvmin,
       adelt, alpha, cauchy, beta, denom, fopt, vquad, diff, ratio, stepa, stepb;
@@ -98,8 +100,17 @@ struct BqState {
   double minf;
 };
 
+// 1-based views of a BqState's arrays (Powell's indexing; element 0 / row 0 / column 0 are never
+// touched), as the subroutines take them.
+#define BQ_A1(name) BQ_AS double* const name = (st).name##_ - 1
+#define BQ_A2(name, C) BQ_AS double(*const name)[C] = (BQ_AS double(*)[C])(&(st).name##_[0][0] - (C) - 1)
+#define BQ_ALIASES(st)                                                                                         \
+  BQ_A1(x); BQ_A1(xl); BQ_A1(xu); BQ_A1(xbase); BQ_A1(fval); BQ_A1(xopt); BQ_A1(gopt); BQ_A1(hq); BQ_A1(pq); \
+  BQ_A1(sl); BQ_A1(su); BQ_A1(xnew); BQ_A1(xalt); BQ_A1(d); BQ_A1(vlag); BQ_A1(w); BQ_A1(gnew); BQ_A1(ptsid); \
+  BQ_A2(xpt, BQN); BQ_A2(bmat, BQN); BQ_A2(zmat, BQNPTM); BQ_A2(ptsaux, BQN)
+
 // ---------------------------------------------------------------- TRSBOX
-BQ_NI void bq_trsbox(const BQ_AS double (*xpt)[BQN + 1], const BQ_AS double* xopt, const BQ_AS double* gopt,
+BQ_NI void bq_trsbox(const BQ_AS double (*xpt)[BQN], const BQ_AS double* xopt, const BQ_AS double* gopt,
                      const BQ_AS double* hq, const BQ_AS double* pq, const BQ_AS double* sl, const BQ_AS double* su,
                      double delta, BQ_AS double* xnew, BQ_AS double* d, BQ_AS double* gnew, BQ_AS double* dsq_out,
                      BQ_AS double* crvmin_out) {
@@ -364,8 +375,8 @@ L210: {
 }
 
 // ---------------------------------------------------------------- ALTMOV
-BQ_NI void bq_altmov(const BQ_AS double (*xpt)[BQN + 1], const BQ_AS double* xopt, const BQ_AS double (*bmat)[BQN + 1],
-                     const BQ_AS double (*zmat)[BQNPTM + 1], const BQ_AS double* sl, const BQ_AS double* su, int kopt,
+BQ_NI void bq_altmov(const BQ_AS double (*xpt)[BQN], const BQ_AS double* xopt, const BQ_AS double (*bmat)[BQN],
+                     const BQ_AS double (*zmat)[BQNPTM], const BQ_AS double* sl, const BQ_AS double* su, int kopt,
                      int knew, double adelt, BQ_AS double* xnew, BQ_AS double* xalt, BQ_AS double* alpha,
                      BQ_AS double* cauchy) {
   const double half = 0.5, one = 1.0, zero = 0.0;
@@ -570,7 +581,7 @@ L120:
 }
 
 // ---------------------------------------------------------------- UPDATE
-BQ_NI void bq_update(BQ_AS double (*bmat)[BQN + 1], BQ_AS double (*zmat)[BQNPTM + 1], BQ_AS double* vlag, double beta,
+BQ_NI void bq_update(BQ_AS double (*bmat)[BQN], BQ_AS double (*zmat)[BQNPTM], BQ_AS double* vlag, double beta,
                      double denom, int knew, BQ_AS double* w) {
   const double one = 1.0, zero = 0.0;
   double ztest = zero, temp, tempa, tempb, alpha, tau;
@@ -630,6 +641,7 @@ BQ_HD double bq_default_step(double x, double lb, double ub) {
 // Returns 0 (then call bq_step with any f) or a negative NLopt error code.
 BQ_HD int bq_begin(BQ_AS BqState& st, const double* x0, const double* lb, const double* ub,
                    double xtol_rel, int maxeval) {
+  BQ_ALIASES(st);
   double dxs[BQN];
   for (int i = 0; i < BQN; ++i) dxs[i] = bq_default_step(x0[i], lb[i], ub[i]);
   for (int i = 0; i < BQN; ++i) st.s[i] = 1.0;
@@ -641,9 +653,9 @@ BQ_HD int bq_begin(BQ_AS BqState& st, const double* x0, const double* lb, const 
       for (i = 1; i < BQN; ++i) st.s[i] = dxs[i] / dxs[0];
   }
   for (int i = 0; i < BQN; ++i) {
-    st.x[i + 1] = x0[i] / st.s[i];
-    st.xl[i + 1] = lb[i] / st.s[i];
-    st.xu[i + 1] = ub[i] / st.s[i];
+    x[i + 1] = x0[i] / st.s[i];
+    xl[i + 1] = lb[i] / st.s[i];
+    xu[i + 1] = ub[i] / st.s[i];
   }
   st.rhobeg = fabs(dxs[0] / st.s[0]);
   st.rhoend = xtol_rel * st.rhobeg;
@@ -653,34 +665,34 @@ BQ_HD int bq_begin(BQ_AS BqState& st, const double* x0, const double* lb, const 
   st.resume = 0;
   st.minf = 0;
   for (int j = 1; j <= BQN; ++j) {
-    const double temp = st.xu[j] - st.xl[j];
+    const double temp = xu[j] - xl[j];
     if (temp < st.rhobeg + st.rhobeg) {
       st.rc = BQR_INVALID_ARGS;
       for (int i = 0; i < BQN; ++i) st.xout[i] = x0[i];
       st.resume = -1;
       return BQR_INVALID_ARGS;
     }
-    st.sl[j] = st.xl[j] - st.x[j];
-    st.su[j] = st.xu[j] - st.x[j];
-    if (st.sl[j] >= -st.rhobeg) {
-      if (st.sl[j] >= 0.0) {
-        st.x[j] = st.xl[j];
-        st.sl[j] = 0.0;
-        st.su[j] = temp;
+    sl[j] = xl[j] - x[j];
+    su[j] = xu[j] - x[j];
+    if (sl[j] >= -st.rhobeg) {
+      if (sl[j] >= 0.0) {
+        x[j] = xl[j];
+        sl[j] = 0.0;
+        su[j] = temp;
       } else {
-        st.x[j] = st.xl[j] + st.rhobeg;
-        st.sl[j] = -st.rhobeg;
-        st.su[j] = bq_max(st.xu[j] - st.x[j], st.rhobeg);
+        x[j] = xl[j] + st.rhobeg;
+        sl[j] = -st.rhobeg;
+        su[j] = bq_max(xu[j] - x[j], st.rhobeg);
       }
-    } else if (st.su[j] <= st.rhobeg) {
-      if (st.su[j] <= 0.0) {
-        st.x[j] = st.xu[j];
-        st.sl[j] = -temp;
-        st.su[j] = 0.0;
+    } else if (su[j] <= st.rhobeg) {
+      if (su[j] <= 0.0) {
+        x[j] = xu[j];
+        sl[j] = -temp;
+        su[j] = 0.0;
       } else {
-        st.x[j] = st.xu[j] - st.rhobeg;
-        st.sl[j] = bq_min(st.xl[j] - st.x[j], -st.rhobeg);
-        st.su[j] = st.rhobeg;
+        x[j] = xu[j] - st.rhobeg;
+        sl[j] = bq_min(xl[j] - x[j], -st.rhobeg);
+        su[j] = st.rhobeg;
       }
     }
   }
@@ -706,6 +718,7 @@ BQ_HD int bq_step(BQ_AS BqState& st, double fin) {
   return r;
 }
 BQ_NI int bq_step_impl(BQ_AS BqState& st, double fin) {
+  BQ_ALIASES(st);
   const double half = 0.5, one = 1.0, ten = 10.0, tenth = 0.1, two = 2.0, zero = 0.0;
   double temp, sum, suma, sumb, bsum, dx, delsq, scaden, biglsq, hdiag, den, errbig, frhosq,
       bdtol, bdtest, curv, fracsq, sumpq, sumz, sumw, densav, pqold, gqsq, gisq, dist;
@@ -719,14 +732,14 @@ BQ_NI int bq_step_impl(BQ_AS BqState& st, double fin) {
   }
 PSTART: {
     for (int j = 1; j <= BQN; ++j) {
-      st.xbase[j] = st.x[j];
-      for (int k = 1; k <= BQNPT; ++k) st.xpt[k][j] = zero;
-      for (int i = 1; i <= BQNDIM; ++i) st.bmat[i][j] = zero;
+      xbase[j] = x[j];
+      for (int k = 1; k <= BQNPT; ++k) xpt[k][j] = zero;
+      for (int i = 1; i <= BQNDIM; ++i) bmat[i][j] = zero;
     }
-    for (int i = 1; i <= BQNH; ++i) st.hq[i] = zero;
+    for (int i = 1; i <= BQNH; ++i) hq[i] = zero;
     for (int k = 1; k <= BQNPT; ++k) {
-      st.pq[k] = zero;
-      for (int j = 1; j <= BQNPTM; ++j) st.zmat[k][j] = zero;
+      pq[k] = zero;
+      for (int j = 1; j <= BQNPTM; ++j) zmat[k][j] = zero;
     }
     st.nf = 0;
     st.kopt = 1;
@@ -737,63 +750,63 @@ PSTART: {
     if (st.nfm <= 2 * BQN) {
       if (st.nfm >= 1 && st.nfm <= BQN) {
         st.stepa = st.rhobeg;
-        if (st.su[st.nfm] == zero) st.stepa = -st.stepa;
-        st.xpt[st.nf][st.nfm] = st.stepa;
+        if (su[st.nfm] == zero) st.stepa = -st.stepa;
+        xpt[st.nf][st.nfm] = st.stepa;
       } else if (st.nfm > BQN) {
-        st.stepa = st.xpt[st.nf - BQN][st.nfx];
+        st.stepa = xpt[st.nf - BQN][st.nfx];
         st.stepb = -st.rhobeg;
-        if (st.sl[st.nfx] == zero) st.stepb = bq_min(two * st.rhobeg, st.su[st.nfx]);
-        if (st.su[st.nfx] == zero) st.stepb = bq_max(-two * st.rhobeg, st.sl[st.nfx]);
-        st.xpt[st.nf][st.nfx] = st.stepb;
+        if (sl[st.nfx] == zero) st.stepb = bq_min(two * st.rhobeg, su[st.nfx]);
+        if (su[st.nfx] == zero) st.stepb = bq_max(-two * st.rhobeg, sl[st.nfx]);
+        xpt[st.nf][st.nfx] = st.stepb;
       }
     }
     for (int j = 1; j <= BQN; ++j) {
-      st.x[j] = bq_min(bq_max(st.xl[j], st.xbase[j] + st.xpt[st.nf][j]), st.xu[j]);
-      if (st.xpt[st.nf][j] == st.sl[j]) st.x[j] = st.xl[j];
-      if (st.xpt[st.nf][j] == st.su[j]) st.x[j] = st.xu[j];
+      x[j] = bq_min(bq_max(xl[j], xbase[j] + xpt[st.nf][j]), xu[j]);
+      if (xpt[st.nf][j] == sl[j]) x[j] = xl[j];
+      if (xpt[st.nf][j] == su[j]) x[j] = xu[j];
     }
-    BQ_CALFUN(st.x, 1);
+    BQ_CALFUN(x, 1);
   }
 PRESUME: {
     const double rhosq = st.rhobeg * st.rhobeg;
     const int nf = st.nf, nfm = st.nfm, nfx = st.nfx;
     st.f = fin;
-    st.fval[nf] = st.f;
+    fval[nf] = st.f;
     if (nf == 1) {
       st.fbeg = st.f;
       st.kopt = 1;
-    } else if (st.f < st.fval[st.kopt]) {
+    } else if (st.f < fval[st.kopt]) {
       st.kopt = nf;
     }
     if (nf <= 2 * BQN + 1) {
       if (nf >= 2 && nf <= BQN + 1) {
-        st.gopt[nfm] = (st.f - st.fbeg) / st.stepa;
+        gopt[nfm] = (st.f - st.fbeg) / st.stepa;
         if (BQNPT < nf + BQN) {
-          st.bmat[1][nfm] = -one / st.stepa;
-          st.bmat[nf][nfm] = one / st.stepa;
-          st.bmat[BQNPT + nfm][nfm] = -half * rhosq;
+          bmat[1][nfm] = -one / st.stepa;
+          bmat[nf][nfm] = one / st.stepa;
+          bmat[BQNPT + nfm][nfm] = -half * rhosq;
         }
       } else if (nf >= BQN + 2) {
         ih = nfx * (nfx + 1) / 2;
         temp = (st.f - st.fbeg) / st.stepb;
         st.diff = st.stepb - st.stepa;
-        st.hq[ih] = two * (temp - st.gopt[nfx]) / st.diff;
-        st.gopt[nfx] = (st.gopt[nfx] * st.stepb - temp * st.stepa) / st.diff;
+        hq[ih] = two * (temp - gopt[nfx]) / st.diff;
+        gopt[nfx] = (gopt[nfx] * st.stepb - temp * st.stepa) / st.diff;
         if (st.stepa * st.stepb < zero) {
-          if (st.f < st.fval[nf - BQN]) {
-            st.fval[nf] = st.fval[nf - BQN];
-            st.fval[nf - BQN] = st.f;
+          if (st.f < fval[nf - BQN]) {
+            fval[nf] = fval[nf - BQN];
+            fval[nf - BQN] = st.f;
             if (st.kopt == nf) st.kopt = nf - BQN;
-            st.xpt[nf - BQN][nfx] = st.stepb;
-            st.xpt[nf][nfx] = st.stepa;
+            xpt[nf - BQN][nfx] = st.stepb;
+            xpt[nf][nfx] = st.stepa;
           }
         }
-        st.bmat[1][nfx] = -(st.stepa + st.stepb) / (st.stepa * st.stepb);
-        st.bmat[nf][nfx] = -half / st.xpt[nf - BQN][nfx];
-        st.bmat[nf - BQN][nfx] = -st.bmat[1][nfx] - st.bmat[nf][nfx];
-        st.zmat[1][nfx] = sqrt(two) / (st.stepa * st.stepb);
-        st.zmat[nf][nfx] = sqrt(half) / rhosq;
-        st.zmat[nf - BQN][nfx] = -st.zmat[1][nfx] - st.zmat[nf][nfx];
+        bmat[1][nfx] = -(st.stepa + st.stepb) / (st.stepa * st.stepb);
+        bmat[nf][nfx] = -half / xpt[nf - BQN][nfx];
+        bmat[nf - BQN][nfx] = -bmat[1][nfx] - bmat[nf][nfx];
+        zmat[1][nfx] = sqrt(two) / (st.stepa * st.stepb);
+        zmat[nf][nfx] = sqrt(half) / rhosq;
+        zmat[nf - BQN][nfx] = -zmat[1][nfx] - zmat[nf][nfx];
       }
     }
     if (st.maxeval > 0 && st.nevals >= st.maxeval) {
@@ -804,10 +817,10 @@ PRESUME: {
   }
   st.xoptsq = zero;
   for (int i = 1; i <= BQN; ++i) {
-    st.xopt[i] = st.xpt[st.kopt][i];
-    st.xoptsq += st.xopt[i] * st.xopt[i];
+    xopt[i] = xpt[st.kopt][i];
+    st.xoptsq += xopt[i] * xopt[i];
   }
-  st.fsave = st.fval[1];
+  st.fsave = fval[1];
   if (st.rc != BQR_SUCCESS) goto L720;
   st.kbase = 1;
   st.rho = st.rhobeg;
@@ -827,23 +840,23 @@ L20:
     for (int j = 1; j <= BQN; ++j) {
       for (int i = 1; i <= j; ++i) {
         ++ih;
-        if (i < j) st.gopt[j] += st.hq[ih] * st.xopt[i];
-        st.gopt[i] += st.hq[ih] * st.xopt[j];
+        if (i < j) gopt[j] += hq[ih] * xopt[i];
+        gopt[i] += hq[ih] * xopt[j];
       }
     }
     if (st.nf > BQNPT) {
       for (int k = 1; k <= BQNPT; ++k) {
         temp = zero;
-        for (int j = 1; j <= BQN; ++j) temp += st.xpt[k][j] * st.xopt[j];
-        temp = st.pq[k] * temp;
-        for (int i = 1; i <= BQN; ++i) st.gopt[i] += temp * st.xpt[k][i];
+        for (int j = 1; j <= BQN; ++j) temp += xpt[k][j] * xopt[j];
+        temp = pq[k] * temp;
+        for (int i = 1; i <= BQN; ++i) gopt[i] += temp * xpt[k][i];
       }
     }
   }
 L60:
   {
   BQ_PT(t_trs);
-  bq_trsbox(st.xpt, st.xopt, st.gopt, st.hq, st.pq, st.sl, st.su, st.delta, st.xnew, st.d, st.gnew,
+  bq_trsbox(xpt, xopt, gopt, hq, pq, sl, su, st.delta, xnew, d, gnew,
             &st.dsq, &st.crvmin);
   BQ_PA(0, t_trs);
   }
@@ -859,11 +872,11 @@ L60:
     bdtol = errbig / st.rho;
     for (int j = 1; j <= BQN; ++j) {
       bdtest = bdtol;
-      if (st.xnew[j] == st.sl[j]) bdtest = st.gnew[j];
-      if (st.xnew[j] == st.su[j]) bdtest = -st.gnew[j];
+      if (xnew[j] == sl[j]) bdtest = gnew[j];
+      if (xnew[j] == su[j]) bdtest = -gnew[j];
       if (bdtest < bdtol) {
-        curv = st.hq[(j + j * j) / 2];
-        for (int k = 1; k <= BQNPT; ++k) curv += st.pq[k] * (st.xpt[k][j] * st.xpt[k][j]);
+        curv = hq[(j + j * j) / 2];
+        for (int k = 1; k <= BQNPT; ++k) curv += pq[k] * (xpt[k][j] * xpt[k][j]);
         bdtest += half * curv * st.rho;
         if (bdtest < bdtol) goto L650;
       }
@@ -876,58 +889,58 @@ L90:
     fracsq = st.xoptsq * .25;
     sumpq = zero;
     for (int k = 1; k <= BQNPT; ++k) {
-      sumpq += st.pq[k];
+      sumpq += pq[k];
       sum = -half * st.xoptsq;
-      for (int i = 1; i <= BQN; ++i) sum += st.xpt[k][i] * st.xopt[i];
-      st.w[BQNPT + k] = sum;
+      for (int i = 1; i <= BQN; ++i) sum += xpt[k][i] * xopt[i];
+      w[BQNPT + k] = sum;
       temp = fracsq - half * sum;
       for (int i = 1; i <= BQN; ++i) {
-        st.w[i] = st.bmat[k][i];
-        st.vlag[i] = sum * st.xpt[k][i] + temp * st.xopt[i];
+        w[i] = bmat[k][i];
+        vlag[i] = sum * xpt[k][i] + temp * xopt[i];
         const int ip = BQNPT + i;
         for (int j = 1; j <= i; ++j)
-          st.bmat[ip][j] = st.bmat[ip][j] + st.w[i] * st.vlag[j] + st.vlag[i] * st.w[j];
+          bmat[ip][j] = bmat[ip][j] + w[i] * vlag[j] + vlag[i] * w[j];
       }
     }
     for (int jj = 1; jj <= BQNPTM; ++jj) {
       sumz = zero;
       sumw = zero;
       for (int k = 1; k <= BQNPT; ++k) {
-        sumz += st.zmat[k][jj];
-        st.vlag[k] = st.w[BQNPT + k] * st.zmat[k][jj];
-        sumw += st.vlag[k];
+        sumz += zmat[k][jj];
+        vlag[k] = w[BQNPT + k] * zmat[k][jj];
+        sumw += vlag[k];
       }
       for (int j = 1; j <= BQN; ++j) {
-        sum = (fracsq * sumz - half * sumw) * st.xopt[j];
-        for (int k = 1; k <= BQNPT; ++k) sum += st.vlag[k] * st.xpt[k][j];
-        st.w[j] = sum;
-        for (int k = 1; k <= BQNPT; ++k) st.bmat[k][j] += sum * st.zmat[k][jj];
+        sum = (fracsq * sumz - half * sumw) * xopt[j];
+        for (int k = 1; k <= BQNPT; ++k) sum += vlag[k] * xpt[k][j];
+        w[j] = sum;
+        for (int k = 1; k <= BQNPT; ++k) bmat[k][j] += sum * zmat[k][jj];
       }
       for (int i = 1; i <= BQN; ++i) {
         const int ip = i + BQNPT;
-        temp = st.w[i];
-        for (int j = 1; j <= i; ++j) st.bmat[ip][j] += temp * st.w[j];
+        temp = w[i];
+        for (int j = 1; j <= i; ++j) bmat[ip][j] += temp * w[j];
       }
     }
     ih = 0;
     for (int j = 1; j <= BQN; ++j) {
-      st.w[j] = -half * sumpq * st.xopt[j];
+      w[j] = -half * sumpq * xopt[j];
       for (int k = 1; k <= BQNPT; ++k) {
-        st.w[j] += st.pq[k] * st.xpt[k][j];
-        st.xpt[k][j] -= st.xopt[j];
+        w[j] += pq[k] * xpt[k][j];
+        xpt[k][j] -= xopt[j];
       }
       for (int i = 1; i <= j; ++i) {
         ++ih;
-        st.hq[ih] = st.hq[ih] + st.w[i] * st.xopt[j] + st.xopt[i] * st.w[j];
-        st.bmat[BQNPT + i][j] = st.bmat[BQNPT + j][i];
+        hq[ih] = hq[ih] + w[i] * xopt[j] + xopt[i] * w[j];
+        bmat[BQNPT + i][j] = bmat[BQNPT + j][i];
       }
     }
     for (int i = 1; i <= BQN; ++i) {
-      st.xbase[i] += st.xopt[i];
-      st.xnew[i] -= st.xopt[i];
-      st.sl[i] -= st.xopt[i];
-      st.su[i] -= st.xopt[i];
-      st.xopt[i] = zero;
+      xbase[i] += xopt[i];
+      xnew[i] -= xopt[i];
+      sl[i] -= xopt[i];
+      su[i] -= xopt[i];
+      xopt[i] = zero;
     }
     st.xoptsq = zero;
   }
@@ -948,56 +961,56 @@ L190:  // ---- RESCUE
     for (int k = 1; k <= BQNPT; ++k) {
       st.distsq = zero;
       for (int j = 1; j <= BQN; ++j) {
-        st.xpt[k][j] -= st.xopt[j];
-        st.distsq += st.xpt[k][j] * st.xpt[k][j];
+        xpt[k][j] -= xopt[j];
+        st.distsq += xpt[k][j] * xpt[k][j];
       }
-      sumpq += st.pq[k];
-      st.w[BQNDIM + k] = st.distsq;
+      sumpq += pq[k];
+      w[BQNDIM + k] = st.distsq;
       winc = bq_max(winc, st.distsq);
-      for (int j = 1; j <= BQNPTM; ++j) st.zmat[k][j] = zero;
+      for (int j = 1; j <= BQNPTM; ++j) zmat[k][j] = zero;
     }
     ih = 0;
     for (int j = 1; j <= BQN; ++j) {
-      st.w[j] = half * sumpq * st.xopt[j];
-      for (int k = 1; k <= BQNPT; ++k) st.w[j] += st.pq[k] * st.xpt[k][j];
+      w[j] = half * sumpq * xopt[j];
+      for (int k = 1; k <= BQNPT; ++k) w[j] += pq[k] * xpt[k][j];
       for (int i = 1; i <= j; ++i) {
         ++ih;
-        st.hq[ih] = st.hq[ih] + st.w[i] * st.xopt[j] + st.w[j] * st.xopt[i];
+        hq[ih] = hq[ih] + w[i] * xopt[j] + w[j] * xopt[i];
       }
     }
     for (int j = 1; j <= BQN; ++j) {
-      st.xbase[j] += st.xopt[j];
-      st.sl[j] -= st.xopt[j];
-      st.su[j] -= st.xopt[j];
-      st.xopt[j] = zero;
-      st.ptsaux[1][j] = bq_min(st.delta, st.su[j]);
-      st.ptsaux[2][j] = bq_max(-st.delta, st.sl[j]);
-      if (st.ptsaux[1][j] + st.ptsaux[2][j] < zero) {
-        temp = st.ptsaux[1][j];
-        st.ptsaux[1][j] = st.ptsaux[2][j];
-        st.ptsaux[2][j] = temp;
+      xbase[j] += xopt[j];
+      sl[j] -= xopt[j];
+      su[j] -= xopt[j];
+      xopt[j] = zero;
+      ptsaux[1][j] = bq_min(st.delta, su[j]);
+      ptsaux[2][j] = bq_max(-st.delta, sl[j]);
+      if (ptsaux[1][j] + ptsaux[2][j] < zero) {
+        temp = ptsaux[1][j];
+        ptsaux[1][j] = ptsaux[2][j];
+        ptsaux[2][j] = temp;
       }
-      if (fabs(st.ptsaux[2][j]) < half * fabs(st.ptsaux[1][j])) st.ptsaux[2][j] = half * st.ptsaux[1][j];
-      for (int i = 1; i <= BQNDIM; ++i) st.bmat[i][j] = zero;
+      if (fabs(ptsaux[2][j]) < half * fabs(ptsaux[1][j])) ptsaux[2][j] = half * ptsaux[1][j];
+      for (int i = 1; i <= BQNDIM; ++i) bmat[i][j] = zero;
     }
-    st.rs_fbase = st.fval[st.kopt];
-    st.ptsid[1] = sfrac;
+    st.rs_fbase = fval[st.kopt];
+    ptsid[1] = sfrac;
     for (int j = 1; j <= BQN; ++j) {
       const int jp = j + 1, jpn = jp + BQN;
-      st.ptsid[jp] = (double)j + sfrac;
+      ptsid[jp] = (double)j + sfrac;
       if (jpn <= BQNPT) {
-        st.ptsid[jpn] = (double)j / (double)BQNP + sfrac;
-        temp = one / (st.ptsaux[1][j] - st.ptsaux[2][j]);
-        st.bmat[jp][j] = -temp + one / st.ptsaux[1][j];
-        st.bmat[jpn][j] = temp + one / st.ptsaux[2][j];
-        st.bmat[1][j] = -st.bmat[jp][j] - st.bmat[jpn][j];
-        st.zmat[1][j] = sqrt(2.) / fabs(st.ptsaux[1][j] * st.ptsaux[2][j]);
-        st.zmat[jp][j] = st.zmat[1][j] * st.ptsaux[2][j] * temp;
-        st.zmat[jpn][j] = -st.zmat[1][j] * st.ptsaux[1][j] * temp;
+        ptsid[jpn] = (double)j / (double)BQNP + sfrac;
+        temp = one / (ptsaux[1][j] - ptsaux[2][j]);
+        bmat[jp][j] = -temp + one / ptsaux[1][j];
+        bmat[jpn][j] = temp + one / ptsaux[2][j];
+        bmat[1][j] = -bmat[jp][j] - bmat[jpn][j];
+        zmat[1][j] = sqrt(2.) / fabs(ptsaux[1][j] * ptsaux[2][j]);
+        zmat[jp][j] = zmat[1][j] * ptsaux[2][j] * temp;
+        zmat[jpn][j] = -zmat[1][j] * ptsaux[1][j] * temp;
       } else {
-        st.bmat[1][j] = -one / st.ptsaux[1][j];
-        st.bmat[jp][j] = one / st.ptsaux[1][j];
-        st.bmat[j + BQNPT][j] = -half * (st.ptsaux[1][j] * st.ptsaux[1][j]);
+        bmat[1][j] = -one / ptsaux[1][j];
+        bmat[jp][j] = one / ptsaux[1][j];
+        bmat[j + BQNPT][j] = -half * (ptsaux[1][j] * ptsaux[1][j]);
       }
     }
     nrem = BQNPT;
@@ -1005,98 +1018,98 @@ L190:  // ---- RESCUE
     kn = st.kopt;
   R80:
     for (int j = 1; j <= BQN; ++j) {
-      temp = st.bmat[kold][j];
-      st.bmat[kold][j] = st.bmat[kn][j];
-      st.bmat[kn][j] = temp;
+      temp = bmat[kold][j];
+      bmat[kold][j] = bmat[kn][j];
+      bmat[kn][j] = temp;
     }
     for (int j = 1; j <= BQNPTM; ++j) {
-      temp = st.zmat[kold][j];
-      st.zmat[kold][j] = st.zmat[kn][j];
-      st.zmat[kn][j] = temp;
+      temp = zmat[kold][j];
+      zmat[kold][j] = zmat[kn][j];
+      zmat[kn][j] = temp;
     }
-    st.ptsid[kold] = st.ptsid[kn];
-    st.ptsid[kn] = zero;
-    st.w[BQNDIM + kn] = zero;
+    ptsid[kold] = ptsid[kn];
+    ptsid[kn] = zero;
+    w[BQNDIM + kn] = zero;
     --nrem;
     if (kn != st.kopt) {
-      temp = st.vlag[kold];
-      st.vlag[kold] = st.vlag[kn];
-      st.vlag[kn] = temp;
-      bq_update(st.bmat, st.zmat, st.vlag, bet2, den2, kn, st.w);
+      temp = vlag[kold];
+      vlag[kold] = vlag[kn];
+      vlag[kn] = temp;
+      bq_update(bmat, zmat, vlag, bet2, den2, kn, w);
       if (nrem == 0) goto R350;
-      for (int k = 1; k <= BQNPT; ++k) st.w[BQNDIM + k] = fabs(st.w[BQNDIM + k]);
+      for (int k = 1; k <= BQNPT; ++k) w[BQNDIM + k] = fabs(w[BQNDIM + k]);
     }
   R120:
     dsqmin = zero;
     for (int k = 1; k <= BQNPT; ++k) {
-      if (st.w[BQNDIM + k] > zero) {
-        if (dsqmin == zero || st.w[BQNDIM + k] < dsqmin) {
+      if (w[BQNDIM + k] > zero) {
+        if (dsqmin == zero || w[BQNDIM + k] < dsqmin) {
           kn = k;
-          dsqmin = st.w[BQNDIM + k];
+          dsqmin = w[BQNDIM + k];
         }
       }
     }
     if (dsqmin == zero) goto R260;
-    for (int j = 1; j <= BQN; ++j) st.w[BQNPT + j] = st.xpt[kn][j];
+    for (int j = 1; j <= BQN; ++j) w[BQNPT + j] = xpt[kn][j];
     for (int k = 1; k <= BQNPT; ++k) {
       sum = zero;
       if (k == st.kopt) {
-      } else if (st.ptsid[k] == zero) {
-        for (int j = 1; j <= BQN; ++j) sum += st.w[BQNPT + j] * st.xpt[k][j];
+      } else if (ptsid[k] == zero) {
+        for (int j = 1; j <= BQN; ++j) sum += w[BQNPT + j] * xpt[k][j];
       } else {
-        ip = (int)st.ptsid[k];
-        if (ip > 0) sum = st.w[BQNPT + ip] * st.ptsaux[1][ip];
-        iq = (int)((double)BQNP * st.ptsid[k] - (double)(ip * BQNP));
+        ip = (int)ptsid[k];
+        if (ip > 0) sum = w[BQNPT + ip] * ptsaux[1][ip];
+        iq = (int)((double)BQNP * ptsid[k] - (double)(ip * BQNP));
         if (iq > 0) {
           iw = 1;
           if (ip == 0) iw = 2;
-          sum += st.w[BQNPT + iq] * st.ptsaux[iw][iq];
+          sum += w[BQNPT + iq] * ptsaux[iw][iq];
         }
       }
-      st.w[k] = half * sum * sum;
+      w[k] = half * sum * sum;
     }
     for (int k = 1; k <= BQNPT; ++k) {
       sum = zero;
-      for (int j = 1; j <= BQN; ++j) sum += st.bmat[k][j] * st.w[BQNPT + j];
-      st.vlag[k] = sum;
+      for (int j = 1; j <= BQN; ++j) sum += bmat[k][j] * w[BQNPT + j];
+      vlag[k] = sum;
     }
     bet2 = zero;
     for (int j = 1; j <= BQNPTM; ++j) {
       sum = zero;
-      for (int k = 1; k <= BQNPT; ++k) sum += st.zmat[k][j] * st.w[k];
+      for (int k = 1; k <= BQNPT; ++k) sum += zmat[k][j] * w[k];
       bet2 -= sum * sum;
-      for (int k = 1; k <= BQNPT; ++k) st.vlag[k] += sum * st.zmat[k][j];
+      for (int k = 1; k <= BQNPT; ++k) vlag[k] += sum * zmat[k][j];
     }
     bsum = zero;
     st.distsq = zero;
     for (int j = 1; j <= BQN; ++j) {
       sum = zero;
-      for (int k = 1; k <= BQNPT; ++k) sum += st.bmat[k][j] * st.w[k];
+      for (int k = 1; k <= BQNPT; ++k) sum += bmat[k][j] * w[k];
       const int jp = j + BQNPT;
-      bsum += sum * st.w[jp];
-      for (int ipp = BQNPT + 1; ipp <= BQNDIM; ++ipp) sum += st.bmat[ipp][j] * st.w[ipp];
-      bsum += sum * st.w[jp];
-      st.vlag[jp] = sum;
-      st.distsq += st.xpt[kn][j] * st.xpt[kn][j];
+      bsum += sum * w[jp];
+      for (int ipp = BQNPT + 1; ipp <= BQNDIM; ++ipp) sum += bmat[ipp][j] * w[ipp];
+      bsum += sum * w[jp];
+      vlag[jp] = sum;
+      st.distsq += xpt[kn][j] * xpt[kn][j];
     }
     bet2 = half * st.distsq * st.distsq + bet2 - bsum;
-    st.vlag[st.kopt] += one;
+    vlag[st.kopt] += one;
     den2 = zero;
     vlmxsq = zero;
     for (int k = 1; k <= BQNPT; ++k) {
-      if (st.ptsid[k] != zero) {
+      if (ptsid[k] != zero) {
         hdiag = zero;
-        for (int j = 1; j <= BQNPTM; ++j) hdiag += st.zmat[k][j] * st.zmat[k][j];
-        den = bet2 * hdiag + st.vlag[k] * st.vlag[k];
+        for (int j = 1; j <= BQNPTM; ++j) hdiag += zmat[k][j] * zmat[k][j];
+        den = bet2 * hdiag + vlag[k] * vlag[k];
         if (den > den2) {
           kold = k;
           den2 = den;
         }
       }
-      vlmxsq = bq_max(vlmxsq, st.vlag[k] * st.vlag[k]);
+      vlmxsq = bq_max(vlmxsq, vlag[k] * vlag[k]);
     }
     if (den2 <= vlmxsq * .01) {
-      st.w[BQNDIM + kn] = -st.w[BQNDIM + kn] - winc;
+      w[BQNDIM + kn] = -w[BQNDIM + kn] - winc;
       goto R120;
     }
     goto R80;
@@ -1105,7 +1118,7 @@ R260:
   st.kpt = 1;
 R260LOOP:
   if (st.kpt > BQNPT) goto R350;
-  if (st.ptsid[st.kpt] == zero) {
+  if (ptsid[st.kpt] == zero) {
     ++st.kpt;
     goto R260LOOP;
   }
@@ -1117,87 +1130,87 @@ R260LOOP:
     const int kpt = st.kpt;
     ih = 0;
     for (int j = 1; j <= BQN; ++j) {
-      st.w[j] = st.xpt[kpt][j];
-      st.xpt[kpt][j] = zero;
-      temp = st.pq[kpt] * st.w[j];
+      w[j] = xpt[kpt][j];
+      xpt[kpt][j] = zero;
+      temp = pq[kpt] * w[j];
       for (int i = 1; i <= j; ++i) {
         ++ih;
-        st.hq[ih] += temp * st.w[i];
+        hq[ih] += temp * w[i];
       }
     }
-    st.pq[kpt] = zero;
-    st.rs_ip = (int)st.ptsid[kpt];
-    st.rs_iq = (int)((double)BQNP * st.ptsid[kpt] - (double)(st.rs_ip * BQNP));
+    pq[kpt] = zero;
+    st.rs_ip = (int)ptsid[kpt];
+    st.rs_iq = (int)((double)BQNP * ptsid[kpt] - (double)(st.rs_ip * BQNP));
     const int ip = st.rs_ip, iq = st.rs_iq;
     int ihp = 0, ihq;
     if (ip > 0) {
-      st.rs_xp = st.ptsaux[1][ip];
-      st.xpt[kpt][ip] = st.rs_xp;
+      st.rs_xp = ptsaux[1][ip];
+      xpt[kpt][ip] = st.rs_xp;
     }
     if (iq > 0) {
-      st.rs_xq = st.ptsaux[1][iq];
-      if (ip == 0) st.rs_xq = st.ptsaux[2][iq];
-      st.xpt[kpt][iq] = st.rs_xq;
+      st.rs_xq = ptsaux[1][iq];
+      if (ip == 0) st.rs_xq = ptsaux[2][iq];
+      xpt[kpt][iq] = st.rs_xq;
     }
     st.rs_vq = st.rs_fbase;
     if (ip > 0) {
       ihp = (ip + ip * ip) / 2;
-      st.rs_vq += st.rs_xp * (st.gopt[ip] + half * st.rs_xp * st.hq[ihp]);
+      st.rs_vq += st.rs_xp * (gopt[ip] + half * st.rs_xp * hq[ihp]);
     }
     if (iq > 0) {
       ihq = (iq + iq * iq) / 2;
-      st.rs_vq += st.rs_xq * (st.gopt[iq] + half * st.rs_xq * st.hq[ihq]);
+      st.rs_vq += st.rs_xq * (gopt[iq] + half * st.rs_xq * hq[ihq]);
       if (ip > 0) {
         const int iw = (ihp > ihq ? ihp : ihq) - (ip > iq ? ip - iq : iq - ip);
-        st.rs_vq += st.rs_xp * st.rs_xq * st.hq[iw];
+        st.rs_vq += st.rs_xp * st.rs_xq * hq[iw];
       }
     }
     for (int k = 1; k <= BQNPT; ++k) {
       temp = zero;
-      if (ip > 0) temp += st.rs_xp * st.xpt[k][ip];
-      if (iq > 0) temp += st.rs_xq * st.xpt[k][iq];
-      st.rs_vq += half * st.pq[k] * temp * temp;
+      if (ip > 0) temp += st.rs_xp * xpt[k][ip];
+      if (iq > 0) temp += st.rs_xq * xpt[k][iq];
+      st.rs_vq += half * pq[k] * temp * temp;
     }
     for (int i = 1; i <= BQN; ++i) {
-      st.w[i] = bq_min(bq_max(st.xl[i], st.xbase[i] + st.xpt[kpt][i]), st.xu[i]);
-      if (st.xpt[kpt][i] == st.sl[i]) st.w[i] = st.xl[i];
-      if (st.xpt[kpt][i] == st.su[i]) st.w[i] = st.xu[i];
+      w[i] = bq_min(bq_max(xl[i], xbase[i] + xpt[kpt][i]), xu[i]);
+      if (xpt[kpt][i] == sl[i]) w[i] = xl[i];
+      if (xpt[kpt][i] == su[i]) w[i] = xu[i];
     }
     ++st.nf;
-    BQ_CALFUN(st.w, 3);
+    BQ_CALFUN(w, 3);
   }
 R260R: {
     const int kpt = st.kpt, ip0 = st.rs_ip, iq0 = st.rs_iq;
     (void)ip0; (void)iq0;
     st.f = fin;
-    st.fval[kpt] = st.f;
-    if (st.f < st.fval[st.kopt]) st.kopt = kpt;
+    fval[kpt] = st.f;
+    if (st.f < fval[st.kopt]) st.kopt = kpt;
     st.diff = st.f - st.rs_vq;
-    for (int i = 1; i <= BQN; ++i) st.gopt[i] += st.diff * st.bmat[kpt][i];
+    for (int i = 1; i <= BQN; ++i) gopt[i] += st.diff * bmat[kpt][i];
     for (int k = 1; k <= BQNPT; ++k) {
       sum = zero;
-      for (int j = 1; j <= BQNPTM; ++j) sum += st.zmat[k][j] * st.zmat[kpt][j];
+      for (int j = 1; j <= BQNPTM; ++j) sum += zmat[k][j] * zmat[kpt][j];
       temp = st.diff * sum;
-      if (st.ptsid[k] == zero) {
-        st.pq[k] += temp;
+      if (ptsid[k] == zero) {
+        pq[k] += temp;
       } else {
-        const int ip = (int)st.ptsid[k];
-        const int iq = (int)((double)BQNP * st.ptsid[k] - (double)(ip * BQNP));
+        const int ip = (int)ptsid[k];
+        const int iq = (int)((double)BQNP * ptsid[k] - (double)(ip * BQNP));
         const int ihq = (iq * iq + iq) / 2;
         if (ip == 0) {
-          st.hq[ihq] += temp * (st.ptsaux[2][iq] * st.ptsaux[2][iq]);
+          hq[ihq] += temp * (ptsaux[2][iq] * ptsaux[2][iq]);
         } else {
           const int ihp = (ip * ip + ip) / 2;
-          st.hq[ihp] += temp * (st.ptsaux[1][ip] * st.ptsaux[1][ip]);
+          hq[ihp] += temp * (ptsaux[1][ip] * ptsaux[1][ip]);
           if (iq > 0) {
-            st.hq[ihq] += temp * (st.ptsaux[1][iq] * st.ptsaux[1][iq]);
+            hq[ihq] += temp * (ptsaux[1][iq] * ptsaux[1][iq]);
             const int iw = (ihp > ihq ? ihp : ihq) - (iq > ip ? iq - ip : ip - iq);
-            st.hq[iw] += temp * st.ptsaux[1][ip] * st.ptsaux[1][iq];
+            hq[iw] += temp * ptsaux[1][ip] * ptsaux[1][iq];
           }
         }
       }
     }
-    st.ptsid[kpt] = zero;
+    ptsid[kpt] = zero;
     ++st.kpt;
     goto R260LOOP;
   }
@@ -1205,8 +1218,8 @@ R350:
   st.xoptsq = zero;
   if (st.kopt != st.kbase) {
     for (int i = 1; i <= BQN; ++i) {
-      st.xopt[i] = st.xpt[st.kopt][i];
-      st.xoptsq += st.xopt[i] * st.xopt[i];
+      xopt[i] = xpt[st.kopt][i];
+      st.xoptsq += xopt[i] * xopt[i];
     }
   }
   if (st.nf < 0) {
@@ -1223,59 +1236,59 @@ R350:
 L210:
   {
   BQ_PT(t_alt);
-  bq_altmov(st.xpt, st.xopt, st.bmat, st.zmat, st.sl, st.su, st.kopt, st.knew, st.adelt, st.xnew,
-            st.xalt, &st.alpha, &st.cauchy);
+  bq_altmov(xpt, xopt, bmat, zmat, sl, su, st.kopt, st.knew, st.adelt, xnew,
+            xalt, &st.alpha, &st.cauchy);
   BQ_PA(1, t_alt);
   }
-  for (int i = 1; i <= BQN; ++i) st.d[i] = st.xnew[i] - st.xopt[i];
+  for (int i = 1; i <= BQN; ++i) d[i] = xnew[i] - xopt[i];
 L230:
   for (int k = 1; k <= BQNPT; ++k) {
     suma = zero;
     sumb = zero;
     sum = zero;
     for (int j = 1; j <= BQN; ++j) {
-      suma += st.xpt[k][j] * st.d[j];
-      sumb += st.xpt[k][j] * st.xopt[j];
-      sum += st.bmat[k][j] * st.d[j];
+      suma += xpt[k][j] * d[j];
+      sumb += xpt[k][j] * xopt[j];
+      sum += bmat[k][j] * d[j];
     }
-    st.w[k] = suma * (half * suma + sumb);
-    st.vlag[k] = sum;
-    st.w[BQNPT + k] = suma;
+    w[k] = suma * (half * suma + sumb);
+    vlag[k] = sum;
+    w[BQNPT + k] = suma;
   }
   st.beta = zero;
   for (int jj = 1; jj <= BQNPTM; ++jj) {
     sum = zero;
-    for (int k = 1; k <= BQNPT; ++k) sum += st.zmat[k][jj] * st.w[k];
+    for (int k = 1; k <= BQNPT; ++k) sum += zmat[k][jj] * w[k];
     st.beta -= sum * sum;
-    for (int k = 1; k <= BQNPT; ++k) st.vlag[k] += sum * st.zmat[k][jj];
+    for (int k = 1; k <= BQNPT; ++k) vlag[k] += sum * zmat[k][jj];
   }
   st.dsq = zero;
   bsum = zero;
   dx = zero;
   for (int j = 1; j <= BQN; ++j) {
-    st.dsq += st.d[j] * st.d[j];
+    st.dsq += d[j] * d[j];
     sum = zero;
-    for (int k = 1; k <= BQNPT; ++k) sum += st.w[k] * st.bmat[k][j];
-    bsum += sum * st.d[j];
+    for (int k = 1; k <= BQNPT; ++k) sum += w[k] * bmat[k][j];
+    bsum += sum * d[j];
     const int jp = BQNPT + j;
-    for (int i = 1; i <= BQN; ++i) sum += st.bmat[jp][i] * st.d[i];
-    st.vlag[jp] = sum;
-    bsum += sum * st.d[j];
-    dx += st.d[j] * st.xopt[j];
+    for (int i = 1; i <= BQN; ++i) sum += bmat[jp][i] * d[i];
+    vlag[jp] = sum;
+    bsum += sum * d[j];
+    dx += d[j] * xopt[j];
   }
   st.beta = dx * dx + st.dsq * (st.xoptsq + dx + dx + half * st.dsq) + st.beta - bsum;
-  st.vlag[st.kopt] += one;
+  vlag[st.kopt] += one;
   if (st.ntrits == 0) {
-    st.denom = st.vlag[st.knew] * st.vlag[st.knew] + st.alpha * st.beta;
+    st.denom = vlag[st.knew] * vlag[st.knew] + st.alpha * st.beta;
     if (st.denom < st.cauchy && st.cauchy > zero) {
       for (int i = 1; i <= BQN; ++i) {
-        st.xnew[i] = st.xalt[i];
-        st.d[i] = st.xnew[i] - st.xopt[i];
+        xnew[i] = xalt[i];
+        d[i] = xnew[i] - xopt[i];
       }
       st.cauchy = zero;
       goto L230;
     }
-    if (st.denom <= half * (st.vlag[st.knew] * st.vlag[st.knew])) {
+    if (st.denom <= half * (vlag[st.knew] * vlag[st.knew])) {
       if (st.nf > st.nresc) goto L190;
       st.rc = BQR_ROUNDOFF;
       goto L720;
@@ -1288,11 +1301,11 @@ L230:
     for (int k = 1; k <= BQNPT; ++k) {
       if (k == st.kopt) continue;
       hdiag = zero;
-      for (int jj = 1; jj <= BQNPTM; ++jj) hdiag += st.zmat[k][jj] * st.zmat[k][jj];
-      den = st.beta * hdiag + st.vlag[k] * st.vlag[k];
+      for (int jj = 1; jj <= BQNPTM; ++jj) hdiag += zmat[k][jj] * zmat[k][jj];
+      den = st.beta * hdiag + vlag[k] * vlag[k];
       st.distsq = zero;
       for (int j = 1; j <= BQN; ++j) {
-        temp = st.xpt[k][j] - st.xopt[j];
+        temp = xpt[k][j] - xopt[j];
         st.distsq += temp * temp;
       }
       temp = st.distsq / delsq;
@@ -1302,7 +1315,7 @@ L230:
         st.knew = k;
         st.denom = den;
       }
-      biglsq = bq_max(biglsq, temp * (st.vlag[k] * st.vlag[k]));
+      biglsq = bq_max(biglsq, temp * (vlag[k] * vlag[k]));
     }
     if (scaden <= half * biglsq) {
       if (st.nf > st.nresc) goto L190;
@@ -1312,44 +1325,44 @@ L230:
   }
 L360:
   for (int i = 1; i <= BQN; ++i) {
-    st.x[i] = bq_min(bq_max(st.xl[i], st.xbase[i] + st.xnew[i]), st.xu[i]);
-    if (st.xnew[i] == st.sl[i]) st.x[i] = st.xl[i];
-    if (st.xnew[i] == st.su[i]) st.x[i] = st.xu[i];
+    x[i] = bq_min(bq_max(xl[i], xbase[i] + xnew[i]), xu[i]);
+    if (xnew[i] == sl[i]) x[i] = xl[i];
+    if (xnew[i] == su[i]) x[i] = xu[i];
   }
   if (st.maxeval > 0 && st.nevals >= st.maxeval) {
     st.rc = BQR_MAXEVAL;
     goto L720;
   }
   ++st.nf;
-  BQ_CALFUN(st.x, 2);
+  BQ_CALFUN(x, 2);
 L360R:
   st.f = fin;
   if (st.ntrits == -1) {
     st.fsave = st.f;
     st.rc = BQR_XTOL;
-    if (st.fsave < st.fval[st.kopt]) {
+    if (st.fsave < fval[st.kopt]) {
       st.minf = st.f;
-      for (int i = 0; i < BQN; ++i) st.xout[i] = st.x[i + 1] * st.s[i];
+      for (int i = 0; i < BQN; ++i) st.xout[i] = x[i + 1] * st.s[i];
       st.resume = -1;
       return BQ_DONE;
     }
     goto L720;
   }
-  st.fopt = st.fval[st.kopt];
+  st.fopt = fval[st.kopt];
   st.vquad = zero;
   ih = 0;
   for (int j = 1; j <= BQN; ++j) {
-    st.vquad += st.d[j] * st.gopt[j];
+    st.vquad += d[j] * gopt[j];
     for (int i = 1; i <= j; ++i) {
       ++ih;
-      temp = st.d[i] * st.d[j];
+      temp = d[i] * d[j];
       if (i == j) temp = half * temp;
-      st.vquad += st.hq[ih] * temp;
+      st.vquad += hq[ih] * temp;
     }
   }
   for (int k = 1; k <= BQNPT; ++k) {
-    temp = st.w[BQNPT + k];
-    st.vquad += half * st.pq[k] * (temp * temp);
+    temp = w[BQNPT + k];
+    st.vquad += half * pq[k] * (temp * temp);
   }
   st.diff = st.f - st.fopt - st.vquad;
   st.diffc = st.diffb;
@@ -1375,11 +1388,11 @@ L360R:
       st.knew = 0;
       for (int k = 1; k <= BQNPT; ++k) {
         hdiag = zero;
-        for (int jj = 1; jj <= BQNPTM; ++jj) hdiag += st.zmat[k][jj] * st.zmat[k][jj];
-        den = st.beta * hdiag + st.vlag[k] * st.vlag[k];
+        for (int jj = 1; jj <= BQNPTM; ++jj) hdiag += zmat[k][jj] * zmat[k][jj];
+        den = st.beta * hdiag + vlag[k] * vlag[k];
         st.distsq = zero;
         for (int j = 1; j <= BQN; ++j) {
-          temp = st.xpt[k][j] - st.xnew[j];
+          temp = xpt[k][j] - xnew[j];
           st.distsq += temp * temp;
         }
         temp = st.distsq / delsq;
@@ -1389,7 +1402,7 @@ L360R:
           st.knew = k;
           st.denom = den;
         }
-        biglsq = bq_max(biglsq, temp * (st.vlag[k] * st.vlag[k]));
+        biglsq = bq_max(biglsq, temp * (vlag[k] * vlag[k]));
       }
       if (scaden <= half * biglsq) {
         st.knew = ksav;
@@ -1399,102 +1412,102 @@ L360R:
   }
   {
   BQ_PT(t_upd);
-  bq_update(st.bmat, st.zmat, st.vlag, st.beta, st.denom, st.knew, st.w);
+  bq_update(bmat, zmat, vlag, st.beta, st.denom, st.knew, w);
   BQ_PA(2, t_upd);
   }
   ih = 0;
-  pqold = st.pq[st.knew];
-  st.pq[st.knew] = zero;
+  pqold = pq[st.knew];
+  pq[st.knew] = zero;
   for (int i = 1; i <= BQN; ++i) {
-    temp = pqold * st.xpt[st.knew][i];
+    temp = pqold * xpt[st.knew][i];
     for (int j = 1; j <= i; ++j) {
       ++ih;
-      st.hq[ih] += temp * st.xpt[st.knew][j];
+      hq[ih] += temp * xpt[st.knew][j];
     }
   }
   for (int jj = 1; jj <= BQNPTM; ++jj) {
-    temp = st.diff * st.zmat[st.knew][jj];
-    for (int k = 1; k <= BQNPT; ++k) st.pq[k] += temp * st.zmat[k][jj];
+    temp = st.diff * zmat[st.knew][jj];
+    for (int k = 1; k <= BQNPT; ++k) pq[k] += temp * zmat[k][jj];
   }
-  st.fval[st.knew] = st.f;
+  fval[st.knew] = st.f;
   for (int i = 1; i <= BQN; ++i) {
-    st.xpt[st.knew][i] = st.xnew[i];
-    st.w[i] = st.bmat[st.knew][i];
+    xpt[st.knew][i] = xnew[i];
+    w[i] = bmat[st.knew][i];
   }
   for (int k = 1; k <= BQNPT; ++k) {
     suma = zero;
-    for (int jj = 1; jj <= BQNPTM; ++jj) suma += st.zmat[st.knew][jj] * st.zmat[k][jj];
+    for (int jj = 1; jj <= BQNPTM; ++jj) suma += zmat[st.knew][jj] * zmat[k][jj];
     sumb = zero;
-    for (int j = 1; j <= BQN; ++j) sumb += st.xpt[k][j] * st.xopt[j];
+    for (int j = 1; j <= BQN; ++j) sumb += xpt[k][j] * xopt[j];
     temp = suma * sumb;
-    for (int i = 1; i <= BQN; ++i) st.w[i] += temp * st.xpt[k][i];
+    for (int i = 1; i <= BQN; ++i) w[i] += temp * xpt[k][i];
   }
-  for (int i = 1; i <= BQN; ++i) st.gopt[i] += st.diff * st.w[i];
+  for (int i = 1; i <= BQN; ++i) gopt[i] += st.diff * w[i];
   if (st.f < st.fopt) {
     st.kopt = st.knew;
     st.xoptsq = zero;
     ih = 0;
     for (int j = 1; j <= BQN; ++j) {
-      st.xopt[j] = st.xnew[j];
-      st.xoptsq += st.xopt[j] * st.xopt[j];
+      xopt[j] = xnew[j];
+      st.xoptsq += xopt[j] * xopt[j];
       for (int i = 1; i <= j; ++i) {
         ++ih;
-        if (i < j) st.gopt[j] += st.hq[ih] * st.d[i];
-        st.gopt[i] += st.hq[ih] * st.d[j];
+        if (i < j) gopt[j] += hq[ih] * d[i];
+        gopt[i] += hq[ih] * d[j];
       }
     }
     for (int k = 1; k <= BQNPT; ++k) {
       temp = zero;
-      for (int j = 1; j <= BQN; ++j) temp += st.xpt[k][j] * st.d[j];
-      temp = st.pq[k] * temp;
-      for (int i = 1; i <= BQN; ++i) st.gopt[i] += temp * st.xpt[k][i];
+      for (int j = 1; j <= BQN; ++j) temp += xpt[k][j] * d[j];
+      temp = pq[k] * temp;
+      for (int i = 1; i <= BQN; ++i) gopt[i] += temp * xpt[k][i];
     }
   }
   if (st.ntrits > 0) {
     for (int k = 1; k <= BQNPT; ++k) {
-      st.vlag[k] = st.fval[k] - st.fval[st.kopt];
-      st.w[k] = zero;
+      vlag[k] = fval[k] - fval[st.kopt];
+      w[k] = zero;
     }
     for (int j = 1; j <= BQNPTM; ++j) {
       sum = zero;
-      for (int k = 1; k <= BQNPT; ++k) sum += st.zmat[k][j] * st.vlag[k];
-      for (int k = 1; k <= BQNPT; ++k) st.w[k] += sum * st.zmat[k][j];
+      for (int k = 1; k <= BQNPT; ++k) sum += zmat[k][j] * vlag[k];
+      for (int k = 1; k <= BQNPT; ++k) w[k] += sum * zmat[k][j];
     }
     for (int k = 1; k <= BQNPT; ++k) {
       sum = zero;
-      for (int j = 1; j <= BQN; ++j) sum += st.xpt[k][j] * st.xopt[j];
-      st.w[k + BQNPT] = st.w[k];
-      st.w[k] = sum * st.w[k];
+      for (int j = 1; j <= BQN; ++j) sum += xpt[k][j] * xopt[j];
+      w[k + BQNPT] = w[k];
+      w[k] = sum * w[k];
     }
     gqsq = zero;
     gisq = zero;
     for (int i = 1; i <= BQN; ++i) {
       sum = zero;
-      for (int k = 1; k <= BQNPT; ++k) sum = sum + st.bmat[k][i] * st.vlag[k] + st.xpt[k][i] * st.w[k];
-      if (st.xopt[i] == st.sl[i]) {
-        temp = bq_min(zero, st.gopt[i]);
+      for (int k = 1; k <= BQNPT; ++k) sum = sum + bmat[k][i] * vlag[k] + xpt[k][i] * w[k];
+      if (xopt[i] == sl[i]) {
+        temp = bq_min(zero, gopt[i]);
         gqsq += temp * temp;
         temp = bq_min(zero, sum);
         gisq += temp * temp;
-      } else if (st.xopt[i] == st.su[i]) {
-        temp = bq_max(zero, st.gopt[i]);
+      } else if (xopt[i] == su[i]) {
+        temp = bq_max(zero, gopt[i]);
         gqsq += temp * temp;
         temp = bq_max(zero, sum);
         gisq += temp * temp;
       } else {
-        gqsq += st.gopt[i] * st.gopt[i];
+        gqsq += gopt[i] * gopt[i];
         gisq += sum * sum;
       }
-      st.vlag[BQNPT + i] = sum;
+      vlag[BQNPT + i] = sum;
     }
     ++st.itest;
     if (gqsq < ten * gisq) st.itest = 0;
     if (st.itest >= 3) {
       const int imax = BQNPT > BQNH ? BQNPT : BQNH;
       for (int i = 1; i <= imax; ++i) {
-        if (i <= BQN) st.gopt[i] = st.vlag[BQNPT + i];
-        if (i <= BQNPT) st.pq[i] = st.w[BQNPT + i];
-        if (i <= BQNH) st.hq[i] = zero;
+        if (i <= BQN) gopt[i] = vlag[BQNPT + i];
+        if (i <= BQNPT) pq[i] = w[BQNPT + i];
+        if (i <= BQNH) hq[i] = zero;
         st.itest = 0;
       }
     }
@@ -1510,7 +1523,7 @@ L650:
   for (int k = 1; k <= BQNPT; ++k) {
     sum = zero;
     for (int j = 1; j <= BQN; ++j) {
-      temp = st.xpt[k][j] - st.xopt[j];
+      temp = xpt[k][j] - xopt[j];
       sum += temp * temp;
     }
     if (sum > st.distsq) {
@@ -1547,16 +1560,16 @@ L680:
   if (st.ntrits == -1) goto L360;
   st.rc = BQR_XTOL;
 L720:
-  if (st.fval[st.kopt] <= st.fsave) {
+  if (fval[st.kopt] <= st.fsave) {
     for (int i = 1; i <= BQN; ++i) {
-      st.x[i] = bq_min(bq_max(st.xl[i], st.xbase[i] + st.xopt[i]), st.xu[i]);
-      if (st.xopt[i] == st.sl[i]) st.x[i] = st.xl[i];
-      if (st.xopt[i] == st.su[i]) st.x[i] = st.xu[i];
+      x[i] = bq_min(bq_max(xl[i], xbase[i] + xopt[i]), xu[i]);
+      if (xopt[i] == sl[i]) x[i] = xl[i];
+      if (xopt[i] == su[i]) x[i] = xu[i];
     }
-    st.f = st.fval[st.kopt];
+    st.f = fval[st.kopt];
   }
   st.minf = st.f;
-  for (int i = 0; i < BQN; ++i) st.xout[i] = st.x[i + 1] * st.s[i];
+  for (int i = 0; i < BQN; ++i) st.xout[i] = x[i + 1] * st.s[i];
   st.resume = -1;
   return BQ_DONE;
 }

@@ -202,7 +202,7 @@ struct pmvs_scene {
   ExpandBuffers xbuf;
   DBuf<pmvs_patch> fpatches;
   DBuf<int> fkeep;
-  int grid = 0, refine_grid = 0, tslots = 1204;
+  int grid = 0, refine_grid = 0, tslots = 1206;
   // expansion sharding (pmvs_scene_set_shard) and the kept result of pmvs_expand_run(out = NULL)
   int shard_rank = 0, shard_world = 1;
   pmvs_allgather_fn shard_fn = nullptr;
@@ -425,10 +425,10 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
   sc->grid = std::max(1, prop.multiProcessorCount) * gpc;
   // tuning knobs (defaults measured on MI355X): refine wavefronts per CU and the
   // number of texture slots one cooperative objective chunk packs
-  int wpc = 8;  // 1204: 19 KB LDS, <= 256 registers -> 8 resident per CU
+  int wpc = 8;  // 1206: 19.5 KB LDS, <= 256 registers -> 8 resident per CU
   if (const char* e = getenv("PMVS_REFINE_WAVES_PER_CU")) wpc = std::max(1, std::min(32, atoi(e)));
   if (const char* e = getenv("PMVS_REFINE_CONFIG")) sc->tslots = atoi(e);
-  if (sc->tslots != 804 && sc->tslots != 808 && sc->tslots != 1204 && sc->tslots != 1608 && sc->tslots != 2408) sc->tslots = 1204;
+  if (sc->tslots != 804 && sc->tslots != 807 && sc->tslots != 808 && sc->tslots != 1206 && sc->tslots != 1204 && sc->tslots != 1608 && sc->tslots != 2408) sc->tslots = 1206;
   sc->refine_grid = std::max(1, prop.multiProcessorCount) * wpc;
   if (sc->scratch.alloc((size_t)sc->grid * PMVS_MAX_IMAGES * PMVS_MAX_IMAGES) != hipSuccess)
     return bail(fail(PMVS_ENOMEM, "scratch"));

@@ -830,8 +830,9 @@ __device__ void post_candidate(const DScene& s, WaveLds<WS>& L, const RefineJob&
 template <int WS, int TSLOTS, int NC>
 struct RefLds {
   static constexpr int S = WS * WS;
+  static constexpr int SP = (S + 3) & ~3;  // channel rows padded to 16 B (float4 reads)
   BqState bq[NC];                    // optimizer state of the wave's NC chains (lane c owns bq[c])
-  float tex[TSLOTS][S][4];
+  alignas(16) float tex[TSLOTS][3][SP];  // per texture: R, G, B rows of the S samples
   float ave[TSLOTS][4];
   long long jbase[TSLOTS];
   int jvalid[TSLOTS], jW[TSLOTS], jreq[TSLOTS], jidx[TSLOTS];
@@ -975,7 +976,7 @@ __device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS, NC>& C, int njobs
       r += (float)(a1[q] & 0xff) * f10 + (float)(b1[q] & 0xff) * f11;
       g += (float)((a1[q] >> 8) & 0xff) * f10 + (float)((b1[q] >> 8) & 0xff) * f11;
       b += (float)((a1[q] >> 16) & 0xff) * f10 + (float)((b1[q] >> 16) & 0xff) * f11;
-      C.tex[t][k][0] = r; C.tex[t][k][1] = g; C.tex[t][k][2] = b;
+      C.tex[t][0][k] = r; C.tex[t][1][k] = g; C.tex[t][2][k] = b;
     }
   }
   __syncthreads();
@@ -983,19 +984,31 @@ __device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS, NC>& C, int njobs
   // --- normalize (optim.cpp:1031-1067), one lane per texture
   if (lane < njobs && C.jvalid[lane]) {
     const int t = lane;
-    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
-    for (int i = 0; i < S; ++i) {
-      const float4 q = *reinterpret_cast<const float4*>(C.tex[t][i]);
-      a0 += q.x; a1 += q.y; a2 += q.z;
+    const float *X = C.tex[t][0], *Y = C.tex[t][1], *Z = C.tex[t][2];
+    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;  // each channel summed in sample order
+    int i = 0;
+    for (; i + 4 <= S; i += 4) {
+      const float4 x = *reinterpret_cast<const float4*>(X + i), y = *reinterpret_cast<const float4*>(Y + i),
+                   z = *reinterpret_cast<const float4*>(Z + i);
+      a0 += x.x; a1 += y.x; a2 += z.x;
+      a0 += x.y; a1 += y.y; a2 += z.y;
+      a0 += x.z; a1 += y.z; a2 += z.z;
+      a0 += x.w; a1 += y.w; a2 += z.w;
     }
+    for (; i < S; ++i) { a0 += X[i]; a1 += Y[i]; a2 += Z[i]; }
     const float fs3 = (float)S;
     a0 = __fdiv_rn(a0, fs3); a1 = __fdiv_rn(a1, fs3); a2 = __fdiv_rn(a2, fs3);
     float ave2 = 0.0f;
-    for (int i = 0; i < S; ++i) {
-      const float4 q = *reinterpret_cast<const float4*>(C.tex[t][i]);
-      const float f0 = a0 - q.x, f1 = a1 - q.y, f2 = a2 - q.z;
+    auto sq = [&](float x, float y, float z) {
+      const float f0 = a0 - x, f1 = a1 - y, f2 = a2 - z;
       ave2 += f0 * f0 + f1 * f1 + f2 * f2;
+    };
+    for (i = 0; i + 4 <= S; i += 4) {
+      const float4 x = *reinterpret_cast<const float4*>(X + i), y = *reinterpret_cast<const float4*>(Y + i),
+                   z = *reinterpret_cast<const float4*>(Z + i);
+      sq(x.x, y.x, z.x); sq(x.y, y.y, z.y); sq(x.z, y.z, z.z); sq(x.w, y.w, z.w);
     }
+    for (; i < S; ++i) sq(X[i], Y[i], Z[i]);
     ave2 = fsqrt_rn(__fdiv_rn(ave2, (float)(3 * S)));
     if (ave2 == 0.0f) ave2 = 1.0f;
     C.ave[t][0] = a0; C.ave[t][1] = a1; C.ave[t][2] = a2; C.ave[t][3] = ave2;
@@ -1005,9 +1018,9 @@ __device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS, NC>& C, int njobs
     const int t = u / S, k = u - t * S;
     if (!C.jvalid[t]) continue;
     const float a2 = C.ave[t][3];
-    C.tex[t][k][0] = __fdiv_rn(C.tex[t][k][0] - C.ave[t][0], a2);
-    C.tex[t][k][1] = __fdiv_rn(C.tex[t][k][1] - C.ave[t][1], a2);
-    C.tex[t][k][2] = __fdiv_rn(C.tex[t][k][2] - C.ave[t][2], a2);
+    C.tex[t][0][k] = __fdiv_rn(C.tex[t][0][k] - C.ave[t][0], a2);
+    C.tex[t][1][k] = __fdiv_rn(C.tex[t][1][k] - C.ave[t][1], a2);
+    C.tex[t][2][k] = __fdiv_rn(C.tex[t][2][k] - C.ave[t][2], a2);
   }
   __syncthreads();
   PROF_MARK(5);
@@ -1016,13 +1029,23 @@ __device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS, NC>& C, int njobs
     const int t = lane, ref = C.rfirst[C.jreq[t]];
     float r = 0.0f;
     if (C.jvalid[ref] && C.jvalid[t]) {
-      float ans = 0.0f;
-      for (int i = 0; i < S; ++i) {
-        const float4 p = *reinterpret_cast<const float4*>(C.tex[ref][i]);
-        const float4 q = *reinterpret_cast<const float4*>(C.tex[t][i]);
-        ans += p.x * q.x;
-        ans += p.y * q.y;
-        ans += p.z * q.z;
+      float ans = 0.0f;  // per sample R, G, B products, in sample order
+      const float *PX = C.tex[ref][0], *PY = C.tex[ref][1], *PZ = C.tex[ref][2];
+      const float *QX = C.tex[t][0], *QY = C.tex[t][1], *QZ = C.tex[t][2];
+      int i = 0;
+      for (; i + 4 <= S; i += 4) {
+        const float4 px = *reinterpret_cast<const float4*>(PX + i), py = *reinterpret_cast<const float4*>(PY + i),
+                     pz = *reinterpret_cast<const float4*>(PZ + i), qx = *reinterpret_cast<const float4*>(QX + i),
+                     qy = *reinterpret_cast<const float4*>(QY + i), qz = *reinterpret_cast<const float4*>(QZ + i);
+        ans += px.x * qx.x; ans += py.x * qy.x; ans += pz.x * qz.x;
+        ans += px.y * qx.y; ans += py.y * qy.y; ans += pz.y * qz.y;
+        ans += px.z * qx.z; ans += py.z * qy.z; ans += pz.z * qz.z;
+        ans += px.w * qx.w; ans += py.w * qy.w; ans += pz.w * qz.w;
+      }
+      for (; i < S; ++i) {
+        ans += PX[i] * QX[i];
+        ans += PY[i] * QY[i];
+        ans += PZ[i] * QZ[i];
       }
       r = robustincc((float)(1.0 - (double)__fdiv_rn(ans, (float)(3 * S))));
     }
@@ -1037,7 +1060,8 @@ __device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS, NC>& C, int njobs
 // kernels that call them use the same value.  Measured on C2 (tools/sweep_variants.sh,
 // profiles/r02g_sweeps.txt): 2 waves of 4 chains with 12 texture slots (19 KB LDS, 8 per CU)
 // beat 1 wave of 8 chains with the 512-register inlined optimizer by 17 %; 3 or 4 waves per SIMD
-// (168 / 128 registers) spill and lose 40-50 %.
+// (168 / 128 registers) spill and lose 40-50 %.  With the compacted BqState (1736 B) and 12-byte
+// texture samples, 6 chains x 12 slots fit the same 20 KB (default 1206, +6 %).
 #ifndef REFINE_WPE
 #define REFINE_WPE(NC) 2
 #endif
@@ -1436,9 +1460,11 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
   switch (tslots) {
     case 804: hipLaunchKernelGGL((refine_v2_kernel<WS, 8, 4>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     case 808: hipLaunchKernelGGL((refine_v2_kernel<WS, 8, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 807: hipLaunchKernelGGL((refine_v2_kernel<WS, 8, 7>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     case 1608: hipLaunchKernelGGL((refine_v2_kernel<WS, 16, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     case 2408: hipLaunchKernelGGL((refine_v2_kernel<WS, 24, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
-    default: hipLaunchKernelGGL((refine_v2_kernel<WS, 12, 4>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 1204: hipLaunchKernelGGL((refine_v2_kernel<WS, 12, 4>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    default: hipLaunchKernelGGL((refine_v2_kernel<WS, 12, 6>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
   }
   (void)hipEventRecord(ev[2], stream);
   hipLaunchKernelGGL((post_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_jobs, d_out, n, d_st);
