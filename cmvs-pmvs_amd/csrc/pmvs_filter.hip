@@ -1715,12 +1715,14 @@ __global__ void gather_slots_kernel(const int* __restrict__ slots, int m, const 
 // Collected patches: flag = 1 (clearFlags + collectPatches(queue), patchOrganizerS.cpp) and their
 // _tmp in collect order (the queue's initial contents).
 __global__ void collect_flags_kernel(pmvs_patch* __restrict__ P, const int* __restrict__ order, int na,
-                                     float* __restrict__ qtmp) {
+                                     float* __restrict__ qtmp, int* __restrict__ rank) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= na) return;
   pmvs_patch& q = P[order[i]];
   q.flag = 1;
-  qtmp[i] = q.tmp;
+  const float t = q.tmp;
+  qtmp[i] = (t == 0.0f) ? 0.0f : t;  // -0 as +0: the radix order then agrees with QCmp's `<`
+  rank[i] = i;
 }
 
 // Compact per-candidate record the host commit reads (instead of two full patch records):
@@ -1847,7 +1849,8 @@ static hipError_t grow(T*& p, size_t& cap, size_t need) {
 void delete_commit_work(CommitWork* w);  // after CommitWork's definition
 ExpandBuffers::~ExpandBuffers() {
   void* ps[] = {parents, cand_coord, cand_ok, cand, prep, status, slots, cand2, prep2, res, outp, ostatus, counts, alive,
-                pg_head, vp_head, d_item, d_next, pool_used, tcells, tvals, qtmp, crec, acc, dupd, cellinit, occ};
+                pg_head, vp_head, d_item, d_next, pool_used, tcells, tvals, qtmp, crec, acc, dupd, cellinit, occ,
+                qkey, qrank, qrank2, qsort_tmp};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete_commit_work(cm);
@@ -2404,16 +2407,37 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   set_delta();
   // ---- device state of the commit: CExpand's _counts (unsigned char, clearCounts) and whether
   // pgrids holds a patch, per target cell; the host keeps only the queue
-  std::vector<int> order(c.nalive);
+  // The collected patches enter the queue in collect order (seq = collect rank); their max-_tmp
+  // order (QCmp: _tmp descending, ties by seq) is a stable descending radix sort on the device.
+  std::vector<int> order(c.nalive), srank(c.nalive);
   std::vector<float> qtmp(c.nalive);
-  FCHK(grow(X.qtmp, X.cap_qtmp, (size_t)std::max(1, c.nalive)));
+  const size_t na1 = (size_t)std::max(1, c.nalive);
+  FCHK(grow(X.qtmp, X.cap_qtmp, na1));
+  FCHK(grow(X.qkey, X.cap_qkey, na1));
+  FCHK(grow(X.qrank, X.cap_qrank, na1));
+  FCHK(grow(X.qrank2, X.cap_qrank2, na1));
   FCHK(grow(X.occ, X.cap_occ, (size_t)ncells));
-  if (c.nalive)
-    hipLaunchKernelGGL(collect_flags_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, dP, B.order, c.nalive, X.qtmp);
+  if (c.nalive) {
+    hipLaunchKernelGGL(collect_flags_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, dP, B.order, c.nalive, X.qtmp,
+                       X.qrank);
+    size_t tb = 0;
+    FCHK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, X.qtmp, X.qkey, X.qrank, X.qrank2, c.nalive, 0, 32, st));
+    if (tb > X.cap_qsort) {
+      if (X.qsort_tmp) FCHK(hipFree(X.qsort_tmp));
+      X.qsort_tmp = nullptr;
+      X.cap_qsort = 0;
+      FCHK(hipMalloc(&X.qsort_tmp, tb));
+      X.cap_qsort = tb;
+    }
+    tb = X.cap_qsort;
+    FCHK(hipcub::DeviceRadixSort::SortPairsDescending(X.qsort_tmp, tb, X.qtmp, X.qkey, X.qrank, X.qrank2, c.nalive, 0, 32,
+                                                      st));
+  }
   hipLaunchKernelGGL(occ_init_kernel, dim3(nblk(ncells)), dim3(256), 0, st, B.pg_off, ncells, X.occ);
   if (c.nalive) {
     FCHK(hipMemcpyAsync(order.data(), B.order, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
-    FCHK(hipMemcpyAsync(qtmp.data(), X.qtmp, c.nalive * sizeof(float), hipMemcpyDeviceToHost, st));
+    FCHK(hipMemcpyAsync(qtmp.data(), X.qkey, c.nalive * sizeof(float), hipMemcpyDeviceToHost, st));
+    FCHK(hipMemcpyAsync(srank.data(), X.qrank2, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
   }
   FCHK(grow(X.counts, X.cap_cnt, (size_t)ncells));
   FCHK(hipMemsetAsync(X.counts, 0, ncells, st));
@@ -2421,9 +2445,8 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   // The max-_tmp queue (P_compare; ties: earlier push first): the collected patches as a sorted
   // run, the patches pushed during the run in a heap, popped by merging the two.
   std::vector<QItem> initial(c.nalive);
-  for (int i = 0; i < c.nalive; ++i) initial[i] = {qtmp[i], (long long)i, order[i]};
+  for (int j = 0; j < c.nalive; ++j) initial[j] = {qtmp[j], (long long)srank[j], order[srank[j]]};
   const QCmp less;  // less(a, b): a has lower priority than b
-  std::sort(initial.begin(), initial.end(), [&](const QItem& a, const QItem& b) { return less(b, a); });
   size_t ihead = 0;
   std::priority_queue<QItem, std::vector<QItem>, QCmp> queue;
   long long seq = c.nalive;

@@ -60,6 +60,10 @@ struct ExpandBuffers {
   int* tcells = nullptr;        // cells whose counts a commit changed, and their values
   unsigned short* cellinit = nullptr;  // per-cell {count, occupied} staged for the host mirror
   float* qtmp = nullptr;        // _tmp of the collected patches (queue)
+  float* qkey = nullptr;        // the initial queue sorted on the device: keys, collect ranks, temp
+  int *qrank = nullptr, *qrank2 = nullptr;
+  void* qsort_tmp = nullptr;
+  size_t cap_qkey = 0, cap_qrank = 0, cap_qrank2 = 0, cap_qsort = 0;
   int *crec = nullptr, *acc = nullptr;  // commit records; committed record indexes
   int2* dupd = nullptr;         // (parent, failed-direction bits) of a wave
   unsigned char* tvals = nullptr;
