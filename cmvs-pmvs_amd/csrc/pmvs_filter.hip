@@ -1641,31 +1641,30 @@ hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n,
     if (ne) FCHK(hipMemcpyAsync(edges.data(), B.edges, ne * sizeof(int), hipMemcpyDeviceToHost, st));
     FCHK(hipMemcpyAsync(order.data(), B.order, na * sizeof(int), hipMemcpyDeviceToHost, st));
     FCHK(hipStreamSynchronize(st));
-    // filterSmallGroups label BFS (filter.cpp:520-562) in collect order
-    std::vector<int> label(na, -1);
-    int id = -1;
-    std::deque<int> q;
+    // filterSmallGroups label BFS (filter.cpp:520-562) in collect order.  Every patch enters
+    // the queue once, so one array holds all the BFS queues back to back; a component is
+    // qv[start, tail) when its BFS ends, and only its size matters (threshold below).
+    const int threshold = std::max(20, na / 10000);
+    std::vector<unsigned char> seen(na, 0);
+    std::vector<int> qv(na), flags(n, 0);
+    int tail = 0;
     for (int pid = 0; pid < na; ++pid) {
-      if (label[pid] != -1) continue;
-      label[pid] = ++id;
-      q.push_back(pid);
-      while (!q.empty()) {
-        const int pt = q.front();
-        q.pop_front();
-        for (int e = eoff[pt]; e < eoff[pt + 1]; ++e) {
+      if (seen[pid]) continue;
+      const int start = tail;
+      seen[pid] = 1;
+      qv[tail++] = pid;
+      for (int h = start; h < tail; ++h) {
+        const int pt = qv[h];
+        for (int e = eoff[pt], e1 = eoff[pt + 1]; e < e1; ++e) {
           const int j = edges[e];
-          if (label[j] != -1) continue;
-          label[j] = id;
-          q.push_back(j);
+          if (seen[j]) continue;
+          seen[j] = 1;
+          qv[tail++] = j;
         }
       }
+      if (tail - start < threshold)
+        for (int k = start; k < tail; ++k) flags[order[qv[k]]] = 1;
     }
-    std::vector<int> size(id + 1, 0);
-    for (int l : label) ++size[l];
-    const int threshold = std::max(20, na / 10000);
-    std::vector<int> flags(n, 0);
-    for (int k = 0; k < na; ++k)
-      if (size[label[k]] < threshold) flags[order[k]] = 1;
     FCHK(hipMemcpyAsync(B.flags, flags.data(), n * sizeof(int), hipMemcpyHostToDevice, st));
     // _flag = collect index of every collected patch (filter.cpp:538-542)
     hipLaunchKernelGGL(flag_rank_kernel, dim3(nblk(na)), dim3(256), 0, st, dP, B.order, na);
@@ -1691,16 +1690,21 @@ static inline float __int_as_float_h(int v) {
   return f;
 }
 
+// Queue entry: key = order-preserving bits of _tmp (-0 as +0) << 32 | ~seq, so that one unsigned
+// compare is P_compare (patchOrganizerS.hpp:10-15: max _tmp) with ties to the earlier push.
 struct QItem {
-  float tmp;
-  long long seq;
+  unsigned long long key;
   int p;
 };
-struct QCmp {  // max-heap on _tmp (P_compare, patchOrganizerS.hpp:10-15); ties: earlier push first
-  bool operator()(const QItem& a, const QItem& b) const {
-    if (a.tmp != b.tmp) return a.tmp < b.tmp;
-    return a.seq > b.seq;
-  }
+static inline unsigned long long qkey(float tmp, long long seq) {
+  if (tmp == 0.0f) tmp = 0.0f;
+  unsigned u;
+  std::memcpy(&u, &tmp, sizeof(u));
+  u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((unsigned long long)u << 32) | (0xffffffffull - (unsigned long long)seq);
+}
+struct QCmp {  // max-heap on key
+  bool operator()(const QItem& a, const QItem& b) const { return a.key < b.key; }
 };
 
 __global__ void gather_slots_kernel(const int* __restrict__ slots, int m, const pmvs_candidate* __restrict__ cin,
@@ -2445,7 +2449,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   // The max-_tmp queue (P_compare; ties: earlier push first): the collected patches as a sorted
   // run, the patches pushed during the run in a heap, popped by merging the two.
   std::vector<QItem> initial(c.nalive);
-  for (int j = 0; j < c.nalive; ++j) initial[j] = {qtmp[j], (long long)srank[j], order[srank[j]]};
+  for (int j = 0; j < c.nalive; ++j) initial[j] = {qkey(qtmp[j], srank[j]), order[srank[j]]};
   const QCmp less;  // less(a, b): a has lower priority than b
   size_t ihead = 0;
   std::priority_queue<QItem, std::vector<QItem>, QCmp> queue;
@@ -2606,7 +2610,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
       const int added = co.nacc;
       if (added > 0 && nmodel + added > cap) return hipErrorOutOfMemory;
       stats[6] += added;
-      for (const int2& u : co.push) queue.push({__int_as_float_h(u.x), seq++, u.y});
+      for (const int2& u : co.push) queue.push({qkey(__int_as_float_h(u.x), seq++), u.y});
       T.mark(7);
       if (added > 0) {
         pool_need = X.pool_host + (size_t)co.entries;
