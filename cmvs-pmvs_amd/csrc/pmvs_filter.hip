@@ -266,7 +266,10 @@ __global__ void depth_map_kernel(DScene s, FilterDev F, unsigned long long* __re
   for (int j = 0; j < 2; ++j)
     for (int k = 0; k < 2; ++k) {
       if (xs[k] < 0 || gw <= xs[k] || ys[j] < 0 || gh <= ys[j]) continue;
-      atomicMin(&dpkey[F.tgoff[t] + (long long)ys[j] * gw + xs[k]], key);
+      unsigned long long* cell = &dpkey[F.tgoff[t] + (long long)ys[j] * gw + xs[k]];
+      // the stored minimum only decreases, so a (possibly stale) value <= key means the atomic
+      // could not change the cell: skip it (most updates of a dense model)
+      if (key < *cell) atomicMin(cell, key);
     }
 }
 
@@ -1636,10 +1639,13 @@ hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n,
       FCHK(hipMalloc((void**)&B.edges, B.edges_cap * sizeof(int)));
     }
     hipLaunchKernelGGL(group_edges_kernel, dim3(nblk(na)), dim3(256), 0, st, s, c.dev(), 1, B.edge_off, B.cnt, B.edges);
-    std::vector<int> eoff(na + 1), edges(ne ? ne : 1), order(na), fixv(n);
-    FCHK(hipMemcpyAsync(eoff.data(), B.edge_off, (na + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
-    if (ne) FCHK(hipMemcpyAsync(edges.data(), B.edges, ne * sizeof(int), hipMemcpyDeviceToHost, st));
-    FCHK(hipMemcpyAsync(order.data(), B.order, na * sizeof(int), hipMemcpyDeviceToHost, st));
+    FCHK(B.pin.ensure(((size_t)na + 1 + (size_t)ne + (size_t)na) * sizeof(int)));
+    const int* eoff = B.pin.as<int>();
+    const int* edges = eoff + (na + 1);
+    const int* order = edges + ne;
+    FCHK(hipMemcpyAsync(B.pin.as<int>(), B.edge_off, (na + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
+    if (ne) FCHK(hipMemcpyAsync(B.pin.as<int>((size_t)(na + 1) * sizeof(int)), B.edges, ne * sizeof(int), hipMemcpyDeviceToHost, st));
+    FCHK(hipMemcpyAsync(B.pin.as<int>(((size_t)na + 1 + ne) * sizeof(int)), B.order, na * sizeof(int), hipMemcpyDeviceToHost, st));
     FCHK(hipStreamSynchronize(st));
     // filterSmallGroups label BFS (filter.cpp:520-562) in collect order.  Every patch enters
     // the queue once, so one array holds all the BFS queues back to back; a component is
@@ -2413,8 +2419,10 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   // pgrids holds a patch, per target cell; the host keeps only the queue
   // The collected patches enter the queue in collect order (seq = collect rank); their max-_tmp
   // order (QCmp: _tmp descending, ties by seq) is a stable descending radix sort on the device.
-  std::vector<int> order(c.nalive), srank(c.nalive);
-  std::vector<float> qtmp(c.nalive);
+  FCHK(X.pin.ensure(3 * (size_t)std::max(1, c.nalive) * sizeof(int)));
+  int* order = X.pin.as<int>();
+  int* srank = order + c.nalive;
+  float* qtmp = reinterpret_cast<float*>(srank + c.nalive);
   const size_t na1 = (size_t)std::max(1, c.nalive);
   FCHK(grow(X.qtmp, X.cap_qtmp, na1));
   FCHK(grow(X.qkey, X.cap_qkey, na1));
@@ -2439,9 +2447,9 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   }
   hipLaunchKernelGGL(occ_init_kernel, dim3(nblk(ncells)), dim3(256), 0, st, B.pg_off, ncells, X.occ);
   if (c.nalive) {
-    FCHK(hipMemcpyAsync(order.data(), B.order, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
-    FCHK(hipMemcpyAsync(qtmp.data(), X.qkey, c.nalive * sizeof(float), hipMemcpyDeviceToHost, st));
-    FCHK(hipMemcpyAsync(srank.data(), X.qrank2, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
+    FCHK(hipMemcpyAsync(order, B.order, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
+    FCHK(hipMemcpyAsync(qtmp, X.qkey, c.nalive * sizeof(float), hipMemcpyDeviceToHost, st));
+    FCHK(hipMemcpyAsync(srank, X.qrank2, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
   }
   FCHK(grow(X.counts, X.cap_cnt, (size_t)ncells));
   FCHK(hipMemsetAsync(X.counts, 0, ncells, st));

@@ -22,7 +22,29 @@ hipError_t launch_patch_colors(const DScene& s, int n, const float* coords, cons
                                hipStream_t stream);
 
 // ---- filter pass (pmvs_filter.hip)
+// Page-locked host staging (hipHostMalloc), grown on demand: the large per-pass downloads
+// (filterSmallGroups' edge lists, the expansion queue's initial order) at full PCIe rate.
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t c = bytes + bytes / 4 + 4096;
+    const hipError_t e = hipHostMalloc(&p, c, hipHostMallocDefault);
+    if (e == hipSuccess) cap = c;
+    return e;
+  }
+  template <class T>
+  T* as(size_t offset_bytes = 0) const { return reinterpret_cast<T*>(static_cast<char*>(p) + offset_bytes); }
+  ~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+};
 struct FilterBuffers {
+  PinnedBuf pin;  // host staging of the small-groups BFS inputs
   unsigned long long *preg = nullptr, *vreg = nullptr, *keys = nullptr, *keys2 = nullptr, *dpkey = nullptr,
                      *safe = nullptr;
   long long* tgoff = nullptr;
@@ -47,6 +69,7 @@ constexpr int kMaxWave = 65536;  // parents per expansion wave (device slot arra
 struct CommitWork;  // device commit scratch (pmvs_filter.hip)
 struct ExpandBuffers {
   CommitWork* cm = nullptr;
+  PinnedBuf pin;  // host staging of the initial queue (order, sorted keys and ranks)
   unsigned char* occ = nullptr;  // per target cell: pgrids holds a patch (device commit)
   size_t cap_occ = 0;
   int *parents = nullptr, *cand_ok = nullptr, *status = nullptr, *slots = nullptr, *ostatus = nullptr, *alive = nullptr;
