@@ -1263,9 +1263,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(REFINE_WPE(N
 // ==================================================================== kernels
 namespace pmvsdev {
 
-// Kernel 1: preProcess, one wavefront per candidate, persistent with a device work queue.
+// Kernel 1: preProcess, one wavefront per candidate, persistent with a device work queue.  Pre and
+// post are latency-bound wave-per-candidate walks: a 256-register budget (2 waves per SIMD, the
+// persistent grid's 8 per CU) instead of the 324 the inlined code would take (1 per SIMD).
 template <int WS>
-__global__ __launch_bounds__(64) void pre_kernel(DScene s, const pmvs_candidate* __restrict__ in,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void pre_kernel(DScene s, const pmvs_candidate* __restrict__ in,
                                                   RefineJob* __restrict__ jobs, int n, DevStats* st) {
   __shared__ WaveLds<WS> L;
   unsigned long long acc[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -1286,7 +1288,7 @@ __global__ __launch_bounds__(64) void pre_kernel(DScene s, const pmvs_candidate*
 
 // Kernel 3: postProcess, one wavefront per candidate.
 template <int WS>
-__global__ __launch_bounds__(64) void post_kernel(DScene s, const RefineJob* __restrict__ jobs,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void post_kernel(DScene s, const RefineJob* __restrict__ jobs,
                                                    pmvs_refined* __restrict__ out, int n, DevStats* st) {
   __shared__ WaveLds<WS> L;
   unsigned long long acc[7] = {0, 0, 0, 0, 0, 0, 0};
