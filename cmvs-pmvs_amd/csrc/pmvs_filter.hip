@@ -1500,6 +1500,15 @@ static hipError_t build_lists(Ctx& c, int vis) {
   return hipGetLastError();
 }
 
+__global__ void flag01_kernel(const int* __restrict__ v, int n, int* __restrict__ f) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) f[k] = v[k] != 0;
+}
+__global__ void scatter_index_kernel(const int* __restrict__ f, const int* __restrict__ off, int n, int* __restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n && f[k]) out[off[k]] = k;
+}
+
 // CPatchOrganizerS::collectPatches: collect ranks and order
 static hipError_t collect(Ctx& c) {
   FilterBuffers& B = c.B;
@@ -1574,15 +1583,15 @@ hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n,
     hipLaunchKernelGGL(exact_patch_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, s, c.dev(), B.safe, B.preg, B.vreg,
                        B.need, B.counters + 2);
   {
-    std::vector<int> need(n);
-    FCHK(hipMemcpyAsync(need.data(), B.need, n * sizeof(int), hipMemcpyDeviceToHost, st));
-    FCHK(hipStreamSynchronize(st));
-    std::vector<int> lst;
-    for (int p = 0; p < n; ++p)
-      if (need[p]) lst.push_back(p);
-    const int m = (int)lst.size();
+    // the patches that need setRefImage, in index order: compacted on the device
+    hipLaunchKernelGGL(flag01_kernel, dim3(nblk(n)), dim3(256), 0, st, B.need, n, B.cnt);
+    FCHK(hipMemsetAsync(B.cnt + n, 0, sizeof(int), st));
+    size_t tb = B.temp_bytes;
+    FCHK(hipcub::DeviceScan::ExclusiveSum(B.temp, tb, B.cnt, B.off, n + 1, st));
+    hipLaunchKernelGGL(scatter_index_kernel, dim3(nblk(n)), dim3(256), 0, st, B.cnt, B.off, n, B.list);
+    int m = 0;
+    FCHK(read_int(B.off + n, &m, st));
     if (m) {
-      FCHK(hipMemcpyAsync(B.list, lst.data(), m * sizeof(int), hipMemcpyHostToDevice, st));
       FCHK(launch_filter_refimage(s, dP, B.list, m, grid, st));
       hipLaunchKernelGGL(exact_after_ref_kernel, dim3(nblk(m)), dim3(256), 0, st, s, dP, B.list, m, B.preg, B.vreg,
                          B.counters + 2);
