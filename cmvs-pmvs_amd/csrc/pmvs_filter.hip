@@ -61,6 +61,8 @@ constexpr int NB_SCR = NB_CAP * 8;
 // Persistent workgroups per CU-grid unit for the NbLds kernels (neighbor_kernel, depth_post_kernel,
 // empty_blocks_kernel): twice the organizer grid, since ~8 KB of LDS and <= 107 VGPRs leave room.
 constexpr int NB_GRID_MULT = 2;
+// doubles of NbLds.nb + NbLds.seq that filterQuad's lls rows (6 per neighbour) may use
+constexpr int NB_LLS_LDS = (NB_CAP * 2 * 4) / 8;
 __device__ __forceinline__ int lane_id_w() { return threadIdx.x & 63; }
 // Wave-uniform copies (SGPR) of values that are uniform by construction but loaded from memory:
 // every branch or loop around a barrier is driven by one of these, never by a VGPR value.
@@ -462,7 +464,7 @@ __global__ void exact_after_ref_kernel(DScene s, const pmvs_patch* __restrict__ 
 // --------------------------------------------------------------------------- filterNeighbor
 struct NbLds {
   int sb[64], so[64], sl[64];  // gather_neighbors: per-slot list start, flattened offset, list kind
-  int nb[NB_CAP];
+  alignas(8) int nb[NB_CAP];   // nb and seq are adjacent: filterQuad's lls rows reuse them
   float seq[NB_CAP];  // values summed in the reference's order by one lane (filterQuad)
   float units[PMVS_MAX_IMAGES];
   int cnt, overflow;
@@ -602,7 +604,9 @@ __device__ __attribute__((noinline)) void lls5_jacobi(NbLds& L, const double* M,
 }
 
 // Out of line: its registers do not add to the latency-bound neighbour walks of the callers (whose
-// occupancy is register-limited); M / r rows in global scratch, the 5 x 5 stage in NbLds.
+// occupancy is register-limited); M / r rows in global scratch, the 5 x 5 stage in NbLds.  The
+// one-lane row loops are unrolled by 8 so their (independent) row loads are in flight together;
+// the sums stay sequential in row order.
 __device__ __attribute__((noinline)) void lls5_wave(NbLds& L, double* M, double* r, int n) {
   constexpr int N = 5;
   const double eps = 2.220446049250313e-16, dmin = 2.2250738585072014e-308;
@@ -627,6 +631,7 @@ __device__ __attribute__((noinline)) void lls5_wave(NbLds& L, double* M, double*
   // column norms (one lane per column, rows in order)
   if (lane < N) {
     double sq = 0.0;
+    #pragma unroll 8
     for (int i = 0; i < n; ++i) sq += M[(size_t)i * N + lane] * M[(size_t)i * N + lane];
     L.nu[lane] = L.nd[lane] = sqrt(sq);
     L.perm[lane] = lane;
@@ -656,6 +661,7 @@ __device__ __attribute__((noinline)) void lls5_wave(NbLds& L, double* M, double*
     bar();
     if (lane == 0) {  // makeHouseholderInPlace
       double tail = 0.0;
+      #pragma unroll 8
       for (int i = k + 1; i < n; ++i) tail += M[(size_t)i * N + k] * M[(size_t)i * N + k];
       const double c0 = M[(size_t)k * N + k];
       double beta, tau, den = 0.0;
@@ -679,9 +685,11 @@ __device__ __attribute__((noinline)) void lls5_wave(NbLds& L, double* M, double*
     if (tauk != 0.0 && lane > k && lane < N) {  // applyHouseholderOnTheLeft, column j = lane
       const int j = lane;
       double t = 0.0;
+      #pragma unroll 8
       for (int i = k + 1; i < n; ++i) t += M[(size_t)i * N + k] * M[(size_t)i * N + j];
       t += M[(size_t)k * N + j];
       M[(size_t)k * N + j] -= tauk * t;
+      #pragma unroll 8
       for (int i = k + 1; i < n; ++i) M[(size_t)i * N + j] -= (tauk * M[(size_t)i * N + k]) * t;
     }
     bar();
@@ -694,6 +702,7 @@ __device__ __attribute__((noinline)) void lls5_wave(NbLds& L, double* M, double*
       const double t2 = t * (q * q);
       if (t2 <= downdate) {
         double sq = 0.0;
+        #pragma unroll 8
         for (int i = k + 1; i < n; ++i) sq += M[(size_t)i * N + j] * M[(size_t)i * N + j];
         L.nd[j] = L.nu[j] = sqrt(sq);
       } else {
@@ -708,6 +717,7 @@ __device__ __attribute__((noinline)) void lls5_wave(NbLds& L, double* M, double*
     if (tauk == 0.0) continue;
     if (lane == 0) {
       double t = 0.0;
+      #pragma unroll 8
       for (int i = k + 1; i < n; ++i) t += M[(size_t)i * N + k] * r[i];
       t += r[k];
       L.den = t;
@@ -910,7 +920,11 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, c
     __syncthreads();
   }
   const int n = imin(uni(L.cnt), NB_CAP);
+#if defined(NBX_SKIP_SORT)  // timing experiment only (tools): the final sort skipped
+  return n;
+#else
   return sort_unique_lds(L.nb, n, &L.cnt);
+#endif
 }
 
 // CFilter::filterQuad (filter.cpp:387-446) on the neighbours in L.nb[0..n); returns 1 = reject.
@@ -948,6 +962,16 @@ __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, d
     for (int k = 0; k < 4; ++k) d[k] = F.P[L.nb[a]].coord[k] - q.coord[k];
     const float fx = __fdiv_rn(dot4(d, xdir), h), fy = __fdiv_rn(dot4(d, ydir), h), fz = dot4(d, q.normal);
     gx[a] = fx; gy[a] = fy; gz[a] = fz;
+  }
+  // The lls rows: in LDS over the neighbour list and seq[] (free until the residuals) when they
+  // fit -- the solver's many wave barriers then drain LDS traffic only -- else in global scratch.
+  __syncthreads();
+  if (n * 6 <= NB_LLS_LDS) {
+    M = reinterpret_cast<double*>(L.nb);
+    r = M + (size_t)n * 5;
+  }
+  for (int a = lane; a < n; a += 64) {
+    const float fx = gx[a], fy = gy[a], fz = gz[a];  // this lane's own stores
     M[(size_t)a * 5 + 0] = (double)(fx * fx);
     M[(size_t)a * 5 + 1] = (double)(fy * fy);
     M[(size_t)a * 5 + 2] = (double)(fx * fy);
@@ -957,7 +981,12 @@ __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, d
   }
   __threadfence_block();
   __syncthreads();
+#if defined(NBX_SKIP_LLS)  // timing experiment only (tools): the quadric fit skipped
+  if (lane < 5) L.x[lane] = 0.0f;
+  __syncthreads();
+#else
   lls5_wave(L, M, r, n);
+#endif
   for (int a = lane; a < n; a += 64) {  // the residuals in parallel (each lane its own rows)
     const float fx = gx[a], fy = gy[a];
     L.seq[a] = L.x[0] * (fx * fx) + L.x[1] * (fy * fy) + L.x[2] * (fx * fy) + L.x[3] * fx + L.x[4] * fy - gz[a];
