@@ -863,7 +863,7 @@ pmvs_status pmvs_patch_colors(pmvs_scene* sc, int32_t n, const float* coords4, c
 
 pmvs_status pmvs_filter_run(pmvs_scene* sc, pmvs_patch* patches, int32_t n, int32_t* keep, pmvs_filter_stats* stats) {
   if (!sc || n < 0 || (n > 0 && (!patches || !keep))) return fail(PMVS_EINVAL, "null argument");
-  if (sc->ds.tnum > 64) return fail(PMVS_EUNSUPPORTED, "filter pass: more than 64 target images");
+  if (sc->ds.tnum > PMVS_MAX_TARGETS) return fail(PMVS_EUNSUPPORTED, "filter pass: more than %d target images", PMVS_MAX_TARGETS);
   for (int i = 0; i < n; ++i) {
     const pmvs_patch& p = patches[i];
     if (p.num_images < 1 || p.num_images > PMVS_MAX_IMAGES || p.num_vimages < 0 || p.num_vimages > PMVS_MAX_IMAGES)
@@ -1045,7 +1045,7 @@ pmvs_status pmvs_expand_run(pmvs_scene* sc, const pmvs_patch* patches, const int
   if (!sc || n < 0 || (n > 0 && (!patches || !alive)) || (!keep && (!out || !alive_out)) || !n_out || cap < n)
     return fail(PMVS_EINVAL, "invalid argument");
   if (wave < 1 || wave > kMaxWave) return fail(PMVS_EINVAL, "wave must be in [1, %d]", kMaxWave);
-  if (sc->ds.tnum > 64) return fail(PMVS_EUNSUPPORTED, "expansion: more than 64 target images");
+  if (sc->ds.tnum > PMVS_MAX_TARGETS) return fail(PMVS_EUNSUPPORTED, "expansion: more than %d target images", PMVS_MAX_TARGETS);
   pmvs_status st;
   if ((st = check_patches(sc, patches, n))) return st;
   if (stats) std::memset(stats, 0, sizeof(*stats));
@@ -1092,7 +1092,7 @@ pmvs_status pmvs_run_loop(pmvs_scene* sc, const pmvs_patch* seeds, int32_t n, fl
   if (!sc || n < 0 || (n > 0 && !seeds) || !n_out || iterations < 0 || cap < n || min_candidates < 0)
     return fail(PMVS_EINVAL, "invalid argument");
   if (wave < 1 || wave > kMaxWave) return fail(PMVS_EINVAL, "wave must be in [1, %d]", kMaxWave);
-  if (sc->ds.tnum > 64) return fail(PMVS_EUNSUPPORTED, "expansion: more than 64 target images");
+  if (sc->ds.tnum > PMVS_MAX_TARGETS) return fail(PMVS_EUNSUPPORTED, "expansion: more than %d target images", PMVS_MAX_TARGETS);
   pmvs_status st;
   if ((st = check_patches(sc, seeds, n))) return st;
   *n_out = 0;

@@ -284,12 +284,12 @@ __global__ void vimages_kernel(DScene s, FilterDev F, int additive, unsigned lon
   const int p = F.order[i];
   pmvs_patch& q = F.P[p];
   if (!additive) q.num_vimages = 0;
-  unsigned long long used = 0ull;  // bit t (tnum <= 64)
+  unsigned long long used[PMVS_MAX_TARGETS / 64] = {};  // bit t: target t is already in a list
   for (int k = 0; k < q.num_images; ++k)
-    if (q.images[k] < s.tnum) used |= 1ull << q.images[k];
-  for (int k = 0; k < q.num_vimages; ++k) used |= 1ull << q.vimages[k];
+    if (q.images[k] < s.tnum) used[q.images[k] >> 6] |= 1ull << (q.images[k] & 63);
+  for (int k = 0; k < q.num_vimages; ++k) used[q.vimages[k] >> 6] |= 1ull << (q.vimages[k] & 63);
   for (int t = 0; t < s.tnum; ++t) {
-    if (used & (1ull << t)) continue;
+    if (used[t >> 6] & (1ull << (t & 63))) continue;
     const DView& v = s.views[t];
     float ic[3];
     project(v, q.coord, s.level, ic);
@@ -1453,7 +1453,7 @@ hipError_t FilterBuffers::reserve(int n_, long long ncells_, int tnum_, int grid
   cap_cells = std::max(ncells_, cap_cells);
   cap_grid = std::max(grid_, cap_grid);
   const size_t ne = (size_t)cap_n * PMVS_MAX_IMAGES;
-  FCHK(dalloc(preg, cap_n)); FCHK(dalloc(vreg, cap_n)); FCHK(dalloc(tgoff, 65));
+  FCHK(dalloc(preg, cap_n)); FCHK(dalloc(vreg, cap_n)); FCHK(dalloc(tgoff, PMVS_MAX_TARGETS + 1));
   FCHK(dalloc(cnt, cap_n + 1)); FCHK(dalloc(off, cap_n + 1));
   FCHK(dalloc(keys, std::max(ne, (size_t)cap_n))); FCHK(dalloc(keys2, std::max(ne, (size_t)cap_n)));
   FCHK(dalloc(cellcnt, cap_cells + 1)); FCHK(dalloc(pg_off, cap_cells + 1)); FCHK(dalloc(vp_off, cap_cells + 1));

@@ -25,6 +25,7 @@ extern "C" {
 #endif
 
 #define PMVS_MAX_IMAGES 64 /* capacity of one patch's image list (reference: unbounded vector) */
+#define PMVS_MAX_TARGETS 256 /* target images (timages) per scene: a C5 cluster is maximage 70 plus overlap */
 #define PMVS_MAX_TAU 16    /* max textures in the objective: tau = min(2*minImageNum, num) */
 #define PMVS_MAX_LEVEL 4   /* reference MyPow2 table limits level to <= 4 (optim.cpp:808-811) */
 

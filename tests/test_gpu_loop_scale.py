@@ -70,6 +70,30 @@ def test_loop_50_views_matches_oracle(gpu_available, oracle_mod):
     assert out_g.tobytes() == out_o.tobytes() or _same_patches(out_g, out_o)
 
 
+@pytest.mark.timeout(900)
+def test_loop_80_targets_matches_oracle(gpu_available, oracle_mod):
+    """More than 64 target images in one scene (PMVS_MAX_TARGETS; a C5 cluster is maximage 70
+    plus overlap views): an 80-view ring, all targets, full loop vs the oracle."""
+    import pmvs_amd as P
+    from test_gpu_parity_matrix import _same_patches
+    inp, p, cands = _scene(80, 320, 180, 200, seed=5)
+    assert inp.num_targets == 80
+    g = P.Scene(inp)
+    seeds = _seeds(g, cands)
+    cap = 1 << 20
+    out_g, log_g = g.run_loop(seeds, inp.threshold, cap=cap, **PROD)
+    g.close()
+    o = oracle_mod.OracleScene(inp)
+    out_o, log_o = o.run_loop(seeds, inp.threshold, cap=cap, nthreads=_threads(), **PROD)
+    o.close()
+    print(f"80-target loop: seeds {len(seeds)} -> {[it['patches'] for it in log_o]} patches")
+    assert len(out_o) > 10 * len(seeds)
+    assert max(int(m) for m in out_g["images"][:, 0]) >= 64  # reference images beyond 64 are used
+    for a, b in zip(log_g, log_o):
+        assert a["patches"] == b["patches"], (a, b)
+    assert out_g.tobytes() == out_o.tobytes() or _same_patches(out_g, out_o)
+
+
 def _cells(inp, model):
     """Covered target cells: every (target image, cell) some patch is registered in -- the
     CPatchOrganizerS::_pgrids entries the expansion tries to fill (patchOrganizerS.cpp:308-330)."""
