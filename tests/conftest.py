@@ -16,7 +16,20 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: longer CPU tests")
 
 
+def _newest(paths):
+    return max((os.path.getmtime(p) for p in paths if os.path.exists(p)), default=0.0)
+
+
 def _make(path):
+    """Build in-tree, unless the built artefacts are already newer than every source (the GPU box
+    receives the prebuilt libraries without the object files: rebuilding there is not needed)."""
+    if os.path.basename(path) == "cmvs-pmvs_amd":
+        outs = [os.path.join(path, f) for f in ("libpmvs_amd.so", "pmvs2", "genOption")]
+        srcs = [os.path.join(path, "csrc", f) for f in os.listdir(os.path.join(path, "csrc"))]
+        srcs += [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
+        srcs.append(os.path.join(path, "Makefile"))
+        if all(os.path.exists(o) for o in outs) and min(os.path.getmtime(o) for o in outs) >= _newest(srcs):
+            return
     subprocess.run(["make", "-C", path, "-s"], check=True)
 
 
