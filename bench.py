@@ -30,7 +30,8 @@ process per GPU:
     reference runs one pmvs2 per cluster option file (genOption.cpp:73-108); no data-path
     collective, only barriers and the SUM / MAX reductions of the counters and the time.
   --mode shard (strong scaling): all ranks run ONE scene; every expansion wave's refinements are
-    split over the ranks and all-gathered over RCCL (pmvs_scene_set_shard + DistExchange).
+    split over the ranks and all-gathered over RCCL (pmvs_scene_set_shard_rccl: a C++ RCCL
+    communicator, device-to-device records).
 """
 import argparse
 import json
@@ -271,8 +272,10 @@ def main():
     seeds = P.patches_from_refined(res)
     t_scene = time.time() - t0
     ex = None
-    if shard:
-        ex = P.DistExchange(device=dev)
+    if shard:  # native RCCL communicator (C++), records all-gathered device to device
+        uid = [P.RcclExchange.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ex = P.RcclExchange(rank, world, uid[0], device=local)
         ex.attach(scene)
 
     def step():

@@ -207,6 +207,7 @@ struct pmvs_scene {
   int shard_rank = 0, shard_world = 1;
   pmvs_allgather_fn shard_fn = nullptr;
   void* shard_ctx = nullptr;
+  pmvs_rccl* shard_rccl = nullptr;  // set: the records go device to device (pmvs_scene_set_shard_rccl)
   int xkept = -1, lkept = -1;   // models kept on the device for pmvs_expand_fetch / pmvs_loop_fetch
   std::vector<int> xalive;
   DBuf<pmvs_patch> fpatches2;   // compaction target of pmvs_run_loop
@@ -977,6 +978,10 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
     pmvs_allgather_fn fn = sc->shard_fn;
     void* ctx = sc->shard_ctx;
     sh.exchange = [fn, ctx](const void* send, size_t bytes, void* recv) { return fn(ctx, send, (int64_t)bytes, recv); };
+    if (pmvs_rccl* comm = sc->shard_rccl)
+      sh.exchange_dev = [comm](const void* dsend, size_t bytes, void* drecv, hipStream_t st) {
+        return pmvs_rccl_allgather_device(comm, dsend, (int64_t)bytes, drecv, st);
+      };
   }
   long long sv[8];
   const auto t0 = std::chrono::steady_clock::now();
@@ -1156,7 +1161,15 @@ pmvs_status pmvs_scene_set_shard(pmvs_scene* sc, int32_t rank, int32_t world, pm
   sc->shard_world = world;
   sc->shard_fn = fn;
   sc->shard_ctx = ctx;
+  sc->shard_rccl = nullptr;
   return PMVS_OK;
+}
+
+pmvs_status pmvs_scene_set_shard_rccl(pmvs_scene* sc, int32_t rank, int32_t world, pmvs_rccl* comm) {
+  if (!sc || !comm || world < 1 || rank < 0 || rank >= world) return fail(PMVS_EINVAL, "invalid shard");
+  const pmvs_status st = pmvs_scene_set_shard(sc, rank, world, &pmvs_rccl_allgather, comm);
+  if (st == PMVS_OK) sc->shard_rccl = comm;
+  return st;
 }
 
 // ---- in-process all-gather among threads (generation-counted barrier)

@@ -1898,7 +1898,7 @@ void delete_commit_work(CommitWork* w);  // after CommitWork's definition
 ExpandBuffers::~ExpandBuffers() {
   void* ps[] = {parents, cand_coord, cand_ok, cand, prep, status, slots, cand2, prep2, res, outp, ostatus, counts, alive,
                 pg_head, vp_head, d_item, d_next, pool_used, tcells, tvals, qtmp, crec, acc, dupd, cellinit, occ,
-                qkey, qrank, qrank2, qsort_tmp};
+                qkey, qrank, qrank2, qsort_tmp, xsd, xrd};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete_commit_work(cm);
@@ -2609,9 +2609,21 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
         // patch[chunk]] per rank; the other ranks' ranges are uploaded so every rank holds all m
         // refined records
         const size_t bytes = (size_t)chunk * (sizeof(int) + sizeof(pmvs_patch));
-        xsend.assign(bytes, 0);
-        xrecv.assign(bytes * G, 0);
-        if (lerr == hipSuccess && mine > 0) {
+        const bool dev = (bool)sh.exchange_dev;  // RCCL: device to device on this stream
+        if (dev) {
+          if (lerr == hipSuccess) lerr = grow(X.xsd, X.cap_xsd, std::max<size_t>(bytes, 1));
+          if (lerr == hipSuccess) lerr = grow(X.xrd, X.cap_xrd, std::max<size_t>(bytes * G, 1));
+          if (lerr == hipSuccess && mine > 0) {
+            lerr = hipMemcpyAsync(X.xsd, X.ostatus + lo, mine * sizeof(int), hipMemcpyDeviceToDevice, st);
+            if (lerr == hipSuccess)
+              lerr = hipMemcpyAsync(X.xsd + (size_t)chunk * sizeof(int), X.outp + lo, (size_t)mine * sizeof(pmvs_patch),
+                                    hipMemcpyDeviceToDevice, st);
+          }
+        } else {
+          xsend.assign(bytes, 0);
+          xrecv.assign(bytes * G, 0);
+        }
+        if (!dev && lerr == hipSuccess && mine > 0) {
           lerr = hipMemcpyAsync(xsend.data(), X.ostatus + lo, mine * sizeof(int), hipMemcpyDeviceToHost, st);
           if (lerr == hipSuccess)
             lerr = hipMemcpyAsync(xsend.data() + (size_t)chunk * sizeof(int), X.outp + lo, (size_t)mine * sizeof(pmvs_patch),
@@ -2628,15 +2640,17 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
         }
         FCHK(lerr);
         if (ovf) return hipErrorOutOfMemory;  // more than NB_CAP neighbours (reported by the API)
-        if (sh.exchange(xsend.data(), bytes, xrecv.data()) != 0) return hipErrorUnknown;
+        if (dev ? sh.exchange_dev(X.xsd, bytes, X.xrd, st) != 0 : sh.exchange(xsend.data(), bytes, xrecv.data()) != 0)
+          return hipErrorUnknown;
         agreed = false;
         for (int r = 0; r < G; ++r) {
-          const char* b = xrecv.data() + (size_t)r * bytes;
           const int rlo = std::min(m, r * chunk), rhi = std::min(m, rlo + chunk);
           if (r == R || rhi <= rlo) continue;
-          FCHK(hipMemcpyAsync(X.ostatus + rlo, b, (rhi - rlo) * sizeof(int), hipMemcpyHostToDevice, st));
+          const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+          const char* b = dev ? X.xrd + (size_t)r * bytes : xrecv.data() + (size_t)r * bytes;
+          FCHK(hipMemcpyAsync(X.ostatus + rlo, b, (rhi - rlo) * sizeof(int), kind, st));
           FCHK(hipMemcpyAsync(X.outp + rlo, b + (size_t)chunk * sizeof(int), (size_t)(rhi - rlo) * sizeof(pmvs_patch),
-                              hipMemcpyHostToDevice, st));
+                              kind, st));
         }
         if (inject && inj_where == 'a' && stats[7] == inj_wave) return hipErrorOutOfMemory;
       }

@@ -87,6 +87,8 @@ struct ExpandBuffers {
   int *qrank = nullptr, *qrank2 = nullptr;
   void* qsort_tmp = nullptr;
   size_t cap_qkey = 0, cap_qrank = 0, cap_qrank2 = 0, cap_qsort = 0;
+  char *xsd = nullptr, *xrd = nullptr;  // device payload of the sharded exchange (send, all ranks)
+  size_t cap_xsd = 0, cap_xrd = 0;
   int *crec = nullptr, *acc = nullptr;  // commit records; committed record indexes
   int2* dupd = nullptr;         // (parent, failed-direction bits) of a wave
   unsigned char* tvals = nullptr;
@@ -101,9 +103,12 @@ struct ExpandBuffers {
 using RefineFn = std::function<hipError_t(const pmvs_candidate* d_in, int n, pmvs_refined* d_out)>;
 // All-gather of `bytes` per rank into recv (world * bytes, rank order); 0 = OK.
 using ExchangeFn = std::function<int(const void* send, size_t bytes, void* recv)>;
+// Device all-gather on the given stream (RCCL); empty = the payload goes through `exchange`.
+using ExchangeDevFn = std::function<int(const void* dsend, size_t bytes, void* drecv, hipStream_t st)>;
 struct Shard {
   int rank = 0, world = 1;
   ExchangeFn exchange;
+  ExchangeDevFn exchange_dev;
 };
 // dP[0, n0): the device-resident model (grown in place, contents kept); d_alive[0, n0) marks the
 // patches the organizer holds; cap bounds the result size *n_out.

@@ -129,7 +129,9 @@ EXPORTS = ["pmvs_last_error", "pmvs_device_count", "pmvs_scene_create", "pmvs_sc
            "pmvs_synth_candidates", "pmvs_selftest_math", "pmvs_selftest_bobyqa", "pmvs_camera_load",
            "pmvs_ppm_load", "pmvs_options_load", "pmvs_options_free", "pmvs_write_patches", "pmvs_write_pset",
            "pmvs_write_ply", "pmvs_patch_colors", "pmvs_filter_run",
-           "pmvs_expand_run", "pmvs_expand_fetch", "pmvs_run_loop", "pmvs_loop_fetch", "pmvs_scene_set_shard", "pmvs_thread_exchange_create",
+           "pmvs_expand_run", "pmvs_expand_fetch", "pmvs_run_loop", "pmvs_loop_fetch", "pmvs_scene_set_shard", "pmvs_scene_set_shard_rccl", "pmvs_rccl_unique_id",
+           "pmvs_rccl_create", "pmvs_rccl_destroy", "pmvs_rccl_allgather", "pmvs_rccl_allgather_device",
+           "pmvs_thread_exchange_create",
            "pmvs_thread_exchange_ctx", "pmvs_thread_allgather", "pmvs_thread_exchange_destroy", "pmvs_detect_features",
            "pmvs_seed_run", "pmvs_selftest_lls", "pmvs_image_load", "pmvs_pnm_mask_load", "pmvs_set_edge"]
 
@@ -191,6 +193,13 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
                                   C.c_int32, C.POINTER(C.c_int32), C.c_void_p]
     lib.pmvs_loop_fetch.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     lib.pmvs_scene_set_shard.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
+    lib.pmvs_rccl_unique_id.argtypes = [C.c_void_p]
+    lib.pmvs_rccl_create.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.POINTER(C.c_void_p)]
+    lib.pmvs_rccl_destroy.argtypes = [C.c_void_p]
+    lib.pmvs_rccl_destroy.restype = None
+    lib.pmvs_rccl_allgather.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
+    lib.pmvs_rccl_allgather.restype = C.c_int
+    lib.pmvs_scene_set_shard_rccl.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]
     lib.pmvs_thread_exchange_create.argtypes = [C.c_int32]
     lib.pmvs_thread_exchange_create.restype = C.c_void_p
     lib.pmvs_thread_exchange_ctx.argtypes = [C.c_void_p, C.c_int32]
@@ -680,6 +689,42 @@ class ThreadExchange:
     def close(self):
         if self.handle:
             self.lib.pmvs_thread_exchange_destroy(self.handle)
+            self.handle = None
+
+
+class RcclExchange:
+    """Native RCCL communicator of the sharded expansion (pmvs_rccl_*): one process per GPU; the
+    per-wave records go device to device on the scene's stream.  Rank 0 creates the 128-byte id
+    (unique_id()) and every rank receives it (e.g. torch.distributed.broadcast_object_list)."""
+
+    def __init__(self, rank: int, world: int, uid: bytes, device: int = 0):
+        self.lib = load_library()
+        self.rank, self.world = rank, world
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        h = C.c_void_p()
+        _check(self.lib.pmvs_rccl_create(device, rank, world, buf, C.byref(h)))
+        self.handle = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * 128)()
+        _check(load_library().pmvs_rccl_unique_id(buf))
+        return bytes(buf)
+
+    def allgather(self, data: bytes) -> bytes:
+        n = len(data)
+        out = (C.c_uint8 * (n * self.world))()
+        src = (C.c_uint8 * max(1, n)).from_buffer_copy(data if n else b"\0")
+        if self.lib.pmvs_rccl_allgather(self.handle, src, n, out) != 0:
+            raise PmvsError("pmvs_rccl_allgather failed")
+        return bytes(out)
+
+    def attach(self, scene: "Scene"):
+        _check(self.lib.pmvs_scene_set_shard_rccl(scene.handle, self.rank, self.world, self.handle))
+
+    def close(self):
+        if self.handle:
+            self.lib.pmvs_rccl_destroy(self.handle)
             self.handle = None
 
 

@@ -323,6 +323,19 @@ pmvs_status pmvs_seed_run(pmvs_scene* scene, const pmvs_point* points, const int
 typedef int (*pmvs_allgather_fn)(void* ctx, const void* send, int64_t bytes, void* recv);
 pmvs_status pmvs_scene_set_shard(pmvs_scene* scene, int32_t rank, int32_t world, pmvs_allgather_fn fn, void* ctx);
 
+/* Native RCCL communicator (one process per GPU; librccl.so.1 opened at run time).  Rank 0 calls
+ * pmvs_rccl_unique_id and shares the 128 bytes with every rank (any channel); each rank calls
+ * pmvs_rccl_create on its device, then pmvs_scene_set_shard_rccl: the expansion's per-wave
+ * records are then all-gathered device to device on the scene's stream (ncclAllGather), and the
+ * 8-byte error headers through pmvs_rccl_allgather (a pmvs_allgather_fn on host buffers). */
+typedef struct pmvs_rccl pmvs_rccl;
+pmvs_status pmvs_rccl_unique_id(uint8_t* id128);
+pmvs_status pmvs_rccl_create(int32_t device, int32_t rank, int32_t world, const uint8_t* id128, pmvs_rccl** out);
+void pmvs_rccl_destroy(pmvs_rccl* comm);
+int pmvs_rccl_allgather(void* comm, const void* send, int64_t bytes, void* recv);
+int pmvs_rccl_allgather_device(void* comm, const void* dsend, int64_t bytes, void* drecv, void* hip_stream);
+pmvs_status pmvs_scene_set_shard_rccl(pmvs_scene* scene, int32_t rank, int32_t world, pmvs_rccl* comm);
+
 /* An in-process all-gather among `world` threads (one scene per thread, e.g. several scenes on
  * one GPU): pmvs_thread_allgather with ctx = pmvs_thread_exchange_ctx(group, rank). */
 typedef struct pmvs_thread_exchange pmvs_thread_exchange;
