@@ -929,6 +929,36 @@ pmvs_status check_patches(const pmvs_scene* sc, const pmvs_patch* patches, int n
   return PMVS_OK;
 }
 
+// The scene's shard (pmvs_scene_set_shard / _rccl) as the organizer code takes it.
+Shard make_shard(const pmvs_scene* sc) {
+  Shard sh;
+  if (sc->shard_fn && sc->shard_world > 1) {
+    sh.rank = sc->shard_rank;
+    sh.world = sc->shard_world;
+    pmvs_allgather_fn fn = sc->shard_fn;
+    void* ctx = sc->shard_ctx;
+    sh.exchange = [fn, ctx](const void* send, size_t bytes, void* recv) { return fn(ctx, send, (int64_t)bytes, recv); };
+    if (pmvs_rccl* comm = sc->shard_rccl)
+      sh.exchange_dev = [comm](const void* dsend, size_t bytes, void* drecv, hipStream_t st) {
+        return pmvs_rccl_allgather_device(comm, dsend, (int64_t)bytes, drecv, st);
+      };
+  }
+  return sh;
+}
+
+// Loop-level 8-byte header {error, 0} of the sharded loop: a rank that fails outside the
+// expansion's / filter's own exchanges sends it once (its peers receive it in place of their next
+// expansion batch header), and every rank sends {0} when the loop ends.  Returns 0 = every rank
+// OK, 1 = some rank failed, -1 = the exchange itself failed.
+int loop_header(const Shard& sh, int err) {
+  int h[2] = {err, 0};
+  std::vector<int> all(2 * (size_t)sh.world, 0);
+  if (sh.exchange(h, sizeof(h), all.data()) != 0) return -1;
+  for (int r = 0; r < sh.world; ++r)
+    if (all[2 * r] != 0) return 1;
+  return 0;
+}
+
 std::vector<long long> target_cells(pmvs_scene* sc) {
   std::vector<long long> tgoff(sc->ds.tnum + 1, 0);
   sc->xbuf.gw.assign(sc->ds.tnum, 0);
@@ -971,18 +1001,7 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
     return launch_refine(sc->ds, d_in, sc->jobs.p, d_out, m, sc->stats.p, sc->grid, sc->refine_grid, sc->tslots,
                          sc->stream, sc->kev);
   };
-  Shard sh;
-  if (sc->shard_fn && sc->shard_world > 1) {
-    sh.rank = sc->shard_rank;
-    sh.world = sc->shard_world;
-    pmvs_allgather_fn fn = sc->shard_fn;
-    void* ctx = sc->shard_ctx;
-    sh.exchange = [fn, ctx](const void* send, size_t bytes, void* recv) { return fn(ctx, send, (int64_t)bytes, recv); };
-    if (pmvs_rccl* comm = sc->shard_rccl)
-      sh.exchange_dev = [comm](const void* dsend, size_t bytes, void* drecv, hipStream_t st) {
-        return pmvs_rccl_allgather_device(comm, dsend, (int64_t)bytes, drecv, st);
-      };
-  }
+  const Shard sh = make_shard(sc);
   long long sv[8];
   const auto t0 = std::chrono::steady_clock::now();
   const hipError_t e = expand_pass(sc->ds, sc->fbuf, sc->xbuf, sc->fpatches.p, sc->fpatches.n, n0, sc->xbuf.alive, cap,
@@ -1013,7 +1032,9 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
 }
 
 // One filter pass on the device-resident model sc->fpatches[0, n); keep flags in sc->fkeep.
-pmvs_status filter_device(pmvs_scene* sc, int n, pmvs_filter_stats* stats) {
+// *handled (sharded loop): whether the peers already know of a failure returned here.
+pmvs_status filter_device(pmvs_scene* sc, int n, pmvs_filter_stats* stats, bool* handled = nullptr) {
+  if (handled) *handled = false;
   if (stats) std::memset(stats, 0, sizeof(*stats));
   if (n == 0) return PMVS_OK;
   pmvs_status st;
@@ -1021,8 +1042,15 @@ pmvs_status filter_device(pmvs_scene* sc, int n, pmvs_filter_stats* stats) {
   std::vector<long long> tgoff = target_cells(sc);
   HIPCHK(hipEventRecord(sc->ev0, sc->stream));
   int counts[4], overflow = 0;
-  HIPCHK(filter_pass(sc->ds, sc->fbuf, sc->fpatches.p, n, tgoff[sc->ds.tnum], tgoff.data(), sc->grid, sc->stream, counts,
-                     &overflow, sc->fkeep.p));
+  const Shard sh = make_shard(sc);
+  bool fh = true;
+  const hipError_t fe = filter_pass(sc->ds, sc->fbuf, sc->fpatches.p, n, tgoff[sc->ds.tnum], tgoff.data(), sc->grid,
+                                    sc->stream, counts, &overflow, sc->fkeep.p, &sh, &fh);
+  if (fe != hipSuccess) {
+    if (handled) *handled = fh;
+    return fail(PMVS_EDEVICE, "filter pass: %s", hipGetErrorString(fe));
+  }
+  if (handled) *handled = true;  // overflow is all-gathered: every rank returns it together
   HIPCHK(hipEventRecord(sc->ev1, sc->stream));
   HIPCHK(hipStreamSynchronize(sc->stream));
   if (overflow) return fail(PMVS_EUNSUPPORTED, "filterNeighbor: %d patches with more than 1024 neighbours", overflow);
@@ -1110,23 +1138,31 @@ pmvs_status pmvs_run_loop(pmvs_scene* sc, const pmvs_patch* seeds, int32_t n, fl
   // (findMatch.cpp:23-28): before = threshold - 0.3f (findMatch.cpp:104)
   float ncc = threshold, before = threshold - 0.3f;
   int cthr = 4, depth = 1, cur = n;
+  // Sharded: a failure the peers have not seen is announced with one loop header (loop_header).
+  const Shard lsh = make_shard(sc);
+  auto fail_loop = [&](pmvs_status s0, bool peers_know) {
+    if (lsh.world > 1 && !peers_know) (void)loop_header(lsh, 1);
+    return s0;
+  };
   for (int it = 0; it < iterations; ++it) {
     sc->ds.depth = depth;
     sc->ds.nccThreshold = ncc;
     sc->ds.nccThresholdBefore = before;
-    if (grow_alive(sc, std::max(cur, 1))) return fail(PMVS_ENOMEM, "alive flags");
-    HIPCHK(fill_int(sc->xbuf.alive, cur, 1, sc->stream));
+    if (grow_alive(sc, std::max(cur, 1))) return fail_loop(fail(PMVS_ENOMEM, "alive flags"), false);
+    if (fill_int(sc->xbuf.alive, cur, 1, sc->stream) != hipSuccess) return fail_loop(fail(PMVS_EDEVICE, "alive flags"), false);
     pmvs_loop_iter li{};
     li.depth = depth;
     int nn = cur;
     if (cur > 0 && (st = expand_device(sc, cur, wave, min_candidates, cthr, (it == 0 && (flags & PMVS_EXPAND_AFTER_SEEDS)) ? 1 : 0, cap,
                                        &nn, &li.expand)))
       return st;
-    if ((st = filter_device(sc, nn, &li.filter))) return st;
+    bool handled = true;
+    if ((st = filter_device(sc, nn, &li.filter, &handled))) return fail_loop(st, handled);
     int kept = 0;
     if (nn > 0) {
-      if ((st = ensure_keep_data(sc, sc->fpatches2, sc->fpatches.n))) return st;
-      HIPCHK(compact_model(sc->fbuf, sc->fpatches.p, nn, sc->fkeep.p, sc->fpatches2.p, &kept, sc->stream));
+      if ((st = ensure_keep_data(sc, sc->fpatches2, sc->fpatches.n))) return fail_loop(st, false);
+      if (compact_model(sc->fbuf, sc->fpatches.p, nn, sc->fkeep.p, sc->fpatches2.p, &kept, sc->stream) != hipSuccess)
+        return fail_loop(fail(PMVS_EDEVICE, "model compaction"), false);
       std::swap(sc->fpatches.p, sc->fpatches2.p);
       std::swap(sc->fpatches.n, sc->fpatches2.n);
     }
@@ -1138,7 +1174,8 @@ pmvs_status pmvs_run_loop(pmvs_scene* sc, const pmvs_patch* seeds, int32_t n, fl
     cthr = 2;
     ++depth;
   }
-  HIPCHK(hipStreamSynchronize(sc->stream));
+  if (hipStreamSynchronize(sc->stream) != hipSuccess) return fail_loop(fail(PMVS_EDEVICE, "loop synchronisation"), false);
+  if (lsh.world > 1 && loop_header(lsh, 0) != 0) return fail(PMVS_EDEVICE, "sharded loop: another rank failed");
   *n_out = cur;
   sc->lkept = cur;
   return PMVS_OK;

@@ -1009,9 +1009,13 @@ __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, d
 
 // CFilter::filterNeighborThread (filter.cpp:358-385): findNeighbors(patch, ., 0, 4, 2, 1), reject
 // with fewer than 6 neighbours or a failed quadric fit.  One wavefront per patch.
+// Sharded loop (world > 1): a rank tests only the patches whose reference image it owns
+// (target t belongs to rank t mod world); the others are left to their owners
+// and the reject flags are all-gathered afterwards (filter_pass).
 __global__ __launch_bounds__(64) void neighbor_kernel(DScene s, FilterDev F, double* __restrict__ scratch,
                                                       int* __restrict__ reject, int* __restrict__ overflow,
-                                                      int* __restrict__ queue, int* __restrict__ dbg_counts) {
+                                                      int* __restrict__ queue, int* __restrict__ dbg_counts, int rank,
+                                                      int world) {
   __shared__ NbLds L;
   const int lane = threadIdx.x;
   double* M = scratch + (size_t)blockIdx.x * NB_SCR;
@@ -1024,7 +1028,8 @@ __global__ __launch_bounds__(64) void neighbor_kernel(DScene s, FilterDev F, dou
     const int p = F.order[i];
     const pmvs_patch& q = F.P[p];
     int rej = 0;  // _fix patches are kept; no early `continue` (see depth_post_kernel)
-    if (!uni(q.fix)) {
+    const bool mine = world <= 1 || uni(q.images[0]) % world == rank;
+    if (mine && !uni(q.fix)) {
       const int n = gather_neighbors(s, F, L, q, 4.0f, 2, 1);
       if (lane == 0 && L.overflow) atomicAdd(overflow, 1);
       if (lane == 0 && dbg_counts) dbg_counts[p] = L.overflow ? -n : n;
@@ -1442,7 +1447,7 @@ static hipError_t dalloc(T*& p, size_t n) {
 
 FilterBuffers::~FilterBuffers() {
   void* ps[] = {preg, vreg, tgoff, cnt, off, keys, keys2, cellcnt, pg_off, pg_items, vp_off, vp_items, dpkey,
-                order, rank, unit0, flags, safe, need, list, scratch, counters, temp, edge_off, edges};
+                order, rank, unit0, flags, safe, need, list, scratch, counters, temp, edge_off, edges, rbits};
   for (void* p : ps)
     if (p) (void)hipFree(p);
 }
@@ -1538,6 +1543,18 @@ __global__ void scatter_index_kernel(const int* __restrict__ f, const int* __res
   if (k < n && f[k]) out[off[k]] = k;
 }
 
+__global__ void pack_bits_kernel(const int* __restrict__ f, int n, unsigned* __restrict__ bits) {
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w * 32 >= n) return;
+  unsigned v = 0u;
+  for (int b = 0; b < 32 && w * 32 + b < n; ++b) v |= (f[w * 32 + b] != 0 ? 1u : 0u) << b;
+  bits[w] = v;
+}
+__global__ void unpack_bits_kernel(const unsigned* __restrict__ bits, int n, int* __restrict__ f) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) f[k] = (bits[k >> 5] >> (k & 31)) & 1u;
+}
+
 // CPatchOrganizerS::collectPatches: collect ranks and order
 static hipError_t collect(Ctx& c) {
   FilterBuffers& B = c.B;
@@ -1585,8 +1602,17 @@ static hipError_t apply_flags(Ctx& c, int* removed) {
 
 }  // namespace
 
-hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n, long long ncells, const long long* h_tgoff,
-                       int grid, hipStream_t st, int counts[4], int* overflow, int* keep_dev) {
+static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n, long long ncells,
+                                   const long long* h_tgoff, int grid, hipStream_t st, int counts[4], int* overflow,
+                                   int* keep_dev, const Shard* sh, int& phase) {
+  const bool part = sh && sh->world > 1;
+  phase = 0;  // 0: before the flag exchange, 1: at it (every rank sees the outcome), 2: after it
+  // test hook (tests/test_gpu_expand.py): PMVS_TEST_SHARD_FAIL="rank:0:f|g" fails that rank's
+  // filter pass before (f) or after (g) its flag exchange
+  int inj_rank = -1, inj_wave = -1;
+  char inj_where = 0;
+  if (const char* e = getenv("PMVS_TEST_SHARD_FAIL")) (void)sscanf(e, "%d:%d:%c", &inj_rank, &inj_wave, &inj_where);
+  const bool inject = part && inj_rank == sh->rank;
   dbg(st, "start");
   FCHK(B.reserve(n, ncells, s.tnum, grid * NB_GRID_MULT));
   dbg(st, "reserve");
@@ -1631,11 +1657,13 @@ hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n,
   FCHK(set_dm_vgrids(c, 1));
   dbg(st, "set_dm_vgrids(1) after exact");
   // ---- filterNeighbor(1)
+  if (inject && inj_where == 'f') return hipErrorOutOfMemory;
   FCHK(hipMemsetAsync(B.flags, 0, n * sizeof(int), st));
   FCHK(hipMemsetAsync(B.counters + 3, 0, 5 * sizeof(int), st));
   if (c.nalive)
     hipLaunchKernelGGL(neighbor_kernel, dim3(std::min(grid * NB_GRID_MULT, c.nalive)), dim3(64), 0, st, s, c.dev(), B.scratch, B.flags,
-                       B.counters + 3, B.counters + 4, getenv("PMVS_FILTER_DEBUG") ? B.need : nullptr);
+                       B.counters + 3, B.counters + 4, getenv("PMVS_FILTER_DEBUG") ? B.need : nullptr, part ? sh->rank : 0,
+                       part ? sh->world : 1);
   dbg(st, "neighbor kernel");
   if (getenv("PMVS_FILTER_DEBUG")) {
     std::vector<int> cnts(n), ord(c.nalive);
@@ -1651,6 +1679,39 @@ hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n,
             cnts[ord[0]], c.nalive > 1 ? cnts[ord[1]] : 0, c.nalive > 2 ? cnts[ord[2]] : 0);
   }
   FCHK(read_int(B.counters + 3, overflow, st));
+  if (part) {
+    // all-gather of {error, overflow, reject bits} per rank; a rank's bits cover the patches it owns
+    const int nw = (n + 31) / 32;
+    if ((size_t)nw + 1 > B.cap_rbits) {
+      if (B.rbits) (void)hipFree(B.rbits);
+      B.rbits = nullptr;
+      B.cap_rbits = 0;
+      FCHK(hipMalloc((void**)&B.rbits, ((size_t)nw + 1) * sizeof(unsigned)));
+      B.cap_rbits = (size_t)nw + 1;
+    }
+    if (nw) hipLaunchKernelGGL(pack_bits_kernel, dim3(nblk(nw)), dim3(256), 0, st, B.flags, n, B.rbits);
+    std::vector<unsigned> mine(2 + (size_t)nw, 0u), all((2 + (size_t)nw) * sh->world, 0u);
+    if (nw) FCHK(hipMemcpyAsync(mine.data() + 2, B.rbits, (size_t)nw * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    FCHK(hipStreamSynchronize(st));
+    mine[1] = (unsigned)*overflow;
+    phase = 1;
+    if (sh->exchange(mine.data(), mine.size() * sizeof(unsigned), all.data()) != 0) return hipErrorUnknown;
+    int ovf = 0;
+    for (int r = 0; r < sh->world; ++r) {
+      const unsigned* a = all.data() + (size_t)r * mine.size();
+      if (a[0] != 0) return hipErrorUnknown;  // a peer failed before the exchange
+      ovf += (int)a[1];
+      if (r != sh->rank)
+        for (int w = 0; w < nw; ++w) mine[2 + w] |= a[2 + w];
+    }
+    *overflow = ovf;
+    phase = 2;
+    if (inject && inj_where == 'g') return hipErrorOutOfMemory;
+    if (nw) {
+      FCHK(hipMemcpyAsync(B.rbits, mine.data() + 2, (size_t)nw * sizeof(unsigned), hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(unpack_bits_kernel, dim3(nblk(n)), dim3(256), 0, st, B.rbits, n, B.flags);
+    }
+  }
   {
     int errs[2] = {0, 0};
     FCHK(hipMemcpy(errs, B.counters + 6, 2 * sizeof(int), hipMemcpyDeviceToHost));
@@ -1722,6 +1783,28 @@ hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n,
   FCHK(collect(c));
   hipLaunchKernelGGL(keep_kernel, dim3(nblk(n)), dim3(256), 0, st, n, B.preg, B.rank, keep_dev);
   return hipGetLastError();
+}
+
+// Sharded (world > 1): filter_pass makes exactly one all-gather (the filterNeighbor flags).  A rank
+// that fails before it still sends its {error} payload, so its peers fail with it; *handled says
+// whether the peers have seen this rank's failure (else the caller sends an abort header).
+hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n, long long ncells, const long long* h_tgoff,
+                       int grid, hipStream_t st, int counts[4], int* overflow, int* keep_dev, const Shard* sh,
+                       bool* handled) {
+  int phase = 0;
+  hipError_t e = filter_pass_impl(s, B, dP, n, ncells, h_tgoff, grid, st, counts, overflow, keep_dev, sh, phase);
+  if (handled) *handled = true;
+  if (e != hipSuccess && sh && sh->world > 1 && n > 0) {
+    if (phase == 0) {  // the peers wait in the flag exchange: send them this rank's error there
+      const size_t words = 2 + (size_t)(n + 31) / 32;
+      std::vector<unsigned> mine(words, 0u), all(words * sh->world, 0u);
+      mine[0] = 1u;
+      (void)sh->exchange(mine.data(), words * sizeof(unsigned), all.data());
+    } else if (phase == 2 && handled) {
+      *handled = false;  // failed after the exchange: the caller announces it (loop header)
+    }
+  }
+  return e;
 }
 
 

@@ -55,13 +55,14 @@ struct FilterBuffers {
   double* scratch = nullptr;
   void* temp = nullptr;
   size_t temp_bytes = 0, edges_cap = 0;
+  unsigned* rbits = nullptr;  // sharded filterNeighbor: packed reject flags
+  size_t cap_rbits = 0;
   int cap_n = 0, cap_grid = 0;
   long long cap_cells = 0;
   hipError_t reserve(int n, long long ncells, int tnum, int grid);
   ~FilterBuffers();
 };
-hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n, long long ncells, const long long* h_tgoff,
-                       int grid, hipStream_t st, int counts[4], int* overflow, int* keep_dev);
+
 hipError_t launch_filter_refimage(const DScene& s, pmvs_patch* P, const int* list, int m, int grid, hipStream_t stream);
 
 // ---- expansion run (pmvs_filter.hip)
@@ -112,6 +113,11 @@ struct Shard {
 };
 // dP[0, n0): the device-resident model (grown in place, contents kept); d_alive[0, n0) marks the
 // patches the organizer holds; cap bounds the result size *n_out.
+// One CFilter::run pass on the device model; sharded (sh->world > 1) filterNeighbor runs on the
+// patches this rank owns and the flags are all-gathered (one exchange per pass).
+hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n, long long ncells, const long long* h_tgoff,
+                       int grid, hipStream_t st, int counts[4], int* overflow, int* keep_dev, const Shard* sh = nullptr,
+                       bool* handled = nullptr);
 hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs_patch*& dP, size_t& dP_cap, int n0,
                        const int* d_alive, int cap, long long ncells, const long long* h_tgoff, int wave, int cthr,
                        int flags, int grid, hipStream_t st, const RefineFn& refine, const Shard& sh, long long stats[8],

@@ -209,6 +209,21 @@ def test_sharded_expand_rank_failure_fails_all_ranks(gpu_available, monkeypatch,
     assert all(isinstance(e, P.PmvsError) for e in errs), errs
 
 
+@pytest.mark.parametrize("where", ["f", "g"])
+def test_sharded_loop_filter_failure_fails_all_ranks(gpu_available, monkeypatch, where):
+    """The sharded loop's filter pass (owner-partitioned filterNeighbor, one flag all-gather):
+    a failure on rank 1 before (f) or after (g) that exchange makes both ranks return an error."""
+    import pmvs_amd as P
+    inp, p = P.synth_scene(6, 480, 360, level=1, supersample=2)
+    g = P.Scene(inp)
+    pa = seed_model(P, g, inp, p, 200, 7)
+    g.close()
+    monkeypatch.setenv("PMVS_TEST_SHARD_FAIL", f"1:0:{where}")
+    errs = run_sharded(P, inp, pa, 2, lambda sc, m, **kw: sc.run_loop(m, inp.threshold, **kw), expect_errors=True,
+                       wave=512)
+    assert all(isinstance(e, P.PmvsError) for e in errs), errs
+
+
 def test_sharded_full_loop_matches_single_rank(gpu_available):
     import pmvs_amd as P
     inp, p = P.synth_scene(6, 480, 360, level=1, supersample=2)
