@@ -1158,15 +1158,17 @@ __global__ __launch_bounds__(64) void empty_blocks_kernel(DScene s, FilterDev F,
 // status: -1 no candidate, 1 rejected, 0 goes to preProcess (pmvs_candidate written).
 __global__ void prepare_kernel(DScene s, FilterDev F, const unsigned char* __restrict__ counts, const int* __restrict__ parents,
                                int np, const float* __restrict__ cand_coord, const int* __restrict__ cand_ok,
-                               pmvs_candidate* __restrict__ cout, pmvs_patch* __restrict__ prep, int* __restrict__ status,
-                               int cthr, int only) {
+                               pmvs_candidate* __restrict__ cout_all, pmvs_patch* __restrict__ prep_all,
+                               int* __restrict__ status, int cthr, int only, const int* __restrict__ cidx) {
   const int slot = blockIdx.x * blockDim.x + threadIdx.x;
   if (slot >= np * 6) return;
   if (!cand_ok[slot] || (only >= 0 && slot != only)) { status[slot] = -1; return; }
+  // candidate and prepared-patch records exist for the free directions only (compact index)
+  const int ci = cidx[slot];
   const pmvs_patch& par = F.P[parents[slot / 6]];
   float coord[4];
   for (int c = 0; c < 4; ++c) coord[c] = cand_coord[4 * slot + c];
-  pmvs_patch& q = prep[slot];
+  pmvs_patch& q = prep_all[ci];
   for (int c = 0; c < 4; ++c) { q.coord[c] = coord[c]; q.normal[c] = par.normal[c]; }
   int ni = 0;
   for (int k = 0; k < par.num_images; ++k) {  // setGridsImages (patchOrganizerS.cpp:383-399)
@@ -1214,14 +1216,14 @@ __global__ void prepare_kernel(DScene s, FilterDev F, const unsigned char* __res
   int ne = 0;
   if (!st) {  // removeImagesEdge (optim.cpp:384-396)
     for (int k = 0; k < ni; ++k)
-      if (get_edge(s, s.views[q.images[k]], coord, s.level)) cout[slot].images[ne++] = q.images[k];
+      if (get_edge(s, s.views[q.images[k]], coord, s.level)) cout_all[ci].images[ne++] = q.images[k];
     if (ne == 0) st = 1;
   }
   status[slot] = st;
   if (!st) {
-    for (int c = 0; c < 4; ++c) { cout[slot].coord[c] = coord[c]; cout[slot].normal[c] = par.normal[c]; }
-    cout[slot].dscale = 0.0f;
-    cout[slot].num_images = ne;
+    for (int c = 0; c < 4; ++c) { cout_all[ci].coord[c] = coord[c]; cout_all[ci].normal[c] = par.normal[c]; }
+    cout_all[ci].dscale = 0.0f;
+    cout_all[ci].num_images = ne;
   }
 }
 
@@ -1555,6 +1557,45 @@ __global__ void unpack_bits_kernel(const unsigned* __restrict__ bits, int n, int
   if (k < n) f[k] = (bits[k >> 5] >> (k & 31)) & 1u;
 }
 
+// filterSmallGroups labels on the device (filter_pass): see the comment at the call.
+__global__ void lab_init_kernel(int* __restrict__ lab, int na) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < na) lab[i] = i;
+}
+__global__ void lab_relax_kernel(const int* __restrict__ eoff, const int* __restrict__ edges, int na, int* lab,
+                                 int* changed) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= na) return;
+  const int li = lab[i];
+  bool any = false;
+  for (int e = eoff[i]; e < eoff[i + 1]; ++e) {
+    const int j = edges[e];
+    if (li < lab[j]) {
+      atomicMin(&lab[j], li);
+      any = true;
+    }
+  }
+  if (any) atomicOr(changed, 1);
+}
+__global__ void lab_jump_kernel(int* lab, int na, int* changed) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= na) return;
+  const int l = lab[i], ll = lab[l];
+  if (ll < l) {
+    atomicMin(&lab[i], ll);
+    atomicOr(changed, 1);
+  }
+}
+__global__ void lab_count_kernel(const int* __restrict__ lab, int na, int* __restrict__ csize) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < na) atomicAdd(&csize[lab[i]], 1);
+}
+__global__ void lab_flags_kernel(const int* __restrict__ lab, const int* __restrict__ csize, const int* __restrict__ order,
+                                 int na, int threshold, int* __restrict__ flags) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < na && csize[lab[i]] < threshold) flags[order[i]] = 1;
+}
+
 // CPatchOrganizerS::collectPatches: collect ranks and order
 static hipError_t collect(Ctx& c) {
   FilterBuffers& B = c.B;
@@ -1738,39 +1779,33 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
       FCHK(hipMalloc((void**)&B.edges, B.edges_cap * sizeof(int)));
     }
     hipLaunchKernelGGL(group_edges_kernel, dim3(nblk(na)), dim3(256), 0, st, s, c.dev(), 1, B.edge_off, B.cnt, B.edges);
-    FCHK(B.pin.ensure(((size_t)na + 1 + (size_t)ne + (size_t)na) * sizeof(int)));
-    const int* eoff = B.pin.as<int>();
-    const int* edges = eoff + (na + 1);
-    const int* order = edges + ne;
-    FCHK(hipMemcpyAsync(B.pin.as<int>(), B.edge_off, (na + 1) * sizeof(int), hipMemcpyDeviceToHost, st));
-    if (ne) FCHK(hipMemcpyAsync(B.pin.as<int>((size_t)(na + 1) * sizeof(int)), B.edges, ne * sizeof(int), hipMemcpyDeviceToHost, st));
-    FCHK(hipMemcpyAsync(B.pin.as<int>(((size_t)na + 1 + ne) * sizeof(int)), B.order, na * sizeof(int), hipMemcpyDeviceToHost, st));
-    FCHK(hipStreamSynchronize(st));
-    // filterSmallGroups label BFS (filter.cpp:520-562) in collect order.  Every patch enters
-    // the queue once, so one array holds all the BFS queues back to back; a component is
-    // qv[start, tail) when its BFS ends, and only its size matters (threshold below).
+    // filterSmallGroups' labelling (filter.cpp:520-562): a BFS from every unlabelled patch in
+    // collect order over the directed neighbour edges.  The label it gives patch j is the
+    // smallest collect index m from which j is reachable (m is unlabelled when its turn comes --
+    // an earlier root reaching m would reach j -- and no node of a path m -> j can carry an
+    // earlier label, for the same reason), so the labels are a fixpoint: lab[j] = min over edges
+    // i -> j of lab[i], accelerated by lab[j] = lab[lab[j]] (reachability is transitive).  Computed
+    // on the device; only the component sizes matter (threshold below).
     const int threshold = std::max(20, na / 10000);
-    std::vector<unsigned char> seen(na, 0);
-    std::vector<int> qv(na), flags(n, 0);
-    int tail = 0;
-    for (int pid = 0; pid < na; ++pid) {
-      if (seen[pid]) continue;
-      const int start = tail;
-      seen[pid] = 1;
-      qv[tail++] = pid;
-      for (int h = start; h < tail; ++h) {
-        const int pt = qv[h];
-        for (int e = eoff[pt], e1 = eoff[pt + 1]; e < e1; ++e) {
-          const int j = edges[e];
-          if (seen[j]) continue;
-          seen[j] = 1;
-          qv[tail++] = j;
-        }
+    int* lab = B.need;   // free after filterExact
+    int* csize = B.list;
+    int* changed = B.counters + 5;
+    hipLaunchKernelGGL(lab_init_kernel, dim3(nblk(na)), dim3(256), 0, st, lab, na);
+    for (int it = 0;; ++it) {
+      FCHK(hipMemsetAsync(changed, 0, sizeof(int), st));
+      for (int r = 0; r < 4; ++r) {
+        if (ne) hipLaunchKernelGGL(lab_relax_kernel, dim3(nblk(na)), dim3(256), 0, st, B.edge_off, B.edges, na, lab, changed);
+        hipLaunchKernelGGL(lab_jump_kernel, dim3(nblk(na)), dim3(256), 0, st, lab, na, changed);
       }
-      if (tail - start < threshold)
-        for (int k = start; k < tail; ++k) flags[order[qv[k]]] = 1;
+      int ch = 0;
+      FCHK(read_int(changed, &ch, st));
+      if (!ch) break;
+      if (it > na) return hipErrorIllegalState;  // cannot happen: every round lowers some label
     }
-    FCHK(hipMemcpyAsync(B.flags, flags.data(), n * sizeof(int), hipMemcpyHostToDevice, st));
+    FCHK(hipMemsetAsync(csize, 0, na * sizeof(int), st));
+    hipLaunchKernelGGL(lab_count_kernel, dim3(nblk(na)), dim3(256), 0, st, lab, na, csize);
+    FCHK(hipMemsetAsync(B.flags, 0, n * sizeof(int), st));
+    hipLaunchKernelGGL(lab_flags_kernel, dim3(nblk(na)), dim3(256), 0, st, lab, csize, B.order, na, threshold, B.flags);
     // _flag = collect index of every collected patch (filter.cpp:538-542)
     hipLaunchKernelGGL(flag_rank_kernel, dim3(nblk(na)), dim3(256), 0, st, dP, B.order, na);
     // fixed patches are never removed (filter.cpp:590)
@@ -1836,11 +1871,11 @@ struct QCmp {  // max-heap on key
 
 __global__ void gather_slots_kernel(const int* __restrict__ slots, int m, const pmvs_candidate* __restrict__ cin,
                                     const pmvs_patch* __restrict__ prep, pmvs_candidate* __restrict__ cout,
-                                    pmvs_patch* __restrict__ pout) {
+                                    pmvs_patch* __restrict__ pout, const int* __restrict__ cidx) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= m) return;
-  cout[k] = cin[slots[k]];
-  pout[k] = prep[slots[k]];
+  cout[k] = cin[cidx[slots[k]]];
+  pout[k] = prep[cidx[slots[k]]];
 }
 
 // Collected patches: flag = 1 (clearFlags + collectPatches(queue), patchOrganizerS.cpp) and their
@@ -1981,7 +2016,7 @@ void delete_commit_work(CommitWork* w);  // after CommitWork's definition
 ExpandBuffers::~ExpandBuffers() {
   void* ps[] = {parents, cand_coord, cand_ok, cand, prep, status, slots, cand2, prep2, res, outp, ostatus, counts, alive,
                 pg_head, vp_head, d_item, d_next, pool_used, tcells, tvals, qtmp, crec, acc, dupd, cellinit, occ,
-                qkey, qrank, qrank2, qsort_tmp, xsd, xrd};
+                qkey, qrank, qrank2, qsort_tmp, xsd, xrd, cidx};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete_commit_work(cm);
@@ -2627,8 +2662,33 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
     } while (W > 1 && ndirs < min_cands && !q_empty());
     const int np = (int)parents.size();
     stats[0] += np;
-    FCHK(grow(X.cand, X.cap_cand, (size_t)np * 6));
-    FCHK(grow(X.prep, X.cap_prep, (size_t)np * 6));
+    // compact index of the free directions: the candidate / prepared-patch records are sized by
+    // them, not by 6 x parents (late waves pop most of the queue, few directions are free)
+    FCHK(grow(X.cidx, X.cap_cidx, (size_t)np * 6 + 1));
+    FCHK(hipMemsetAsync(X.cidx + (size_t)np * 6, 0, sizeof(int), st));
+    {
+      size_t tb = 0;
+      FCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, X.cand_ok, X.cidx, np * 6, st));
+      if (tb > X.cap_qsort) {
+        if (X.qsort_tmp) FCHK(hipFree(X.qsort_tmp));
+        X.qsort_tmp = nullptr;
+        X.cap_qsort = 0;
+        FCHK(hipMalloc(&X.qsort_tmp, tb));
+        X.cap_qsort = tb;
+      }
+      tb = X.cap_qsort;
+      FCHK(hipcub::DeviceScan::ExclusiveSum(X.qsort_tmp, tb, X.cand_ok, X.cidx, np * 6, st));
+    }
+    int nok = 0;
+    {
+      int last_ok = 0, last_idx = 0;
+      FCHK(hipMemcpyAsync(&last_ok, X.cand_ok + (size_t)np * 6 - 1, sizeof(int), hipMemcpyDeviceToHost, st));
+      FCHK(hipMemcpyAsync(&last_idx, X.cidx + (size_t)np * 6 - 1, sizeof(int), hipMemcpyDeviceToHost, st));
+      FCHK(hipStreamSynchronize(st));
+      nok = last_idx + (last_ok != 0);
+    }
+    FCHK(grow(X.cand, X.cap_cand, (size_t)std::max(nok, 1)));
+    FCHK(grow(X.prep, X.cap_prep, (size_t)std::max(nok, 1)));
     FCHK(grow(X.status, X.cap_status, (size_t)np * 6));
     // wave = 1 is the reference's schedule: the parent's directions are prepared, refined and
     // committed one after the other (expand.cpp:92-101); wider waves batch every candidate.
@@ -2645,7 +2705,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
     for (const int only : batches) {
       c.n = nmodel;
       hipLaunchKernelGGL(prepare_kernel, dim3(nblk((long long)np * 6)), dim3(256), 0, st, s, c.dev(), X.counts, X.parents,
-                         np, X.cand_coord, X.cand_ok, X.cand, X.prep, X.status, cthr, only);
+                         np, X.cand_coord, X.cand_ok, X.cand, X.prep, X.status, cthr, only, X.cidx);
       FCHK(hipPeekAtLastError());
       std::vector<int> status((size_t)np * 6);
       FCHK(hipMemcpyAsync(status.data(), X.status, (size_t)np * 6 * sizeof(int), hipMemcpyDeviceToHost, st));
@@ -2673,7 +2733,8 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
           FCHK(grow(X.outp, X.cap_outp, (size_t)m));
           FCHK(grow(X.ostatus, X.cap_ost, (size_t)m));
           FCHK(hipMemcpyAsync(X.slots, slots.data(), m * sizeof(int), hipMemcpyHostToDevice, st));
-          hipLaunchKernelGGL(gather_slots_kernel, dim3(nblk(m)), dim3(256), 0, st, X.slots, m, X.cand, X.prep, X.cand2, X.prep2);
+          hipLaunchKernelGGL(gather_slots_kernel, dim3(nblk(m)), dim3(256), 0, st, X.slots, m, X.cand, X.prep, X.cand2, X.prep2,
+                             X.cidx);
           if (mine > 0) {
             FCHK(refine(X.cand2 + lo, mine, X.res + lo));
             T.mark(4);

@@ -90,6 +90,8 @@ struct ExpandBuffers {
   size_t cap_qkey = 0, cap_qrank = 0, cap_qrank2 = 0, cap_qsort = 0;
   char *xsd = nullptr, *xrd = nullptr;  // device payload of the sharded exchange (send, all ranks)
   size_t cap_xsd = 0, cap_xrd = 0;
+  int* cidx = nullptr;  // wave slot -> compact index of its free direction (candidate / prep records)
+  size_t cap_cidx = 0;
   int *crec = nullptr, *acc = nullptr;  // commit records; committed record indexes
   int2* dupd = nullptr;         // (parent, failed-direction bits) of a wave
   unsigned char* tvals = nullptr;
