@@ -1586,9 +1586,15 @@ __global__ void lab_jump_kernel(int* lab, int na, int* changed) {
     atomicOr(changed, 1);
   }
 }
+// Most patches share a few labels (one big component per surface): the lanes holding the wave's
+// first label add it with one atomic, the others one each (no same-address atomic storm).
 __global__ void lab_count_kernel(const int* __restrict__ lab, int na, int* __restrict__ csize) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < na) atomicAdd(&csize[lab[i]], 1);
+  const int l = (i < na) ? lab[i] : -1;
+  const int l0 = __shfl(l, 0, 64);
+  const unsigned long long same = __ballot(i < na && l == l0);
+  if (i < na && l != l0) atomicAdd(&csize[l], 1);
+  if ((threadIdx.x & 63) == 0 && same) atomicAdd(&csize[l0], (int)__popcll(same));
 }
 __global__ void lab_flags_kernel(const int* __restrict__ lab, const int* __restrict__ csize, const int* __restrict__ order,
                                  int na, int threshold, int* __restrict__ flags) {
