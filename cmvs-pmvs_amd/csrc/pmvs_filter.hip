@@ -252,18 +252,33 @@ __global__ void unit0_kernel(DScene s, const pmvs_patch* __restrict__ P, int n, 
 }
 
 // CFilter::setDepthMapsThread (filter.cpp:689-725): one thread per (collected patch, target).
-__global__ void depth_map_kernel(DScene s, FilterDev F, unsigned long long* __restrict__ dpkey) {
+// The collected patches' coordinates in collect order (the depth-map pass reads them once per
+// target, coalesced, instead of re-reading 1.6 KB patch records).
+__global__ void coordc_kernel(const pmvs_patch* __restrict__ P, const int* __restrict__ order, int na,
+                              float4* __restrict__ coordc) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= na) return;
+  const float* c = P[order[i]].coord;
+  coordc[i] = make_float4(c[0], c[1], c[2], c[3]);
+}
+
+// setDepthMaps: one thread per (target, collected patch), target-major so that neighbouring
+// threads hold neighbouring patches (collect order is by image and cell) and their atomics hit
+// nearby cells of the same map.
+__global__ void depth_map_kernel(DScene s, FilterDev F, const float4* __restrict__ coordc,
+                                 unsigned long long* __restrict__ dpkey) {
   const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= (long long)F.nalive * F.tnum) return;
-  const int i = (int)(g / F.tnum), t = (int)(g - (long long)i * F.tnum);
-  const pmvs_patch& q = F.P[F.order[i]];
+  const int t = (int)(g / F.nalive), i = (int)(g - (long long)t * F.nalive);
+  const float4 c4 = coordc[i];
+  const float coord[4] = {c4.x, c4.y, c4.z, c4.w};
   const DView& v = s.views[t];
   float ic[3];
-  project(v, q.coord, s.level, ic);
+  project(v, coord, s.level, ic);
   const float fx = __fdiv_rn(ic[0], (float)s.csize), fy = __fdiv_rn(ic[1], (float)s.csize);
   const int xs[2] = {(int)floor((double)fx), (int)ceil((double)fx)};
   const int ys[2] = {(int)floor((double)fy), (int)ceil((double)fy)};
-  const unsigned long long key = ((unsigned long long)depth_bits(depth_of(v, q.coord)) << 32) | (unsigned)i;
+  const unsigned long long key = ((unsigned long long)depth_bits(depth_of(v, coord)) << 32) | (unsigned)i;
   const int gw = gwidth(s, t), gh = gheight(s, t);
   for (int j = 0; j < 2; ++j)
     for (int k = 0; k < 2; ++k) {
@@ -1449,7 +1464,7 @@ static hipError_t dalloc(T*& p, size_t n) {
 
 FilterBuffers::~FilterBuffers() {
   void* ps[] = {preg, vreg, tgoff, cnt, off, keys, keys2, cellcnt, pg_off, pg_items, vp_off, vp_items, dpkey,
-                order, rank, unit0, flags, safe, need, list, scratch, counters, temp, edge_off, edges, rbits};
+                order, rank, unit0, flags, safe, need, list, scratch, counters, temp, edge_off, edges, rbits, coordc};
   for (void* p : ps)
     if (p) (void)hipFree(p);
 }
@@ -1465,6 +1480,7 @@ hipError_t FilterBuffers::reserve(int n_, long long ncells_, int tnum_, int grid
   FCHK(dalloc(keys, std::max(ne, (size_t)cap_n))); FCHK(dalloc(keys2, std::max(ne, (size_t)cap_n)));
   FCHK(dalloc(cellcnt, cap_cells + 1)); FCHK(dalloc(pg_off, cap_cells + 1)); FCHK(dalloc(vp_off, cap_cells + 1));
   FCHK(dalloc(pg_items, ne)); FCHK(dalloc(vp_items, ne)); FCHK(dalloc(dpkey, cap_cells));
+  FCHK(dalloc(coordc, cap_n));
   FCHK(dalloc(order, cap_n)); FCHK(dalloc(rank, cap_n)); FCHK(dalloc(unit0, cap_n)); FCHK(dalloc(flags, cap_n));
   FCHK(dalloc(safe, cap_n)); FCHK(dalloc(need, cap_n)); FCHK(dalloc(list, cap_n));
   FCHK(dalloc(scratch, (size_t)cap_grid * NB_SCR)); FCHK(dalloc(counters, 8));
@@ -1627,7 +1643,9 @@ static hipError_t set_dm_vgrids(Ctx& c, int additive) {
   dbg(c.st, "  collect");
   FCHK(hipMemsetAsync(B.dpkey, 0xff, c.ncells * sizeof(unsigned long long), c.st));
   if (c.nalive > 0)
-    hipLaunchKernelGGL(depth_map_kernel, dim3(nblk((long long)c.nalive * c.s.tnum)), dim3(256), 0, c.st, c.s, c.dev(),
+    hipLaunchKernelGGL(coordc_kernel, dim3(nblk(c.nalive)), dim3(256), 0, c.st, c.P, B.order, c.nalive, B.coordc);
+  if (c.nalive > 0)
+    hipLaunchKernelGGL(depth_map_kernel, dim3(nblk((long long)c.nalive * c.s.tnum)), dim3(256), 0, c.st, c.s, c.dev(), B.coordc,
                        B.dpkey);
   dbg(c.st, "  depth");
   FCHK(hipMemsetAsync(B.vreg, 0, c.n * sizeof(unsigned long long), c.st));
@@ -2564,7 +2582,11 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   FCHK(collect(c));
   FCHK(hipMemsetAsync(B.dpkey, 0xff, ncells * sizeof(unsigned long long), st));
   if (c.nalive > 0 && !(flags & 1))  // after the seed phase the depth maps are still empty
-    hipLaunchKernelGGL(depth_map_kernel, dim3(nblk((long long)c.nalive * s.tnum)), dim3(256), 0, st, s, c.dev(), B.dpkey);
+  {
+    hipLaunchKernelGGL(coordc_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, dP, B.order, c.nalive, B.coordc);
+    hipLaunchKernelGGL(depth_map_kernel, dim3(nblk((long long)c.nalive * s.tnum)), dim3(256), 0, st, s, c.dev(), B.coordc,
+                       B.dpkey);
+  }
   FCHK(build_lists(c, 1));
   // ---- registrations committed by this run: per-cell chains (no per-wave rebuild of the CSR)
   FCHK(grow(X.pg_head, X.cap_pghead, (size_t)ncells));

@@ -56,6 +56,7 @@ struct FilterBuffers {
   void* temp = nullptr;
   size_t temp_bytes = 0, edges_cap = 0;
   unsigned* rbits = nullptr;  // sharded filterNeighbor: packed reject flags
+  float4* coordc = nullptr;   // collected patches' coordinates in collect order (depth maps)
   size_t cap_rbits = 0;
   int cap_n = 0, cap_grid = 0;
   long long cap_cells = 0;
