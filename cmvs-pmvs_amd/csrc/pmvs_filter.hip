@@ -422,14 +422,23 @@ __global__ void exact_patch_kernel(DScene s, FilterDev F, const unsigned long lo
   const unsigned long long sm = safe[p] & preg[p];
   int ni = 0;
   int imgs[PMVS_MAX_IMAGES], grd[PMVS_MAX_IMAGES][2];
-  for (int t = 0; t < s.tnum; ++t)
-    for (int k = 0; k < q.num_images; ++k)
-      if (q.images[k] == t && ((sm >> k) & 1ull)) {
-        imgs[ni] = t;
-        grd[ni][0] = q.grids[k][0];
-        grd[ni][1] = q.grids[k][1];
-        ni++;
-      }
+  // the kept target entries in ascending image order (the reference loops over the targets and
+  // looks each up in the list, filter.cpp:305-330): entry k goes to the number of kept target
+  // entries before it in (image, list position) order
+  const int n0 = q.num_images;
+  for (int k = 0; k < n0; ++k) {
+    const int t = q.images[k];
+    if (t >= s.tnum || !((sm >> k) & 1ull)) continue;
+    int pos = 0;
+    for (int k2 = 0; k2 < n0; ++k2) {
+      const int t2 = q.images[k2];
+      pos += (t2 < s.tnum && ((sm >> k2) & 1ull) && (t2 < t || (t2 == t && k2 < k)));  // ties in list order
+    }
+    imgs[pos] = t;
+    grd[pos][0] = q.grids[k][0];
+    grd[pos][1] = q.grids[k][1];
+    ni++;
+  }
   q.timages = ni;
   for (int k = 0; k < q.num_images; ++k)
     if (s.tnum <= q.images[k]) {
