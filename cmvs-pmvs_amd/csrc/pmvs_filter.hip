@@ -95,6 +95,9 @@ struct FilterDev {
   // nullptr in the filter pass.
   const int* pg_dhead; const int* vp_dhead;
   const int* d_item; const int* d_next;
+  // Filter pass only: the collected patches' coordinates in collect order (the dpkey payload),
+  // so depth tests read 16 B instead of a patch record; nullptr in the expansion.
+  const float4* coordc;
 };
 
 
@@ -141,12 +144,20 @@ __device__ int is_visible_q(const DScene& s, const FilterDev& F, const pmvs_patc
   if (s.depth == 0) return 1;
   const unsigned long long key = F.dpkey[F.tgoff[t] + (long long)iy * gwidth(s, t) + ix];
   if (key == ~0ull) return 1;
-  const int d = F.order[(int)(key & 0xffffffffull)];
+  const int rk = (int)(key & 0xffffffffull);
+  float pc[4];
+  if (F.coordc) {
+    const float4 c4 = F.coordc[rk];
+    pc[0] = c4.x; pc[1] = c4.y; pc[2] = c4.z; pc[3] = c4.w;
+  } else {
+    const float* c = F.P[F.order[rk]].coord;
+    for (int k = 0; k < 4; ++k) pc[k] = c[k];
+  }
   const DView& v = s.views[t];
   float ray[4] = {q.coord[0] - v.center[0], q.coord[1] - v.center[1], q.coord[2] - v.center[2], q.coord[3] - v.center[3]};
   unitize4(ray);
   float dd[4];
-  for (int k = 0; k < 4; ++k) dd[k] = q.coord[k] - F.P[d].coord[k];
+  for (int k = 0; k < 4; ++k) dd[k] = q.coord[k] - pc[k];
   const float diff = dot4(ray, dd);
   const double fd = 2.0 + (double)dot4(ray, q.normal);
   const float factor = (float)((fd < 2.0) ? fd : 2.0);  // std::min(2.0, .)
@@ -1518,6 +1529,7 @@ struct Ctx {
   hipStream_t st;
   int nalive = 0, npg = 0, nvp = 0;
   const int *pg_dhead = nullptr, *vp_dhead = nullptr, *d_item = nullptr, *d_next = nullptr;
+  const float4* coordc = nullptr;
   FilterDev dev() const {
     FilterDev F{};
     F.P = P; F.n = n; F.preg = B.preg; F.vreg = B.vreg; F.tgoff = B.tgoff; F.tnum = s.tnum;
@@ -1525,6 +1537,7 @@ struct Ctx {
     F.dpkey = B.dpkey; F.order = B.order; F.rank = B.rank; F.nalive = nalive; F.unit0 = B.unit0;
     F.ncells = ncells; F.npg = npg; F.nvp = nvp; F.err = B.counters + 6;
     F.pg_dhead = pg_dhead; F.vp_dhead = vp_dhead; F.d_item = d_item; F.d_next = d_next;
+    F.coordc = coordc;
     return F;
   }
 };
@@ -1692,6 +1705,7 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
   dbg(st, "reserve");
   FCHK(hipMemcpyAsync(B.tgoff, h_tgoff, (s.tnum + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
   Ctx c{s, B, dP, n, ncells, grid, st};
+  c.coordc = B.coordc;  // written with every depth map of this pass (set_dm_vgrids)
   for (int k = 0; k < 4; ++k) counts[k] = 0;
   *overflow = 0;
   hipLaunchKernelGGL(init_reg_kernel, dim3(nblk(n)), dim3(256), 0, st, s, dP, n, B.preg, B.vreg);
