@@ -101,6 +101,17 @@ struct FilterDev {
 };
 
 
+// filterNeighbor's deferred quadric fits (neighbor_kernel -> quad_lane_kernel): per job the rows'
+// fx, fy, fz (3n floats at 3 * offset) and the solver's n x 5 system plus Q^T b (6n doubles at
+// 6 * offset); offsets from a row counter, jobs {patch, offset, n}.  f == nullptr: no deferral.
+struct QuadJobs {
+  float* f;
+  double* rows;
+  int4* jobs;
+  unsigned long long* rows_used;
+  int* njobs;
+  unsigned long long cap_rows;
+};
 
 // --------------------------------------------------------------------------- small helpers
 __device__ __forceinline__ unsigned int depth_bits(float d) {
@@ -788,14 +799,27 @@ __device__ int sort_unique_lds(int* a, int n, int* cnt_slot) {
       }
       __syncthreads();
     }
-  if (lane == 0) {
-    int u = 0;
-    for (int i = 0; i < n; ++i)
-      if (u == 0 || a[i] != a[u - 1]) a[u++] = a[i];
-    *cnt_slot = u;
+  // unique, 64 per round: keep a[i] != a[i-1] (a[i-1] carried in a register across rounds, since
+  // the compaction may already have overwritten it), positions by a wave prefix count.  Writes
+  // land at or below the round's own reads, so one barrier between reads and writes suffices.
+  int u = 0, carry = 0;
+  for (int base = 0; base < n; base += 64) {
+    const int i = base + lane;
+    const int x = (i < n) ? a[i] : 0x7fffffff;
+    int prev = __shfl_up(x, 1);
+    if (lane == 0) prev = carry;
+    const bool keep = i < n && (i == 0 || x != prev);
+    const unsigned long long m = __ballot(keep);
+    const int before = __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+    carry = __shfl(x, 63);
+    __syncthreads();
+    if (keep) a[u + before] = x;
+    u += __popcll(m);
+    __syncthreads();
   }
+  if (lane == 0) *cnt_slot = u;
   __syncthreads();
-  return uni(*cnt_slot);
+  return uni(u);
 }
 
 // CFilter::filterNeighborThread (filter.cpp:358-385) + findNeighbors(..., 0, 4, 2, 1)
@@ -963,8 +987,10 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, c
 }
 
 // CFilter::filterQuad (filter.cpp:387-446) on the neighbours in L.nb[0..n); returns 1 = reject.
+// fout != nullptr: the rows' fx[n], fy[n], fz[n] go there and the fit is left to quad_lane_kernel
+// (returns -1).
 __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, double* M, double* r,
-                                const pmvs_patch& q, int n) {
+                                const pmvs_patch& q, int n, float* fout = nullptr) {
   const int lane = lane_id_w();
   n = uni(n);
   float xdir[4] = {0, 0, 0, 0}, ydir[4] = {0, 0, 0, 0};
@@ -976,9 +1002,9 @@ __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, d
   ydir[0] = z[1] * xdir[2] - z[2] * xdir[1];
   ydir[1] = z[2] * xdir[0] - z[0] * xdir[2];
   ydir[2] = z[0] * xdir[1] - z[1] * xdir[0];
-  float* gx = reinterpret_cast<float*>(r + NB_CAP);  // fx, fy, fz in the workgroup's global scratch
-  float* gy = gx + NB_CAP;
-  float* gz = gy + NB_CAP;
+  float* gx = fout ? fout : reinterpret_cast<float*>(r + NB_CAP);  // fx, fy, fz (workgroup's global scratch)
+  float* gy = gx + (fout ? n : NB_CAP);
+  float* gz = gy + (fout ? n : NB_CAP);
   for (int a = lane; a < n; a += 64) {  // the distances in parallel, their sum in order below
     float d[4];
     for (int k = 0; k < 4; ++k) d[k] = F.P[L.nb[a]].coord[k] - q.coord[k];
@@ -998,6 +1024,7 @@ __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, d
     const float fx = __fdiv_rn(dot4(d, xdir), h), fy = __fdiv_rn(dot4(d, ydir), h), fz = dot4(d, q.normal);
     gx[a] = fx; gy[a] = fy; gz[a] = fz;
   }
+  if (fout) return -1;
   // The lls rows: in LDS over the neighbour list and seq[] (free until the residuals) when they
   // fit -- the solver's many wave barriers then drain LDS traffic only -- else in global scratch.
   __syncthreads();
@@ -1022,19 +1049,24 @@ __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, d
 #else
   lls5_wave(L, M, r, n);
 #endif
-  for (int a = lane; a < n; a += 64) {  // the residuals in parallel (each lane its own rows)
+  // The residual terms |r_a| / u2 in parallel (each lane its own rows; every lane computes the same
+  // u2), into the lls rows' space (free now), then their float += double sum in the reference's order.
+  const int inum = imin(s.tau, q.num_images);
+  float u2 = 0.0f;
+  for (int k = 0; k < inum; ++k) u2 += get_unit(s, s.views[q.images[k]], q.coord);
+  u2 = __fdiv_rn(u2, (float)inum);
+  double* term = M;
+  for (int a = lane; a < n; a += 64) {
     const float fx = gx[a], fy = gy[a];
-    L.seq[a] = L.x[0] * (fx * fx) + L.x[1] * (fy * fy) + L.x[2] * (fx * fy) + L.x[3] * fx + L.x[4] * fy - gz[a];
+    const float ra = L.x[0] * (fx * fx) + L.x[1] * (fy * fy) + L.x[2] * (fx * fy) + L.x[3] * fx + L.x[4] * fy - gz[a];
+    term[a] = fabs((double)ra) / (double)u2;
   }
+  __threadfence_block();
   __syncthreads();
   if (lane == 0) {
-    const int inum = imin(s.tau, q.num_images);
-    float u2 = 0.0f;
-    for (int k = 0; k < inum; ++k) u2 += get_unit(s, s.views[q.images[k]], q.coord);
-    u2 = __fdiv_rn(u2, (float)inum);
     float residual = 0.0f;
     for (int a = 0; a < n; ++a)  // in the reference's order
-      residual = (float)((double)residual + fabs((double)L.seq[a]) / (double)u2);  // float += double
+      residual = (float)((double)residual + term[a]);  // float += double
     residual = __fdiv_rn(residual, (float)(n - 5));
     L.cnt = (residual < s.quad ? 0 : 1);
   }
@@ -1050,7 +1082,7 @@ __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, d
 __global__ __launch_bounds__(64) void neighbor_kernel(DScene s, FilterDev F, double* __restrict__ scratch,
                                                       int* __restrict__ reject, int* __restrict__ overflow,
                                                       int* __restrict__ queue, int* __restrict__ dbg_counts, int rank,
-                                                      int world) {
+                                                      int world, QuadJobs qj) {
   __shared__ NbLds L;
   const int lane = threadIdx.x;
   double* M = scratch + (size_t)blockIdx.x * NB_SCR;
@@ -1068,11 +1100,291 @@ __global__ __launch_bounds__(64) void neighbor_kernel(DScene s, FilterDev F, dou
       const int n = gather_neighbors(s, F, L, q, 4.0f, 2, 1);
       if (lane == 0 && L.overflow) atomicAdd(overflow, 1);
       if (lane == 0 && dbg_counts) dbg_counts[p] = L.overflow ? -n : n;
-      rej = (n < 6) ? 1 : filter_quad_wave(s, F, L, M, r, q, n);
+      if (n < 6) {
+        rej = 1;
+      } else {
+        // room for the rows in the deferred-fit buffers? (else the fit runs here, same result)
+        unsigned long long o = ~0ull;
+        if (lane == 0 && qj.f) o = atomicAdd(qj.rows_used, (unsigned long long)n);
+        const unsigned long long lo = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(o & 0xffffffffull));
+        const unsigned long long hi = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(o >> 32));
+        o = (hi << 32) | lo;
+        if (o + (unsigned long long)n <= qj.cap_rows) {
+          filter_quad_wave(s, F, L, M, r, q, n, qj.f + 3ull * o);
+          if (lane == 0) {
+            const int k = atomicAdd(qj.njobs, 1);
+            qj.jobs[k] = make_int4(p, (int)o, n, 0);
+          }
+        } else {
+          rej = filter_quad_wave(s, F, L, M, r, q, n);
+        }
+      }
     }
     if (lane == 0) reject[p] = rej;
     __syncthreads();
   }
+}
+
+// filterQuad's fit and residual test for the patches neighbor_kernel deferred, one lane per patch:
+// Cmylapack::lls as the oracle's lls5 (oracle/filter_oracle.h, Eigen JacobiSVD semantics) in its
+// sequential operation order -- which is also lls5_wave's (per-column sums in row order) -- so the
+// decision is the same as the in-wave fit's.  The n x 5 system (column-major) and Q^T b live in
+// the job's slice of qj.rows; the 5 x 5 Jacobi stage in registers / private memory.
+__device__ __forceinline__ double dmaxd2(double a, double b) { return (a < b) ? b : a; }  // std::max
+__global__ __launch_bounds__(256) void quad_lane_kernel(DScene s, FilterDev F, QuadJobs qj, int* __restrict__ reject) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= *qj.njobs) return;
+  constexpr int N = 5;
+  const double eps = 2.220446049250313e-16, dmin = 2.2250738585072014e-308;
+  const int4 jb = qj.jobs[k];
+  const int p = jb.x, n = jb.z;
+  const size_t o = (size_t)jb.y;
+  const float* gx = qj.f + 3 * o;
+  const float* gy = gx + n;
+  const float* gz = gy + n;
+  double* M = qj.rows + 6 * o;  // at(i, j) = M[j * n + i]
+  double* r = M + (size_t)5 * n;
+  double scale = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const float fx = gx[i], fy = gy[i];
+    const double a[5] = {(double)(fx * fx), (double)(fy * fy), (double)(fx * fy), (double)fx, (double)fy};
+    for (int j = 0; j < N; ++j) {
+      M[(size_t)j * n + i] = a[j];
+      scale = dmaxd2(scale, fabs(a[j]));
+    }
+    r[i] = (double)gz[i];
+  }
+  float x[N] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  if (isfinite(scale)) {
+    if (scale == 0.0) scale = 1.0;
+    for (size_t u = 0; u < (size_t)n * N; ++u) M[u] = M[u] / scale;
+    auto at = [&](int i, int j) -> double& { return M[(size_t)j * n + i]; };
+    // ---- column-pivoting Householder QR
+    int perm[N];
+    double nu[N], nd[N], tau[N];
+    for (int j = 0; j < N; ++j) {
+      perm[j] = j;
+      double sq = 0.0;
+      for (int i = 0; i < n; ++i) sq += at(i, j) * at(i, j);
+      nd[j] = nu[j] = sqrt(sq);
+    }
+    const double downdate = sqrt(eps);
+    for (int kk = 0; kk < N; ++kk) {
+      int big = kk;
+      for (int j = kk + 1; j < N; ++j)
+        if (nu[j] > nu[big]) big = j;
+      if (big != kk) {
+        for (int i = 0; i < n; ++i) { const double t = at(i, kk); at(i, kk) = at(i, big); at(i, big) = t; }
+        double t = nu[kk]; nu[kk] = nu[big]; nu[big] = t;
+        t = nd[kk]; nd[kk] = nd[big]; nd[big] = t;
+        const int pk = perm[kk]; perm[kk] = perm[big]; perm[big] = pk;
+      }
+      double tail = 0.0;
+      for (int i = kk + 1; i < n; ++i) tail += at(i, kk) * at(i, kk);
+      const double c0 = at(kk, kk);
+      double beta;
+      if (tail <= dmin) {
+        tau[kk] = 0.0;
+        beta = c0;
+        for (int i = kk + 1; i < n; ++i) at(i, kk) = 0.0;
+      } else {
+        beta = sqrt(c0 * c0 + tail);
+        if (c0 >= 0.0) beta = -beta;
+        const double den = c0 - beta;
+        for (int i = kk + 1; i < n; ++i) at(i, kk) = at(i, kk) / den;
+        tau[kk] = (beta - c0) / beta;
+      }
+      at(kk, kk) = beta;
+      if (tau[kk] != 0.0)
+        for (int j = kk + 1; j < N; ++j) {
+          double t = 0.0;
+          for (int i = kk + 1; i < n; ++i) t += at(i, kk) * at(i, j);
+          t += at(kk, j);
+          at(kk, j) -= tau[kk] * t;
+          for (int i = kk + 1; i < n; ++i) at(i, j) -= (tau[kk] * at(i, kk)) * t;
+        }
+      for (int j = kk + 1; j < N; ++j) {
+        if (nu[j] == 0.0) continue;
+        double t = fabs(at(kk, j)) / nu[j];
+        t = (1.0 + t) * (1.0 - t);
+        if (t < 0.0) t = 0.0;
+        const double qq = nu[j] / nd[j];
+        const double t2 = t * (qq * qq);
+        if (t2 <= downdate) {
+          double sq = 0.0;
+          for (int i = kk + 1; i < n; ++i) sq += at(i, j) * at(i, j);
+          nd[j] = nu[j] = sqrt(sq);
+        } else {
+          nu[j] *= sqrt(t);
+        }
+      }
+    }
+    for (int kk = 0; kk < N; ++kk) {  // Q^T b
+      if (tau[kk] == 0.0) continue;
+      double t = 0.0;
+      for (int i = kk + 1; i < n; ++i) t += at(i, kk) * r[i];
+      t += r[kk];
+      r[kk] -= tau[kk] * t;
+      for (int i = kk + 1; i < n; ++i) r[i] -= (tau[kk] * at(i, kk)) * t;
+    }
+    // ---- two-sided Jacobi on R
+    double W[N][N], U[N][N], V[N][N];
+    for (int i = 0; i < N; ++i)
+      for (int j = 0; j < N; ++j) {
+        W[i][j] = (j >= i) ? at(i, j) : 0.0;
+        U[i][j] = V[i][j] = (i == j) ? 1.0 : 0.0;
+      }
+    double maxd = 0.0;
+    for (int i = 0; i < N; ++i) maxd = dmaxd2(maxd, fabs(W[i][i]));
+    bool finished = false;
+    for (int sweep = 0; !finished && sweep < 100; ++sweep) {
+      finished = true;
+#pragma unroll
+      for (int pp = 1; pp < N; ++pp)
+#pragma unroll
+        for (int q = 0; q < pp; ++q) {
+          const double thr = dmaxd2(dmin, 2.0 * eps * maxd);
+          if (!(fabs(W[pp][q]) > thr || fabs(W[q][pp]) > thr)) continue;
+          finished = false;
+          double m00 = W[pp][pp], m01 = W[pp][q], m10 = W[q][pp], m11 = W[q][q];
+          const double t = m00 + m11, d = m10 - m01;
+          double c1 = 1.0, s1 = 0.0;
+          if (!(fabs(d) < dmin)) {
+            const double u = t / d;
+            const double tmp = sqrt(1.0 + u * u);
+            s1 = 1.0 / tmp;
+            c1 = u / tmp;
+          }
+          {
+            const double a0 = m00, a1 = m01, b0 = m10, b1 = m11;
+            m00 = c1 * a0 + s1 * b0; m01 = c1 * a1 + s1 * b1;
+            m10 = -s1 * a0 + c1 * b0; m11 = -s1 * a1 + c1 * b1;
+          }
+          double cr = 1.0, sr = 0.0;
+          const double deno = 2.0 * fabs(m01);
+          if (!(deno < dmin)) {
+            const double tau_ = (m00 - m11) / deno;
+            const double w = sqrt(tau_ * tau_ + 1.0);
+            const double tt = (tau_ > 0.0) ? 1.0 / (tau_ + w) : 1.0 / (tau_ - w);
+            const double sign_t = tt > 0.0 ? 1.0 : -1.0;
+            const double nn = 1.0 / sqrt(tt * tt + 1.0);
+            sr = -sign_t * (m01 / fabs(m01)) * fabs(tt) * nn;
+            cr = nn;
+          }
+          const double cl = c1 * cr - s1 * (-sr);
+          const double sl = c1 * (-sr) + s1 * cr;
+#pragma unroll
+          for (int j = 0; j < N; ++j) {  // W rows pp, q by j_left
+            const double xp = W[pp][j], xq = W[q][j];
+            W[pp][j] = cl * xp + sl * xq;
+            W[q][j] = -sl * xp + cl * xq;
+          }
+#pragma unroll
+          for (int i = 0; i < N; ++i) {  // U columns pp, q by j_left^T
+            const double xp = U[i][pp], xq = U[i][q];
+            U[i][pp] = cl * xp - (-sl) * xq;
+            U[i][q] = (-sl) * xp + cl * xq;
+          }
+#pragma unroll
+          for (int i = 0; i < N; ++i) {  // W columns pp, q by j_right
+            const double xp = W[i][pp], xq = W[i][q];
+            W[i][pp] = cr * xp - sr * xq;
+            W[i][q] = sr * xp + cr * xq;
+          }
+#pragma unroll
+          for (int i = 0; i < N; ++i) {  // V columns pp, q by j_right
+            const double xp = V[i][pp], xq = V[i][q];
+            V[i][pp] = cr * xp - sr * xq;
+            V[i][q] = sr * xp + cr * xq;
+          }
+          maxd = dmaxd2(maxd, dmaxd2(fabs(W[pp][pp]), fabs(W[q][q])));
+        }
+    }
+    // ---- singular values, signs, scale; sorted descending (selection, unrolled: register arrays)
+    double sv[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      sv[i] = fabs(W[i][i]);
+      if (W[i][i] < 0.0)
+#pragma unroll
+        for (int kk = 0; kk < N; ++kk) U[kk][i] = -U[kk][i];
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) sv[i] *= scale;
+    int nonzero = N;
+    bool stop = false;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      if (stop) continue;
+      int pos = i;
+#pragma unroll
+      for (int j = i + 1; j < N; ++j)
+        if (sv[j] > sv[pos]) pos = j;
+      double svp = sv[i];
+#pragma unroll
+      for (int j = i + 1; j < N; ++j)
+        if (pos == j) svp = sv[j];
+      if (svp == 0.0) {
+        nonzero = i;
+        stop = true;
+        continue;
+      }
+#pragma unroll
+      for (int j = i + 1; j < N; ++j)
+        if (pos == j) {
+          double t = sv[i]; sv[i] = sv[j]; sv[j] = t;
+#pragma unroll
+          for (int kk = 0; kk < N; ++kk) {
+            t = U[kk][i]; U[kk][i] = U[kk][j]; U[kk][j] = t;
+            t = V[kk][i]; V[kk][i] = V[kk][j]; V[kk][j] = t;
+          }
+        }
+    }
+    int rank = 0;
+    if (nonzero > 0) {
+      const double pre = dmaxd2(sv[0] * (N * eps), dmin);
+      int i = nonzero - 1;
+#pragma unroll
+      for (int c = N - 1; c >= 0; --c)
+        if (c == i && sv[c] < pre) --i;
+      rank = i + 1;
+    }
+    double y[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      y[i] = 0.0;
+      if (i < rank) {
+        double t = 0.0;
+#pragma unroll
+        for (int kk = 0; kk < N; ++kk) t += U[kk][i] * r[kk];
+        y[i] = t / sv[i];
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < N; ++kk) {
+      double t = 0.0;
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        if (i < rank) t += V[kk][i] * y[i];
+#pragma unroll
+      for (int c = 0; c < N; ++c)
+        if (perm[kk] == c) x[c] = (float)t;
+    }
+  }
+  // filterQuad's residual test (as filter_quad_wave's tail)
+  const pmvs_patch& q = F.P[p];
+  const int inum = imin(s.tau, q.num_images);
+  float u2 = 0.0f;
+  for (int i = 0; i < inum; ++i) u2 += get_unit(s, s.views[q.images[i]], q.coord);
+  u2 = __fdiv_rn(u2, (float)inum);
+  float residual = 0.0f;
+  for (int a = 0; a < n; ++a) {
+    const float fx = gx[a], fy = gy[a];
+    const float ra = x[0] * (fx * fx) + x[1] * (fy * fy) + x[2] * (fx * fy) + x[3] * fx + x[4] * fy - gz[a];
+    residual = (float)((double)residual + fabs((double)ra) / (double)u2);  // float += double
+  }
+  residual = __fdiv_rn(residual, (float)(n - 5));
+  reject[p] = (residual < s.quad ? 0 : 1);
 }
 
 // --------------------------------------------------------------------------- filterSmallGroups
@@ -1484,7 +1796,8 @@ static hipError_t dalloc(T*& p, size_t n) {
 
 FilterBuffers::~FilterBuffers() {
   void* ps[] = {preg, vreg, tgoff, cnt, off, keys, keys2, cellcnt, pg_off, pg_items, vp_off, vp_items, dpkey,
-                order, rank, unit0, flags, safe, need, list, scratch, counters, temp, edge_off, edges, rbits, coordc};
+                order, rank, unit0, flags, safe, need, list, scratch, counters, temp, edge_off, edges, rbits, coordc,
+                qf, qrows, qjobs, qctr};
   for (void* p : ps)
     if (p) (void)hipFree(p);
 }
@@ -1505,6 +1818,11 @@ hipError_t FilterBuffers::reserve(int n_, long long ncells_, int tnum_, int grid
   FCHK(dalloc(safe, cap_n)); FCHK(dalloc(need, cap_n)); FCHK(dalloc(list, cap_n));
   FCHK(dalloc(scratch, (size_t)cap_grid * NB_SCR)); FCHK(dalloc(counters, 8));
   FCHK(dalloc(edge_off, cap_n + 1));
+  // deferred filterQuad fits: up to 48 rows per patch on average, at most 2^27 rows (7.5 GB);
+  // patches past the capacity are fitted in neighbor_kernel itself
+  cap_qrows = std::min((size_t)cap_n * 48, (size_t)1 << 27);
+  FCHK(dalloc(qf, cap_qrows * 3)); FCHK(dalloc(qrows, cap_qrows * 6)); FCHK(dalloc(qjobs, cap_n));
+  FCHK(dalloc(qctr, 2));
   size_t t1 = 0, t2 = 0;
   FCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, t1, keys, keys2, (int)ne));
   FCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, cellcnt, pg_off, (int)(cap_cells + 1)));
@@ -1748,10 +2066,17 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
   if (inject && inj_where == 'f') return hipErrorOutOfMemory;
   FCHK(hipMemsetAsync(B.flags, 0, n * sizeof(int), st));
   FCHK(hipMemsetAsync(B.counters + 3, 0, 5 * sizeof(int), st));
-  if (c.nalive)
+  if (c.nalive) {
+    // PMVS_QUAD_ROWS caps the deferred-fit rows (tests: 0 = every fit in the wave, small = a mix)
+    QuadJobs qj{B.qf, B.qrows, B.qjobs, B.qctr, reinterpret_cast<int*>(B.qctr + 1), (unsigned long long)B.cap_qrows};
+    if (const char* e = getenv("PMVS_QUAD_ROWS")) qj.cap_rows = std::min(qj.cap_rows, (unsigned long long)atoll(e));
+    if (qj.cap_rows == 0) qj.f = nullptr;
+    FCHK(hipMemsetAsync(B.qctr, 0, 2 * sizeof(unsigned long long), st));
     hipLaunchKernelGGL(neighbor_kernel, dim3(std::min(grid * NB_GRID_MULT, c.nalive)), dim3(64), 0, st, s, c.dev(), B.scratch, B.flags,
                        B.counters + 3, B.counters + 4, getenv("PMVS_FILTER_DEBUG") ? B.need : nullptr, part ? sh->rank : 0,
-                       part ? sh->world : 1);
+                       part ? sh->world : 1, qj);
+    if (qj.f) hipLaunchKernelGGL(quad_lane_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, s, c.dev(), qj, B.flags);
+  }
   dbg(st, "neighbor kernel");
   if (getenv("PMVS_FILTER_DEBUG")) {
     std::vector<int> cnts(n), ord(c.nalive);

@@ -58,6 +58,12 @@ struct FilterBuffers {
   unsigned* rbits = nullptr;  // sharded filterNeighbor: packed reject flags
   float4* coordc = nullptr;   // collected patches' coordinates in collect order (depth maps)
   size_t cap_rbits = 0;
+  // filterNeighbor's deferred quadric fits (pmvs_filter.hip QuadJobs)
+  float* qf = nullptr;
+  double* qrows = nullptr;
+  int4* qjobs = nullptr;
+  unsigned long long* qctr = nullptr;  // [0] rows used, [1] low 32 bits: jobs
+  size_t cap_qrows = 0;
   int cap_n = 0, cap_grid = 0;
   long long cap_cells = 0;
   hipError_t reserve(int n, long long ncells, int tnum, int grid);

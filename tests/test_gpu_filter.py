@@ -85,3 +85,23 @@ def test_filter_depth0_and_empty(gpu_available, oracle_mod):
     assert len(keep) == 0 and st["kept"] == 0
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("cap", ["0", "20000"], ids=["all_in_wave", "mixed"])
+def test_filter_quad_deferral_paths(gpu_available, oracle_mod, monkeypatch, cap):
+    """filterNeighbor's quadric fits run either per lane after the neighbour walk
+    (quad_lane_kernel, the default) or inside the walk's wavefront when the deferred-row buffer is
+    full; PMVS_QUAD_ROWS caps that buffer so both paths (and a mix) meet the oracle."""
+    import pmvs_amd as P
+    monkeypatch.setenv("PMVS_QUAD_ROWS", cap)
+    inp, p = P.synth_scene(8, 960, 540, level=1, supersample=2, nthreads=16)
+    g = P.Scene(inp)
+    o = oracle_mod.OracleScene(inp)
+    pa = make_patch_set(P, g, inp, p, 30000, 11)
+    for sc in (g, o):
+        sc.set_thresholds(inp.threshold, inp.threshold - 0.3, 1)
+    out_g, keep_g, st_g = g.filter_run(pa)
+    out_o, keep_o, counts_o = o.filter_run(pa)
+    g.close()
+    o.close()
+    compare(out_g, keep_g, st_g, out_o, keep_o, counts_o)
