@@ -1128,37 +1128,51 @@ __global__ __launch_bounds__(64) void neighbor_kernel(DScene s, FilterDev F, dou
 // filterQuad's fit and residual test for the patches neighbor_kernel deferred, one lane per patch:
 // Cmylapack::lls as the oracle's lls5 (oracle/filter_oracle.h, Eigen JacobiSVD semantics) in its
 // sequential operation order -- which is also lls5_wave's (per-column sums in row order) -- so the
-// decision is the same as the in-wave fit's.  The n x 5 system (column-major) and Q^T b live in
-// the job's slice of qj.rows; the 5 x 5 Jacobi stage in registers / private memory.
+// decision is the same as the in-wave fit's.  Jobs run in descending row count (qsorted: 64-bit
+// keys (2047 - n) << 32 | job), so a wavefront's 64 lanes have similar loop trips and its chunk of
+// the row pool is 64 x (first lane's n) rows; element (row i, column j; j = 5 is Q^T b) of lane l
+// sits at pool[6 * qoff[chunk] + (6 i + j) * 64 + l], so every column walk is a coalesced 512-B
+// access.  The 5 x 5 Jacobi stage runs in registers.
 __device__ __forceinline__ double dmaxd2(double a, double b) { return (a < b) ? b : a; }  // std::max
-__global__ __launch_bounds__(256) void quad_lane_kernel(DScene s, FilterDev F, QuadJobs qj, int* __restrict__ reject) {
+__global__ void quad_chunk_rows_kernel(const unsigned long long* __restrict__ qsorted, int njobs, int* __restrict__ crows) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c * 64 < njobs) crows[c] = 64 * (2047 - (int)(qsorted[(size_t)c * 64] >> 32));
+}
+__global__ void quad_keys_kernel(const int4* __restrict__ jobs, int njobs, unsigned long long* __restrict__ keys) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= *qj.njobs) return;
+  if (k < njobs) keys[k] = ((unsigned long long)(2047 - jobs[k].z) << 32) | (unsigned)k;
+}
+__global__ __launch_bounds__(256) void quad_lane_kernel(DScene s, FilterDev F, QuadJobs qj, const unsigned long long* __restrict__ qsorted,
+                                                        const int* __restrict__ qoff, int njobs, int* __restrict__ reject) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= njobs) return;
   constexpr int N = 5;
   const double eps = 2.220446049250313e-16, dmin = 2.2250738585072014e-308;
-  const int4 jb = qj.jobs[k];
+  const int4 jb = qj.jobs[(int)(qsorted[k] & 0xffffffffull)];
   const int p = jb.x, n = jb.z;
   const size_t o = (size_t)jb.y;
   const float* gx = qj.f + 3 * o;
   const float* gy = gx + n;
   const float* gz = gy + n;
-  double* M = qj.rows + 6 * o;  // at(i, j) = M[j * n + i]
-  double* r = M + (size_t)5 * n;
+  double* base = qj.rows + 6 * (size_t)qoff[k >> 6] + (k & 63);
+  double* M = base;  // at(i, j) = M[(6 i + j) * 64]
   double scale = 0.0;
   for (int i = 0; i < n; ++i) {
     const float fx = gx[i], fy = gy[i];
     const double a[5] = {(double)(fx * fx), (double)(fy * fy), (double)(fx * fy), (double)fx, (double)fy};
     for (int j = 0; j < N; ++j) {
-      M[(size_t)j * n + i] = a[j];
+      M[(size_t)(6 * i + j) * 64] = a[j];
       scale = dmaxd2(scale, fabs(a[j]));
     }
-    r[i] = (double)gz[i];
+    M[(size_t)(6 * i + 5) * 64] = (double)gz[i];
   }
   float x[N] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
   if (isfinite(scale)) {
     if (scale == 0.0) scale = 1.0;
-    for (size_t u = 0; u < (size_t)n * N; ++u) M[u] = M[u] / scale;
-    auto at = [&](int i, int j) -> double& { return M[(size_t)j * n + i]; };
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < N; ++j) M[(size_t)(6 * i + j) * 64] = M[(size_t)(6 * i + j) * 64] / scale;
+    auto rr = [&](int i) -> double& { return M[(size_t)(6 * i + 5) * 64]; };
+    auto at = [&](int i, int j) -> double& { return M[(size_t)(6 * i + j) * 64]; };
     // ---- column-pivoting Householder QR
     int perm[N];
     double nu[N], nd[N], tau[N];
@@ -1222,10 +1236,10 @@ __global__ __launch_bounds__(256) void quad_lane_kernel(DScene s, FilterDev F, Q
     for (int kk = 0; kk < N; ++kk) {  // Q^T b
       if (tau[kk] == 0.0) continue;
       double t = 0.0;
-      for (int i = kk + 1; i < n; ++i) t += at(i, kk) * r[i];
-      t += r[kk];
-      r[kk] -= tau[kk] * t;
-      for (int i = kk + 1; i < n; ++i) r[i] -= (tau[kk] * at(i, kk)) * t;
+      for (int i = kk + 1; i < n; ++i) t += at(i, kk) * rr(i);
+      t += rr(kk);
+      rr(kk) -= tau[kk] * t;
+      for (int i = kk + 1; i < n; ++i) rr(i) -= (tau[kk] * at(i, kk)) * t;
     }
     // ---- two-sided Jacobi on R
     double W[N][N], U[N][N], V[N][N];
@@ -1356,7 +1370,7 @@ __global__ __launch_bounds__(256) void quad_lane_kernel(DScene s, FilterDev F, Q
       if (i < rank) {
         double t = 0.0;
 #pragma unroll
-        for (int kk = 0; kk < N; ++kk) t += U[kk][i] * r[kk];
+        for (int kk = 0; kk < N; ++kk) t += U[kk][i] * rr(kk);
         y[i] = t / sv[i];
       }
     }
@@ -1797,7 +1811,7 @@ static hipError_t dalloc(T*& p, size_t n) {
 FilterBuffers::~FilterBuffers() {
   void* ps[] = {preg, vreg, tgoff, cnt, off, keys, keys2, cellcnt, pg_off, pg_items, vp_off, vp_items, dpkey,
                 order, rank, unit0, flags, safe, need, list, scratch, counters, temp, edge_off, edges, rbits, coordc,
-                qf, qrows, qjobs, qctr};
+                qf, qrows, qjobs, qctr, qkeys, qkeys2, qcrows, qoff};
   for (void* p : ps)
     if (p) (void)hipFree(p);
 }
@@ -1820,15 +1834,20 @@ hipError_t FilterBuffers::reserve(int n_, long long ncells_, int tnum_, int grid
   FCHK(dalloc(edge_off, cap_n + 1));
   // deferred filterQuad fits: up to 48 rows per patch on average, at most 2^27 rows (7.5 GB);
   // patches past the capacity are fitted in neighbor_kernel itself
+  // quad_lane_kernel's row pool: jobs sorted by descending n, so the 64-lane chunks' rows
+  // (64 x their first n) sum to at most every job's n plus 64 x NB_CAP
   cap_qrows = std::min((size_t)cap_n * 48, (size_t)1 << 27);
-  FCHK(dalloc(qf, cap_qrows * 3)); FCHK(dalloc(qrows, cap_qrows * 6)); FCHK(dalloc(qjobs, cap_n));
-  FCHK(dalloc(qctr, 2));
+  FCHK(dalloc(qf, cap_qrows * 3)); FCHK(dalloc(qrows, (cap_qrows + 64 * (size_t)NB_CAP) * 6)); FCHK(dalloc(qjobs, cap_n));
+  FCHK(dalloc(qctr, 2)); FCHK(dalloc(qkeys, cap_n)); FCHK(dalloc(qkeys2, cap_n));
+  FCHK(dalloc(qcrows, cap_n / 64 + 2)); FCHK(dalloc(qoff, cap_n / 64 + 2));
   size_t t1 = 0, t2 = 0;
   FCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, t1, keys, keys2, (int)ne));
   FCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, cellcnt, pg_off, (int)(cap_cells + 1)));
   size_t t3 = 0;
   FCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t3, cnt, off, cap_n + 1));
-  temp_bytes = std::max(t1, std::max(t2, t3));
+  size_t t4 = 0;
+  FCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, t4, qkeys, qkeys2, cap_n, 0, 43));
+  temp_bytes = std::max(std::max(t1, t4), std::max(t2, t3));
   if (temp) (void)hipFree(temp);
   temp = nullptr;
   FCHK(hipMalloc(&temp, temp_bytes ? temp_bytes : 1));
@@ -2075,7 +2094,21 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
     hipLaunchKernelGGL(neighbor_kernel, dim3(std::min(grid * NB_GRID_MULT, c.nalive)), dim3(64), 0, st, s, c.dev(), B.scratch, B.flags,
                        B.counters + 3, B.counters + 4, getenv("PMVS_FILTER_DEBUG") ? B.need : nullptr, part ? sh->rank : 0,
                        part ? sh->world : 1, qj);
-    if (qj.f) hipLaunchKernelGGL(quad_lane_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, s, c.dev(), qj, B.flags);
+    if (qj.f) {
+      int nj = 0;
+      FCHK(read_int(qj.njobs, &nj, st));
+      if (nj > 0) {
+        const int nch = (nj + 63) / 64;
+        hipLaunchKernelGGL(quad_keys_kernel, dim3(nblk(nj)), dim3(256), 0, st, B.qjobs, nj, B.qkeys);
+        size_t tb = B.temp_bytes;
+        FCHK(hipcub::DeviceRadixSort::SortKeys(B.temp, tb, B.qkeys, B.qkeys2, nj, 0, 43, st));
+        hipLaunchKernelGGL(quad_chunk_rows_kernel, dim3(nblk(nch)), dim3(256), 0, st, B.qkeys2, nj, B.qcrows);
+        tb = B.temp_bytes;
+        FCHK(hipcub::DeviceScan::ExclusiveSum(B.temp, tb, B.qcrows, B.qoff, nch, st));
+        hipLaunchKernelGGL(quad_lane_kernel, dim3(nblk(nj)), dim3(256), 0, st, s, c.dev(), qj, B.qkeys2, B.qoff, nj,
+                           B.flags);
+      }
+    }
   }
   dbg(st, "neighbor kernel");
   if (getenv("PMVS_FILTER_DEBUG")) {

@@ -63,6 +63,8 @@ struct FilterBuffers {
   double* qrows = nullptr;
   int4* qjobs = nullptr;
   unsigned long long* qctr = nullptr;  // [0] rows used, [1] low 32 bits: jobs
+  unsigned long long *qkeys = nullptr, *qkeys2 = nullptr;  // jobs by descending row count
+  int *qcrows = nullptr, *qoff = nullptr;                  // per 64-job chunk: pool rows, offsets
   size_t cap_qrows = 0;
   int cap_n = 0, cap_grid = 0;
   long long cap_cells = 0;
