@@ -1142,10 +1142,19 @@ __global__ void quad_keys_kernel(const int4* __restrict__ jobs, int njobs, unsig
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < njobs) keys[k] = ((unsigned long long)(2047 - jobs[k].z) << 32) | (unsigned)k;
 }
+__device__ inline void quad_lane_job(const DScene& s, const FilterDev& F, const QuadJobs& qj,
+                                     const unsigned long long* __restrict__ qsorted, const int* __restrict__ qoff, int k,
+                                     int* __restrict__ reject);
 __global__ __launch_bounds__(256) void quad_lane_kernel(DScene s, FilterDev F, QuadJobs qj, const unsigned long long* __restrict__ qsorted,
                                                         const int* __restrict__ qoff, int njobs, int* __restrict__ reject) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= njobs) return;
+  // grid-stride over the jobs: a capped grid (PMVS_QUAD_WAVES_PER_CU) bounds the row working set
+  // of the resident wavefronts
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < njobs; k += gridDim.x * blockDim.x)
+    quad_lane_job(s, F, qj, qsorted, qoff, k, reject);
+}
+__device__ inline void quad_lane_job(const DScene& s, const FilterDev& F, const QuadJobs& qj,
+                                                                   const unsigned long long* __restrict__ qsorted,
+                                                                   const int* __restrict__ qoff, int k, int* __restrict__ reject) {
   constexpr int N = 5;
   const double eps = 2.220446049250313e-16, dmin = 2.2250738585072014e-308;
   const int4 jb = qj.jobs[(int)(qsorted[k] & 0xffffffffull)];
@@ -2105,7 +2114,10 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
         hipLaunchKernelGGL(quad_chunk_rows_kernel, dim3(nblk(nch)), dim3(256), 0, st, B.qkeys2, nj, B.qcrows);
         tb = B.temp_bytes;
         FCHK(hipcub::DeviceScan::ExclusiveSum(B.temp, tb, B.qcrows, B.qoff, nch, st));
-        hipLaunchKernelGGL(quad_lane_kernel, dim3(nblk(nj)), dim3(256), 0, st, s, c.dev(), qj, B.qkeys2, B.qoff, nj,
+        unsigned qgrid = nblk(nj);
+        if (const char* e = getenv("PMVS_QUAD_WAVES_PER_CU"))  // 0 = one lane per job, no cap
+          if (atoi(e) > 0) qgrid = std::min(qgrid, (unsigned)std::max(1, grid / 8 * atoi(e) / 4));
+        hipLaunchKernelGGL(quad_lane_kernel, dim3(qgrid), dim3(256), 0, st, s, c.dev(), qj, B.qkeys2, B.qoff, nj,
                            B.flags);
       }
     }
