@@ -51,6 +51,14 @@ _RCFG = int(os.environ.get("PMVS_REFINE_CONFIG", "1206"))  # texture slots * 100
 REFINE_KERNEL = f"refine_v2_kernel<7,{_RCFG // 100},{_RCFG % 100}>"
 
 
+_T0 = time.time()
+
+
+def log(msg):
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    print(f"[bench {time.time() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -61,7 +69,10 @@ def parse():
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--level", type=int, default=0)
-    ap.add_argument("--seeds", type=int, default=5000)
+    ap.add_argument("--seed-mode", choices=("features", "synthetic"), default="features",
+                    help="features: the seed phase on the device (Harris/DoG + CSeed::run, findMatch.cpp:187-193); "
+                         "synthetic: refine --seeds synthetic seed-path candidates")
+    ap.add_argument("--seeds", type=int, default=5000, help="synthetic seed candidates (--seed-mode synthetic)")
     ap.add_argument("--wave", type=int, default=32768)
     ap.add_argument("--min-candidates", type=int, default=131072)
     ap.add_argument("--iterations", type=int, default=3)
@@ -69,7 +80,9 @@ def parse():
     ap.add_argument("--no-c2", action="store_true", help="skip the configs[1] refine-kernel side measurement")
     ap.add_argument("--only-c2", action="store_true", help="only the configs[1] refine-kernel measurement (profiling)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="refine-only CPU sample time budget")
-    ap.add_argument("--cpu-waves", type=int, default=2, help="expansion waves in the CPU loop sample")
+    ap.add_argument("--cpu-waves", type=int, default=2, help="expansion waves per iteration in the CPU loop sample")
+    ap.add_argument("--cpu-iterations", type=int, default=3,
+                    help="loop iterations sampled by the CPU baseline / full-size parity check (1..iterations)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -118,23 +131,90 @@ def host_cpus():
     return {"usable": usable, "logical": logical, "affinity": affinity, "cgroup_quota_cpus": quota, "model": model}
 
 
-def cpu_loop_baseline(P, inp, sp, seeds, args):
-    """Loop-level CPU baseline (see the module docstring): refined patches committed per second by
-    the oracle's threaded expansion on the C3 scene, first --cpu-waves waves of iteration 1."""
+PATCH_SCALARS = ("coord", "normal", "ncc", "dscale", "ascale", "tmp", "timages", "flag", "fix", "num_images",
+                 "num_vimages", "dflag")
+
+
+def patch_mismatches(a, b):
+    """Records of two pmvs_patch arrays that differ in any defined field (floats bit for bit, the
+    image / vimage lists up to their counts); -1 when the lengths differ."""
+    if len(a) != len(b):
+        return -1
+    bad = np.zeros(len(a), bool)
+    for f in PATCH_SCALARS:
+        x, y = np.ascontiguousarray(a[f]), np.ascontiguousarray(b[f])
+        if x.dtype.kind == "f":
+            x, y = x.view(np.uint32), y.view(np.uint32)
+        d = x != y
+        bad |= d.reshape(len(a), -1).any(axis=1)
+    for lst, grd, cnt in (("images", "grids", "num_images"), ("vimages", "vgrids", "num_vimages")):
+        k = np.arange(a[lst].shape[1])[None, :]
+        m = k < b[cnt][:, None]
+        bad |= ((a[lst] != b[lst]) & m).any(axis=1)
+        bad |= ((a[grd] != b[grd]).any(axis=2) & m).any(axis=1)
+    return int(bad.sum())
+
+
+def iteration_thresholds(threshold, t):
+    """(ncc, before, depth, count_threshold) of loop iteration t (0-based) as pmvs_run_loop / CFindMatch
+    set them: before = threshold - 0.3f, both -= 0.05f per iteration, depth 1.., _countThreshold1 4 -> 2
+    (findMatch.cpp:23-28, 104) -- float arithmetic."""
+    ncc = np.float32(threshold)
+    before = np.float32(ncc - np.float32(0.3))
+    for _ in range(t):
+        ncc = np.float32(ncc - np.float32(0.05))
+        before = np.float32(before - np.float32(0.05))
+    return float(ncc), float(before), t + 1, 4 if t == 0 else 2
+
+
+def loop_samples(P, scene, inp, seeds, args):
+    """Full-size parity and the loop-level CPU baseline on the rank-0 C3 scene.
+
+    For each sampled loop iteration t the model at the start of t (the seeds, or the device loop's
+    model after t iterations) is expanded for --cpu-waves waves with the production schedule, once on
+    the device (pmvs_expand_run with PMVS_EXPAND_MAX_WAVES) and once by the CPU oracle (the same wave
+    schedule; findEmptyBlocks, preparation and refinement on a std::thread pool over every CPU this
+    process may use, commit serial).  parity: the two results record for record.  cpu_baseline:
+    patches the oracle committed per second of its waves, over all sampled iterations."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
     cpus = host_cpus()
     threads = args.cpu_threads or cpus["usable"]
     o = O.OracleScene(inp)
-    ncc = np.float32(inp.threshold)
-    o.set_thresholds(float(ncc), float(np.float32(ncc - np.float32(0.3))), 1)
-    _, _, st = o.expand_run(seeds, wave=args.wave, count_threshold=4, cap=max(1 << 20, 64 * len(seeds)),
-                            after_seeds=True, min_candidates=args.min_candidates, nthreads=threads,
-                            max_waves=args.cpu_waves)
-    loop_s = o.last_wave_s
+    parity, per_iter = [], []
+    added = 0
+    wave_s = 0.0
+    for t in range(max(1, min(args.cpu_iterations, args.iterations))):
+        log(f"parity / CPU sample: iteration {t + 1}")
+        if t == 0:
+            model = seeds
+        else:
+            model, _ = scene.run_loop(seeds, inp.threshold, iterations=t, wave=args.wave,
+                                      min_candidates=args.min_candidates)
+        ncc, before, depth, cthr = iteration_thresholds(inp.threshold, t)
+        kw = dict(wave=args.wave, count_threshold=cthr, after_seeds=(t == 0), min_candidates=args.min_candidates)
+        cap = len(model) + 16 * args.wave * args.cpu_waves + max(args.min_candidates, 1024) * args.cpu_waves * 6
+        scene.set_thresholds(ncc, before, depth)
+        g_out, g_alive, g_st = scene.expand_run(model, cap=cap, max_waves=args.cpu_waves, **kw)
+        o.set_thresholds(ncc, before, depth)
+        o_out, o_alive, o_st = o.expand_run(model, cap=cap, nthreads=threads, max_waves=args.cpu_waves, **kw)
+        mism = patch_mismatches(g_out, o_out)
+        same_stats = all(g_st[k] == o_st[k] for k in o_st)
+        ok = mism == 0 and same_stats and bool(np.array_equal(g_alive, o_alive))
+        parity.append({"iteration": t + 1, "model_in": int(len(model)), "waves": int(o_st["waves"]),
+                       "candidates": int(o_st["candidates"]), "added": int(o_st["added"]),
+                       "records": int(len(o_out)), "mismatched_records": mism, "stats_equal": same_stats, "ok": ok})
+        per_iter.append({"iteration": t + 1, "added": int(o_st["added"]), "wave_s": round(o.last_wave_s, 3),
+                         "value": round(o_st["added"] / max(o.last_wave_s, 1e-9), 1)})
+        added += o_st["added"]
+        wave_s += o.last_wave_s
+        del g_out, o_out, model
+    scene.set_thresholds(*iteration_thresholds(inp.threshold, 0)[:2], 0)
     # refine-only side figure: preProcess -> refinePatch -> postProcess on seed-path candidates
+    sp = P.synth_params(len(inp.images), inp.images[0].shape[1], inp.images[0].shape[0], level=inp.level)
     sample = P.synth_candidates(sp, inp.projections, 400000, seed=0xC0FFEE)
     done = acc = 0
+    o.set_thresholds(*iteration_thresholds(inp.threshold, 0)[:2], 0)
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < args.cpu_seconds and done < len(sample):
         r, rs = o.refine_batch(sample[done:done + 2000], nthreads=threads)
@@ -142,15 +222,21 @@ def cpu_loop_baseline(P, inp, sp, seeds, args):
         acc += rs["accepted"]
     tr = time.perf_counter() - t0
     o.close()
-    return {"value": round(float(st["added"]) / loop_s, 1), "unit": "refined patches/s", "cores": threads,
-            "kind": "port",
-            "sample": f"first {st['waves']} expansion waves (wave {args.wave}, min_candidates {args.min_candidates}) "
-                      f"of iteration 1 on the rank-0 C3 scene from its {len(seeds)} seeds: {st['parents']} parents, "
-                      f"{st['candidates']} candidates, {st['added']} patches committed in {loop_s:.2f} s; "
-                      f"oracle/liboracle.so (CPU restatement), {threads} threads",
-            "host": cpus,
-            "refine_only": {"value": round(acc / tr, 1), "unit": "refined patches/s",
-                            "sample": f"{done} seed-path candidates, preProcess->refinePatch->postProcess, {tr:.1f} s"}}
+    first = per_iter[0]
+    cpu = {"value": round(added / max(wave_s, 1e-9), 1), "unit": "refined patches/s", "cores": threads, "kind": "port",
+           "sample": f"first {args.cpu_waves} expansion waves (wave {args.wave}, min_candidates {args.min_candidates}) "
+                     f"of each of loop iterations 1..{len(per_iter)} on the rank-0 C3 scene (iteration t starts from "
+                     f"the device loop's model after t-1 iterations; the same waves run on the device and match record "
+                     f"for record, parity_c3_first_waves): {added} patches committed in {wave_s:.2f} s; "
+                     f"oracle/liboracle.so (CPU restatement), {threads} threads",
+           "per_iteration": per_iter,
+           "first_waves_iteration1": {"value": first["value"], "unit": "refined patches/s",
+                                      "sample": f"first {args.cpu_waves} waves of iteration 1 only: {first['added']} "
+                                                f"patches in {first['wave_s']} s"},
+           "host": cpus,
+           "refine_only": {"value": round(acc / tr, 1), "unit": "refined patches/s",
+                           "sample": f"{done} seed-path candidates, preProcess->refinePatch->postProcess, {tr:.1f} s"}}
+    return cpu, parity
 
 
 def model_checks(model, inp, hashes):
@@ -265,12 +351,30 @@ def main():
     inp, sp = P.synth_scene(args.views, args.width, args.height, level=args.level, supersample=2, nthreads=16,
                             seed=tex_seed)
     t_synth = time.time() - t0
+    log(f"scene rendered ({args.views} x {args.width}x{args.height}) in {t_synth:.1f} s")
     t0 = time.time()
     scene = P.Scene(inp, device=local)
-    cands = P.synth_candidates(sp, inp.projections, args.seeds, seed=rank_seed(0 if shard else rank))
-    res, _ = scene.refine_batch(cands)
-    seeds = P.patches_from_refined(res)
     t_scene = time.time() - t0
+    t0 = time.time()
+    seed_info = {"mode": args.seed_mode}
+    if args.seed_mode == "features":
+        # CFindMatch::init's feature detection (findMatch.cpp:79-82, fcsize 16) and the seed phase
+        # CSeed::run (findMatch.cpp:193) on the device
+        points = [scene.detect_features(v) for v in range(args.views)]
+        t_feat = time.time() - t0
+        log(f"features: {sum(len(p) for p in points)} points in {t_feat:.1f} s; seed phase ...")
+        seeds, sst = scene.seed_run(points)
+        seed_info.update(points=int(sum(len(p) for p in points)), seed_patches=int(len(seeds)),
+                         features_s=round(t_feat, 2), seed_s=round(time.time() - t0 - t_feat, 2),
+                         trial=sst["trial"], passed=sst["pass"], candidates=sst["candidates"], refined=sst["refined"])
+        del points
+    else:
+        cands = P.synth_candidates(sp, inp.projections, args.seeds, seed=rank_seed(0 if shard else rank))
+        res, _ = scene.refine_batch(cands)
+        seeds = P.patches_from_refined(res)
+        seed_info.update(candidates=args.seeds, seed_patches=int(len(seeds)))
+    t_seed = time.time() - t0
+    log(f"{len(seeds)} seed patches ({args.seed_mode}) in {t_seed:.1f} s")
     ex = None
     if shard:  # native RCCL communicator (C++), records all-gathered device to device
         uid = [P.RcclExchange.unique_id() if rank == 0 else None]
@@ -284,8 +388,9 @@ def main():
 
     import hashlib
     hashes = []
-    for _ in range(args.warmup):
+    for w in range(args.warmup):
         model, _ = step()
+        log(f"warmup step {w + 1}/{args.warmup}: {len(model)} patches")
         hashes.append(hashlib.sha1(model.view(np.uint8)).hexdigest())
         del model
     if dist:
@@ -294,9 +399,10 @@ def main():
     t0 = time.perf_counter()
     logs = []
     last = None
-    for _ in range(args.steps):
-        last, log = step()
-        logs.append((len(last), log))
+    for k in range(args.steps):
+        last, it_log = step()
+        logs.append((len(last), it_log))
+        log(f"timed step {k + 1}/{args.steps}: {len(last)} patches")
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -304,12 +410,12 @@ def main():
     hashes.append(hashlib.sha1(last.view(np.uint8)).hexdigest())  # after the timed region
 
     def tot(key):
-        return sum(it["expand"][key] for _, log in logs for it in log)
+        return sum(it["expand"][key] for _, lg in logs for it in lg)
     added = tot("added")
     own_added = added if (not shard or rank == 0) else 0  # shard mode: one shared model
     refined, evals, tex_valid, refine_ms = tot("refined"), tot("evals"), tot("tex_valid"), tot("refine_ms")
     expand_s = tot("wall_ms") / 1e3
-    filter_s = sum(it["filter"]["kernel_ms"] for _, log in logs for it in log) / 1e3
+    filter_s = sum(it["filter"]["kernel_ms"] for _, lg in logs for it in lg) / 1e3
     (added_all, refined_all, evals_all), elapsed_max = reduce_over_ranks(dist, [own_added, refined, evals], elapsed,
                                                                          dev)
     launches = tot("refine_launches")
@@ -323,9 +429,9 @@ def main():
     if rank == 0:
         checks = model_checks(last, inp, hashes)
         del last
-        cpu = None
-        if not args.no_cpu_baseline:
-            cpu = cpu_loop_baseline(P, inp, sp, seeds, args)
+        cpu = parity = None
+        if not args.no_cpu_baseline and not shard:
+            cpu, parity = loop_samples(P, scene, inp, seeds, args)
         first = logs[0][1]
         result = {
             "metric": METRIC,
@@ -339,15 +445,17 @@ def main():
             "scaling": "strong" if shard else "weak",
             "vs_baseline": None,
             "dtype": "f32 (f64 optimizer)",
-            "data": "synthetic (textured-sphere ring rendered by pmvs_synth_ring; seed model from refined "
-                    "synthetic seed candidates)",
+            "data": "synthetic (textured-sphere ring rendered by pmvs_synth_ring; seed model from "
+                    + ("Harris/DoG features + the seed phase on the device)" if args.seed_mode == "features" else
+                       "refined synthetic seed candidates)"),
             "config": {
                 "workload": f"C3: {args.views}-view {args.width}x{args.height} synthetic ring, level {args.level}, "
-                            f"full expand->optim->filter loop ({args.iterations} iterations) from {args.seeds} "
-                            f"seed candidates" + (", one scene sharded over all GPUs" if shard else
-                                                  ", one cluster per GPU"),
+                            f"full expand->optim->filter loop ({args.iterations} iterations) from "
+                            + (f"the device seed phase's {len(seeds)} seed patches" if args.seed_mode == "features" else
+                               f"{args.seeds} synthetic seed candidates")
+                            + (", one scene sharded over all GPUs" if shard else ", one cluster per GPU"),
                 "views": args.views, "width": args.width, "height": args.height, "level": args.level,
-                "seed_candidates": args.seeds, "seed_patches": int(len(seeds)), "wave": args.wave,
+                "seed_mode": args.seed_mode, "seed_patches": int(len(seeds)), "wave": args.wave,
                 "min_candidates": args.min_candidates, "iterations": args.iterations, "wsize": 7, "csize": 2,
                 "minImageNum": 3, "threshold": 0.7,
                 "parallelism": f"{'wave-sharded' if shard else 'cluster-per-GPU'} x{world}",
@@ -364,12 +472,19 @@ def main():
                             "filter_ms": round(it["filter"]["kernel_ms"], 1)} for it in first],
             "refine_c2": c2,
             "cpu_baseline": cpu,
+            "parity_c3_first_waves": None if parity is None else all(p["ok"] for p in parity),
+            "parity_c3_detail": parity,
             "checks": checks,
-            "setup_s": {"synth": round(t_synth, 2), "scene_and_seeds": round(t_scene, 2)},
+            "seed_phase": seed_info,
+            "setup_s": {"synth": round(t_synth, 2), "scene": round(t_scene, 2), "seed": round(t_seed, 2)},
         }
         print(json.dumps(result), flush=True)
         if not checks["ok"]:
             print(f"bench.py: C3 model checks failed: {checks}", file=sys.stderr, flush=True)
+        if parity is not None and not result["parity_c3_first_waves"]:
+            print(f"bench.py: full-size parity against the oracle FAILED: {parity}", file=sys.stderr, flush=True)
+            scene.close()
+            sys.exit(3)
     scene.close()
     if dist:
         dist.barrier()

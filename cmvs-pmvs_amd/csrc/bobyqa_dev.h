@@ -25,7 +25,11 @@
 // immediate offsets, and a register peak of the routine itself rather than of the whole inlined
 // kernel (the inlined optimizer hoisted state into ~470 VGPR+AGPR and capped the refine kernel at
 // one wavefront per SIMD).  Host builds (tests/csrc/bq_host.cpp) see plain pointers.
-#if defined(__HIP_DEVICE_COMPILE__)
+// -DBQ_PRIVATE (experiment builds): the state lives in per-lane private memory (scratch) instead,
+// so a wavefront can hold 64 chains.
+#if defined(__HIP_DEVICE_COMPILE__) && defined(BQ_PRIVATE)
+#define BQ_AS __attribute__((address_space(5)))
+#elif defined(__HIP_DEVICE_COMPILE__)
 #define BQ_AS __attribute__((address_space(3)))
 #else
 #define BQ_AS

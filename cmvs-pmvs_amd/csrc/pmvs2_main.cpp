@@ -15,6 +15,7 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <climits>
 #include <cmath>
@@ -23,6 +24,7 @@
 #include <cstring>
 #include <iostream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/pmvs_amd.h"
@@ -120,43 +122,76 @@ int main(int argc, char* argv[]) {
     return 1;
   }
 
-  // ---- CPhotoSetS::init (photoSetS.cpp:12-80): 8-digit names, else 4-digit
+  // ---- CPhotoSetS::init (photoSetS.cpp:12-80): 8-digit names, else 4-digit.  The reference decodes
+  // the views one after the other; here a pool of host threads decodes them (PMVS_IO_THREADS, default
+  // min(16, cores)), and failures are reported in view order as the serial loop would.
   std::vector<View> views(num);
+  std::vector<std::string> errors(num);
+  std::vector<pmvs_status> status(num, PMVS_OK);
   std::cerr << "Reading images: " << std::flush;
-  for (int index = 0; index < num; ++index) {
-    const int image = images[index];
-    char b8[64], b4[64];
-    std::snprintf(b8, sizeof(b8), "%08d", image);
-    std::snprintf(b4, sizeof(b4), "%04d", image);
-    const std::string v8 = prefix + "visualize/" + b8;
-    const std::string id = (exists(v8 + ".ppm") || exists(v8 + ".jpg")) ? b8 : b4;
-    View& v = views[index];
-    const std::string name = complete_name(prefix + "visualize/" + id, true);
-    CHECK("image", pmvs_image_load(name.c_str(), &v.w, &v.h, nullptr));
-    v.rgb.resize((size_t)v.w * v.h * 3);
-    CHECK("image", pmvs_image_load(name.c_str(), &v.w, &v.h, v.rgb.data()));
-    CHECK("camera", pmvs_camera_load((prefix + "txt/" + id + ".txt").c_str(), v.proj));
-    for (int k = 0; k < 2; ++k) {
-      const std::string m = complete_name(prefix + (k == 0 ? "masks/" : "edges/") + id, false);
-      if (m.size() < 4 || (m.compare(m.size() - 4, 4, ".pgm") && m.compare(m.size() - 4, 4, ".pbm"))) continue;
-      int mw = 0, mh = 0;
-      std::vector<uint8_t>& dst = k == 0 ? v.mask : v.edge;
-      CHECK("mask/edge", pmvs_pnm_mask_load(m.c_str(), &mw, &mh, nullptr));
-      if (mw != v.w || mh != v.h) {
-        std::cerr << "pmvs2: " << m << " is " << mw << "x" << mh << ", image " << v.w << "x" << v.h << std::endl;
-        return 1;
+  {
+    std::atomic<int> next{0};
+    auto load_one = [&](int index) -> pmvs_status {
+      const int image = images[index];
+      char b8[64], b4[64];
+      std::snprintf(b8, sizeof(b8), "%08d", image);
+      std::snprintf(b4, sizeof(b4), "%04d", image);
+      const std::string v8 = prefix + "visualize/" + b8;
+      const std::string id = (exists(v8 + ".ppm") || exists(v8 + ".jpg")) ? b8 : b4;
+      View& v = views[index];
+      const std::string name = complete_name(prefix + "visualize/" + id, true);
+      pmvs_status st;
+      errors[index] = "image";
+      if ((st = pmvs_image_load(name.c_str(), &v.w, &v.h, nullptr))) return st;
+      v.rgb.resize((size_t)v.w * v.h * 3);
+      if ((st = pmvs_image_load(name.c_str(), &v.w, &v.h, v.rgb.data()))) return st;
+      errors[index] = "camera";
+      if ((st = pmvs_camera_load((prefix + "txt/" + id + ".txt").c_str(), v.proj))) return st;
+      for (int k = 0; k < 2; ++k) {
+        const std::string m = complete_name(prefix + (k == 0 ? "masks/" : "edges/") + id, false);
+        if (m.size() < 4 || (m.compare(m.size() - 4, 4, ".pgm") && m.compare(m.size() - 4, 4, ".pbm"))) continue;
+        int mw = 0, mh = 0;
+        std::vector<uint8_t>& dst = k == 0 ? v.mask : v.edge;
+        errors[index] = "mask/edge";
+        if ((st = pmvs_pnm_mask_load(m.c_str(), &mw, &mh, nullptr))) return st;
+        if (mw != v.w || mh != v.h) {
+          errors[index] = m + " is " + std::to_string(mw) + "x" + std::to_string(mh) + ", image " + std::to_string(v.w) +
+                          "x" + std::to_string(v.h);
+          return PMVS_EINVAL;
+        }
+        dst.resize((size_t)mw * mh);
+        if ((st = pmvs_pnm_mask_load(m.c_str(), &mw, &mh, dst.data()))) return st;
       }
-      dst.resize((size_t)mw * mh);
-      CHECK("mask/edge", pmvs_pnm_mask_load(m.c_str(), &mw, &mh, dst.data()));
+      // CFindMatch::init: _pss.setEdge(_setEdge) replaces the edge maps (findMatch.cpp:74-76)
+      if (opt->set_edge != 0.0f) {
+        v.edge.resize((size_t)v.w * v.h);
+        errors[index] = "setEdge";
+        if ((st = pmvs_set_edge(v.rgb.data(), v.w, v.h, opt->set_edge, v.edge.data()))) return st;
+      }
+      return PMVS_OK;
+    };
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    const int nthreads = std::max(1, std::min({num, env_int("PMVS_IO_THREADS", std::min(16, hw))}));
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nthreads; ++t)
+      pool.emplace_back([&]() {
+        for (int index; (index = next.fetch_add(1)) < num;) {
+          status[index] = load_one(index);
+          if (status[index] != PMVS_OK && errors[index].find(' ') == std::string::npos)
+            errors[index] += std::string(": ") + pmvs_last_error();  // the worker's own last error
+        }
+      });
+    for (auto& t : pool) t.join();
+  }
+  for (int index = 0; index < num; ++index) {
+    if (status[index] != PMVS_OK) {
+      std::cerr << std::endl << "pmvs2: " << errors[index] << " (status " << (int)status[index] << ")" << std::endl;
+      return 1;
     }
-    // CFindMatch::init: _pss.setEdge(_setEdge) replaces the edge maps (findMatch.cpp:74-76)
-    if (opt->set_edge != 0.0f) {
-      v.edge.resize((size_t)v.w * v.h);
-      CHECK("setEdge", pmvs_set_edge(v.rgb.data(), v.w, v.h, opt->set_edge, v.edge.data()));
-    }
-    std::cerr << '*' << std::flush;
+    std::cerr << '*';
   }
   std::cerr << std::endl;
+  const double t_read = now_s();
 
   // ---- the device scene (CFindMatch::init, findMatch.cpp:30-107)
   std::vector<pmvs_view_desc> vd(num);
@@ -215,9 +250,10 @@ int main(int argc, char* argv[]) {
   // ---- seed phase (CSeed::run, findMatch.cpp:193)
   int32_t nseeds = 0;
   pmvs_seed_stats sst{};
-  std::vector<pmvs_patch> seeds(std::max<size_t>(1024, points.size()));
-  CHECK("seeds", pmvs_seed_run(sc, points.data(), npts.data(), env_int("PMVS_SEED_BATCH", 0), seeds.data(),
-                               (int32_t)seeds.size(), &nseeds, &sst));
+  CHECK("seeds", pmvs_seed_run(sc, points.data(), npts.data(), env_int("PMVS_SEED_BATCH", 0), nullptr, 0, &nseeds,
+                               &sst));
+  std::vector<pmvs_patch> seeds(std::max(nseeds, 1));
+  CHECK("seeds", pmvs_seed_fetch(sc, seeds.data(), nseeds));
   seeds.resize(nseeds);
   std::cerr << "Total pass fail0 fail1 refinepatch: " << sst.trial << ' ' << sst.pass << ' ' << sst.fail0 << ' '
             << sst.fail1 << ' ' << sst.pass + sst.fail1 << std::endl;

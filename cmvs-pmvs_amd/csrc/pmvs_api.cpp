@@ -209,6 +209,8 @@ struct pmvs_scene {
   void* shard_ctx = nullptr;
   pmvs_rccl* shard_rccl = nullptr;  // set: the records go device to device (pmvs_scene_set_shard_rccl)
   int xkept = -1, lkept = -1;   // models kept on the device for pmvs_expand_fetch / pmvs_loop_fetch
+  std::vector<pmvs_patch> skept; // seeds kept for pmvs_seed_fetch (pmvs_seed_run with out = NULL, cap = 0)
+  bool seeds_kept = false;
   std::vector<int> xalive;
   DBuf<pmvs_patch> fpatches2;   // compaction target of pmvs_run_loop
   FeatBuffers feat;             // feature-detection scratch (pmvs_detect_features)
@@ -429,7 +431,7 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
   int wpc = 8;  // 1206: 19.5 KB LDS, <= 256 registers -> 8 resident per CU
   if (const char* e = getenv("PMVS_REFINE_WAVES_PER_CU")) wpc = std::max(1, std::min(32, atoi(e)));
   if (const char* e = getenv("PMVS_REFINE_CONFIG")) sc->tslots = atoi(e);
-  if (sc->tslots != 804 && sc->tslots != 807 && sc->tslots != 808 && sc->tslots != 1206 && sc->tslots != 1204 && sc->tslots != 1608 && sc->tslots != 2408) sc->tslots = 1206;
+  if (!refine_config_supported(sc->tslots)) sc->tslots = 1206;
   sc->refine_grid = std::max(1, prop.multiProcessorCount) * wpc;
   if (sc->scratch.alloc((size_t)sc->grid * PMVS_MAX_IMAGES * PMVS_MAX_IMAGES) != hipSuccess)
     return bail(fail(PMVS_ENOMEM, "scratch"));
@@ -602,6 +604,9 @@ pmvs_status pmvs_detect_features(pmvs_scene* sc, int32_t view, int32_t fcsize, p
 pmvs_status pmvs_seed_run(pmvs_scene* sc, const pmvs_point* points, const int32_t* num_points, int32_t batch,
                           pmvs_patch* out, int32_t cap, int32_t* n_out, pmvs_seed_stats* stats) {
   if (!sc || !num_points || !n_out || cap < 0 || (cap > 0 && !out)) return fail(PMVS_EINVAL, "null argument");
+  const bool keep = !out && cap == 0;  // the scene keeps the seeds; pmvs_seed_fetch copies them out
+  sc->seeds_kept = false;
+  std::vector<pmvs_patch>().swap(sc->skept);
   if (sc->ds.depth != 0) return fail(PMVS_EINVAL, "the seed phase runs at depth 0 (scene depth %d)", sc->ds.depth);
   long long np = 0;
   for (int i = 0; i < sc->ds.num; ++i) {
@@ -645,8 +650,23 @@ pmvs_status pmvs_seed_run(pmvs_scene* sc, const pmvs_point* points, const int32_
     stats->refined = so.stats[4]; stats->rounds = so.stats[5]; stats->candidates = so.stats[6];
     stats->wall_ms = so.wall_ms; stats->gen_ms = so.gen_ms; stats->refine_ms = so.refine_ms;
   }
+  if (keep) {
+    sc->skept.swap(so.seeds);
+    sc->seeds_kept = true;
+    return PMVS_OK;
+  }
   if (ns > cap) return fail(PMVS_EINVAL, "seed phase: %d seeds, capacity %d", ns, cap);
   if (ns) std::memcpy(out, so.seeds.data(), (size_t)ns * sizeof(pmvs_patch));
+  return PMVS_OK;
+}
+
+pmvs_status pmvs_seed_fetch(pmvs_scene* sc, pmvs_patch* out, int32_t n) {
+  if (!sc || n < 0 || (n > 0 && !out)) return fail(PMVS_EINVAL, "invalid argument");
+  if (!sc->seeds_kept || (size_t)n != sc->skept.size())
+    return fail(PMVS_EINVAL, "seed_fetch: %d seeds kept, %d asked", sc->seeds_kept ? (int)sc->skept.size() : -1, n);
+  if (n) std::memcpy(out, sc->skept.data(), (size_t)n * sizeof(pmvs_patch));
+  sc->seeds_kept = false;
+  std::vector<pmvs_patch>().swap(sc->skept);
   return PMVS_OK;
 }
 
@@ -974,8 +994,21 @@ std::vector<long long> target_cells(pmvs_scene* sc) {
 
 // One expansion run on the device-resident model sc->fpatches[0, n0) with alive flags
 // sc->xbuf.alive; *n_out patches afterwards.
+// Test hook (tests/test_gpu_expand.py): PMVS_TEST_SHARD_FAIL="rank:0:x" (after the expansion's last
+// exchange) or "rank:0:s" (after the filter pass's last exchange) makes that rank fail locally there,
+// as an asynchronous kernel fault surfacing at the stream synchronisation would.
+bool test_local_fail(const pmvs_scene* sc, char where) {
+  const char* e = getenv("PMVS_TEST_SHARD_FAIL");
+  int r = -1, w = -1;
+  char c = 0;
+  return e && sc->shard_world > 1 && sscanf(e, "%d:%d:%c", &r, &w, &c) == 3 && r == sc->shard_rank && c == where;
+}
+
+// *handled (sharded loop): whether the peers already know of a failure returned here -- true only
+// for failures expand_pass reported through its own header exchanges.
 pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int cthr, int flags, int cap, int* n_out,
-                          pmvs_expand_stats* stats) {
+                          pmvs_expand_stats* stats, bool* handled = nullptr) {
+  if (handled) *handled = false;
   const std::vector<long long> tgoff = target_cells(sc);
   // refine-work accounting: device counters accumulate over the run (only the work-queue heads
   // are reset per launch); the refine-kernel time of each launch is read at the next one, when
@@ -1007,10 +1040,13 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
   const hipError_t e = expand_pass(sc->ds, sc->fbuf, sc->xbuf, sc->fpatches.p, sc->fpatches.n, n0, sc->xbuf.alive, cap,
                                    tgoff[sc->ds.tnum], tgoff.data(), wave, cthr, flags, sc->grid, sc->stream, refine, sh,
                                    sv, n_out, min_cands);
+  if (handled) *handled = e != hipSuccess;  // expand_pass ends every failure with a header all ranks see
   if (e == hipErrorOutOfMemory)
     return fail(PMVS_EUNSUPPORTED, "expansion: capacity %d exceeded or a patch has more than 1024 neighbours", cap);
   if (e == hipErrorUnknown && sh.world > 1) return fail(PMVS_EDEVICE, "expansion: the shard exchange or another rank failed");
   HIPCHK(e);
+  if (handled) *handled = false;  // from here on a failure is this rank's alone
+  if (test_local_fail(sc, 'x')) return fail(PMVS_EDEVICE, "expansion: injected local failure (test)");
   HIPCHK(hipStreamSynchronize(sc->stream));
   take_time();
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1050,9 +1086,12 @@ pmvs_status filter_device(pmvs_scene* sc, int n, pmvs_filter_stats* stats, bool*
     if (handled) *handled = fh;
     return fail(PMVS_EDEVICE, "filter pass: %s", hipGetErrorString(fe));
   }
-  if (handled) *handled = true;  // overflow is all-gathered: every rank returns it together
+  // kernels launched after the pass's last exchange (small groups, collect, keep) fault only at
+  // this synchronisation, on this rank alone: *handled stays false so the loop announces it
   HIPCHK(hipEventRecord(sc->ev1, sc->stream));
+  if (test_local_fail(sc, 's')) return fail(PMVS_EDEVICE, "filter pass: injected local failure (test)");
   HIPCHK(hipStreamSynchronize(sc->stream));
+  if (handled) *handled = true;  // overflow is all-gathered: every rank returns it together
   if (overflow) return fail(PMVS_EUNSUPPORTED, "filterNeighbor: %d patches with more than 1024 neighbours", overflow);
   if (stats) {
     float ms = 0;
@@ -1153,9 +1192,10 @@ pmvs_status pmvs_run_loop(pmvs_scene* sc, const pmvs_patch* seeds, int32_t n, fl
     pmvs_loop_iter li{};
     li.depth = depth;
     int nn = cur;
+    bool xhandled = true;
     if (cur > 0 && (st = expand_device(sc, cur, wave, min_candidates, cthr, (it == 0 && (flags & PMVS_EXPAND_AFTER_SEEDS)) ? 1 : 0, cap,
-                                       &nn, &li.expand)))
-      return st;
+                                       &nn, &li.expand, &xhandled)))
+      return fail_loop(st, xhandled);
     bool handled = true;
     if ((st = filter_device(sc, nn, &li.filter, &handled))) return fail_loop(st, handled);
     int kept = 0;

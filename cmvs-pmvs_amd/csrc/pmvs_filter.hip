@@ -2116,7 +2116,12 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
         FCHK(hipcub::DeviceScan::ExclusiveSum(B.temp, tb, B.qcrows, B.qoff, nch, st));
         unsigned qgrid = nblk(nj);
         if (const char* e = getenv("PMVS_QUAD_WAVES_PER_CU"))  // 0 = one lane per job, no cap
-          if (atoi(e) > 0) qgrid = std::min(qgrid, (unsigned)std::max(1, grid / 8 * atoi(e) / 4));
+          if (atoi(e) > 0) {
+            int dev = 0, cus = 0;
+            FCHK(hipGetDevice(&dev));
+            FCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            qgrid = std::min(qgrid, (unsigned)std::max(1, cus * atoi(e) / 4));  // 4 wavefronts per 256-lane block
+          }
         hipLaunchKernelGGL(quad_lane_kernel, dim3(qgrid), dim3(256), 0, st, s, c.dev(), qj, B.qkeys2, B.qoff, nj,
                            B.flags);
       }
@@ -3053,7 +3058,8 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   CommitOut co;
   T.mark(0);
   std::vector<int> okh;
-  while (!q_empty()) {
+  const long long max_waves = (long long)((unsigned)flags >> 8);  // PMVS_EXPAND_MAX_WAVES (0 = unbounded)
+  while (!q_empty() && (max_waves <= 0 || stats[7] < max_waves)) {
     stats[7]++;
     if (inject && inj_where == 'b' && stats[7] == inj_wave) return hipErrorOutOfMemory;
     // A wave: chunks of W parents (queue order) until it holds min_cands candidate directions

@@ -17,6 +17,7 @@
 #include <iomanip>
 #include <limits>
 #include <map>
+#include <mutex>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -26,8 +27,9 @@
 // libjpeg's API types (the image's libjpeg 9 headers); the library itself is loaded at run time
 // (dlopen), so the product has no link-time JPEG dependency and reports PMVS_EUNSUPPORTED for
 // .jpg inputs where libjpeg is absent.
-#if __has_include("/opt/conda/include/jpeglib.h")
-#include "/opt/conda/include/jpeglib.h"
+// The Makefile finds jpeglib.h (JPEG_INC) and warns when it is missing.
+#if __has_include(<jpeglib.h>)
+#include <jpeglib.h>
 #define PMVS_HAVE_JPEG_HEADERS 1
 #endif
 
@@ -214,8 +216,13 @@ struct JpegApi {
   JDIMENSION (*read_scanlines)(j_decompress_ptr, JSAMPARRAY, JDIMENSION);
   boolean (*finish)(j_decompress_ptr);
   void (*destroy)(j_decompress_ptr);
-  bool load() {
-    if (h) return true;
+  std::once_flag once;
+  bool ok = false;
+  bool load() {  // thread-safe: pmvs2 decodes views on a pool of host threads
+    std::call_once(once, [this]() { ok = open(); });
+    return ok;
+  }
+  bool open() {
     for (const char* name : {"libjpeg.so.9", "/opt/conda/lib/libjpeg.so.9", "libjpeg.so"}) {
       h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
       if (h) break;
@@ -350,6 +357,7 @@ pmvs_status pmvs_pnm_mask_load(const char* path, int32_t* width, int32_t* height
     size_t count = 0;
     for (size_t i = 0; i < bcount && count < n; ++i) {
       ifstr.read((char*)&uc, 1);
+      if (!ifstr) return pmvs_io_fail(PMVS_EINVAL, "%s: truncated", path);
       for (int j = 0; j < 8 && count < n; ++j, ++count) {
         out[count] = (uc >> 7) ? 0 : 255;
         uc <<= 1;

@@ -831,7 +831,9 @@ template <int WS, int TSLOTS, int NC>
 struct RefLds {
   static constexpr int S = WS * WS;
   static constexpr int SP = (S + 3) & ~3;  // channel rows padded to 16 B (float4 reads)
+#if !defined(BQ_PRIVATE)
   BqState bq[NC];                    // optimizer state of the wave's NC chains (lane c owns bq[c])
+#endif
   alignas(16) float tex[TSLOTS][3][SP];  // per texture: R, G, B rows of the S samples
   float ave[TSLOTS][4];
   long long jbase[TSLOTS];
@@ -839,7 +841,7 @@ struct RefLds {
   float jleft[TSLOTS][2], jdx[TSLOTS][2], jdy[TSLOTS][2];
   float jres[TSLOTS];
   float geo[NC][16];                 // requesting lane: coord, normal, pxaxis, pyaxis
-  int views[NC][PMVS_MAX_TAU];       // requesting lane: first size images
+  unsigned short views[NC][PMVS_MAX_TAU];  // requesting lane: first size images
   int rsize[NC], rfirst[NC];
 };
 
@@ -1073,7 +1075,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(REFINE_WPE(N
     DScene s, RefineJob* __restrict__ jobs, int n, DevStats* st) {
   __shared__ RefLds<WS, TSLOTS, NC> C;
   const int lane = lane_id();
+#if defined(BQ_PRIVATE)
+  BqState bq_priv;
+  BQ_AS BqState& bq = *(BQ_AS BqState*)&bq_priv;
+#else
   BQ_AS BqState& bq = *(BQ_AS BqState*)&C.bq[lane < NC ? lane : 0];
+#endif
   RefineSetup R;
   int cand = -1, need = 0, evals = 0, size = 0, nimg = 0, rc = 0;
   bool exhausted = lane >= NC;  // lanes >= NC only help evaluate
@@ -1442,6 +1449,18 @@ __global__ void unpack_rgba_kernel(const uint32_t* __restrict__ in, uint8_t* __r
 
 namespace pmvsdev {
 
+// refine_v2_kernel instantiations (texture slots * 100 + chains per wavefront)
+bool refine_config_supported(int tslots) {
+  switch (tslots) {
+    case 804: case 807: case 808: case 1204: case 1206: case 1608: case 2408: return true;
+#if defined(BQ_PRIVATE)
+    case 1264: case 2464: case 1232: case 2432: case 1216: case 2448: case 3232: case 3248: case 3264: case 4832:
+    case 4864: return true;
+#endif
+    default: return false;
+  }
+}
+
 template <int WS>
 static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out,
                                    int n, DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream,
@@ -1466,6 +1485,19 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
     case 1608: hipLaunchKernelGGL((refine_v2_kernel<WS, 16, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     case 2408: hipLaunchKernelGGL((refine_v2_kernel<WS, 24, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     case 1204: hipLaunchKernelGGL((refine_v2_kernel<WS, 12, 4>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+#if defined(BQ_PRIVATE)
+    case 1264: hipLaunchKernelGGL((refine_v2_kernel<WS, 12, 64>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 2464: hipLaunchKernelGGL((refine_v2_kernel<WS, 24, 64>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 1232: hipLaunchKernelGGL((refine_v2_kernel<WS, 12, 32>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 2432: hipLaunchKernelGGL((refine_v2_kernel<WS, 24, 32>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 1216: hipLaunchKernelGGL((refine_v2_kernel<WS, 12, 16>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 2448: hipLaunchKernelGGL((refine_v2_kernel<WS, 24, 48>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 3232: hipLaunchKernelGGL((refine_v2_kernel<WS, 32, 32>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 3248: hipLaunchKernelGGL((refine_v2_kernel<WS, 32, 48>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 3264: hipLaunchKernelGGL((refine_v2_kernel<WS, 32, 64>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 4832: hipLaunchKernelGGL((refine_v2_kernel<WS, 48, 32>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 4864: hipLaunchKernelGGL((refine_v2_kernel<WS, 48, 64>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+#endif
     default: hipLaunchKernelGGL((refine_v2_kernel<WS, 12, 6>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
   }
   (void)hipEventRecord(ev[2], stream);
@@ -1667,11 +1699,17 @@ __device__ __forceinline__ double bq_test_f(int kind, const double* v) {
 template <int C>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BQ_CALLER_WPE))) void bobyqa_lds_kernel(int kind, const double* __restrict__ x0, int n, int maxeval,
                                                         double* __restrict__ out) {
-  __shared__ BqState sts[C];
   const int lane = threadIdx.x;
   const int i = blockIdx.x * C + lane;
+#if defined(BQ_PRIVATE)
+  BqState st_priv;
+  if (lane >= C || i >= n) return;
+  BQ_AS BqState& st = *(BQ_AS BqState*)&st_priv;
+#else
+  __shared__ BqState sts[C];
   if (lane >= C || i >= n) return;
   BQ_AS BqState& st = *(BQ_AS BqState*)&sts[lane];
+#endif
   const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999}, ub[3] = {HUGE_VAL, 23.99999, 23.99999};
   double x[3] = {x0[3 * i], x0[3 * i + 1], x0[3 * i + 2]};
   bq_begin(st, x, lb, ub, 1e-7, maxeval);
@@ -1687,10 +1725,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BQ_CALLER_WP
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BQ_CALLER_WPE))) void bobyqa_wave_kernel(int kind, const double* __restrict__ x0, int n, int maxeval,
                                                          double* __restrict__ out) {
+#if defined(BQ_PRIVATE)
+  BqState st_;  // lane 0's
+#else
   __shared__ BqState st_;
+#endif
   BQ_AS BqState& st = *(BQ_AS BqState*)&st_;
   __shared__ int stepv;
-  __shared__ double fres;
+  __shared__ double fres, xes[3];
   const int i = blockIdx.x;
   if (i >= n) return;
   const int lane = threadIdx.x;
@@ -1702,10 +1744,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BQ_CALLER_WP
   }
   __syncthreads();
   for (;;) {
-    if (lane == 0) stepv = bq_step(st, fres);
+    if (lane == 0) {
+      stepv = bq_step(st, fres);
+      for (int k = 0; k < 3; ++k) xes[k] = st.xeval[k];
+    }
     __syncthreads();
     if (stepv != BQ_NEED_F) break;
-    const double xe[3] = {st.xeval[0], st.xeval[1], st.xeval[2]};
+    const double xe[3] = {xes[0], xes[1], xes[2]};
     const double f = bq_test_f(kind, xe);
     __syncthreads();
     if (lane == 0) fres = f;

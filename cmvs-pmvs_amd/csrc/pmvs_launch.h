@@ -6,6 +6,7 @@
 #include <vector>
 
 namespace pmvsdev {
+bool refine_config_supported(int tslots);  // PMVS_REFINE_CONFIG values this build instantiates
 hipError_t launch_refine(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out, int n,
                          DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream, hipEvent_t* ev);
 hipError_t launch_incc_eval(const DScene& s, const pmvs_eval_query* d_q, int n, double* d_out, DevStats* d_st,

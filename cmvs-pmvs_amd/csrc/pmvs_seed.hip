@@ -651,20 +651,25 @@ hipError_t seed_pass(const DScene& s, const std::vector<DView>& hv, const SeedIn
       }
       return -1;
     };
-    // requests for the cells from the cursor on, against the current state (read-only)
+    // requests for the cells from the cursor on, against the current state (read-only).  A cell
+    // whose earlier requests all failed gets twice as many the next time (creq: requests so far), so
+    // a point that tries many epipolar candidates before two succeed costs O(log) rounds, not one
+    // round per per_cell candidates; the replay is exact whatever was requested.
+    std::vector<int> creq(std::max(ncells_p, 1), 0);
     auto speculate = [&](std::vector<int>& req) {
       req.clear();
       int c2 = ci, p2 = pi;
       bool first = true;
       while (c2 < ncells_p && (int)req.size() < budget) {
         int unknown = 0;
+        const int quota = std::min(4096, std::max(per_cell, creq[c2]));
         bool cell_done = false;
         const int npts_cell = cellstart[c2 + 1] - cellstart[c2];
         if (!(first && in_point) && p2 == 0) {
           const int c = p0cell[cellstart[c2]];
           if (!can_add(index, c % gw[index], c / gw[index])) { ++c2; p2 = 0; first = false; continue; }
         }
-        for (; p2 < npts_cell && !cell_done && unknown < per_cell; ++p2) {
+        for (; p2 < npts_cell && !cell_done && unknown < quota; ++p2) {
           int v0 = 0, cnt = 0;
           const std::vector<int>* list;
           if (first && in_point) { list = &vcp; v0 = vi; cnt = count; }
@@ -677,11 +682,12 @@ hipError_t seed_pass(const DScene& s, const std::vector<DView>& hv, const SeedIn
             } else if (state[cid] == 0) {
               state[cid] = 1;
               req.push_back(cid);
-              if (++unknown >= per_cell) break;
+              if (++unknown >= quota) break;
             }
           }
           if (cnt > 0) cell_done = true;  // this point adds a patch: the cell is finished
         }
+        creq[c2] += unknown;
         first = false;
         ++c2;
         p2 = 0;

@@ -46,16 +46,41 @@ static double value_noise(double x, double y, double z, uint64_t seed) {
   return y0 + (y1 - y0) * tz;
 }
 
-static void albedo(const double* p, uint64_t seed, double* rgb) {
+static void albedo(const double* p, uint64_t seed, double* rgb, double lowtex = 0.0) {
   const double freqs[3] = {8.0, 16.0, 32.0};
   const double amps[3] = {0.5, 0.3, 0.2};
+  // low-texture regions (hard mode): contrast x 0.05 where a low-frequency field is below `lowtex`,
+  // with a short linear transition
+  double contrast = 1.0;
+  if (lowtex > 0.0) {
+    const double lf = value_noise(p[0] * 2.5 + 11.0, p[1] * 2.5 - 7.0, p[2] * 2.5 + 2.0, seed ^ 0x10E7E7ull);
+    const double c = std::min(1.0, std::max(0.0, (lf - lowtex) / 0.04 + 0.5));
+    contrast = 0.05 + 0.95 * c;
+  }
   for (int c = 0; c < 3; ++c) {
     double v = 0.0;
     for (int o = 0; o < 3; ++o)
       v += amps[o] * value_noise(p[0] * freqs[o] + 17.0 * c, p[1] * freqs[o] - 5.0 * c, p[2] * freqs[o] + 3.0 * c, seed + 101 * c + o);
-    v = (v - 0.5) * 2.2 + 0.5;  // stretch towards full range
+    v = (v - 0.5) * 2.2 * contrast + 0.5;  // stretch towards full range
     rgb[c] = std::min(1.0, std::max(0.0, v));
   }
+}
+
+// Hard-mode helpers: a uniform in [0, 1) from a hash, approximately Gaussian noise (sum of four
+// uniforms), the per-view gain/bias, the occluder's centre.
+static inline double hash_unit(uint64_t h) { return (double)(mix64(h) >> 11) * (1.0 / 9007199254740992.0); }
+static inline double hash_gauss(uint64_t h) {
+  double u = 0.0;
+  for (int k = 0; k < 4; ++k) u += hash_unit(h * 4 + (uint64_t)k);
+  return (u - 2.0) * 1.7320508075688772;  // variance 4/12 -> 1
+}
+static void occluder_centre(const pmvs_synth_params& p, double* oc) {
+  // on the ring's arc a third of the way round the cameras, at radius 2.2, slightly above the plane
+  const double step = p.arc_step_deg > 0.0 ? p.arc_step_deg * M_PI / 180.0 : 2.0 * M_PI / (double)p.num_views;
+  const double th = step * (double)(p.num_views - 1) / 3.0;
+  oc[0] = 2.2 * std::cos(th);
+  oc[1] = 2.2 * std::sin(th);
+  oc[2] = 0.1;
 }
 
 struct Cam {
@@ -93,6 +118,12 @@ static void make_camera(const pmvs_synth_params& p, int i, Cam& cam, float* P) {
 static void render_view(const pmvs_synth_params& p, int i, const Cam& cam, uint8_t* rgb) {
   const int W = p.width, H = p.height, ss = std::max(1, std::min(4, p.supersample));
   const uint64_t bgseed = p.seed * 7919ull + (uint64_t)i * 104729ull + 17;
+  const uint64_t vseed = mix64(p.seed ^ (0xB1A5ull + (uint64_t)i * 0x9E37ull));
+  const double gain = 1.0 + p.gain_sigma * hash_gauss(vseed), bias = p.bias_sigma * hash_gauss(vseed ^ 0x5A5Aull);
+  double oc[3] = {0, 0, 0};
+  const double orad = p.occluder_radius;
+  if (orad > 0.0) occluder_centre(p, oc);
+  const double oC[3] = {cam.C[0] - oc[0], cam.C[1] - oc[1], cam.C[2] - oc[2]};
   for (int y = 0; y < H; ++y) {
     for (int x = 0; x < W; ++x) {
       double acc[3] = {0, 0, 0};
@@ -108,11 +139,25 @@ static void render_view(const pmvs_synth_params& p, int i, const Cam& cam, uint8
           const double b = cam.C[0] * d[0] + cam.C[1] * d[1] + cam.C[2] * d[2];
           const double c = cam.C[0] * cam.C[0] + cam.C[1] * cam.C[1] + cam.C[2] * cam.C[2] - 1.0;
           const double disc = b * b - c;
-          if (disc > 0.0) {
-            const double tt = -b - std::sqrt(disc);
+          double tt = disc > 0.0 ? -b - std::sqrt(disc) : -1.0;
+          bool occ = false;
+          if (orad > 0.0) {  // the occluding sphere, when nearer
+            const double ob = oC[0] * d[0] + oC[1] * d[1] + oC[2] * d[2];
+            const double odisc = ob * ob - (oC[0] * oC[0] + oC[1] * oC[1] + oC[2] * oC[2] - orad * orad);
+            if (odisc > 0.0) {
+              const double ot = -ob - std::sqrt(odisc);
+              if (ot > 0.0 && (tt < 0.0 || ot < tt)) { tt = ot; occ = true; }
+            }
+          }
+          if (tt > 0.0) {
             const double hp[3] = {cam.C[0] + tt * d[0], cam.C[1] + tt * d[1], cam.C[2] + tt * d[2]};
             double col[3];
-            albedo(hp, p.seed, col);
+            if (occ) {
+              const double q[3] = {(hp[0] - oc[0]) / orad, (hp[1] - oc[1]) / orad, (hp[2] - oc[2]) / orad};
+              albedo(q, p.seed ^ 0x0CC1ull, col);
+            } else {
+              albedo(hp, p.seed, col, p.lowtex);
+            }
             for (int k = 0; k < 3; ++k) acc[k] += col[k];
             hits++;
           } else {
@@ -124,7 +169,10 @@ static void render_view(const pmvs_synth_params& p, int i, const Cam& cam, uint8
       (void)hits;
       uint8_t* o = rgb + ((size_t)y * W + x) * 3;
       for (int k = 0; k < 3; ++k) {
-        const double val = acc[k] / (ss * ss) * 255.0;
+        double lin = acc[k] / (ss * ss);
+        if (p.noise_sigma > 0.0) lin += p.noise_sigma * hash_gauss(vseed ^ (((uint64_t)y * W + x) * 3 + k) * 0x2545F491ull);
+        lin = lin * gain + bias;
+        const double val = lin * 255.0;
         o[k] = (uint8_t)std::min(255.0, std::max(0.0, std::floor(val + 0.5)));
       }
     }

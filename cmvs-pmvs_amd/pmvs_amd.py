@@ -120,7 +120,16 @@ class SynthParams(C.Structure):
     _fields_ = [("num_views", C.c_int32), ("num_targets", C.c_int32), ("width", C.c_int32),
                 ("height", C.c_int32), ("supersample", C.c_int32), ("level", C.c_int32),
                 ("seed", C.c_uint64), ("ring_radius", C.c_double), ("height_offset", C.c_double),
-                ("focal_scale", C.c_double), ("arc_step_deg", C.c_double)]
+                ("focal_scale", C.c_double), ("arc_step_deg", C.c_double), ("gain_sigma", C.c_double),
+                ("bias_sigma", C.c_double), ("noise_sigma", C.c_double), ("lowtex", C.c_double),
+                ("occluder_radius", C.c_double)]
+
+
+# the photometrically hard synthetic mode (pmvs_synth_params): per-view gain / bias, sensor noise,
+# low-texture regions and an occluder, so final NCCs spread over ~0.4-1 and image selection
+# (constraintImages, optim.cpp:192-206) and filterOutside gains (filter.cpp:62-71) see values near
+# their thresholds
+HARD = dict(gain_sigma=0.15, bias_sigma=0.04, noise_sigma=0.08, lowtex=0.5, occluder_radius=0.3)
 
 
 EXPORTS = ["pmvs_last_error", "pmvs_device_count", "pmvs_scene_create", "pmvs_scene_destroy",
@@ -133,7 +142,7 @@ EXPORTS = ["pmvs_last_error", "pmvs_device_count", "pmvs_scene_create", "pmvs_sc
            "pmvs_rccl_create", "pmvs_rccl_destroy", "pmvs_rccl_allgather", "pmvs_rccl_allgather_device",
            "pmvs_thread_exchange_create",
            "pmvs_thread_exchange_ctx", "pmvs_thread_allgather", "pmvs_thread_exchange_destroy", "pmvs_detect_features",
-           "pmvs_seed_run", "pmvs_selftest_lls", "pmvs_image_load", "pmvs_pnm_mask_load", "pmvs_set_edge"]
+           "pmvs_seed_run", "pmvs_seed_fetch", "pmvs_selftest_lls", "pmvs_image_load", "pmvs_pnm_mask_load", "pmvs_set_edge"]
 
 # int fn(void* ctx, const void* send, int64_t bytes, void* recv): all-gather (pmvs_allgather_fn)
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p)
@@ -162,6 +171,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
                                          C.POINTER(C.c_int32)]
     lib.pmvs_seed_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
                                   C.POINTER(C.c_int32), C.POINTER(SeedStats)]
+    lib.pmvs_seed_fetch.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     lib.pmvs_incc_eval.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(Stats)]
     lib.pmvs_refine_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(Stats)]
     lib.pmvs_refine_batch_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
@@ -365,11 +375,16 @@ class Scene:
         """CSeed::run on the device (pmvs_seed_run) from per-view feature points (POINT_DTYPE arrays,
         or float [n, 4] = x, y, response, type): (seed patches in addPatch order, stats)."""
         flat, npts = points_flat(points)
-        cap = int(cap or max(1024, int(npts.sum())))
-        out = np.zeros(cap, PATCH_DTYPE)
         n = C.c_int32(0)
         st = SeedStats()
-        _check(self.lib.pmvs_seed_run(self.handle, _ptr(flat), _ptr(npts), int(batch), _ptr(out), cap, C.byref(n),
+        if cap is None:  # the scene keeps the seeds; fetch exactly their number
+            _check(self.lib.pmvs_seed_run(self.handle, _ptr(flat), _ptr(npts), int(batch), None, 0, C.byref(n),
+                                          C.byref(st)))
+            out = np.zeros(n.value, PATCH_DTYPE)
+            _check(self.lib.pmvs_seed_fetch(self.handle, _ptr(out), n.value))
+            return out, st.as_dict()
+        out = np.zeros(int(cap), PATCH_DTYPE)
+        _check(self.lib.pmvs_seed_run(self.handle, _ptr(flat), _ptr(npts), int(batch), _ptr(out), int(cap), C.byref(n),
                                       C.byref(st)))
         return out[:n.value].copy(), st.as_dict()
 
@@ -409,18 +424,20 @@ class Scene:
         return pa, keep, st.as_dict()
 
     def expand_run(self, patches: np.ndarray, alive=None, wave: int = 1, count_threshold: int = 4, cap=None,
-                   after_seeds: bool = False, min_candidates: int = 0):
+                   after_seeds: bool = False, min_candidates: int = 0, max_waves: int = 0):
         """One CExpand::run on the device (expand.cpp:17-406): returns (patches, alive, stats).
 
         The result holds the input patches (flags updated) followed by the new ones; `cap` bounds
-        its size (default: 2^30).  Collective when a shard is set (set_shard)."""
+        its size (default: 2^30).  max_waves > 0 stops after that many waves (bounded parity
+        samples; PMVS_EXPAND_MAX_WAVES).  Collective when a shard is set (set_shard)."""
         pa = np.ascontiguousarray(patches, PATCH_DTYPE)
         al = np.ones(len(pa), np.int32) if alive is None else np.ascontiguousarray(alive, np.int32)
         cap = int(cap or (1 << 30))
         n_out = C.c_int32(0)
         st = ExpandStats()
         _check(self.lib.pmvs_expand_run(self.handle, _ptr(pa), _ptr(al), len(pa), wave, min_candidates, count_threshold,
-                                        int(after_seeds), None, None, cap, C.byref(n_out), C.byref(st)))
+                                        int(after_seeds) | (int(max_waves) << 8), None, None, cap, C.byref(n_out),
+                                        C.byref(st)))
         out = np.empty(n_out.value, PATCH_DTYPE)
         aout = np.empty(n_out.value, np.int32)
         _check(self.lib.pmvs_expand_fetch(self.handle, _ptr(out), _ptr(aout), n_out.value))
@@ -631,7 +648,7 @@ def device_count() -> int:
 def synth_params(num_views: int, width: int, height: int, num_targets: Optional[int] = None,
                  supersample: int = 2, level: int = 1, seed: int = 0x504D5653,
                  ring_radius: float = 4.0, height_offset: float = 0.3, focal_scale: float = 1.16,
-                 arc_step_deg: Optional[float] = None) -> SynthParams:
+                 arc_step_deg: Optional[float] = None, hard: bool = False) -> SynthParams:
     p = SynthParams()
     p.num_views = num_views
     p.num_targets = num_views if num_targets is None else num_targets
@@ -642,6 +659,8 @@ def synth_params(num_views: int, width: int, height: int, num_targets: Optional[
     p.ring_radius, p.height_offset, p.focal_scale = ring_radius, height_offset, focal_scale
     # cameras every min(360/V, 15) degrees: a full ring for V >= 24, an arc otherwise
     p.arc_step_deg = min(360.0 / num_views, 15.0) if arc_step_deg is None else arc_step_deg
+    for k, v in (HARD if hard else {}).items():
+        setattr(p, k, v)
     return p
 
 
@@ -663,9 +682,10 @@ def synth_candidates(p: SynthParams, proj: np.ndarray, n: int, seed: int = 0x5EE
 
 
 def synth_scene(num_views: int, width: int, height: int, level: int = 1, num_targets: Optional[int] = None,
-                supersample: int = 2, nthreads: int = 8, seed: int = 0x504D5653, **opts) -> SceneInputs:
+                supersample: int = 2, nthreads: int = 8, seed: int = 0x504D5653, hard: bool = False,
+                arc_step_deg: Optional[float] = None, **opts) -> SceneInputs:
     p = synth_params(num_views, width, height, num_targets=num_targets, supersample=supersample, level=level,
-                     seed=seed)
+                     seed=seed, hard=hard, arc_step_deg=arc_step_deg)
     rgb, proj = synth_ring(p, nthreads=nthreads)
     return SceneInputs(images=[rgb[i] for i in range(num_views)], projections=proj,
                        num_targets=p.num_targets, level=level, **opts), p

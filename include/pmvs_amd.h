@@ -261,6 +261,9 @@ pmvs_status pmvs_filter_run(pmvs_scene* scene, pmvs_patch* patches, int32_t n, i
  * With a shard set (pmvs_scene_set_shard) the call is collective: every rank passes the same
  * model and arguments and gets the same result. */
 #define PMVS_EXPAND_AFTER_SEEDS 1 /* model straight from the seed phase: no depth maps yet (findMatch.cpp:193-202) */
+/* flags bits 8..31: stop after that many waves (0 = run until the queue is empty).  Not a reference
+ * behaviour: it bounds full-size parity samples against the CPU oracle, which has the same bound. */
+#define PMVS_EXPAND_MAX_WAVES(n) ((int32_t)((uint32_t)(n) << 8))
 typedef struct pmvs_expand_stats {
   int64_t parents, candidates, fail_prep, fail_pre, fail_post, fail_commit, added, waves;
   double wall_ms;
@@ -302,7 +305,9 @@ pmvs_status pmvs_loop_fetch(pmvs_scene* scene, pmvs_patch* out, int32_t n);
  * two succeed (preProcess -> refinePatch -> postProcess, seed.cpp:387-414).  Refinement is batched
  * and speculative; the result equals the sequential one for any batch size.  Runs at depth 0 with
  * the scene's current thresholds (CFindMatch::init values).  Writes the seed patches in addPatch
- * order (at most cap; *n_out = their number) -- the `seeds` input of pmvs_run_loop. */
+ * order (at most cap; *n_out = their number) -- the `seeds` input of pmvs_run_loop.  With out = NULL
+ * and cap = 0 the scene keeps the seeds and pmvs_seed_fetch copies them out (size the array from
+ * *n_out first). */
 typedef struct pmvs_seed_stats {
   int64_t trial, pass, fail0, fail1; /* initialMatchSub calls and outcomes (seed.cpp:94-100) */
   int64_t refined;                   /* candidates refined on the device (incl. speculative ones) */
@@ -313,6 +318,8 @@ typedef struct pmvs_seed_stats {
 } pmvs_seed_stats;
 pmvs_status pmvs_seed_run(pmvs_scene* scene, const pmvs_point* points, const int32_t* num_points, int32_t batch,
                           pmvs_patch* out, int32_t cap, int32_t* n_out, pmvs_seed_stats* stats);
+/* Copies the seeds the last pmvs_seed_run kept (out = NULL, cap = 0) and releases them; n = *n_out. */
+pmvs_status pmvs_seed_fetch(pmvs_scene* scene, pmvs_patch* out, int32_t n);
 
 /* Multi-GPU sharding of the expansion: one scene per GPU/rank, all holding the
  * same model.  Each wave's candidates are split into contiguous rank ranges for the refine and
@@ -413,6 +420,11 @@ typedef struct pmvs_synth_params {
   double height_offset;  /* alternating camera height (0.3) */
   double focal_scale;    /* f = focal_scale * width */
   double arc_step_deg;   /* angular spacing of the cameras on the ring (0 = 360/num_views) */
+  /* photometrically hard mode (all 0 = the plain scene): per-view gain N(1, gain_sigma) and bias
+   * N(0, bias_sigma), per-pixel sensor noise of std noise_sigma (intensities in [0, 1]), low-texture
+   * regions where a low-frequency noise field is below `lowtex` (texture contrast x 0.05), and a
+   * textured occluding sphere of radius occluder_radius between the ring and the main sphere. */
+  double gain_sigma, bias_sigma, noise_sigma, lowtex, occluder_radius;
 } pmvs_synth_params;
 
 /* Renders num_views RGB8 images (rgb: num_views*width*height*3 bytes, may be NULL to get only

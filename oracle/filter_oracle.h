@@ -262,6 +262,7 @@ static int filter_outside(Organizer& o, std::vector<FPatch>& P) {
   std::vector<float> gains(o.ppatches.size());
   parallel_for(g_threads, o.ppatches.size(), [&](int, size_t k) { gains[k] = compute_gain(o, P, P[o.ppatches[k]]); });
   int count = 0;
+  for (size_t k = 0; k < o.ppatches.size(); ++k) diag(2, std::fabs(gains[k]) < 0.05f);
   for (size_t k = 0; k < o.ppatches.size(); ++k)
     if (gains[k] < 0.0) {
       remove_patch(o, P, o.ppatches[k]);

@@ -619,14 +619,26 @@ static void add_images(const OScene& s, OPatch& p) {
   }
 }
 
+// Near-threshold diagnostics (test infrastructure: how many decisions a parity workload puts close
+// to a threshold, so a bit-exact match there means something).  [0] constraintImages tests,
+// [1] those with |incc - (1 - thr)| < 0.02; [2] filterOutside gains, [3] those with |gain| < 0.05;
+// [4] refined patches, [5] those with |ncc - nccThreshold| < 0.02.
+static std::atomic<long long> g_diag[6];
+static inline void diag(int k, bool near) {
+  g_diag[k].fetch_add(1, std::memory_order_relaxed);
+  if (near) g_diag[k + 1].fetch_add(1, std::memory_order_relaxed);
+}
+
 // COptim::constraintImages, optim.cpp:192-206.
 static void constraint_images(const OScene& s, OCtx& c, OPatch& p, float thr) {
   std::vector<float> inccs;
   set_inccs(s, c, p, inccs, p.images, 0);
   std::vector<int> ni;
   ni.push_back(p.images[0]);
-  for (int i = 1; i < (int)p.images.size(); ++i)
+  for (int i = 1; i < (int)p.images.size(); ++i) {
+    diag(0, std::fabs(inccs[i] - (1.0f - thr)) < 0.02f);
     if (inccs[i] < 1.0f - thr) ni.push_back(p.images[i]);
+  }
   p.images.swap(ni);
 }
 
@@ -793,6 +805,7 @@ static int refine_patch(const OScene& s, OCtx& c, OPatch& p, int* evals) {
   if (success) {
     decode(s, c, p.coord, p.normal, x);
     p.ncc = (float)(1.0 - unrobustincc((float)compute_incc(s, c, p.coord, p.normal, p.images, 1)));
+    diag(4, std::fabs(p.ncc - s.nccThreshold) < 0.02f);
   }
   return (int)rc;
 }
@@ -860,6 +873,14 @@ static void init_ctx(const OScene& s, OCtx& c) {
 using namespace oracle;
 
 extern "C" {
+
+// Near-threshold decision counts accumulated since the last reset (see g_diag).
+void oracle_diag(long long* out, int reset) {
+  for (int k = 0; k < 6; ++k) {
+    if (out) out[k] = g_diag[k].load();
+    if (reset) g_diag[k] = 0;
+  }
+}
 
 void* oracle_scene_create(const pmvs_scene_desc* d) {
   OScene* s = new OScene();

@@ -57,6 +57,7 @@ def lib():
                                              C.c_void_p, C.c_int]
         L.oracle_seed_geometry.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
                                            C.c_void_p, C.c_void_p]
+        L.oracle_diag.argtypes = [C.c_void_p, C.c_int]
         L.oracle_lls5.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
         L.oracle_bobyqa_test.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_int, C.POINTER(C.c_int)]
@@ -279,6 +280,16 @@ class OracleScene:
         st = P.Stats()
         lib().oracle_refine_batch(self.h, _p(cands), len(cands), _p(out), nthreads, C.byref(st))
         return out, st.as_dict()
+
+
+def near_threshold(reset=True):
+    """Near-threshold decision counts of the oracle since the last reset: constraintImages tests
+    (optim.cpp:192-206) within 0.02 of 1 - threshold, filterOutside gains (filter.cpp:62-71) within
+    0.05 of 0, refined NCCs within 0.02 of the threshold."""
+    out = np.zeros(6, np.int64)
+    lib().oracle_diag(_p(out), int(reset))
+    return {"constraint_tests": int(out[0]), "constraint_near": int(out[1]), "gains": int(out[2]),
+            "gains_near": int(out[3]), "refined": int(out[4]), "ncc_near": int(out[5])}
 
 
 def lls5(A, b):

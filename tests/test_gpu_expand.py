@@ -209,10 +209,12 @@ def test_sharded_expand_rank_failure_fails_all_ranks(gpu_available, monkeypatch,
     assert all(isinstance(e, P.PmvsError) for e in errs), errs
 
 
-@pytest.mark.parametrize("where", ["f", "g"])
+@pytest.mark.parametrize("where", ["f", "g", "s", "x"])
 def test_sharded_loop_filter_failure_fails_all_ranks(gpu_available, monkeypatch, where):
     """The sharded loop's filter pass (owner-partitioned filterNeighbor, one flag all-gather):
-    a failure on rank 1 before (f) or after (g) that exchange makes both ranks return an error."""
+    a failure on rank 1 before (f) or after (g) that exchange makes both ranks return an error;
+    so does a local failure after the filter's last exchange (s) or after the expansion's last
+    exchange (x) -- an asynchronous fault surfacing at that rank's stream synchronisation."""
     import pmvs_amd as P
     inp, p = P.synth_scene(6, 480, 360, level=1, supersample=2)
     g = P.Scene(inp)

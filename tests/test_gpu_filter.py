@@ -87,13 +87,18 @@ def test_filter_depth0_and_empty(gpu_available, oracle_mod):
     o.close()
 
 
-@pytest.mark.parametrize("cap", ["0", "20000"], ids=["all_in_wave", "mixed"])
-def test_filter_quad_deferral_paths(gpu_available, oracle_mod, monkeypatch, cap):
+@pytest.mark.parametrize("cap,qwaves", [("0", "0"), ("20000", "0"), ("-1", "1")],
+                         ids=["all_in_wave", "mixed", "lane_grid_stride"])
+def test_filter_quad_deferral_paths(gpu_available, oracle_mod, monkeypatch, cap, qwaves):
     """filterNeighbor's quadric fits run either per lane after the neighbour walk
     (quad_lane_kernel, the default) or inside the walk's wavefront when the deferred-row buffer is
-    full; PMVS_QUAD_ROWS caps that buffer so both paths (and a mix) meet the oracle."""
+    full; PMVS_QUAD_ROWS caps that buffer so both paths (and a mix) meet the oracle.
+    PMVS_QUAD_WAVES_PER_CU = 1 caps the fit kernel's grid, so each lane fits several jobs
+    (the grid-stride path)."""
     import pmvs_amd as P
-    monkeypatch.setenv("PMVS_QUAD_ROWS", cap)
+    if cap != "-1":
+        monkeypatch.setenv("PMVS_QUAD_ROWS", cap)
+    monkeypatch.setenv("PMVS_QUAD_WAVES_PER_CU", qwaves)
     inp, p = P.synth_scene(8, 960, 540, level=1, supersample=2, nthreads=16)
     g = P.Scene(inp)
     o = oracle_mod.OracleScene(inp)

@@ -35,9 +35,9 @@ def _threads():
         return max(1, min(16, os.cpu_count() or 1))
 
 
-def _scene(views, w, h, nseeds, seed=21):
+def _scene(views, w, h, nseeds, seed=21, hard=False):
     import pmvs_amd as P
-    inp, p = P.synth_scene(views, w, h, level=0, csize=2, supersample=2, nthreads=_threads())
+    inp, p = P.synth_scene(views, w, h, level=0, csize=2, supersample=2, nthreads=_threads(), hard=hard)
     return inp, p, P.synth_candidates(p, inp.projections, nseeds, seed=seed)
 
 
@@ -48,20 +48,26 @@ def _seeds(g, cands):
 
 
 @pytest.mark.timeout(900)
-def test_loop_50_views_matches_oracle(gpu_available, oracle_mod):
+@pytest.mark.parametrize("hard", [False, True], ids=["plain", "hard"])
+def test_loop_50_views_matches_oracle(gpu_available, oracle_mod, hard):
     import pmvs_amd as P
     from test_gpu_parity_matrix import _same_patches
-    inp, p, cands = _scene(50, 640, 360, 300)
+    inp, p, cands = _scene(50, 640, 360, 300, hard=hard)
     g = P.Scene(inp)
     seeds = _seeds(g, cands)
     cap = 1 << 20
     out_g, log_g = g.run_loop(seeds, inp.threshold, cap=cap, **PROD)
     g.close()
     o = oracle_mod.OracleScene(inp)
+    oracle_mod.near_threshold(reset=True)
     out_o, log_o = o.run_loop(seeds, inp.threshold, cap=cap, nthreads=_threads(), **PROD)
+    near = oracle_mod.near_threshold(reset=True)
     o.close()
-    print(f"50-view loop: seeds {len(seeds)} -> {[it['patches'] for it in log_o]} patches")
-    assert len(out_o) > 50 * len(seeds)
+    print(f"50-view loop ({'hard' if hard else 'plain'}): seeds {len(seeds)} -> {[it['patches'] for it in log_o]} "
+          f"patches, ncc p1/p50 {np.percentile(out_o['ncc'], [1, 50]).round(3).tolist()}, near-threshold {near}")
+    assert len(out_o) > (10 if hard else 50) * len(seeds)
+    if hard:
+        assert near["constraint_near"] >= 100 and near["gains_near"] >= 10, near
     for a, b in zip(log_g, log_o):
         assert a["patches"] == b["patches"], (a, b)
         assert {k: v for k, v in a["expand"].items() if k not in P.ExpandStats.WORK} == b["expand"]
@@ -134,7 +140,8 @@ def _chamfer(a, b):
 def _gap(inp, ref, prod):
     cr, cp = _cells(inp, ref), _cells(inp, prod)
     unit = float(np.mean(ref["dscale"]))
-    h = np.linspace(0.0, 1.0, 21)
+    # NCC bins over [threshold - 0.3, 1] (the range accepted patches can take; 0.4 .. 1 here)
+    h = np.linspace(float(inp.threshold) - 0.3, 1.0, 21)
     hr = np.histogram(ref["ncc"], h)[0] / len(ref)
     hp = np.histogram(prod["ncc"], h)[0] / len(prod)
     dr, dp = _dilate(cr), _dilate(cp)
@@ -154,11 +161,12 @@ def _gap(inp, ref, prod):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("views,w,h,nseeds", [(10, 400, 300, 150), (50, 320, 180, 300)],
-                         ids=["10v_400x300", "50v_320x180"])
-def test_schedule_gap_vs_single_thread(gpu_available, views, w, h, nseeds):
+@pytest.mark.parametrize("views,w,h,nseeds,hard", [(10, 400, 300, 150, False), (50, 320, 180, 300, False),
+                                                   (10, 400, 300, 150, True)],
+                         ids=["10v_400x300", "50v_320x180", "10v_400x300_hard"])
+def test_schedule_gap_vs_single_thread(gpu_available, views, w, h, nseeds, hard):
     import pmvs_amd as P
-    inp, p, cands = _scene(views, w, h, nseeds)
+    inp, p, cands = _scene(views, w, h, nseeds, hard=hard)
     g = P.Scene(inp)
     seeds = _seeds(g, cands)
     cap = 1 << 20

@@ -35,13 +35,19 @@ CONFIGS = {
                                   opts=dict(sequence=3, max_angle_deg=25.0, threshold=0.6),
                                   vis="ring2"),
     "min4_thr08": dict(views=10, w=400, h=300, level=1, opts=dict(min_image_num=4, threshold=0.8)),
+    # photometrically hard scenes (per-view gain/bias, sensor noise, low-texture regions, an occluder):
+    # final NCCs spread over ~0.6-1 and image selection / filterOutside decisions sit near their thresholds
+    "hard_level0": dict(views=10, w=400, h=300, level=0, hard=True),
+    "hard_level1_masks": dict(views=8, w=480, h=360, level=1, hard=True, masks=True, edges=True,
+                              opts=dict(threshold=0.6)),
 }
+HARD_NEAR_MIN = {"constraint_near": 20, "gains_near": 2}  # near-threshold decisions a hard loop must make
 
 
 def build(cfg):
     import pmvs_amd as P
     inp, p = P.synth_scene(cfg["views"], cfg["w"], cfg["h"], level=cfg["level"], num_targets=cfg.get("targets"),
-                           supersample=2, **cfg.get("opts", {}))
+                           supersample=2, hard=cfg.get("hard", False), **cfg.get("opts", {}))
     V = cfg["views"]
     if cfg.get("masks"):
         inp.masks = blob_masks(V, cfg["h"], cfg["w"], 1, keep=0.9)
@@ -148,9 +154,16 @@ def test_full_loop_matrix(gpu_available, oracle_mod, name):
     r, _ = g.refine_batch(cands)
     seeds = P.patches_from_refined(r)
     out_g, log_g = g.run_loop(seeds, inp.threshold, wave=128, min_candidates=256)
+    oracle_mod.near_threshold(reset=True)
     out_o, log_o = o.run_loop(seeds, inp.threshold, wave=128, min_candidates=256)
+    near = oracle_mod.near_threshold(reset=True)
     g.close()
     o.close()
+    print(f"{name}: {[it['patches'] for it in log_o]} patches, ncc p1/p50 "
+          f"{np.percentile(out_o['ncc'], [1, 50]).round(3).tolist()}, near-threshold decisions {near}")
+    if CONFIGS[name].get("hard"):
+        for k, v in HARD_NEAR_MIN.items():
+            assert near[k] >= v, (name, near)
     assert len(seeds) > 0 and len(out_o) > len(seeds)
     for a, b in zip(log_g, log_o):
         assert a["patches"] == b["patches"], (a, b)
