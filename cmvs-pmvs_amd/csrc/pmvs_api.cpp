@@ -208,6 +208,16 @@ struct pmvs_scene {
   pmvs_allgather_fn shard_fn = nullptr;
   void* shard_ctx = nullptr;
   pmvs_rccl* shard_rccl = nullptr;  // set: the records go device to device (pmvs_scene_set_shard_rccl)
+  // cluster boundary exchange (pmvs_scene_set_cluster)
+  int cl_rank = 0, cl_world = 1;
+  pmvs_allgather_fn cl_fn = nullptr;
+  void* cl_ctx = nullptr;
+  pmvs_rccl* cl_rccl = nullptr;
+  DBuf<unsigned char> cl_shared;
+  DBuf<int> cl_ids, cl_id2idx;
+  int cl_maxid = -1;
+  ClusterBuffers cbuf;
+  RefineHost rhost;             // host libm step of every refine batch (launch_refine)
   int xkept = -1, lkept = -1;   // models kept on the device for pmvs_expand_fetch / pmvs_loop_fetch
   std::vector<pmvs_patch> skept; // seeds kept for pmvs_seed_fetch (pmvs_seed_run with out = NULL, cap = 0)
   bool seeds_kept = false;
@@ -227,6 +237,7 @@ struct pmvs_scene {
   DBuf<float> tout;
   DBuf<int> tvalid;
   ~pmvs_scene() {
+    cl_shared.release(); cl_ids.release(); cl_id2idx.release();
     fpatches2.release(); views.release(); pyr.release(); masks.release(); edges.release(); vis_off.release(); vis.release();
     bindexes.release(); scratch.release(); stats.release(); jobs.release(); fpatches.release(); fkeep.release(); cand.release(); res.release(); evq.release();
     evout.release(); tq.release(); tout.release(); tvalid.release();
@@ -287,10 +298,14 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
     for (int t = 0; t < d->num_targets; ++t) {
       long long w = d->views[t].width, h = d->views[t].height;
       for (int l = 0; l < d->level; ++l) { w /= 2; h /= 2; }
-      cells += ((w + d->csize - 1) / d->csize) * ((h + d->csize - 1) / d->csize);
+      const long long gw = (w + d->csize - 1) / d->csize, gh = (h + d->csize - 1) / d->csize;
+      // pmvs_patch keeps cell coordinates as int16 (include/pmvs_amd.h)
+      if (gw > 32767 || gh > 32767) return fail(PMVS_EUNSUPPORTED, "view %d: %lld x %lld cells (at most 32767 a side)", t, gw, gh);
+      cells += gw * gh;
     }
     if (cells > INT_MAX) return fail(PMVS_EUNSUPPORTED, "%lld target cells at level %d exceed 2^31 - 1", cells, d->level);
   }
+  if (d->num_views > 32767) return fail(PMVS_EUNSUPPORTED, "%d views (pmvs_patch image indexes are 16-bit)", d->num_views);
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(PMVS_EDEVICE, "no HIP device available");
   if (device < 0 || device >= ndev) return fail(PMVS_EINVAL, "device %d of %d", device, ndev);
@@ -636,11 +651,13 @@ pmvs_status pmvs_seed_run(pmvs_scene* sc, const pmvs_point* points, const int32_
     hipError_t e = hipMemsetAsync(&sc->stats.p->queue, 0, 3 * sizeof(unsigned long long), sc->stream);
     if (e != hipSuccess) return e;
     return launch_refine(sc->ds, d_in, sc->jobs.p, d_out, m, sc->stats.p, sc->grid, sc->refine_grid, sc->tslots,
-                         sc->stream, sc->kev);
+                         sc->stream, sc->kev, sc->rhost);
   };
   SeedOutput so;
   const hipError_t e = seed_pass(sc->ds, sc->hviews, in, sc->stream, refine, so);
   if (e == hipErrorOutOfMemory) return fail(PMVS_ENOMEM, "seed phase: device memory");
+  if (e == hipErrorNotSupported)
+    return fail(PMVS_EUNSUPPORTED, "seed phase: a candidate's image list exceeds %d entries", PMVS_MAX_IMAGES);
   HIPCHK(e);
   sc->last_refine = false;
   const int ns = (int)so.seeds.size();
@@ -752,7 +769,7 @@ pmvs_status pmvs_refine_batch_device(pmvs_scene* sc, const pmvs_candidate* d_in,
   HIPCHK(hipMemsetAsync(sc->stats.p, 0, sizeof(DevStats), sc->stream));
   HIPCHK(hipEventRecord(sc->ev0, sc->stream));
   HIPCHK(launch_refine(sc->ds, d_in, sc->jobs.p, d_out, n, sc->stats.p, sc->grid, sc->refine_grid, sc->tslots, sc->stream,
-                       sc->kev));
+                       sc->kev, sc->rhost));
   HIPCHK(hipEventRecord(sc->ev1, sc->stream));
   sc->last_refine = true;
   return PMVS_OK;
@@ -909,8 +926,11 @@ pmvs_status pmvs_filter_run(pmvs_scene* sc, pmvs_patch* patches, int32_t n, int3
   HIPCHK(hipMemcpyAsync(sc->fpatches.p, patches, (size_t)n * sizeof(pmvs_patch), hipMemcpyHostToDevice, sc->stream));
   HIPCHK(hipEventRecord(sc->ev0, sc->stream));
   int counts[4], overflow = 0;
-  HIPCHK(filter_pass(sc->ds, sc->fbuf, sc->fpatches.p, n, tgoff[sc->ds.tnum], tgoff.data(), sc->grid, sc->stream, counts,
-                     &overflow, sc->fkeep.p));
+  const hipError_t fe = filter_pass(sc->ds, sc->fbuf, sc->fpatches.p, n, tgoff[sc->ds.tnum], tgoff.data(), sc->grid,
+                                    sc->stream, counts, &overflow, sc->fkeep.p);
+  if (fe == hipErrorNotSupported)
+    return fail(PMVS_EUNSUPPORTED, "filter pass: a patch is visible in more than %d target images", PMVS_MAX_IMAGES);
+  HIPCHK(fe);
   HIPCHK(hipEventRecord(sc->ev1, sc->stream));
   HIPCHK(hipMemcpyAsync(patches, sc->fpatches.p, (size_t)n * sizeof(pmvs_patch), hipMemcpyDeviceToHost, sc->stream));
   HIPCHK(hipMemcpyAsync(keep, sc->fkeep.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, sc->stream));
@@ -959,6 +979,23 @@ Shard make_shard(const pmvs_scene* sc) {
     void* ctx = sc->shard_ctx;
     sh.exchange = [fn, ctx](const void* send, size_t bytes, void* recv) { return fn(ctx, send, (int64_t)bytes, recv); };
     if (pmvs_rccl* comm = sc->shard_rccl)
+      sh.exchange_dev = [comm](const void* dsend, size_t bytes, void* drecv, hipStream_t st) {
+        return pmvs_rccl_allgather_device(comm, dsend, (int64_t)bytes, drecv, st);
+      };
+  }
+  return sh;
+}
+
+// The scene's cluster exchange channel (pmvs_scene_set_cluster / _rccl).
+Shard make_cluster_shard(const pmvs_scene* sc) {
+  Shard sh;
+  if (sc->cl_fn && sc->cl_world > 1) {
+    sh.rank = sc->cl_rank;
+    sh.world = sc->cl_world;
+    pmvs_allgather_fn fn = sc->cl_fn;
+    void* ctx = sc->cl_ctx;
+    sh.exchange = [fn, ctx](const void* send, size_t bytes, void* recv) { return fn(ctx, send, (int64_t)bytes, recv); };
+    if (pmvs_rccl* comm = sc->cl_rccl)
       sh.exchange_dev = [comm](const void* dsend, size_t bytes, void* drecv, hipStream_t st) {
         return pmvs_rccl_allgather_device(comm, dsend, (int64_t)bytes, drecv, st);
       };
@@ -1032,7 +1069,7 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
     ++launches;
     pending = true;
     return launch_refine(sc->ds, d_in, sc->jobs.p, d_out, m, sc->stats.p, sc->grid, sc->refine_grid, sc->tslots,
-                         sc->stream, sc->kev);
+                         sc->stream, sc->kev, sc->rhost);
   };
   const Shard sh = make_shard(sc);
   long long sv[8];
@@ -1042,7 +1079,9 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
                                    sv, n_out, min_cands);
   if (handled) *handled = e != hipSuccess;  // expand_pass ends every failure with a header all ranks see
   if (e == hipErrorOutOfMemory)
-    return fail(PMVS_EUNSUPPORTED, "expansion: capacity %d exceeded or a patch has more than 1024 neighbours", cap);
+    return fail(PMVS_EUNSUPPORTED,
+                "expansion: capacity %d exceeded, a patch has more than 1024 neighbours, or a patch's image / "
+                "visible-target list exceeds %d entries", cap, PMVS_MAX_IMAGES);
   if (e == hipErrorUnknown && sh.world > 1) return fail(PMVS_EDEVICE, "expansion: the shard exchange or another rank failed");
   HIPCHK(e);
   if (handled) *handled = false;  // from here on a failure is this rank's alone
@@ -1084,6 +1123,8 @@ pmvs_status filter_device(pmvs_scene* sc, int n, pmvs_filter_stats* stats, bool*
                                     sc->stream, counts, &overflow, sc->fkeep.p, &sh, &fh);
   if (fe != hipSuccess) {
     if (handled) *handled = fh;
+    if (fe == hipErrorNotSupported)
+      return fail(PMVS_EUNSUPPORTED, "filter pass: a patch is visible in more than %d target images", PMVS_MAX_IMAGES);
     return fail(PMVS_EDEVICE, "filter pass: %s", hipGetErrorString(fe));
   }
   // kernels launched after the pass's last exchange (small groups, collect, keep) fault only at
@@ -1179,9 +1220,22 @@ pmvs_status pmvs_run_loop(pmvs_scene* sc, const pmvs_patch* seeds, int32_t n, fl
   int cthr = 4, depth = 1, cur = n;
   // Sharded: a failure the peers have not seen is announced with one loop header (loop_header).
   const Shard lsh = make_shard(sc);
+  const Shard csh = make_cluster_shard(sc);  // cluster boundary exchange (pmvs_scene_set_cluster)
+  if (lsh.world > 1 && csh.world > 1) return fail(PMVS_EINVAL, "a scene is either sharded or a cluster, not both");
+  const Shard& hsh = (csh.world > 1) ? csh : lsh;  // the channel of the loop's error headers
   auto fail_loop = [&](pmvs_status s0, bool peers_know) {
-    if (lsh.world > 1 && !peers_know) (void)loop_header(lsh, 1);
+    if (hsh.world > 1 && !peers_know) (void)loop_header(hsh, 1);
     return s0;
+  };
+  // the model without foreign patches, compacted through fpatches2
+  auto drop = [&](int n, int* kept) -> pmvs_status {
+    if (n == 0) { *kept = 0; return PMVS_OK; }
+    if (ensure_keep_data(sc, sc->fpatches2, std::max(sc->fpatches.n, (size_t)n))) return fail(PMVS_ENOMEM, "model");
+    if (drop_foreign(sc->fbuf, sc->fpatches.p, n, sc->fpatches2.p, kept, sc->stream) != hipSuccess)
+      return fail(PMVS_EDEVICE, "foreign patches");
+    std::swap(sc->fpatches.p, sc->fpatches2.p);
+    std::swap(sc->fpatches.n, sc->fpatches2.n);
+    return PMVS_OK;
   };
   for (int it = 0; it < iterations; ++it) {
     sc->ds.depth = depth;
@@ -1208,14 +1262,35 @@ pmvs_status pmvs_run_loop(pmvs_scene* sc, const pmvs_patch* seeds, int32_t n, fl
     }
     cur = kept;
     li.patches = kept;
+    if (csh.world > 1 && it + 1 < iterations) {  // cluster boundary exchange before the next iteration
+      int own = 0;
+      if ((st = drop(cur, &own))) return fail_loop(st, false);
+      li.patches = own;
+      const ClusterMaps cm{sc->cl_shared.p, sc->cl_ids.p, sc->cl_id2idx.p, sc->cl_maxid};
+      long long xs[3] = {0, 0, 0};
+      bool agreed = false;
+      int nn2 = own;
+      const hipError_t xe = cluster_exchange(sc->ds, sc->cbuf, cm, sc->fpatches.p, own, sc->fpatches.p, sc->fpatches.n, &nn2,
+                                             csh, sc->stream, xs, agreed);
+      if (xe != hipSuccess) return fail_loop(fail(PMVS_EDEVICE, "cluster exchange: %s", hipGetErrorString(xe)), agreed);
+      cur = nn2;
+      li.boundary_sent = xs[0];
+      li.boundary_received = xs[1];
+      li.boundary_inserted = xs[2];
+    }
     if (iters) iters[it] = li;
     ncc -= 0.05f;
     before -= 0.05f;
     cthr = 2;
     ++depth;
   }
+  if (csh.world > 1) {  // the cluster's own patches only
+    int own = 0;
+    if ((st = drop(cur, &own))) return fail_loop(st, false);
+    cur = own;
+  }
   if (hipStreamSynchronize(sc->stream) != hipSuccess) return fail_loop(fail(PMVS_EDEVICE, "loop synchronisation"), false);
-  if (lsh.world > 1 && loop_header(lsh, 0) != 0) return fail(PMVS_EDEVICE, "sharded loop: another rank failed");
+  if (hsh.world > 1 && loop_header(hsh, 0) != 0) return fail(PMVS_EDEVICE, "sharded loop: another rank failed");
   *n_out = cur;
   sc->lkept = cur;
   return PMVS_OK;
@@ -1240,6 +1315,66 @@ pmvs_status pmvs_scene_set_shard(pmvs_scene* sc, int32_t rank, int32_t world, pm
   sc->shard_ctx = ctx;
   sc->shard_rccl = nullptr;
   return PMVS_OK;
+}
+
+pmvs_status pmvs_scene_set_cluster(pmvs_scene* sc, int32_t rank, int32_t world, const int32_t* image_ids,
+                                   pmvs_allgather_fn fn, void* ctx) {
+  if (!sc || world < 1 || rank < 0 || rank >= world || (world > 1 && (!fn || !image_ids)))
+    return fail(PMVS_EINVAL, "invalid cluster");
+  sc->cl_world = 1;
+  sc->cl_fn = nullptr;
+  sc->cl_rccl = nullptr;
+  if (world == 1) return PMVS_OK;
+  const int num = sc->ds.num, tnum = sc->ds.tnum;
+  int maxid = -1;
+  for (int i = 0; i < num; ++i) {
+    if (image_ids[i] < 0) return fail(PMVS_EINVAL, "image_ids[%d] = %d", i, image_ids[i]);
+    maxid = std::max(maxid, image_ids[i]);
+  }
+  if (maxid > (1 << 26)) return fail(PMVS_EUNSUPPORTED, "image number %d", maxid);
+  std::vector<int> id2idx((size_t)maxid + 1, -1);
+  for (int i = 0; i < num; ++i) {
+    if (id2idx[image_ids[i]] >= 0) return fail(PMVS_EINVAL, "image number %d appears twice", image_ids[i]);
+    id2idx[image_ids[i]] = i;
+  }
+  // all-gather of the target image numbers (collective): a target is shared when another cluster
+  // has it as a target too
+  std::vector<int> mine(1 + PMVS_MAX_TARGETS, -1), all((size_t)(1 + PMVS_MAX_TARGETS) * world, -1);
+  mine[0] = tnum;
+  for (int t = 0; t < tnum; ++t) mine[1 + t] = image_ids[t];
+  if (fn(ctx, mine.data(), (int64_t)(mine.size() * sizeof(int)), all.data()) != 0)
+    return fail(PMVS_EDEVICE, "cluster setup: the all-gather failed");
+  std::vector<unsigned char> shared(std::max(tnum, 1), 0);
+  for (int r = 0; r < world; ++r) {
+    if (r == rank) continue;
+    const int* o = all.data() + (size_t)r * (1 + PMVS_MAX_TARGETS);
+    for (int k = 0; k < std::min(o[0], PMVS_MAX_TARGETS); ++k) {
+      const int id = o[1 + k];
+      if (0 <= id && id <= maxid && id2idx[id] >= 0 && id2idx[id] < tnum) shared[id2idx[id]] = 1;
+    }
+  }
+  HIPCHK(hipSetDevice(sc->device));
+  pmvs_status st;
+  if ((st = ensure(sc->cl_shared, shared.size())) || (st = ensure(sc->cl_ids, (size_t)num)) ||
+      (st = ensure(sc->cl_id2idx, id2idx.size())))
+    return st;
+  HIPCHK(hipMemcpy(sc->cl_shared.p, shared.data(), shared.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(sc->cl_ids.p, image_ids, (size_t)num * sizeof(int), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(sc->cl_id2idx.p, id2idx.data(), id2idx.size() * sizeof(int), hipMemcpyHostToDevice));
+  sc->cl_maxid = maxid;
+  sc->cl_rank = rank;
+  sc->cl_world = world;
+  sc->cl_fn = fn;
+  sc->cl_ctx = ctx;
+  return PMVS_OK;
+}
+
+pmvs_status pmvs_scene_set_cluster_rccl(pmvs_scene* sc, int32_t rank, int32_t world, const int32_t* image_ids,
+                                        pmvs_rccl* comm) {
+  if (!sc || !comm) return fail(PMVS_EINVAL, "invalid cluster");
+  const pmvs_status st = pmvs_scene_set_cluster(sc, rank, world, image_ids, &pmvs_rccl_allgather, comm);
+  if (st == PMVS_OK && world > 1) sc->cl_rccl = comm;
+  return st;
 }
 
 pmvs_status pmvs_scene_set_shard_rccl(pmvs_scene* sc, int32_t rank, int32_t world, pmvs_rccl* comm) {

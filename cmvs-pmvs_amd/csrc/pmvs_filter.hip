@@ -69,12 +69,45 @@ __device__ __forceinline__ int lane_id_w() { return threadIdx.x & 63; }
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ float uni_f(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
 
+__host__ __device__ inline Reg reg_zero() {
+  Reg r;
+  for (int k = 0; k < REGW; ++k) r.w[k] = 0ull;
+  return r;
+}
+__host__ __device__ inline Reg reg_first(int n) {  // entries 0 .. n-1
+  Reg r;
+  for (int k = 0; k < REGW; ++k)
+    r.w[k] = (n >= 64 * (k + 1)) ? ~0ull : (n > 64 * k ? ((1ull << (n - 64 * k)) - 1ull) : 0ull);
+  return r;
+}
+__host__ __device__ inline void reg_set(Reg& r, int i) { r.w[i >> 6] |= 1ull << (i & 63); }
+__host__ __device__ inline bool reg_test(const Reg& r, int i) { return (r.w[i >> 6] >> (i & 63)) & 1ull; }
+__device__ inline int reg_popc(const Reg& r) {
+  int c = 0;
+  for (int k = 0; k < REGW; ++k) c += __popcll(r.w[k]);
+  return c;
+}
+__host__ __device__ inline Reg reg_and(const Reg& a, const Reg& b) {
+  Reg r;
+  for (int k = 0; k < REGW; ++k) r.w[k] = a.w[k] & b.w[k];
+  return r;
+}
+// visits the set entries in increasing order: for (int i = reg_next(m, -1); i >= 0; i = reg_next(m, i))
+__device__ inline int reg_next(const Reg& r, int i) {
+  for (int k = (i + 1) >> 6; k < REGW; ++k) {
+    const int b = (k == ((i + 1) >> 6)) ? ((i + 1) & 63) : 0;
+    const unsigned long long m = (b >= 64) ? 0ull : (r.w[k] & (~0ull << b));
+    if (m) return 64 * k + __builtin_ctzll(m);
+  }
+  return -1;
+}
+
 struct FilterDev {
   const DScene* dummy;
   pmvs_patch* P;
   int n;
-  unsigned long long* preg;
-  unsigned long long* vreg;
+  Reg* preg;
+  Reg* vreg;
   const long long* tgoff;  // [tnum + 1] global cell offsets of the target images
   int tnum;
   // CSR organizer
@@ -88,6 +121,7 @@ struct FilterDev {
   long long ncells;
   int npg, nvp;        // entries in the pgrids / vpgrids lists
   int* err;            // [0] count, [1] first code (defensive bounds checks)
+  int* lovf;           // patches whose image / vimage list would exceed PMVS_MAX_IMAGES (an error, never a clamp)
   // Expansion only: registrations committed since the CSR lists were built, as per-cell chains
   // (head per cell, -1 = empty; item/next in a shared entry pool).  Every expansion reader is
   // insensitive to the order inside a cell list (findNeighbors sorts and uniques, computeGain
@@ -181,43 +215,41 @@ __device__ int is_visible(const DScene& s, const FilterDev& F, int p, int t, int
 // --------------------------------------------------------------------------- organizer build
 // CPatchOrganizerS::addPatch (patchOrganizerS.cpp:308-324): register every target entry of the
 // input patches (out-of-grid cells, undefined in the reference, are not registered).
-__global__ void init_reg_kernel(DScene s, const pmvs_patch* __restrict__ P, int n, unsigned long long* __restrict__ preg,
-                                unsigned long long* __restrict__ vreg) {
+__global__ void init_reg_kernel(DScene s, const pmvs_patch* __restrict__ P, int n, Reg* __restrict__ preg,
+                                Reg* __restrict__ vreg) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
   const pmvs_patch& q = P[p];
-  unsigned long long m = 0ull;
+  Reg m = reg_zero();
   for (int i = 0; i < q.num_images; ++i)
-    if (q.images[i] < s.tnum && in_grid(s, q.images[i], q.grids[i][0], q.grids[i][1])) m |= 1ull << i;
+    if (q.images[i] < s.tnum && in_grid(s, q.images[i], q.grids[i][0], q.grids[i][1])) reg_set(m, i);
   preg[p] = m;
-  vreg[p] = 0ull;
+  vreg[p] = reg_zero();
 }
 
-__global__ void keep_kernel(int n, const unsigned long long* __restrict__ preg, const int* __restrict__ rank,
+__global__ void keep_kernel(int n, const Reg* __restrict__ preg, const int* __restrict__ rank,
                             int* __restrict__ keep) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
   keep[p] = (rank[p] >= 0) ? 1 : 0;
 }
 
-__global__ void count_entries_kernel(const pmvs_patch* __restrict__ P, int n, const unsigned long long* __restrict__ reg,
+__global__ void count_entries_kernel(const pmvs_patch* __restrict__ P, int n, const Reg* __restrict__ reg,
                                      int vis, int* __restrict__ cnt) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
-  cnt[p] = __popcll(reg[p]);
+  cnt[p] = reg_popc(reg[p]);
 }
 
 __global__ void emit_entries_kernel(DScene s, const pmvs_patch* __restrict__ P, int n,
-                                    const unsigned long long* __restrict__ reg, int vis, const int* __restrict__ off,
+                                    const Reg* __restrict__ reg, int vis, const int* __restrict__ off,
                                     const long long* __restrict__ tgoff, unsigned long long* __restrict__ keys) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
-  unsigned long long m = reg[p];
+  const Reg m = reg[p];
   int o = off[p];
   const pmvs_patch& q = P[p];
-  while (m) {
-    const int i = __builtin_ctzll(m);
-    m &= m - 1;
+  for (int i = reg_next(m, -1); i >= 0; i = reg_next(m, i)) {
     const int t = vis ? q.vimages[i] : q.images[i];
     const int ix = vis ? q.vgrids[i][0] : q.grids[i][0];
     const int iy = vis ? q.vgrids[i][1] : q.grids[i][1];
@@ -240,16 +272,14 @@ __global__ void items_kernel(const unsigned long long* __restrict__ keys, int e,
 
 // first registered pgrids cell of each patch (collectPatches order key)
 __global__ void first_cell_kernel(DScene s, const pmvs_patch* __restrict__ P, int n,
-                                  const unsigned long long* __restrict__ preg, const long long* __restrict__ tgoff,
+                                  const Reg* __restrict__ preg, const long long* __restrict__ tgoff,
                                   unsigned long long* __restrict__ keys, int* __restrict__ nalive) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
-  unsigned long long m = preg[p];
+  const Reg m = preg[p];
   unsigned long long best = ~0ull;
   const pmvs_patch& q = P[p];
-  while (m) {
-    const int i = __builtin_ctzll(m);
-    m &= m - 1;
+  for (int i = reg_next(m, -1); i >= 0; i = reg_next(m, i)) {
     const int t = q.images[i];
     const unsigned long long cell = (unsigned long long)(tgoff[t] + (long long)q.grids[i][1] * gwidth(s, t) + q.grids[i][0]);
     if (cell < best) best = cell;
@@ -315,7 +345,7 @@ __global__ void depth_map_kernel(DScene s, FilterDev F, const float4* __restrict
 // CPatchOrganizerS::setVImagesVGrids (patchOrganizerS.cpp:429-459) per collected patch;
 // vreg = every vimages entry (addPatchVThread registers the first entry per image, and the
 // list never holds an image twice).
-__global__ void vimages_kernel(DScene s, FilterDev F, int additive, unsigned long long* __restrict__ vreg) {
+__global__ void vimages_kernel(DScene s, FilterDev F, int additive, Reg* __restrict__ vreg) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= F.nalive) return;
   const int p = F.order[i];
@@ -334,13 +364,16 @@ __global__ void vimages_kernel(DScene s, FilterDev F, int additive, unsigned lon
     const int iy = ((int)floorf(ic[1] + 0.5f)) / s.csize;
     if (is_visible(s, F, p, t, ix, iy, 0.5f) == 0) continue;
     if (get_edge(s, v, q.coord, s.level) == 0) continue;
-    if (q.num_vimages >= PMVS_MAX_IMAGES) break;
-    q.vimages[q.num_vimages] = t;
-    q.vgrids[q.num_vimages][0] = ix;
-    q.vgrids[q.num_vimages][1] = iy;
+    if (q.num_vimages >= PMVS_MAX_IMAGES) {  // more than PMVS_MAX_IMAGES targets see the patch: the pass fails
+      atomicAdd(F.lovf, 1);
+      break;
+    }
+    q.vimages[q.num_vimages] = (int16_t)t;
+    q.vgrids[q.num_vimages][0] = grid16(ix);
+    q.vgrids[q.num_vimages][1] = grid16(iy);
     q.num_vimages++;
   }
-  vreg[p] = (q.num_vimages >= 64) ? ~0ull : ((1ull << q.num_vimages) - 1ull);
+  vreg[p] = reg_first(q.num_vimages);
 }
 
 // --------------------------------------------------------------------------- filterOutside
@@ -386,13 +419,13 @@ __global__ void clear_fixed_kernel(const pmvs_patch* __restrict__ P, int n, int*
   if (P[p].fix) flags[p] = 0;
 }
 
-__global__ void apply_remove_kernel(int n, const int* __restrict__ remove, unsigned long long* __restrict__ preg,
-                                    unsigned long long* __restrict__ vreg, int* __restrict__ count) {
+__global__ void apply_remove_kernel(int n, const int* __restrict__ remove, Reg* __restrict__ preg,
+                                    Reg* __restrict__ vreg, int* __restrict__ count) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
   if (remove[p]) {
-    preg[p] = 0ull;
-    vreg[p] = 0ull;
+    preg[p] = reg_zero();
+    vreg[p] = reg_zero();
     atomicAdd(count, 1);
   }
 }
@@ -400,7 +433,7 @@ __global__ void apply_remove_kernel(int n, const int* __restrict__ remove, unsig
 // --------------------------------------------------------------------------- filterExact
 // filterExactThread (filter.cpp:291-340): one thread per registered pgrids entry; marks the
 // patch's images[] positions that are safe (visible at the cell or one of its 4 neighbours).
-__global__ void exact_entries_kernel(DScene s, FilterDev F, long long ncells, unsigned long long* __restrict__ safe) {
+__global__ void exact_entries_kernel(DScene s, FilterDev F, long long ncells, Reg* __restrict__ safe) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= ncells) return;
   const int b = F.pg_off[c], e = F.pg_off[c + 1];
@@ -423,7 +456,7 @@ __global__ void exact_entries_kernel(DScene s, FilterDev F, long long ncells, un
     if (ok)
       for (int i = 0; i < q.num_images; ++i)
         if (q.images[i] == t) {
-          atomicOr(&safe[p], 1ull << i);
+          atomicOr(&safe[p].w[i >> 6], 1ull << (i & 63));
           break;
         }
   }
@@ -432,8 +465,8 @@ __global__ void exact_entries_kernel(DScene s, FilterDev F, long long ncells, un
 // filterExact (filter.cpp:234-348) per collected, non-fixed patch: new list = safe targets in
 // increasing image order (the reference's image-major scan) with their cells, then the
 // non-target images; _timages = #safe.  need_ref[p] = 1 when setRefImage + setGrids follow.
-__global__ void exact_patch_kernel(DScene s, FilterDev F, const unsigned long long* __restrict__ safe,
-                                   unsigned long long* __restrict__ preg, unsigned long long* __restrict__ vreg,
+__global__ void exact_patch_kernel(DScene s, FilterDev F, const Reg* __restrict__ safe,
+                                   Reg* __restrict__ preg, Reg* __restrict__ vreg,
                                    int* __restrict__ need_ref, int* __restrict__ removed) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= F.nalive) return;
@@ -441,7 +474,7 @@ __global__ void exact_patch_kernel(DScene s, FilterDev F, const unsigned long lo
   pmvs_patch& q = F.P[p];
   need_ref[p] = 0;
   if (q.fix) return;
-  const unsigned long long sm = safe[p] & preg[p];
+  const Reg sm = reg_and(safe[p], preg[p]);
   int ni = 0;
   int imgs[PMVS_MAX_IMAGES], grd[PMVS_MAX_IMAGES][2];
   // the kept target entries in ascending image order (the reference loops over the targets and
@@ -450,11 +483,11 @@ __global__ void exact_patch_kernel(DScene s, FilterDev F, const unsigned long lo
   const int n0 = q.num_images;
   for (int k = 0; k < n0; ++k) {
     const int t = q.images[k];
-    if (t >= s.tnum || !((sm >> k) & 1ull)) continue;
+    if (t >= s.tnum || !reg_test(sm, k)) continue;
     int pos = 0;
     for (int k2 = 0; k2 < n0; ++k2) {
       const int t2 = q.images[k2];
-      pos += (t2 < s.tnum && ((sm >> k2) & 1ull) && (t2 < t || (t2 == t && k2 < k)));  // ties in list order
+      pos += (t2 < s.tnum && reg_test(sm, k2) && (t2 < t || (t2 == t && k2 < k)));  // ties in list order
     }
     imgs[pos] = t;
     grd[pos][0] = q.grids[k][0];
@@ -475,35 +508,33 @@ __global__ void exact_patch_kernel(DScene s, FilterDev F, const unsigned long lo
     q.grids[k][1] = grd[k][1];
   }
   q.num_images = ni;
-  unsigned long long m = 0ull;
-  for (int k = 0; k < q.timages; ++k) m |= 1ull << k;
-  preg[p] = m;
+  preg[p] = reg_first(q.timages);
   if (s.minImageNum <= ni) {
     need_ref[p] = 1;
   } else {
-    preg[p] = 0ull;
-    vreg[p] = 0ull;
+    preg[p] = reg_zero();
+    vreg[p] = reg_zero();
     atomicAdd(removed, 1);
   }
 }
 
 // after setRefImage: registered = target entries of the (reordered) list; empty list -> removed
 __global__ void exact_after_ref_kernel(DScene s, const pmvs_patch* __restrict__ P, const int* __restrict__ list, int m,
-                                       unsigned long long* __restrict__ preg, unsigned long long* __restrict__ vreg,
+                                       Reg* __restrict__ preg, Reg* __restrict__ vreg,
                                        int* __restrict__ removed) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= m) return;
   const int p = list[k];
   const pmvs_patch& q = P[p];
   if (q.num_images < s.minImageNum) {
-    preg[p] = 0ull;
-    vreg[p] = 0ull;
+    preg[p] = reg_zero();
+    vreg[p] = reg_zero();
     atomicAdd(removed, 1);
     return;
   }
-  unsigned long long r = 0ull;
+  Reg r = reg_zero();
   for (int i = 0; i < q.num_images; ++i)
-    if (q.images[i] < s.tnum) r |= 1ull << i;
+    if (q.images[i] < s.tnum) reg_set(r, i);
   preg[p] = r;
 }
 
@@ -830,14 +861,14 @@ __device__ float compute_radius_wave(const DScene& s, NbLds& L, const pmvs_patch
   const int lane = lane_id_w();
   const int ni = uni(q.num_images);
   __syncthreads();
-  if (lane < ni) {
-    const DView& v = s.views[q.images[lane]];
+  for (int k = lane; k < ni; k += 64) {
+    const DView& v = s.views[q.images[k]];
     float u = get_unit(s, v, q.coord);
     float ray[4] = {v.center[0] - q.coord[0], v.center[1] - q.coord[1], v.center[2] - q.coord[2], v.center[3] - q.coord[3]};
     unitize4(ray);
     const float den = dot4(ray, q.normal);
     u = (0.0f < den) ? __fdiv_rn(u, den) : 1073741824.0f;
-    L.units[lane] = u;
+    L.units[k] = u;
   }
   __syncthreads();
   float m1 = 3.0e38f, m2 = 3.0e38f;  // two smallest (nth_element(begin, begin + 1, end))
@@ -1548,9 +1579,9 @@ __global__ void prepare_kernel(DScene s, FilterDev F, const unsigned char* __res
     const int ix = ((int)floorf(ic[0] + 0.5f)) / s.csize;
     const int iy = ((int)floorf(ic[1] + 0.5f)) / s.csize;
     if (0 <= ix && ix < gwidth(s, t) && 0 <= iy && iy < gheight(s, t)) {
-      q.images[ni] = t;
-      q.grids[ni][0] = ix;
-      q.grids[ni][1] = iy;
+      q.images[ni] = (int16_t)t;
+      q.grids[ni][0] = (int16_t)ix;  // in the grid: fits
+      q.grids[ni][1] = (int16_t)iy;
       ni++;
     }
   }
@@ -1622,6 +1653,7 @@ __global__ __launch_bounds__(64) void depth_post_kernel(DScene s, FilterDev F, c
     // are not guaranteed to reconverge with lane 0 before the next ticket is broadcast.
     const int rstatus = uni(rr.status);
     int st = (rstatus == PMVS_FAIL_POST) ? 3 : 2;
+    if (rstatus == PMVS_FAIL_OVERFLOW && lane == 0) atomicAdd(overflow, 1);  // an error for the run, never a reject
     if (rstatus == PMVS_ACCEPTED) {
     st = 0;
     if (lane == 0) {
@@ -1629,12 +1661,14 @@ __global__ __launch_bounds__(64) void depth_post_kernel(DScene s, FilterDev F, c
       q.ncc = rr.ncc; q.dscale = rr.dscale; q.ascale = rr.ascale; q.tmp = rr.tmp; q.timages = rr.timages;
       q.flag = 1; q.fix = 0; q.dflag = 0; q.num_images = rr.num_images; q.num_vimages = 0;
     }
-    q.images[lane] = (lane < rr.num_images) ? rr.images[lane] : 0;
-    q.grids[lane][0] = (lane < rr.num_images) ? rr.grids[lane][0] : 0;
-    q.grids[lane][1] = (lane < rr.num_images) ? rr.grids[lane][1] : 0;
-    q.vimages[lane] = 0;
-    q.vgrids[lane][0] = 0;
-    q.vgrids[lane][1] = 0;
+    for (int e = lane; e < PMVS_MAX_IMAGES; e += 64) {
+      q.images[e] = (int16_t)((e < rr.num_images) ? rr.images[e] : 0);
+      q.grids[e][0] = grid16((e < rr.num_images) ? rr.grids[e][0] : 0);
+      q.grids[e][1] = grid16((e < rr.num_images) ? rr.grids[e][1] : 0);
+      q.vimages[e] = 0;
+      q.vgrids[e][0] = 0;
+      q.vgrids[e][1] = 0;
+    }
     __syncthreads();
     if (s.depth) {
       // setVImagesVGrids (patchOrganizerS.cpp:429-459): lane t tests target image t
@@ -1660,11 +1694,13 @@ __global__ __launch_bounds__(64) void depth_post_kernel(DScene s, FilterDev F, c
         const int nv = q.num_vimages;
         __syncthreads();
         if (take && nv + pos < PMVS_MAX_IMAGES) {
-          q.vimages[nv + pos] = t;
-          q.vgrids[nv + pos][0] = ix;
-          q.vgrids[nv + pos][1] = iy;
+          q.vimages[nv + pos] = (int16_t)t;
+          q.vgrids[nv + pos][0] = grid16(ix);
+          q.vgrids[nv + pos][1] = grid16(iy);
         }
         __syncthreads();
+        // more than PMVS_MAX_IMAGES visible targets: counted as an overflow (the run fails), never clamped silently
+        if (lane == 0 && nv + __popcll(mask) > PMVS_MAX_IMAGES) atomicAdd(overflow, 1);
         if (lane == 0) q.num_vimages = imin(PMVS_MAX_IMAGES, nv + __popcll(mask));
         __syncthreads();
       }
@@ -1735,8 +1771,8 @@ struct DeltaLists {  // the per-cell chains of FilterDev (expansion), writable
   int* next;
 };
 
-__global__ void add_patches_kernel(DScene s, FilterDev F, int first, int count, int rank0, unsigned long long* __restrict__ preg,
-                                   unsigned long long* __restrict__ vreg, int* __restrict__ order,
+__global__ void add_patches_kernel(DScene s, FilterDev F, int first, int count, int rank0, Reg* __restrict__ preg,
+                                   Reg* __restrict__ vreg, int* __restrict__ order,
                                    unsigned long long* __restrict__ dpkey, float* __restrict__ unit0) {
   const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= (long long)count * s.tnum) return;
@@ -1744,11 +1780,11 @@ __global__ void add_patches_kernel(DScene s, FilterDev F, int first, int count, 
   const int p = first + k;
   const pmvs_patch& q = F.P[p];
   if (t == 0) {
-    unsigned long long m = 0ull;
+    Reg m = reg_zero();
     for (int i = 0; i < q.num_images; ++i)
-      if (q.images[i] < s.tnum && in_grid(s, q.images[i], q.grids[i][0], q.grids[i][1])) m |= 1ull << i;
+      if (q.images[i] < s.tnum && in_grid(s, q.images[i], q.grids[i][0], q.grids[i][1])) reg_set(m, i);
     preg[p] = m;
-    vreg[p] = (q.num_vimages >= 64) ? ~0ull : ((1ull << q.num_vimages) - 1ull);
+    vreg[p] = reg_first(q.num_vimages);
     order[rank0 + k] = p;
     unit0[p] = get_unit(s, s.views[q.images[0]], q.coord);
   }
@@ -1830,7 +1866,11 @@ hipError_t FilterBuffers::reserve(int n_, long long ncells_, int tnum_, int grid
   cap_n = std::max(n_, cap_n);
   cap_cells = std::max(ncells_, cap_cells);
   cap_grid = std::max(grid_, cap_grid);
-  const size_t ne = (size_t)cap_n * PMVS_MAX_IMAGES;
+  // cell-list entries: about 16 per patch to start with (a C3 patch registers ~10-17), grown by
+  // ensure_entries to what build_lists counts -- not cap_n x PMVS_MAX_IMAGES
+  cap_e = std::max(cap_e, (size_t)cap_n * 16);
+  cap_pi = cap_vi = cap_e;
+  const size_t ne = cap_e;
   FCHK(dalloc(preg, cap_n)); FCHK(dalloc(vreg, cap_n)); FCHK(dalloc(tgoff, PMVS_MAX_TARGETS + 1));
   FCHK(dalloc(cnt, cap_n + 1)); FCHK(dalloc(off, cap_n + 1));
   FCHK(dalloc(keys, std::max(ne, (size_t)cap_n))); FCHK(dalloc(keys2, std::max(ne, (size_t)cap_n)));
@@ -1839,7 +1879,7 @@ hipError_t FilterBuffers::reserve(int n_, long long ncells_, int tnum_, int grid
   FCHK(dalloc(coordc, cap_n));
   FCHK(dalloc(order, cap_n)); FCHK(dalloc(rank, cap_n)); FCHK(dalloc(unit0, cap_n)); FCHK(dalloc(flags, cap_n));
   FCHK(dalloc(safe, cap_n)); FCHK(dalloc(need, cap_n)); FCHK(dalloc(list, cap_n));
-  FCHK(dalloc(scratch, (size_t)cap_grid * NB_SCR)); FCHK(dalloc(counters, 8));
+  FCHK(dalloc(scratch, (size_t)cap_grid * NB_SCR)); FCHK(dalloc(counters, 16));
   FCHK(dalloc(edge_off, cap_n + 1));
   // deferred filterQuad fits: up to 48 rows per patch on average, at most 2^27 rows (7.5 GB);
   // patches past the capacity are fitted in neighbor_kernel itself
@@ -1863,6 +1903,29 @@ hipError_t FilterBuffers::reserve(int n_, long long ncells_, int tnum_, int grid
   return hipSuccess;
 }
 
+// Grows the cell-list entry buffers (and the sort's temp storage) to e entries; the other per-patch
+// buffers keep their size.
+hipError_t FilterBuffers::ensure_entries(size_t e, int vis) {
+  size_t& ci = vis ? cap_vi : cap_pi;
+  if (e > ci) {  // only the list being built: the other one's items stay valid
+    ci = std::max(e, ci + ci / 2);
+    FCHK(dalloc(vis ? vp_items : pg_items, ci));
+  }
+  if (e <= cap_e) return hipSuccess;
+  cap_e = std::max(e, cap_e + cap_e / 2);
+  const size_t ne = std::max(cap_e, (size_t)cap_n);
+  FCHK(dalloc(keys, ne)); FCHK(dalloc(keys2, ne));
+  size_t t1 = 0;
+  FCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, t1, keys, keys2, (int)ne));
+  if (t1 > temp_bytes) {
+    if (temp) (void)hipFree(temp);
+    temp = nullptr;
+    temp_bytes = t1;
+    FCHK(hipMalloc(&temp, temp_bytes));
+  }
+  return hipSuccess;
+}
+
 namespace {
 
 struct Ctx {
@@ -1881,7 +1944,7 @@ struct Ctx {
     F.P = P; F.n = n; F.preg = B.preg; F.vreg = B.vreg; F.tgoff = B.tgoff; F.tnum = s.tnum;
     F.pg_off = B.pg_off; F.pg_items = B.pg_items; F.vp_off = B.vp_off; F.vp_items = B.vp_items;
     F.dpkey = B.dpkey; F.order = B.order; F.rank = B.rank; F.nalive = nalive; F.unit0 = B.unit0;
-    F.ncells = ncells; F.npg = npg; F.nvp = nvp; F.err = B.counters + 6;
+    F.ncells = ncells; F.npg = npg; F.nvp = nvp; F.err = B.counters + 6; F.lovf = B.counters + 8;
     F.pg_dhead = pg_dhead; F.vp_dhead = vp_dhead; F.d_item = d_item; F.d_next = d_next;
     F.coordc = coordc;
     return F;
@@ -1896,7 +1959,7 @@ static hipError_t read_int(const int* d, int* h, hipStream_t st) {
 // CSR cell lists from the registration masks (vis = 0: pgrids, 1: vpgrids)
 static hipError_t build_lists(Ctx& c, int vis) {
   FilterBuffers& B = c.B;
-  const unsigned long long* reg = vis ? B.vreg : B.preg;
+  const Reg* reg = vis ? B.vreg : B.preg;
   int* csr_off = vis ? B.vp_off : B.pg_off;
   int* items = vis ? B.vp_items : B.pg_items;
   hipLaunchKernelGGL(count_entries_kernel, dim3(nblk(c.n)), dim3(256), 0, c.st, c.P, c.n, reg, vis, B.cnt);
@@ -1906,6 +1969,8 @@ static hipError_t build_lists(Ctx& c, int vis) {
   int e = 0;
   FCHK(read_int(B.off + c.n, &e, c.st));
   (vis ? c.nvp : c.npg) = e;
+  FCHK(B.ensure_entries((size_t)e, vis));
+  items = vis ? B.vp_items : B.pg_items;  // (re)allocated by ensure_entries
   hipLaunchKernelGGL(emit_entries_kernel, dim3(nblk(c.n)), dim3(256), 0, c.st, c.s, c.P, c.n, reg, vis, B.off, B.tgoff,
                      B.keys);
   tb = B.temp_bytes;
@@ -2054,6 +2119,7 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
   c.coordc = B.coordc;  // written with every depth map of this pass (set_dm_vgrids)
   for (int k = 0; k < 4; ++k) counts[k] = 0;
   *overflow = 0;
+  FCHK(hipMemsetAsync(B.counters + 8, 0, sizeof(int), st));  // vimages list overflows (vimages_kernel)
   hipLaunchKernelGGL(init_reg_kernel, dim3(nblk(n)), dim3(256), 0, st, s, dP, n, B.preg, B.vreg);
   FCHK(set_dm_vgrids(c, 0));
   dbg(st, "set_dm_vgrids(0)");
@@ -2064,7 +2130,7 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
   dbg(st, "outside");
   FCHK(set_dm_vgrids(c, 1));
   // ---- filterExact
-  FCHK(hipMemsetAsync(B.safe, 0, n * sizeof(unsigned long long), st));
+  FCHK(hipMemsetAsync(B.safe, 0, n * sizeof(Reg), st));
   FCHK(hipMemsetAsync(B.counters + 2, 0, sizeof(int), st));
   hipLaunchKernelGGL(exact_entries_kernel, dim3(nblk(ncells)), dim3(256), 0, st, s, c.dev(), ncells, B.safe);
   FCHK(hipMemsetAsync(B.need, 0, n * sizeof(int), st));
@@ -2239,6 +2305,9 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
   FCHK(build_lists(c, 0));
   FCHK(collect(c));
   hipLaunchKernelGGL(keep_kernel, dim3(nblk(n)), dim3(256), 0, st, n, B.preg, B.rank, keep_dev);
+  int lovf = 0;
+  FCHK(read_int(B.counters + 8, &lovf, st));
+  if (lovf) return hipErrorNotSupported;  // a vimages list would exceed PMVS_MAX_IMAGES (reported by the API)
   return hipGetLastError();
 }
 
@@ -2303,7 +2372,7 @@ __global__ void gather_slots_kernel(const int* __restrict__ slots, int m, const 
 // Collected patches: flag = 1 (clearFlags + collectPatches(queue), patchOrganizerS.cpp) and their
 // _tmp in collect order (the queue's initial contents).
 __global__ void collect_flags_kernel(pmvs_patch* __restrict__ P, const int* __restrict__ order, int na,
-                                     float* __restrict__ qtmp, int* __restrict__ rank) {
+                                     float* __restrict__ qtmp, int* __restrict__ rank, int* __restrict__ foreign) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= na) return;
   pmvs_patch& q = P[order[i]];
@@ -2311,6 +2380,7 @@ __global__ void collect_flags_kernel(pmvs_patch* __restrict__ P, const int* __re
   const float t = q.tmp;
   qtmp[i] = (t == 0.0f) ? 0.0f : t;  // -0 as +0: the radix order then agrees with QCmp's `<`
   rank[i] = i;
+  foreign[i] = (q.fix == PMVS_FIX_FOREIGN);  // another cluster's boundary patch: never expanded here
 }
 
 // Compact per-candidate record the host commit reads (instead of two full patch records):
@@ -2380,16 +2450,15 @@ __global__ void dflag_kernel(pmvs_patch* __restrict__ P, const int2* __restrict_
   if (k < n) P[upd[k].x].dflag |= upd[k].y;
 }
 
-__global__ void alive_reg_kernel(int n, const int* __restrict__ alive, unsigned long long* __restrict__ preg,
-                                 unsigned long long* __restrict__ vreg, const pmvs_patch* __restrict__ P) {
+__global__ void alive_reg_kernel(int n, const int* __restrict__ alive, Reg* __restrict__ preg,
+                                 Reg* __restrict__ vreg, const pmvs_patch* __restrict__ P) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
   if (!alive[p]) {
-    preg[p] = 0ull;
-    vreg[p] = 0ull;
+    preg[p] = reg_zero();
+    vreg[p] = reg_zero();
   } else {
-    const int nv = P[p].num_vimages;
-    vreg[p] = (nv >= 64) ? ~0ull : ((1ull << nv) - 1ull);
+    vreg[p] = reg_first(P[p].num_vimages);
   }
 }
 
@@ -3001,10 +3070,11 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   // pgrids holds a patch, per target cell; the host keeps only the queue
   // The collected patches enter the queue in collect order (seq = collect rank); their max-_tmp
   // order (QCmp: _tmp descending, ties by seq) is a stable descending radix sort on the device.
-  FCHK(X.pin.ensure(3 * (size_t)std::max(1, c.nalive) * sizeof(int)));
+  FCHK(X.pin.ensure(4 * (size_t)std::max(1, c.nalive) * sizeof(int)));
   int* order = X.pin.as<int>();
   int* srank = order + c.nalive;
   float* qtmp = reinterpret_cast<float*>(srank + c.nalive);
+  int* qforeign = reinterpret_cast<int*>(qtmp + c.nalive);  // by collect rank
   const size_t na1 = (size_t)std::max(1, c.nalive);
   FCHK(grow(X.qtmp, X.cap_qtmp, na1));
   FCHK(grow(X.qkey, X.cap_qkey, na1));
@@ -3013,7 +3083,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   FCHK(grow(X.occ, X.cap_occ, (size_t)ncells));
   if (c.nalive) {
     hipLaunchKernelGGL(collect_flags_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, dP, B.order, c.nalive, X.qtmp,
-                       X.qrank);
+                       X.qrank, B.need);
     size_t tb = 0;
     FCHK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, X.qtmp, X.qkey, X.qrank, X.qrank2, c.nalive, 0, 32, st));
     if (tb > X.cap_qsort) {
@@ -3032,14 +3102,17 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
     FCHK(hipMemcpyAsync(order, B.order, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
     FCHK(hipMemcpyAsync(qtmp, X.qkey, c.nalive * sizeof(float), hipMemcpyDeviceToHost, st));
     FCHK(hipMemcpyAsync(srank, X.qrank2, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
+    FCHK(hipMemcpyAsync(qforeign, B.need, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
   }
   FCHK(grow(X.counts, X.cap_cnt, (size_t)ncells));
   FCHK(hipMemsetAsync(X.counts, 0, ncells, st));
   FCHK(hipStreamSynchronize(st));
   // The max-_tmp queue (P_compare; ties: earlier push first): the collected patches as a sorted
   // run, the patches pushed during the run in a heap, popped by merging the two.
-  std::vector<QItem> initial(c.nalive);
-  for (int j = 0; j < c.nalive; ++j) initial[j] = {qkey(qtmp[j], srank[j]), order[srank[j]]};
+  std::vector<QItem> initial;
+  initial.reserve(c.nalive);
+  for (int j = 0; j < c.nalive; ++j)  // collectPatches(queue) without other clusters' boundary patches
+    if (!qforeign[srank[j]]) initial.push_back({qkey(qtmp[j], srank[j]), order[srank[j]]});
   const QCmp less;  // less(a, b): a has lower priority than b
   size_t ihead = 0;
   std::priority_queue<QItem, std::vector<QItem>, QCmp> queue;
@@ -3379,5 +3452,186 @@ hipError_t compact_model(FilterBuffers& B, const pmvs_patch* src, int n, const i
 hipError_t fill_int(int* a, int n, int v, hipStream_t st) {
   if (n > 0) hipLaunchKernelGGL(fill_int_kernel, dim3(nblk(n)), dim3(256), 0, st, a, n, v);
   return hipGetLastError();
+}
+
+// ============================================================================ cluster exchange
+// CMVS runs one pmvs2 per cluster (genOption.cpp:73-108); its clusters overlap in target images
+// (CBundle::addImagesP, bundle.cpp:1003-1160), so the same surface is reconstructed by several
+// runs.  With one cluster per GPU, after every loop iteration each rank all-gathers the patches
+// it holds in shared target images and inserts the other ranks' ones as the reference's
+// readPatches inserts another run's patches (patchOrganizerS.cpp:133-197: image2index, _vimages
+// cleared, setGrids, addPatch), fixed (never filtered) and never expanded (PMVS_FIX_FOREIGN): they
+// occupy their cells, so this rank's expansion does not duplicate them, and they take part in the
+// depth maps and visibility tests of the filters.
+__global__ void own_flags_kernel(const pmvs_patch* __restrict__ P, int n, int* __restrict__ keep) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n) keep[p] = (P[p].fix != PMVS_FIX_FOREIGN) ? 1 : 0;
+}
+
+__global__ void boundary_flags_kernel(DScene s, const pmvs_patch* __restrict__ P, int n,
+                                      const unsigned char* __restrict__ shared_t, int* __restrict__ f) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const pmvs_patch& q = P[p];
+  int b = 0;
+  if (q.fix != PMVS_FIX_FOREIGN)
+    for (int k = 0; k < q.num_images; ++k) {
+      const int t = q.images[k];
+      if (t < s.tnum && shared_t[t] && in_grid(s, t, q.grids[k][0], q.grids[k][1])) b = 1;
+    }
+  f[p] = b;
+}
+
+__global__ void boundary_pack_kernel(const pmvs_patch* __restrict__ P, int n, const int* __restrict__ f,
+                                     const int* __restrict__ pos, const int* __restrict__ ids, BRec* __restrict__ out) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n || !f[p]) return;
+  const pmvs_patch& q = P[p];
+  BRec& r = out[pos[p]];
+  for (int c = 0; c < 4; ++c) { r.coord[c] = q.coord[c]; r.normal[c] = q.normal[c]; }
+  r.ncc = q.ncc; r.dscale = q.dscale; r.ascale = q.ascale;
+  r.num_images = q.num_images;
+  for (int k = 0; k < q.num_images; ++k) r.ids[k] = ids[q.images[k]];
+}
+
+// slot j of the received block: rank j / M, record j % M (rank `me` and the padding are skipped)
+__global__ void boundary_insert_kernel(DScene s, const BRec* __restrict__ in, int world, int M, int me,
+                                       const int* __restrict__ cnts, const int* __restrict__ id2idx, int maxid,
+                                       pmvs_patch* __restrict__ outp, int* __restrict__ ok) {
+  const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= (long long)world * M) return;
+  const int r = (int)(j / M), k = (int)(j - (long long)r * M);
+  ok[j] = 0;
+  if (r == me || k >= cnts[r]) return;
+  const BRec& b = in[j];
+  auto map = [&](int id) { return (0 <= id && id <= maxid) ? id2idx[id] : -1; };
+  if (b.num_images < 1 || b.num_images > PMVS_MAX_IMAGES || map(b.ids[0]) < 0) return;  // reference image not here
+  pmvs_patch& q = outp[j];
+  for (int c = 0; c < 4; ++c) { q.coord[c] = b.coord[c]; q.normal[c] = b.normal[c]; }
+  q.ncc = b.ncc; q.dscale = b.dscale; q.ascale = b.ascale; q.tmp = 0.0f;
+  q.flag = 1; q.fix = PMVS_FIX_FOREIGN; q.dflag = 0; q.num_vimages = 0;
+  int ni = 0, nt = 0;
+  for (int e = 0; e < b.num_images; ++e) {  // CPatchOrganizerS::image2index (patchOrganizerS.cpp:16-41)
+    const int v = map(b.ids[e]);
+    if (v < 0) continue;
+    float ic[3];
+    project(s.views[v], q.coord, s.level, ic);  // setGrids (patchOrganizerS.cpp:410-419)
+    q.images[ni] = (int16_t)v;
+    q.grids[ni][0] = grid16(((int)floorf(ic[0] + 0.5f)) / s.csize);
+    q.grids[ni][1] = grid16(((int)floorf(ic[1] + 0.5f)) / s.csize);
+    if (v < s.tnum && in_grid(s, v, q.grids[ni][0], q.grids[ni][1])) ++nt;
+    ++ni;
+  }
+  q.num_images = ni;
+  q.timages = 0;
+  for (int e = 0; e < ni; ++e) q.timages += (q.images[e] < s.tnum);
+  ok[j] = (nt > 0) ? 1 : 0;  // registered in none of this scene's cells: nothing to insert
+}
+
+ClusterBuffers::~ClusterBuffers() {
+  void* ps[] = {send, recv, ins, flags, pos, cnts, temp};
+  for (void* p : ps)
+    if (p) (void)hipFree(p);
+}
+
+static hipError_t scan_count(ClusterBuffers& CB, const int* f, int* pos, int n, int* total, hipStream_t st) {
+  size_t tb = 0;
+  FCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, f, pos, n + 1, st));
+  if (tb > CB.temp_bytes) {
+    if (CB.temp) (void)hipFree(CB.temp);
+    CB.temp = nullptr;
+    CB.temp_bytes = 0;
+    FCHK(hipMalloc(&CB.temp, tb));
+    CB.temp_bytes = tb;
+  }
+  tb = CB.temp_bytes;
+  FCHK(hipcub::DeviceScan::ExclusiveSum(CB.temp, tb, f, pos, n + 1, st));
+  return read_int(pos + n, total, st);
+}
+
+hipError_t drop_foreign(FilterBuffers& B, const pmvs_patch* src, int n, pmvs_patch* dst, int* n_out, hipStream_t st) {
+  *n_out = 0;
+  if (n <= 0) return hipSuccess;
+  FCHK(B.reserve(n, B.cap_cells, 0, B.cap_grid));
+  hipLaunchKernelGGL(own_flags_kernel, dim3(nblk(n)), dim3(256), 0, st, src, n, B.flags);
+  return compact_model(B, src, n, B.flags, dst, n_out, st);
+}
+
+hipError_t cluster_exchange(const DScene& s, ClusterBuffers& CB, const ClusterMaps& cm, const pmvs_patch* src, int n,
+                            pmvs_patch*& dst, size_t& dst_cap, int* n_out, const Shard& sh, hipStream_t st,
+                            long long xstats[3], bool& agreed) {
+  agreed = false;
+  xstats[0] = xstats[1] = xstats[2] = 0;
+  *n_out = n;
+  const int G = sh.world, me = sh.rank;
+  // ---- this rank's boundary patches
+  int m = 0;
+  hipError_t le = grow(CB.flags, CB.cap_flags, (size_t)n + 1);
+  if (le == hipSuccess) le = grow(CB.pos, CB.cap_pos, (size_t)n + 1);
+  if (le == hipSuccess && n > 0) {
+    hipLaunchKernelGGL(boundary_flags_kernel, dim3(nblk(n)), dim3(256), 0, st, s, src, n, cm.shared_t, CB.flags);
+    le = hipMemsetAsync(CB.flags + n, 0, sizeof(int), st);
+    if (le == hipSuccess) le = scan_count(CB, CB.flags, CB.pos, n, &m, st);
+  }
+  if (le == hipSuccess) le = grow(CB.send, CB.cap_send, (size_t)std::max(m, 1));
+  if (le == hipSuccess && m > 0) {
+    hipLaunchKernelGGL(boundary_pack_kernel, dim3(nblk(n)), dim3(256), 0, st, src, n, CB.flags, CB.pos, cm.ids, CB.send);
+    le = hipGetLastError();
+  }
+  // ---- header all-gather {error, count}: every rank learns every count (and any failure)
+  int hdr[2] = {(int)le, m};
+  std::vector<int> hall(2 * (size_t)G, 0);
+  agreed = true;
+  if (sh.exchange(hdr, sizeof(hdr), hall.data()) != 0) return hipErrorUnknown;
+  int M = 0;
+  std::vector<int> cnts(G, 0);
+  for (int r = 0; r < G; ++r) {
+    if (hall[2 * r] != 0 && le == hipSuccess) le = hipErrorUnknown;  // a peer failed
+    cnts[r] = hall[2 * r + 1];
+    M = std::max(M, cnts[r]);
+  }
+  FCHK(le);
+  xstats[0] = m;
+  for (int r = 0; r < G; ++r)
+    if (r != me) xstats[1] += cnts[r];
+  if (M == 0) return hipSuccess;
+  // ---- records: fixed-size blocks of M per rank (device to device over RCCL when available)
+  const size_t bytes = (size_t)M * sizeof(BRec);
+  agreed = false;  // a local failure from here on is announced by the caller (loop header)
+  FCHK(grow(CB.recv, CB.cap_recv, (size_t)M * G));
+  if (sh.exchange_dev) {
+    FCHK(grow_keep(CB.send, CB.cap_send, (size_t)M, (size_t)m, st));  // pad to M records (contents past m unused)
+    if (sh.exchange_dev(CB.send, bytes, CB.recv, st) != 0) return hipErrorUnknown;
+  } else {
+    std::vector<char> hs(bytes, 0), hr(bytes * G);
+    if (m) FCHK(hipMemcpy(hs.data(), CB.send, (size_t)m * sizeof(BRec), hipMemcpyDeviceToHost));
+    if (sh.exchange(hs.data(), bytes, hr.data()) != 0) return hipErrorUnknown;
+    FCHK(hipMemcpyAsync(CB.recv, hr.data(), bytes * G, hipMemcpyHostToDevice, st));
+    FCHK(hipStreamSynchronize(st));
+  }
+  // ---- insertion (readPatches semantics), compacted in rank / record order after the model
+  const size_t slots = (size_t)M * G;
+  FCHK(grow(CB.ins, CB.cap_ins, slots));
+  FCHK(grow(CB.flags, CB.cap_flags, slots + 1));
+  FCHK(grow(CB.pos, CB.cap_pos, slots + 1));
+  if (CB.cap_cnts < G) {
+    if (CB.cnts) (void)hipFree(CB.cnts);
+    CB.cnts = nullptr;
+    FCHK(hipMalloc((void**)&CB.cnts, G * sizeof(int)));
+    CB.cap_cnts = G;
+  }
+  FCHK(hipMemcpyAsync(CB.cnts, cnts.data(), G * sizeof(int), hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(boundary_insert_kernel, dim3(nblk((long long)slots)), dim3(256), 0, st, s, CB.recv, G, M, me, CB.cnts,
+                     cm.id2idx, cm.maxid, CB.ins, CB.flags);
+  FCHK(hipMemsetAsync(CB.flags + slots, 0, sizeof(int), st));
+  int added = 0;
+  FCHK(scan_count(CB, CB.flags, CB.pos, (int)slots, &added, st));
+  xstats[2] = added;
+  if (added == 0) return hipSuccess;
+  FCHK(grow_keep(dst, dst_cap, (size_t)n + added, (size_t)n, st));
+  hipLaunchKernelGGL(compact_kernel, dim3((unsigned)slots), dim3(64), 0, st, CB.ins, (int)slots, CB.flags, CB.pos, dst + n);
+  FCHK(hipGetLastError());
+  *n_out = n + added;
+  return hipSuccess;
 }
 }  // namespace pmvsdev

@@ -15,6 +15,11 @@
 // No MFMA: this is gather + small reductions (HBM/L2-gather bound), see DESIGN.md.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
+#include <thread>
+#include <vector>
+
 #include "bobyqa_dev.h"
 #include "pmvs_device.h"
 
@@ -213,29 +218,24 @@ __device__ __forceinline__ void decode(const DScene& s, const RefineSetup& R, co
   normal[3] = 0.0f;
 }
 
-// COptim::encode, optim.cpp:660-688.
-__device__ __forceinline__ void encode(const DScene& s, const RefineSetup& R, const float* coord, const float* normal,
-                                       double* vect) {
+// COptim::encode, optim.cpp:660-688, up to its transcendental functions: vect[0] and the normal's
+// components (fx, fy, fz) in the reference camera frame.  The angles -- asin(fy), cos of it, acos
+// -- are the optimizer's start point as doubles, so they must carry glibc's bits (glibc 2.35's asin
+// and acos are not correctly rounded: 0.27 % / 0.03 % of float arguments differ from the correctly
+// rounded value by one ulp, and so would any device libm); encode_angles_host finishes them with the
+// host's libm (launch_refine).
+__device__ __forceinline__ void encode_dev(const DScene& s, const RefineSetup& R, const float* coord, const float* normal,
+                                           double* vect0, float* fxyz) {
   const float d[4] = {coord[0] - R.center[0], coord[1] - R.center[1], coord[2] - R.center[2], coord[3] - R.center[3]};
-  vect[0] = (double)__fdiv_rn(dot4(d, R.ray), R.dscale);
+  *vect0 = (double)__fdiv_rn(dot4(d, R.ray), R.dscale);
   const DView& v = s.views[R.ref];
   float n3[3] = {normal[0], normal[1], normal[2]};
   if (normal[3] != 1.0f && normal[3] != 0.0f) {
     n3[0] = __fdiv_rn(n3[0], normal[3]); n3[1] = __fdiv_rn(n3[1], normal[3]); n3[2] = __fdiv_rn(n3[2], normal[3]);
   }
-  const float fx = dot3(v.xaxis, n3), fy = dot3(v.yaxis, n3), fz = dot3(v.zaxis, n3);
-  vect[2] = asin((double)smax(-1.0f, smin(1.0f, fy)));
-  const float cosb = (float)cos(vect[2]);
-  if (cosb == 0.0f) {
-    vect[1] = 0.0;
-  } else {
-    const float sina = __fdiv_rn(fx, cosb);
-    const float cosa = __fdiv_rn(-fz, cosb);
-    vect[1] = acos((double)smax(-1.0f, smin(1.0f, cosa)));
-    if (sina < 0.0f) vect[1] = -vect[1];
-  }
-  vect[1] = vect[1] / (double)R.ascale;
-  vect[2] = vect[2] / (double)R.ascale;
+  fxyz[0] = dot3(v.xaxis, n3);
+  fxyz[1] = dot3(v.yaxis, n3);
+  fxyz[2] = dot3(v.zaxis, n3);
 }
 
 // ---------------------------------------------------------------- objective
@@ -375,13 +375,20 @@ __device__ void constraint_images(const DScene& s, WaveLds<WS>& L, const float* 
     }
     __syncthreads();
   }
-  // order-preserving compaction of images[] by keep flags
-  int newn;
-  const bool keep = lane < n && L.list2[lane];
-  const int pos = ballot_prefix(keep, &newn);
-  const int img = lane < n ? L.images[lane] : 0;
-  __syncthreads();
-  if (keep) L.images[pos] = img;
+  // order-preserving compaction of images[] by keep flags, 64 entries at a time (an entry is
+  // only ever moved down, and a chunk's entries are read before any of its writes)
+  int newn = 0;
+  for (int c = 0; c < n; c += WAVE) {
+    const int k = c + lane;
+    const bool keep = k < n && L.list2[k];
+    const int img = k < n ? L.images[k] : 0;
+    int cnt;
+    const int pos = ballot_prefix(keep, &cnt);
+    __syncthreads();
+    if (keep) L.images[newn + pos] = img;
+    newn += cnt;
+    __syncthreads();
+  }
   if (lane == 0) L.nimg = newn;
   __syncthreads();
 }
@@ -391,28 +398,32 @@ template <int WS>
 __device__ void sort_images(const DScene& s, WaveLds<WS>& L, const float* coord, const float* normal) {
   const int lane = lane_id();
   const int n = L.nimg;
-  bool keep = false;
-  float unit = 0.0f, ray[4] = {0, 0, 0, 0};
-  int img = 0;
-  if (lane < n) {
-    img = L.images[lane];
-    const DView& v = s.views[img];
-    ray[0] = v.center[0] - coord[0]; ray[1] = v.center[1] - coord[1];
-    ray[2] = v.center[2] - coord[2]; ray[3] = v.center[3] - coord[3];
-    unitize4(ray);
-    const float d = dot4(ray, normal);
-    if (!(d <= 0.0f)) {
-      keep = true;
-      unit = __fdiv_rn(get_unit(s, v, coord), d);
+  int m = 0;
+  for (int c = 0; c < n; c += WAVE) {
+    const int k = c + lane;
+    bool keep = false;
+    float unit = 0.0f, ray[4] = {0, 0, 0, 0};
+    int img = 0;
+    if (k < n) {
+      img = L.images[k];
+      const DView& v = s.views[img];
+      ray[0] = v.center[0] - coord[0]; ray[1] = v.center[1] - coord[1];
+      ray[2] = v.center[2] - coord[2]; ray[3] = v.center[3] - coord[3];
+      unitize4(ray);
+      const float d = dot4(ray, normal);
+      if (!(d <= 0.0f)) {
+        keep = true;
+        unit = __fdiv_rn(get_unit(s, v, coord), d);
+      }
     }
-  }
-  int m;
-  const int pos = ballot_prefix(keep, &m);
-  __syncthreads();
-  if (keep) {
-    L.list2[pos] = img;
-    L.fl[pos] = unit;
-    for (int i = 0; i < 4; ++i) L.rays[pos][i] = ray[i];
+    int cnt;
+    const int pos = ballot_prefix(keep, &cnt);
+    if (keep) {
+      L.list2[m + pos] = img;
+      L.fl[m + pos] = unit;
+      for (int i = 0; i < 4; ++i) L.rays[m + pos][i] = ray[i];
+    }
+    m += cnt;
   }
   __syncthreads();
   if (lane == 0) {
@@ -420,19 +431,20 @@ __device__ void sort_images(const DScene& s, WaveLds<WS>& L, const float* coord,
       L.nimg = 0;
     } else {
       L.fl[0] = 0.0f;
-      int alive[PMVS_MAX_IMAGES];
-      for (int i = 0; i < m; ++i) alive[i] = 1;
+      unsigned long long alive[PMVS_MAX_IMAGES / 64];  // bit k: entry k not yet taken
+      for (int w = 0; w < PMVS_MAX_IMAGES / 64; ++w)
+        alive[w] = (m >= 64 * (w + 1)) ? ~0ull : (m > 64 * w ? ((1ull << (m - 64 * w)) - 1ull) : 0ull);
       int out = 0;
       for (int it = 0; it < m; ++it) {
         int index = -1;
         for (int k = 0; k < m; ++k) {
-          if (!alive[k]) continue;
+          if (!((alive[k >> 6] >> (k & 63)) & 1ull)) continue;
           if (index < 0 || L.fl[k] < L.fl[index]) index = k;
         }
         L.images[out++] = L.list2[index];
-        alive[index] = 0;
+        alive[index >> 6] &= ~(1ull << (index & 63));
         for (int j = 0; j < m; ++j) {
-          if (!alive[j]) continue;
+          if (!((alive[j >> 6] >> (j & 63)) & 1ull)) continue;
           const float ftmp = smin(s.sortThreshold, smax(__fdiv_rn(s.sortThreshold, 2.0f), 1.0f - dot4(L.rays[index], L.rays[j])));
           L.fl[j] = L.fl[j] * __fdiv_rn(s.sortThreshold, ftmp);
         }
@@ -472,11 +484,11 @@ template <int WS>
 __device__ int check_angles(const DScene& s, WaveLds<WS>& L, const float* coord, float minA, float maxA) {
   const int lane = lane_id();
   const int n = L.nimg;
-  if (lane < n) {
-    const DView& v = s.views[L.images[lane]];
+  for (int k = lane; k < n; k += WAVE) {
+    const DView& v = s.views[L.images[k]];
     float r[4] = {v.center[0] - coord[0], v.center[1] - coord[1], v.center[2] - coord[2], v.center[3] - coord[3]};
     unitize4(r);
-    for (int i = 0; i < 4; ++i) L.rays[lane][i] = r[i];
+    for (int i = 0; i < 4; ++i) L.rays[k][i] = r[i];
   }
   __syncthreads();
   const int npairs = n * (n - 1) / 2;
@@ -504,25 +516,28 @@ template <int WS>
 __device__ void filter_images_by_angle(const DScene& s, WaveLds<WS>& L, const float* coord, const float* normal) {
   const int lane = lane_id();
   const int n = L.nimg;
-  bool keep = false;
-  int img = 0;
-  if (lane < n) {
-    img = L.images[lane];
-    const DView& v = s.views[img];
-    float ray[4] = {v.center[0] - coord[0], v.center[1] - coord[1], v.center[2] - coord[2], v.center[3] - coord[3]};
-    unitize4(ray);
-    keep = !((double)dot4(ray, normal) < s.cosAngle1);
+  bool refbad = false;
+  int newn = 0;
+  for (int c = 0; c < n; c += WAVE) {
+    const int k = c + lane;
+    bool keep = false;
+    int img = 0;
+    if (k < n) {
+      img = L.images[k];
+      const DView& v = s.views[img];
+      float ray[4] = {v.center[0] - coord[0], v.center[1] - coord[1], v.center[2] - coord[2], v.center[3] - coord[3]};
+      unitize4(ray);
+      keep = !((double)dot4(ray, normal) < s.cosAngle1);
+    }
+    if (c == 0) refbad = !__shfl(keep ? 1 : 0, 0);
+    int cnt;
+    const int pos = ballot_prefix(keep, &cnt);
+    __syncthreads();
+    if (!refbad && keep) L.images[newn + pos] = img;
+    newn += cnt;
+    __syncthreads();
   }
-  const bool refbad = !__shfl(keep ? 1 : 0, 0);
-  int newn;
-  const int pos = ballot_prefix(keep, &newn);
-  __syncthreads();
-  if (refbad) {
-    if (lane == 0) L.nimg = 0;
-  } else {
-    if (keep) L.images[pos] = img;
-    if (lane == 0) L.nimg = newn;
-  }
+  if (lane == 0) L.nimg = refbad ? 0 : newn;
   __syncthreads();
 }
 
@@ -530,11 +545,11 @@ __device__ void filter_images_by_angle(const DScene& s, WaveLds<WS>& L, const fl
 template <int WS>
 __device__ void set_grids(const DScene& s, WaveLds<WS>& L, const float* coord) {
   const int lane = lane_id();
-  if (lane < L.nimg) {
+  for (int k = lane; k < L.nimg; k += WAVE) {
     float ic[3];
-    project(s.views[L.images[lane]], coord, s.level, ic);
-    L.grids[lane][0] = ((int)floorf(ic[0] + 0.5f)) / s.csize;
-    L.grids[lane][1] = ((int)floorf(ic[1] + 0.5f)) / s.csize;
+    project(s.views[L.images[k]], coord, s.level, ic);
+    L.grids[k][0] = ((int)floorf(ic[0] + 0.5f)) / s.csize;
+    L.grids[k][1] = ((int)floorf(ic[1] + 0.5f)) / s.csize;
   }
   __syncthreads();
 }
@@ -546,10 +561,15 @@ __device__ void set_ref_image(const DScene& s, WaveLds<WS>& L, const float* coor
                               unsigned long long* grabs) {
   const int lane = lane_id();
   const int n = L.nimg;
-  const bool tgt = lane < n && L.images[lane] < s.tnum;
-  int m;
-  const int pos = ballot_prefix(tgt, &m);
-  if (tgt) L.list2[pos] = L.images[lane];
+  int m = 0;
+  for (int c = 0; c < n; c += WAVE) {
+    const int k = c + lane;
+    const bool tgt = k < n && L.images[k] < s.tnum;
+    int cnt;
+    const int pos = ballot_prefix(tgt, &cnt);
+    if (tgt) L.list2[m + pos] = L.images[k];
+    m += cnt;
+  }
   __syncthreads();
   if (m == 0) {
     if (lane == 0) L.nimg = 0;
@@ -604,13 +624,13 @@ __device__ void set_ref_image(const DScene& s, WaveLds<WS>& L, const float* coor
       }
     }
   }
-  if (lane < m) mat[lane * PMVS_MAX_IMAGES + lane] = 0.0f;
+  for (int k = lane; k < m; k += WAVE) mat[k * PMVS_MAX_IMAGES + k] = 0.0f;
   __syncthreads();
   // row sums in j order (std::accumulate, float)
-  if (lane < m) {
+  for (int k = lane; k < m; k += WAVE) {
     float sum = 0.0f;
-    for (int j = 0; j < m; ++j) sum = sum + mat[lane * PMVS_MAX_IMAGES + j];
-    L.fl[lane] = sum;
+    for (int j = 0; j < m; ++j) sum = sum + mat[k * PMVS_MAX_IMAGES + j];
+    L.fl[k] = sum;
   }
   __syncthreads();
   if (lane == 0) {
@@ -640,17 +660,19 @@ __device__ void set_ref_image(const DScene& s, WaveLds<WS>& L, const float* coor
 // for one candidate; writes a RefineJob.  acc: [2] grabs.
 template <int WS>
 __device__ void pre_candidate(const DScene& s, WaveLds<WS>& L, const pmvs_candidate& cin, RefineJob& job,
-                              unsigned long long* acc) {
+                              float4& enc, unsigned long long* acc) {
   const int lane = lane_id();
   float coord[4], normal[4];
   for (int i = 0; i < 4; ++i) { coord[i] = cin.coord[i]; normal[i] = cin.normal[i]; }
   float dscale = cin.dscale, ascale = 0.0f;
+  if (lane == 0) enc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // w = 0: no refinement, no angles
   const int n0 = imin(cin.num_images, PMVS_MAX_IMAGES);
   bool badidx = false;
-  if (lane < n0) {
-    const int img = cin.images[lane];
-    badidx = (img < 0 || img >= s.num);
-    L.images[lane] = badidx ? 0 : img;
+  for (int k = lane; k < n0; k += WAVE) {
+    const int img = cin.images[k];
+    const bool bad = (img < 0 || img >= s.num);
+    badidx |= bad;
+    L.images[k] = bad ? 0 : img;
   }
   badidx = __ballot(badidx) != 0;
   if (lane == 0) { L.nimg = n0; L.overflow = (cin.num_images > PMVS_MAX_IMAGES || n0 < 1 || badidx); }
@@ -684,15 +706,15 @@ __device__ void pre_candidate(const DScene& s, WaveLds<WS>& L, const pmvs_candid
   const int ni = L.nimg;
   if (status == PMVS_ACCEPTED) {
     // weights: computeUnits(patch) (optim.cpp:446-471) then min(1, w0 / wi)
-    if (lane < ni) {
-      const DView& v = s.views[L.images[lane]];
+    for (int k = lane; k < ni; k += WAVE) {
+      const DView& v = s.views[L.images[k]];
       float u = get_unit(s, v, coord);
       float ray[4] = {v.center[0] - coord[0], v.center[1] - coord[1], v.center[2] - coord[2], v.center[3] - coord[3]};
       unitize4(ray);
       const float den = dot4(ray, normal);
       if (0.0f < den) u = __fdiv_rn(u, den);
       else u = 1073741824.0f;  // (float)(INT_MAX/2)
-      L.fl[lane] = u;
+      L.fl[k] = u;
     }
     __syncthreads();
     if (lane < ni && lane < PMVS_MAX_TAU) {
@@ -707,18 +729,15 @@ __device__ void pre_candidate(const DScene& s, WaveLds<WS>& L, const pmvs_candid
       R.dscale = dscale;
       R.ascale = s.ascale;
       R.ref = L.images[0];
-      double p[3];
-      encode(s, R, coord, normal, p);
-      const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999};
-      const double ub[3] = {HUGE_VAL, 23.99999, 23.99999};
-      for (int i = 0; i < 3; ++i) {
-        const double m = (ub[i] < p[i]) ? ub[i] : p[i];  // std::min(p, ub)
-        job.x0[i] = (m < lb[i]) ? lb[i] : m;             // std::max(., lb)
-      }
+      double p0;
+      float f[3];
+      encode_dev(s, R, coord, normal, &p0, f);
+      job.x0[0] = p0;  // bounds (-inf, inf): std::max(std::min(p, ub), lb) keeps it
+      enc = make_float4(f[0], f[1], f[2], 1.0f);  // x0[1], x0[2]: encode_angles_host + angles_kernel
       for (int i = 0; i < 4; ++i) { job.center[i] = R.center[i]; job.ray[i] = R.ray[i]; }
     }
   }
-  if (lane < ni) job.images[lane] = L.images[lane];
+  for (int k = lane; k < ni; k += WAVE) job.images[k] = L.images[k];
   if (lane == 0) {
     for (int i = 0; i < 4; ++i) {
       job.coord[i] = coord[i]; job.normal[i] = normal[i];
@@ -748,7 +767,7 @@ __device__ void post_candidate(const DScene& s, WaveLds<WS>& L, const RefineJob&
   int status = job.status, timages = 0;
   float tmp = 0.0f;
   const int ni = job.nimg;
-  if (lane < ni) L.images[lane] = job.images[lane];
+  for (int k = lane; k < ni; k += WAVE) L.images[k] = job.images[k];
   if (lane == 0) { L.nimg = ni; L.overflow = 0; }
   __syncthreads();
   if (status == PMVS_ACCEPTED) {
@@ -797,10 +816,10 @@ __device__ void post_candidate(const DScene& s, WaveLds<WS>& L, const RefineJob&
     if (L.overflow) status = PMVS_FAIL_OVERFLOW;
   }
   const int nout = L.nimg;
-  if (lane < nout) {
-    cout.images[lane] = L.images[lane];
-    cout.grids[lane][0] = (status == PMVS_ACCEPTED) ? L.grids[lane][0] : 0;
-    cout.grids[lane][1] = (status == PMVS_ACCEPTED) ? L.grids[lane][1] : 0;
+  for (int k = lane; k < nout; k += WAVE) {
+    cout.images[k] = L.images[k];
+    cout.grids[k][0] = (status == PMVS_ACCEPTED) ? L.grids[k][0] : 0;
+    cout.grids[k][1] = (status == PMVS_ACCEPTED) ? L.grids[k][1] : 0;
   }
   if (lane == 0) {
     cout.status = status;
@@ -1275,7 +1294,8 @@ namespace pmvsdev {
 // persistent grid's 8 per CU) instead of the 324 the inlined code would take (1 per SIMD).
 template <int WS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void pre_kernel(DScene s, const pmvs_candidate* __restrict__ in,
-                                                  RefineJob* __restrict__ jobs, int n, DevStats* st) {
+                                                  RefineJob* __restrict__ jobs, float4* __restrict__ enc, int n,
+                                                  DevStats* st) {
   __shared__ WaveLds<WS> L;
   unsigned long long acc[7] = {0, 0, 0, 0, 0, 0, 0};
   const int lane = lane_id();
@@ -1288,7 +1308,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void pr
     const int c = __builtin_amdgcn_readfirstlane(L.cand);
     __syncthreads();
     if (c < 0) break;
-    pre_candidate<WS>(s, L, in[c], jobs[c], acc);
+    pre_candidate<WS>(s, L, in[c], jobs[c], enc[c], acc);
   }
   if (lane == 0) atomicAdd(&st->tex_grabs, acc[2]);
 }
@@ -1449,6 +1469,76 @@ __global__ void unpack_rgba_kernel(const uint32_t* __restrict__ in, uint8_t* __r
 
 namespace pmvsdev {
 
+// The optimizer start point's angles (encode's transcendental tail, see encode_dev) with the host's
+// libm, exactly as COptim::encode (optim.cpp:671-686) evaluates them, then std::max(std::min(x,
+// ub), lb) with the angle bounds (optim.cpp:629-634).  Threads for large batches.
+static void encode_angles_host(const float4* enc, int n, float ascale, double2* ang) {
+  auto one = [&](int i) {
+    const float4 e = enc[i];
+    double v1 = 0.0, v2 = 0.0;
+    if (e.w != 0.0f) {
+      const float fx = e.x, fy = e.y, fz = e.z;
+      const float cfy = (1.0f < fy) ? 1.0f : fy;       // std::min(1.0f, fy)
+      v2 = std::asin((double)((cfy < -1.0f) ? -1.0f : cfy));  // std::max(-1.0f, .)
+      const float cosb = (float)std::cos(v2);
+      if (cosb == 0.0f) {
+        v1 = 0.0;
+      } else {
+        const float sina = fx / cosb;
+        const float cosa = -fz / cosb;
+        const float cc = (1.0f < cosa) ? 1.0f : cosa;
+        v1 = std::acos((double)((cc < -1.0f) ? -1.0f : cc));
+        if (sina < 0.0f) v1 = -v1;
+      }
+      v1 = v1 / (double)ascale;
+      v2 = v2 / (double)ascale;
+      const double lb = -23.99999, ub = 23.99999;
+      v1 = (ub < v1) ? ub : v1; v1 = (v1 < lb) ? lb : v1;
+      v2 = (ub < v2) ? ub : v2; v2 = (v2 < lb) ? lb : v2;
+    }
+    ang[i] = make_double2(v1, v2);
+  };
+  const int nt = (n >= 32768) ? std::min(8, (int)std::max(1u, std::thread::hardware_concurrency())) : 1;
+  if (nt == 1) {
+    for (int i = 0; i < n; ++i) one(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&, t]() {
+      for (int i = t; i < n; i += nt) one(i);
+    });
+  for (auto& t : th) t.join();
+}
+
+__global__ void angles_kernel(RefineJob* __restrict__ jobs, const double2* __restrict__ ang, const float4* __restrict__ enc,
+                              int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || enc[i].w == 0.0f) return;
+  jobs[i].x0[1] = ang[i].x;
+  jobs[i].x0[2] = ang[i].y;
+}
+
+hipError_t RefineHost::ensure(size_t n) {
+  if (n <= cap) return hipSuccess;
+  release();
+  cap = std::max(n, (size_t)4096);
+  hipError_t e = hipMalloc((void**)&d_enc, cap * sizeof(float4));
+  if (e == hipSuccess) e = hipMalloc((void**)&d_ang, cap * sizeof(double2));
+  if (e == hipSuccess) e = hipHostMalloc((void**)&h_enc, cap * sizeof(float4));
+  if (e == hipSuccess) e = hipHostMalloc((void**)&h_ang, cap * sizeof(double2));
+  if (e != hipSuccess) cap = 0;
+  return e;
+}
+void RefineHost::release() {
+  if (d_enc) (void)hipFree(d_enc);
+  if (d_ang) (void)hipFree(d_ang);
+  if (h_enc) (void)hipHostFree(h_enc);
+  if (h_ang) (void)hipHostFree(h_ang);
+  d_enc = nullptr; d_ang = nullptr; h_enc = nullptr; h_ang = nullptr;
+  cap = 0;
+}
+
 // refine_v2_kernel instantiations (texture slots * 100 + chains per wavefront)
 bool refine_config_supported(int tslots) {
   switch (tslots) {
@@ -1464,10 +1554,20 @@ bool refine_config_supported(int tslots) {
 template <int WS>
 static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out,
                                    int n, DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream,
-                                   hipEvent_t* ev) {
+                                   hipEvent_t* ev, RefineHost& rh) {
   const int g = grid < n ? grid : n;
+  hipError_t e = rh.ensure((size_t)n);
+  if (e != hipSuccess) return e;
   (void)hipEventRecord(ev[0], stream);
-  hipLaunchKernelGGL((pre_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_in, d_jobs, n, d_st);
+  hipLaunchKernelGGL((pre_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_in, d_jobs, rh.d_enc, n, d_st);
+  // the start point's angles with the host's libm (encode_angles_host): one round trip per batch
+  if ((e = hipMemcpyAsync(rh.h_enc, rh.d_enc, (size_t)n * sizeof(float4), hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(stream)) != hipSuccess)
+    return e;
+  encode_angles_host(rh.h_enc, n, s.ascale, rh.h_ang);
+  if ((e = hipMemcpyAsync(rh.d_ang, rh.h_ang, (size_t)n * sizeof(double2), hipMemcpyHostToDevice, stream)) != hipSuccess)
+    return e;
+  hipLaunchKernelGGL(angles_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_jobs, rh.d_ang, rh.d_enc, n);
   (void)hipEventRecord(ev[1], stream);
   // a request's textures must fit one chunk (TSLOTS >= tau, tau <= PMVS_MAX_TAU = 16): smaller
   // chunk configs are only valid for small tau, otherwise the default 24-slot kernel runs
@@ -1507,12 +1607,13 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
 }
 
 hipError_t launch_refine(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out, int n,
-                         DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream, hipEvent_t* ev) {
+                         DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream, hipEvent_t* ev,
+                         RefineHost& rh) {
   if (n <= 0) return hipSuccess;
   switch (s.wsize) {
-    case 5: return launch_refine_ws<5>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, tslots, stream, ev);
-    case 7: return launch_refine_ws<7>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, tslots, stream, ev);
-    case 9: return launch_refine_ws<9>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, tslots, stream, ev);
+    case 5: return launch_refine_ws<5>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, tslots, stream, ev, rh);
+    case 7: return launch_refine_ws<7>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, tslots, stream, ev, rh);
+    case 9: return launch_refine_ws<9>(s, d_in, d_jobs, d_out, n, d_st, grid, refine_grid, tslots, stream, ev, rh);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1576,20 +1677,20 @@ __global__ __launch_bounds__(64) void filter_refimage_kernel(DScene s, pmvs_patc
   for (int k = blockIdx.x; k < m; k += gridDim.x) {
     pmvs_patch& q = P[list[k]];
     const int n = q.num_images;
-    if (lane < n) L.images[lane] = q.images[lane];
+    for (int j = lane; j < n; j += WAVE) L.images[j] = q.images[j];
     if (lane == 0) { L.nimg = n; L.overflow = 0; }
     __syncthreads();
     float coord[4], normal[4];
     for (int i = 0; i < 4; ++i) { coord[i] = q.coord[i]; normal[i] = q.normal[i]; }
     set_ref_image<WS>(s, L, coord, normal, mat, &grabs);
     const int nn = L.nimg;
-    if (lane < nn) {
-      const int img = L.images[lane];
+    for (int j = lane; j < nn; j += WAVE) {
+      const int img = L.images[j];
       float ic[3];
       project(s.views[img], coord, s.level, ic);
-      q.images[lane] = img;
-      q.grids[lane][0] = ((int)floorf(ic[0] + 0.5f)) / s.csize;
-      q.grids[lane][1] = ((int)floorf(ic[1] + 0.5f)) / s.csize;
+      q.images[j] = (int16_t)img;
+      q.grids[j][0] = grid16(((int)floorf(ic[0] + 0.5f)) / s.csize);
+      q.grids[j][1] = grid16(((int)floorf(ic[1] + 0.5f)) / s.csize);
     }
     if (lane == 0) q.num_images = nn;
     __syncthreads();

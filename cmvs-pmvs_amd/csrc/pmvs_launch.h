@@ -7,8 +7,20 @@
 
 namespace pmvsdev {
 bool refine_config_supported(int tslots);  // PMVS_REFINE_CONFIG values this build instantiates
+// Host staging of the refine batches' start-point angles (encode_angles_host, pmvs_kernels.hip).
+struct RefineHost {
+  float4* d_enc = nullptr;
+  double2* d_ang = nullptr;
+  float4* h_enc = nullptr;   // pinned
+  double2* h_ang = nullptr;  // pinned
+  size_t cap = 0;
+  hipError_t ensure(size_t n);
+  void release();
+  ~RefineHost() { release(); }
+};
 hipError_t launch_refine(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out, int n,
-                         DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream, hipEvent_t* ev);
+                         DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream, hipEvent_t* ev,
+                         RefineHost& rh);
 hipError_t launch_incc_eval(const DScene& s, const pmvs_eval_query* d_q, int n, double* d_out, DevStats* d_st,
                             hipStream_t stream);
 hipError_t launch_grab_tex(const DScene& s, const pmvs_tex_query* d_q, int n, float* d_out, int* d_valid,
@@ -46,8 +58,8 @@ struct PinnedBuf {
 };
 struct FilterBuffers {
   PinnedBuf pin;  // host staging of the small-groups BFS inputs
-  unsigned long long *preg = nullptr, *vreg = nullptr, *keys = nullptr, *keys2 = nullptr, *dpkey = nullptr,
-                     *safe = nullptr;
+  Reg *preg = nullptr, *vreg = nullptr, *safe = nullptr;  // per patch: registered / filterExact-safe list entries
+  unsigned long long *keys = nullptr, *keys2 = nullptr, *dpkey = nullptr;
   long long* tgoff = nullptr;
   int *cnt = nullptr, *off = nullptr, *cellcnt = nullptr, *pg_off = nullptr, *pg_items = nullptr, *vp_off = nullptr,
       *vp_items = nullptr, *order = nullptr, *rank = nullptr, *flags = nullptr, *need = nullptr, *list = nullptr,
@@ -69,7 +81,9 @@ struct FilterBuffers {
   size_t cap_qrows = 0;
   int cap_n = 0, cap_grid = 0;
   long long cap_cells = 0;
+  size_t cap_e = 0, cap_pi = 0, cap_vi = 0;  // entries of keys/keys2, pg_items, vp_items: grown to the lists' size
   hipError_t reserve(int n, long long ncells, int tnum, int grid);
+  hipError_t ensure_entries(size_t e, int vis);
   ~FilterBuffers();
 };
 
@@ -137,6 +151,36 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
 hipError_t compact_model(FilterBuffers& B, const pmvs_patch* src, int n, const int* keep, pmvs_patch* dst, int* nkept,
                          hipStream_t st);
 hipError_t fill_int(int* a, int n, int v, hipStream_t st);
+
+// ---- CMVS cluster boundary exchange (pmvs_scene_set_cluster)
+struct ClusterMaps {              // device tables of one cluster scene
+  const unsigned char* shared_t;  // per local target index: its image is a target of another cluster too
+  const int* ids;                 // per local view index: the global image number
+  const int* id2idx;              // global image number (0 .. maxid) -> local view index, or -1
+  int maxid;
+};
+struct ClusterBuffers {
+  BRec *send = nullptr, *recv = nullptr;
+  pmvs_patch* ins = nullptr;
+  int *flags = nullptr, *pos = nullptr, *cnts = nullptr;
+  void* temp = nullptr;
+  size_t cap_send = 0, cap_recv = 0, cap_ins = 0, cap_flags = 0, cap_pos = 0, temp_bytes = 0;
+  int cap_cnts = 0;
+  ~ClusterBuffers();
+};
+// The model without other clusters' boundary patches (fix != PMVS_FIX_FOREIGN), compacted into dst.
+hipError_t drop_foreign(FilterBuffers& B, const pmvs_patch* src, int n, pmvs_patch* dst, int* n_out, hipStream_t st);
+// One boundary exchange: src[0, n) is this rank's model without foreign patches.  Its boundary
+// patches (registered in a target image another cluster also has as a target) are all-gathered
+// (header {error, count} first, the "visibility counts"; then the records), and every other rank's
+// records whose reference image is one of this scene's views and that project into one of its
+// targets are appended to dst (= src's contents + the inserted patches; grown as needed) as fixed,
+// never-expanded patches (fix = PMVS_FIX_FOREIGN), with grids from CPatchOrganizerS::setGrids.
+// xstats: [0] own boundary patches, [1] records received, [2] inserted.  agreed: the failure (if
+// any) was seen by every rank.
+hipError_t cluster_exchange(const DScene& s, ClusterBuffers& CB, const ClusterMaps& cm, const pmvs_patch* src, int n,
+                            pmvs_patch*& dst, size_t& dst_cap, int* n_out, const Shard& sh, hipStream_t st,
+                            long long xstats[3], bool& agreed);
 hipError_t lls_selftest(const float* A, const float* b, const int* off, int nsys, int total, float* x);
 
 // ---- seed phase (pmvs_seed.hip)

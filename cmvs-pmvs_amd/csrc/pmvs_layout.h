@@ -5,9 +5,27 @@
 
 #include "../../include/pmvs_amd.h"
 
+#if defined(__HIPCC__)
+#define PMVS_HD __host__ __device__
+#else
+#define PMVS_HD
+#endif
+
 namespace pmvsdev {
 
+// A cell coordinate as pmvs_patch stores it (int16): values outside [-32767, 32767] -- only ever
+// projections far outside the image, hence outside every cell grid (< 32768 cells wide / high,
+// checked at scene creation) -- become -32768, which no in-grid test accepts either.
+PMVS_HD inline int16_t grid16(int v) { return (v < -32767 || v > 32767) ? (int16_t)-32768 : (int16_t)v; }
+
 constexpr int MAXL = PMVS_MAX_LEVEL + 3;
+
+// Registration mask of one patch in the device organizer: bit i = list entry i is registered in a
+// cell list (PMVS_MAX_IMAGES entries, 64 per word).
+constexpr int REGW = PMVS_MAX_IMAGES / 64;
+struct Reg {
+  unsigned long long w[REGW];
+};
 constexpr int TEXCAP = 16;  // textures resident in LDS per wave (>= PMVS_MAX_TAU)
 
 struct DView {
@@ -56,6 +74,16 @@ struct RefineJob {
   double x0[3];                // encode()d start point, clamped to the bounds
   float rcoord[4], rnormal[4]; // refine output geometry (decoded on success, else the input)
   int images[PMVS_MAX_IMAGES];
+};
+
+// One boundary patch as the cluster exchange sends it (pmvs_scene_set_cluster): the fields the
+// reference's readPatches reads from another run's output (patchOrganizerS.cpp:133-197, Patch
+// operator>> patch.cpp:6-28) with image NUMBERS (global ids), 560 bytes.
+struct BRec {
+  float coord[4], normal[4];
+  float ncc, dscale, ascale;
+  int num_images;
+  int ids[PMVS_MAX_IMAGES];
 };
 
 struct DevStats {

@@ -602,9 +602,9 @@ hipError_t seed_pass(const DScene& s, const std::vector<DView>& hv, const SeedIn
           pp.ncc = r.ncc; pp.dscale = r.dscale; pp.ascale = r.ascale; pp.tmp = r.tmp; pp.timages = r.timages;
           pp.num_images = r.num_images;
           for (int k = 0; k < r.num_images; ++k) {
-            pp.images[k] = r.images[k];
-            pp.grids[k][0] = r.grids[k][0];
-            pp.grids[k][1] = r.grids[k][1];
+            pp.images[k] = (int16_t)r.images[k];
+            pp.grids[k][0] = grid16(r.grids[k][0]);
+            pp.grids[k][1] = grid16(r.grids[k][1]);
             const int t = r.images[k];
             if (t < tnum && 0 <= r.grids[k][0] && r.grids[k][0] < gw[t] && 0 <= r.grids[k][1] && r.grids[k][1] < gh[t])
               occupied[t][(size_t)r.grids[k][1] * gw[t] + r.grids[k][0]] = 1;  // addPatch at depth 0
@@ -719,7 +719,8 @@ hipError_t seed_pass(const DScene& s, const std::vector<DView>& hv, const SeedIn
           accepted_slot[cid] = (int)accepted.size();
           accepted.push_back(r);
         } else {
-          state[cid] = (r.status == PMVS_FAIL_PRE) ? 2 : 3;  // FAIL_OVERFLOW counts as a postProcess failure
+          if (r.status == PMVS_FAIL_OVERFLOW) return hipErrorNotSupported;  // list capacity: an error, not a reject
+          state[cid] = (r.status == PMVS_FAIL_PRE) ? 2 : 3;
         }
       }
       refined += m;

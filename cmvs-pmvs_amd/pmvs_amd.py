@@ -17,10 +17,11 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PMVS_AMD_LIB", os.path.join(HERE, "libpmvs_amd.so"))
 
-MAX_IMAGES = 64
+MAX_IMAGES = 128
 MAX_TAU = 16
 
 ACCEPTED, FAIL_PRE, FAIL_POST, FAIL_OVERFLOW = 0, 1, 2, 3
+FIX_FOREIGN = 2  # pmvs_patch.fix of another cluster's boundary patch (PMVS_FIX_FOREIGN)
 
 CANDIDATE_DTYPE = np.dtype(
     [("coord", "<f4", 4), ("normal", "<f4", 4), ("dscale", "<f4"), ("num_images", "<i4"),
@@ -36,8 +37,8 @@ EVAL_QUERY_DTYPE = np.dtype(
 PATCH_DTYPE = np.dtype(
     [("coord", "<f4", 4), ("normal", "<f4", 4), ("ncc", "<f4"), ("dscale", "<f4"), ("ascale", "<f4"),
      ("tmp", "<f4"), ("timages", "<i4"), ("flag", "<i4"), ("fix", "<i4"), ("num_images", "<i4"),
-     ("num_vimages", "<i4"), ("dflag", "<i4"), ("images", "<i4", MAX_IMAGES), ("grids", "<i4", (MAX_IMAGES, 2)),
-     ("vimages", "<i4", MAX_IMAGES), ("vgrids", "<i4", (MAX_IMAGES, 2))], align=True)
+     ("num_vimages", "<i4"), ("dflag", "<i4"), ("images", "<i2", MAX_IMAGES), ("grids", "<i2", (MAX_IMAGES, 2)),
+     ("vimages", "<i2", MAX_IMAGES), ("vgrids", "<i2", (MAX_IMAGES, 2))], align=True)
 POINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("response", "<f4"), ("type", "<i4")])  # pmvs_point
 TEX_QUERY_DTYPE = np.dtype(
     [("coord", "<f4", 4), ("pxaxis", "<f4", 4), ("pyaxis", "<f4", 4), ("normal", "<f4", 4),
@@ -90,11 +91,13 @@ class ExpandStats(C.Structure):
 
 
 class LoopIter(C.Structure):
-    _fields_ = [("depth", C.c_int32), ("patches", C.c_int32), ("expand", ExpandStats), ("filter", FilterStats)]
+    _fields_ = [("depth", C.c_int32), ("patches", C.c_int32), ("expand", ExpandStats), ("filter", FilterStats),
+                ("boundary_sent", C.c_int64), ("boundary_received", C.c_int64), ("boundary_inserted", C.c_int64)]
 
     def as_dict(self):
         return {"depth": self.depth, "expand": self.expand.as_dict(), "filter": self.filter.as_dict(),
-                "patches": self.patches}
+                "patches": self.patches, "boundary": {"sent": self.boundary_sent, "received": self.boundary_received,
+                                                      "inserted": self.boundary_inserted}}
 
 
 class SeedStats(C.Structure):
@@ -138,7 +141,8 @@ EXPORTS = ["pmvs_last_error", "pmvs_device_count", "pmvs_scene_create", "pmvs_sc
            "pmvs_synth_candidates", "pmvs_selftest_math", "pmvs_selftest_bobyqa", "pmvs_camera_load",
            "pmvs_ppm_load", "pmvs_options_load", "pmvs_options_free", "pmvs_write_patches", "pmvs_write_pset",
            "pmvs_write_ply", "pmvs_patch_colors", "pmvs_filter_run",
-           "pmvs_expand_run", "pmvs_expand_fetch", "pmvs_run_loop", "pmvs_loop_fetch", "pmvs_scene_set_shard", "pmvs_scene_set_shard_rccl", "pmvs_rccl_unique_id",
+           "pmvs_expand_run", "pmvs_expand_fetch", "pmvs_run_loop", "pmvs_loop_fetch", "pmvs_scene_set_shard", "pmvs_scene_set_shard_rccl", "pmvs_scene_set_cluster",
+           "pmvs_scene_set_cluster_rccl", "pmvs_rccl_unique_id",
            "pmvs_rccl_create", "pmvs_rccl_destroy", "pmvs_rccl_allgather", "pmvs_rccl_allgather_device",
            "pmvs_thread_exchange_create",
            "pmvs_thread_exchange_ctx", "pmvs_thread_allgather", "pmvs_thread_exchange_destroy", "pmvs_detect_features",
@@ -203,6 +207,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
                                   C.c_int32, C.POINTER(C.c_int32), C.c_void_p]
     lib.pmvs_loop_fetch.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     lib.pmvs_scene_set_shard.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
+    lib.pmvs_scene_set_cluster.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.pmvs_scene_set_cluster_rccl.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
     lib.pmvs_rccl_unique_id.argtypes = [C.c_void_p]
     lib.pmvs_rccl_create.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.POINTER(C.c_void_p)]
     lib.pmvs_rccl_destroy.argtypes = [C.c_void_p]
@@ -451,6 +457,16 @@ class Scene:
         ptr = None if fn is None else (fn if isinstance(fn, int) else C.cast(fn, C.c_void_p).value)
         _check(self.lib.pmvs_scene_set_shard(self.handle, rank, world, ptr, ctx))
 
+    def set_cluster(self, rank: int, world: int, image_ids, fn=None, ctx=None):
+        """One CMVS cluster of `world` (pmvs_scene_set_cluster): run_loop then exchanges boundary
+        patches with the other ranks after every iteration.  image_ids: the global image number of
+        each view.  fn: a pmvs_allgather_fn (ThreadExchange.endpoint / DistExchange.fn).  Collective."""
+        ids = np.ascontiguousarray(image_ids, np.int32)
+        assert len(ids) == len(self.inputs.images)
+        self._cluster_keep = (fn, ids)
+        ptr = None if fn is None else (fn if isinstance(fn, int) else C.cast(fn, C.c_void_p).value)
+        _check(self.lib.pmvs_scene_set_cluster(self.handle, rank, world, _ptr(ids), ptr, ctx))
+
     def run_loop(self, seeds: np.ndarray, threshold: float, iterations: int = 3, wave: int = 4096, cap=None,
                  after_seeds: bool = True, native: bool = True, min_candidates: int = 0):
         """CFindMatch::run after the seed phase (findMatch.cpp:196-217): depth 1, then `iterations` x
@@ -635,9 +651,17 @@ def patches_from_refined(refined: np.ndarray) -> np.ndarray:
     """Accepted pmvs_refined records -> pmvs_patch records (the CPatch fields a filter pass reads)."""
     acc = refined[refined["status"] == ACCEPTED]
     p = np.zeros(len(acc), PATCH_DTYPE)
-    for f in ("coord", "normal", "ncc", "dscale", "ascale", "tmp", "timages", "num_images", "images", "grids"):
+    for f in ("coord", "normal", "ncc", "dscale", "ascale", "tmp", "timages", "num_images", "images"):
         p[f] = acc[f]
+    p["grids"] = grid16(acc["grids"])
     return p
+
+
+def grid16(g):
+    """Cell coordinates as pmvs_patch stores them (int16): values outside [-32767, 32767] -- only
+    projections far outside the image, so outside every cell grid -- become -32768 (pmvs_layout.h)."""
+    g = np.asarray(g, np.int64)
+    return np.where((g < -32767) | (g > 32767), -32768, g).astype(np.int16)
 
 
 def device_count() -> int:
@@ -741,6 +765,12 @@ class RcclExchange:
 
     def attach(self, scene: "Scene"):
         _check(self.lib.pmvs_scene_set_shard_rccl(scene.handle, self.rank, self.world, self.handle))
+
+    def attach_cluster(self, scene: "Scene", image_ids):
+        """The scene is this rank's CMVS cluster; its boundary patches go device to device over RCCL."""
+        ids = np.ascontiguousarray(image_ids, np.int32)
+        scene._cluster_keep = (None, ids)
+        _check(self.lib.pmvs_scene_set_cluster_rccl(scene.handle, self.rank, self.world, _ptr(ids), self.handle))
 
     def close(self):
         if self.handle:

@@ -24,7 +24,11 @@
 extern "C" {
 #endif
 
-#define PMVS_MAX_IMAGES 64 /* capacity of one patch's image list (reference: unbounded vector) */
+/* Capacity of one patch's image list and of its visible-target list (reference: unbounded
+ * std::vector, patch.hpp:38,42).  A patch's images are distinct views and its vimages distinct
+ * targets, so both lists always fit for scenes of up to PMVS_MAX_IMAGES views; larger scenes are
+ * supported, and a list that would overflow fails the call with PMVS_EUNSUPPORTED (never a clamp). */
+#define PMVS_MAX_IMAGES 128
 #define PMVS_MAX_TARGETS 256 /* target images (timages) per scene: a C5 cluster is maximage 70 plus overlap */
 #define PMVS_MAX_TAU 16    /* max textures in the objective: tau = min(2*minImageNum, num) */
 #define PMVS_MAX_LEVEL 4   /* reference MyPow2 table limits level to <= 4 (optim.cpp:808-811) */
@@ -43,7 +47,8 @@ typedef enum pmvs_candidate_status {
   PMVS_ACCEPTED = 0,      /* postProcess returned 0 */
   PMVS_FAIL_PRE = 1,      /* COptim::preProcess returned 1 */
   PMVS_FAIL_POST = 2,     /* COptim::postProcess returned 1 */
-  PMVS_FAIL_OVERFLOW = 3  /* image list exceeded PMVS_MAX_IMAGES (not a reference outcome) */
+  PMVS_FAIL_OVERFLOW = 3  /* image list exceeded PMVS_MAX_IMAGES (not a reference outcome; the loop entry
+                             points turn it into a PMVS_EUNSUPPORTED error) */
 } pmvs_candidate_status;
 
 /* One view: CPhoto = CImage (pyramid) + CCamera (projection), reference include/image/photo.hpp. */
@@ -225,16 +230,24 @@ pmvs_status pmvs_selftest_bobyqa(int32_t device, int32_t mode, int32_t kind, con
  * Filter pass over a patch set (PMVS3::CFilter::run, filter.cpp:13-27): the cell organizer
  * (CPatchOrganizerS pgrids / vpgrids / depth maps) is built on the device from the patch
  * array; insertion order = array index.  Runs at the scene's thresholds and depth
- * (pmvs_set_thresholds; the reference runs filters at depth >= 1). */
+ * (pmvs_set_thresholds; the reference runs filters at depth >= 1).
+ * The model record (CPatch, patch.hpp:10-77) keeps its lists as 16-bit view indexes and 16-bit
+ * cell coordinates (scenes of < 32768 views, cell grids < 32768 wide and high: checked by
+ * pmvs_scene_create), so 128-entry lists cost the bytes 64 32-bit entries did. */
 typedef struct pmvs_patch {
   float coord[4], normal[4];
   float ncc, dscale, ascale, tmp;
   int32_t timages, flag, fix, num_images, num_vimages, dflag; /* dflag: CPatch::_dflag (failed expansion directions) */
-  int32_t images[PMVS_MAX_IMAGES];
-  int32_t grids[PMVS_MAX_IMAGES][2];
-  int32_t vimages[PMVS_MAX_IMAGES];
-  int32_t vgrids[PMVS_MAX_IMAGES][2];
+  int16_t images[PMVS_MAX_IMAGES];
+  int16_t grids[PMVS_MAX_IMAGES][2];
+  int16_t vimages[PMVS_MAX_IMAGES];
+  int16_t vgrids[PMVS_MAX_IMAGES][2];
 } pmvs_patch;
+
+/* pmvs_patch.fix: 0 = a patch of this scene, 1 = fixed (CPatch::_fix, patchOrganizerS.cpp:175-197: never
+ * filtered), PMVS_FIX_FOREIGN = another cluster's boundary patch inserted by the cluster exchange
+ * (pmvs_scene_set_cluster): fixed, and never expanded or returned by this scene. */
+#define PMVS_FIX_FOREIGN 2
 
 typedef struct pmvs_filter_stats {
   int64_t input, removed_outside, removed_exact, removed_neighbor, removed_groups, kept;
@@ -292,6 +305,9 @@ typedef struct pmvs_loop_iter {
   int32_t depth, patches; /* patches kept after the filter pass */
   pmvs_expand_stats expand;
   pmvs_filter_stats filter;
+  /* cluster exchange after this iteration (pmvs_scene_set_cluster; 0 otherwise): this rank's boundary
+   * patches sent, the other ranks' records received, the records inserted as foreign patches */
+  int64_t boundary_sent, boundary_received, boundary_inserted;
 } pmvs_loop_iter;
 pmvs_status pmvs_run_loop(pmvs_scene* scene, const pmvs_patch* seeds, int32_t n, float threshold, int32_t iterations,
                           int32_t wave, int32_t min_candidates, int32_t flags, int32_t cap, int32_t* n_out, pmvs_loop_iter* iters);
@@ -342,6 +358,27 @@ void pmvs_rccl_destroy(pmvs_rccl* comm);
 int pmvs_rccl_allgather(void* comm, const void* send, int64_t bytes, void* recv);
 int pmvs_rccl_allgather_device(void* comm, const void* dsend, int64_t bytes, void* drecv, void* hip_stream);
 pmvs_status pmvs_scene_set_shard_rccl(pmvs_scene* scene, int32_t rank, int32_t world, pmvs_rccl* comm);
+
+/* CMVS cluster per GPU with a boundary exchange.  The reference runs one
+ * pmvs2 per cluster option file (genOption.cpp:73-108) and CMVS clusters overlap in their target images
+ * (bundle.cpp:1003-1160, ske.dat).  With a cluster set, pmvs_run_loop on this scene (one rank of
+ * `world`, one scene per GPU) all-gathers after every iteration but the last, through `fn` (or the
+ * native RCCL communicator, device to device), the patches it holds in target images that another
+ * rank also has as targets -- a {error, count} header per rank first (the images' visibility counts),
+ * then the records with image NUMBERS.  Every rank inserts the other ranks' records whose reference
+ * image is one of its views as the reference's readPatches inserts another run's patches
+ * (patchOrganizerS.cpp:133-197: image numbers mapped to indexes, _vimages cleared, setGrids, addPatch),
+ * as fixed patches that are never expanded (fix = PMVS_FIX_FOREIGN): they fill their cells, so the
+ * rank does not reconstruct the surface the others already hold there, and they take part in the
+ * filters' visibility tests.  Foreign patches are never returned: the final model is this cluster's
+ * own patches, and the merged reconstruction is the concatenation of the ranks' models (as the
+ * reference's per-cluster .ply files are merged).  image_ids: num_views global image numbers of the
+ * scene's views (the option file's timages then oimages).  Collective: every rank calls it (it
+ * all-gathers the target lists once).  world = 1 turns it off.  Not combined with a shard. */
+pmvs_status pmvs_scene_set_cluster(pmvs_scene* scene, int32_t rank, int32_t world, const int32_t* image_ids,
+                                   pmvs_allgather_fn fn, void* ctx);
+pmvs_status pmvs_scene_set_cluster_rccl(pmvs_scene* scene, int32_t rank, int32_t world, const int32_t* image_ids,
+                                        pmvs_rccl* comm);
 
 /* An in-process all-gather among `world` threads (one scene per thread, e.g. several scenes on
  * one GPU): pmvs_thread_allgather with ctx = pmvs_thread_exchange_ctx(group, rank). */

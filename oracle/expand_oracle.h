@@ -275,7 +275,8 @@ static void expand_run(const OScene& s, std::vector<FPatch>& P, std::vector<int>
       for (int p : cellv)
         if (P[p].flag == 0) {
           P[p].flag = 1;
-          queue.push({P[p].tmp, seq++, p});
+          // another cluster's boundary patch (pmvs_scene_set_cluster, fix = PMVS_FIX_FOREIGN) is never expanded here
+          if (P[p].fix != PMVS_FIX_FOREIGN) queue.push({P[p].tmp, seq++, p});
         }
   const int W = std::max(1, wave);
   const auto t_waves = std::chrono::steady_clock::now();

@@ -629,6 +629,21 @@ static inline void diag(int k, bool near) {
   if (near) g_diag[k + 1].fetch_add(1, std::memory_order_relaxed);
 }
 
+// Conversions to the C-ABI records (include/pmvs_amd.h): lists hold PMVS_MAX_IMAGES entries and
+// pmvs_patch keeps 16-bit cell coordinates.  A longer list is not truncated: it raises
+// g_list_overflow, which pyoracle turns into an exception.  A cell coordinate outside
+// [-32767, 32767] (a projection far outside the image, so outside every cell grid) is stored as
+// -32768, the rule the device uses too (pmvs_layout.h grid16).
+static std::atomic<int> g_list_overflow{0};
+static inline int list_len(size_t n) {
+  if (n > (size_t)PMVS_MAX_IMAGES) {
+    g_list_overflow = 1;
+    return PMVS_MAX_IMAGES;
+  }
+  return (int)n;
+}
+static inline int16_t cell16(int v) { return (v < -32767 || v > 32767) ? (int16_t)-32768 : (int16_t)v; }
+
 // COptim::constraintImages, optim.cpp:192-206.
 static void constraint_images(const OScene& s, OCtx& c, OPatch& p, float thr) {
   std::vector<float> inccs;
@@ -850,7 +865,7 @@ static void refine_one(const OScene& s, OCtx& c, const pmvs_candidate& in, pmvs_
   out.status = status;
   for (int i = 0; i < 4; ++i) { out.coord[i] = p.coord[i]; out.normal[i] = p.normal[i]; }
   out.ncc = p.ncc; out.dscale = p.dscale; out.ascale = p.ascale; out.tmp = p.tmp; out.timages = p.timages;
-  const int ni = std::min((int)p.images.size(), PMVS_MAX_IMAGES);
+  const int ni = list_len(p.images.size());
   out.num_images = ni;
   for (int i = 0; i < ni; ++i) out.images[i] = p.images[i];
   for (int i = 0; i < (int)p.grids.size() && i < PMVS_MAX_IMAGES; ++i) {
@@ -873,6 +888,29 @@ static void init_ctx(const OScene& s, OCtx& c) {
 using namespace oracle;
 
 extern "C" {
+
+// CPatchOrganizerS::setGrids (patchOrganizerS.cpp:410-419) on pmvs_patch records, with the int16
+// cell narrowing of the C-ABI (cell16); used by the cluster-exchange emulation in the tests.
+void oracle_set_grids(void* h, pmvs_patch* patches, int n) {
+  const OScene& s = *static_cast<const OScene*>(h);
+  for (int i = 0; i < n; ++i) {
+    pmvs_patch& a = patches[i];
+    V4 c;
+    for (int k = 0; k < 4; ++k) c[k] = a.coord[k];
+    for (int k = 0; k < a.num_images; ++k) {
+      const V3 ic = project(s, a.images[k], c, s.level);
+      a.grids[k][0] = cell16(((int)std::floor(ic[0] + 0.5f)) / s.csize);
+      a.grids[k][1] = cell16(((int)std::floor(ic[1] + 0.5f)) / s.csize);
+    }
+  }
+}
+
+// 1 when a result list exceeded PMVS_MAX_IMAGES since the last reset (see list_len).
+int oracle_list_overflow(int reset) {
+  const int v = g_list_overflow.load();
+  if (reset) g_list_overflow = 0;
+  return v;
+}
 
 // Near-threshold decision counts accumulated since the last reset (see g_diag).
 void oracle_diag(long long* out, int reset) {
@@ -1157,10 +1195,14 @@ void oracle_filter_run(void* h, pmvs_patch* patches, int n, int* keep, int* coun
     const FPatch& q = P[i];
     a.timages = q.timages;
     a.flag = q.flag;
-    a.num_images = (int)std::min<size_t>(q.images.size(), PMVS_MAX_IMAGES);
-    for (int k = 0; k < a.num_images; ++k) { a.images[k] = q.images[k]; a.grids[k][0] = q.grids[k].first; a.grids[k][1] = q.grids[k].second; }
-    a.num_vimages = (int)std::min<size_t>(q.vimages.size(), PMVS_MAX_IMAGES);
-    for (int k = 0; k < a.num_vimages; ++k) { a.vimages[k] = q.vimages[k]; a.vgrids[k][0] = q.vgrids[k].first; a.vgrids[k][1] = q.vgrids[k].second; }
+    a.num_images = list_len(q.images.size());
+    for (int k = 0; k < a.num_images; ++k) {
+      a.images[k] = (int16_t)q.images[k]; a.grids[k][0] = cell16(q.grids[k].first); a.grids[k][1] = cell16(q.grids[k].second);
+    }
+    a.num_vimages = list_len(q.vimages.size());
+    for (int k = 0; k < a.num_vimages; ++k) {
+      a.vimages[k] = (int16_t)q.vimages[k]; a.vgrids[k][0] = cell16(q.vgrids[k].first); a.vgrids[k][1] = cell16(q.vgrids[k].second);
+    }
     keep[i] = kp[i];
   }
 }
@@ -1202,10 +1244,14 @@ static void from_fpatch(const FPatch& q, pmvs_patch& a) {
   for (int k = 0; k < 4; ++k) { a.coord[k] = q.coord[k]; a.normal[k] = q.normal[k]; }
   a.ncc = q.ncc; a.dscale = q.dscale; a.ascale = q.ascale; a.tmp = q.tmp;
   a.timages = q.timages; a.flag = q.flag; a.fix = q.fix; a.dflag = q.dflag;
-  a.num_images = (int)std::min<size_t>(q.images.size(), PMVS_MAX_IMAGES);
-  for (int k = 0; k < a.num_images; ++k) { a.images[k] = q.images[k]; a.grids[k][0] = q.grids[k].first; a.grids[k][1] = q.grids[k].second; }
-  a.num_vimages = (int)std::min<size_t>(q.vimages.size(), PMVS_MAX_IMAGES);
-  for (int k = 0; k < a.num_vimages; ++k) { a.vimages[k] = q.vimages[k]; a.vgrids[k][0] = q.vgrids[k].first; a.vgrids[k][1] = q.vgrids[k].second; }
+  a.num_images = list_len(q.images.size());
+  for (int k = 0; k < a.num_images; ++k) {
+    a.images[k] = (int16_t)q.images[k]; a.grids[k][0] = cell16(q.grids[k].first); a.grids[k][1] = cell16(q.grids[k].second);
+  }
+  a.num_vimages = list_len(q.vimages.size());
+  for (int k = 0; k < a.num_vimages; ++k) {
+    a.vimages[k] = (int16_t)q.vimages[k]; a.vgrids[k][0] = cell16(q.vgrids[k].first); a.vgrids[k][1] = cell16(q.vgrids[k].second);
+  }
 }
 
 // One CExpand::run (expand_oracle.h) on the model (patches[i], alive[i]).  Writes the updated

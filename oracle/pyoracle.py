@@ -58,6 +58,8 @@ def lib():
         L.oracle_seed_geometry.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
                                            C.c_void_p, C.c_void_p]
         L.oracle_diag.argtypes = [C.c_void_p, C.c_int]
+        L.oracle_list_overflow.argtypes = [C.c_int]
+        L.oracle_set_grids.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
         L.oracle_lls5.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
         L.oracle_bobyqa_test.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_int, C.POINTER(C.c_int)]
@@ -111,6 +113,12 @@ def ref_detect_features(rgb, mask=None, edge=None, fcsize=16):
 
 def _p(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _check_lists():
+    """The oracle never truncates a list: a result list longer than PMVS_MAX_IMAGES is an error."""
+    if lib().oracle_list_overflow(1):
+        raise RuntimeError(f"oracle: a patch list exceeded PMVS_MAX_IMAGES ({P.MAX_IMAGES})")
 
 
 class OracleScene:
@@ -191,6 +199,7 @@ class OracleScene:
         keep = np.zeros(len(pa), np.int32)
         counts = np.zeros(4, np.int32)
         lib().oracle_filter_run(self.h, _p(pa), len(pa), _p(keep), _p(counts))
+        _check_lists()
         return pa, keep, counts
 
     def expand_run(self, patches, alive=None, wave=1, count_threshold=4, cap=None, after_seeds=False, min_candidates=0,
@@ -207,6 +216,7 @@ class OracleScene:
                                     _p(st), int(nthreads), int(max_waves))
         if m < 0:
             raise RuntimeError("expand_run: capacity too small")
+        _check_lists()
         keys = ("parents", "candidates", "fail_prep", "fail_pre", "fail_post", "fail_commit", "added", "waves")
         stats = dict(zip(keys, st.tolist()))
         self.last_wave_s = st[8] / 1e9  # wall time of the waves (not part of the parity dict)
@@ -247,6 +257,7 @@ class OracleScene:
         m = lib().oracle_seed_run(self.h, _p(flat), _p(npts), _p(out), cap, _p(st))
         if m < 0:
             raise RuntimeError("seed_run: capacity too small")
+        _check_lists()
         return out[:m].copy(), dict(zip(("trial", "pass", "fail0", "fail1"), st.tolist()))
 
     def seed_images(self, num_views, num_targets, tau):
@@ -274,11 +285,18 @@ class OracleScene:
         lib().oracle_seed_geometry(self.h, i0, i1, _p(xy0), _p(xy1), n, _p(F), _p(epd), _p(co))
         return F.reshape(3, 3), epd, co
 
+    def set_grids(self, patches):
+        """CPatchOrganizerS::setGrids on pmvs_patch records (in place)."""
+        pa = np.ascontiguousarray(patches, P.PATCH_DTYPE)
+        lib().oracle_set_grids(self.h, _p(pa), len(pa))
+        return pa
+
     def refine_batch(self, cands, nthreads=1):
         cands = np.ascontiguousarray(cands, P.CANDIDATE_DTYPE)
         out = np.zeros(len(cands), P.REFINED_DTYPE)
         st = P.Stats()
         lib().oracle_refine_batch(self.h, _p(cands), len(cands), _p(out), nthreads, C.byref(st))
+        _check_lists()
         return out, st.as_dict()
 
 

@@ -326,9 +326,9 @@ static void initial_match(SeedState& st, OCtx& ctx, int index, std::vector<pmvs_
             pp.timages = best.timages;
             pp.num_images = best.num_images;
             for (int k = 0; k < best.num_images; ++k) {
-              pp.images[k] = best.images[k];
-              pp.grids[k][0] = best.grids[k][0];
-              pp.grids[k][1] = best.grids[k][1];
+              pp.images[k] = (int16_t)best.images[k];
+              pp.grids[k][0] = cell16(best.grids[k][0]);
+              pp.grids[k][1] = cell16(best.grids[k][1]);
               const int t = best.images[k];
               if (t < s.tnum) {
                 const int gx = best.grids[k][0], gy = best.grids[k][1];

@@ -100,6 +100,56 @@ def test_loop_80_targets_matches_oracle(gpu_available, oracle_mod):
     assert out_g.tobytes() == out_o.tobytes() or _same_patches(out_g, out_o)
 
 
+@pytest.mark.timeout(900)
+def test_loop_tight_arc_100_views_matches_oracle(gpu_available, oracle_mod):
+    """Lists longer than 64 (the round-2 capacity; the reference's _images / _vimages are unbounded
+    vectors, patch.hpp:38,42, and setVImagesVGrids appends every visible target,
+    patchOrganizerS.cpp:420-447): 100 cameras 0.8 degrees apart, so a point is seen by almost every
+    view.  Full loop vs the oracle, patch for patch, with image lists of up to 100 entries and
+    visible-target lists of more than 64."""
+    import pmvs_amd as P
+    from test_gpu_parity_matrix import _same_patches
+    inp, p = P.synth_scene(100, 320, 240, level=0, csize=2, supersample=1, nthreads=_threads(), arc_step_deg=0.8)
+    cands = P.synth_candidates(p, inp.projections, 60, seed=3)
+    g = P.Scene(inp)
+    seeds = _seeds(g, cands)
+    cap = 1 << 21
+    out_g, log_g = g.run_loop(seeds, inp.threshold, cap=cap, **PROD)
+    g.close()
+    o = oracle_mod.OracleScene(inp)
+    out_o, log_o = o.run_loop(seeds, inp.threshold, cap=cap, nthreads=_threads(), **PROD)
+    o.close()
+    print(f"tight arc 100 views: {[it['patches'] for it in log_o]} patches, max images {out_o['num_images'].max()}, "
+          f"max vimages {out_o['num_vimages'].max()}")
+    assert out_o["num_images"].max() > 64 and out_o["num_vimages"].max() > 64
+    for a, b in zip(log_g, log_o):
+        assert a["patches"] == b["patches"], (a, b)
+    assert out_g.tobytes() == out_o.tobytes() or _same_patches(out_g, out_o)
+
+
+def test_list_overflow_is_an_error(gpu_available, oracle_mod):
+    """A list that would exceed PMVS_MAX_IMAGES (more than 128 views see a patch) fails the call
+    with PMVS_EUNSUPPORTED -- never a silent clamp -- on the device, and the oracle raises too.
+    150 cameras 0.9 degrees apart: points towards the ends of the arc are seen by fewer than 128
+    views (seeds), the expansion reaches points seen by more."""
+    import pmvs_amd as P
+    inp, p = P.synth_scene(150, 160, 120, level=0, csize=2, supersample=1, nthreads=_threads(), arc_step_deg=0.9)
+    cands = P.synth_candidates(p, inp.projections, 300, seed=4)
+    g = P.Scene(inp)
+    r, _ = g.refine_batch(cands)
+    print(f"statuses: {np.unique(r['status'], return_counts=True)}")
+    assert (r["status"] == P.FAIL_OVERFLOW).any()  # the batch entry reports it per candidate
+    seeds = P.patches_from_refined(r)
+    if len(seeds):
+        with pytest.raises(P.PmvsError, match="exceeds|visible in more than"):
+            g.run_loop(seeds, inp.threshold, cap=1 << 22, **PROD)
+    g.close()
+    o = oracle_mod.OracleScene(inp)
+    with pytest.raises(RuntimeError, match="PMVS_MAX_IMAGES"):
+        o.refine_batch(cands, nthreads=_threads())
+    o.close()
+
+
 def _cells(inp, model):
     """Covered target cells: every (target image, cell) some patch is registered in -- the
     CPatchOrganizerS::_pgrids entries the expansion tries to fill (patchOrganizerS.cpp:308-330)."""
