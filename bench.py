@@ -32,6 +32,11 @@ process per GPU:
   --mode shard (strong scaling): all ranks run ONE scene; every expansion wave's refinements are
     split over the ranks and all-gathered over RCCL (pmvs_scene_set_shard_rccl: a C++ RCCL
     communicator, device-to-device records).
+  --mode c4 (BASELINE.json configs[3] at 8 GPUs): one ring of --c4-views-per-cluster x N views split
+    into N CMVS-style clusters (consecutive targets, each sharing --c4-overlap views with each
+    neighbour, as CMVS's ske.dat clusters overlap), one per GPU; the loop exchanges the clusters'
+    boundary patches over the native RCCL communicator after every iteration
+    (pmvs_scene_set_cluster_rccl).  value = patches all clusters committed / max time.
 """
 import argparse
 import json
@@ -64,12 +69,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--mode", choices=("cluster", "shard"), default="cluster")
+    ap.add_argument("--mode", choices=("cluster", "shard", "c4"), default="cluster")
+    ap.add_argument("--c4-views-per-cluster", type=int, default=25)
+    ap.add_argument("--c4-overlap", type=int, default=2)
     ap.add_argument("--views", type=int, default=50)
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--level", type=int, default=0)
-    ap.add_argument("--seed-mode", choices=("features", "synthetic"), default="features",
+    ap.add_argument("--seed-mode", choices=("features", "synthetic"), default="synthetic",
                     help="features: the seed phase on the device (Harris/DoG + CSeed::run, findMatch.cpp:187-193); "
                          "synthetic: refine --seeds synthetic seed-path candidates")
     ap.add_argument("--seeds", type=int, default=5000, help="synthetic seed candidates (--seed-mode synthetic)")
@@ -324,6 +331,34 @@ def c2_refine(P, args, dev, rank):
             "roofline": refine_roofline(tv, rms, 3, tr, tl, src)}
 
 
+def c4_cluster(P, args, rank, world):
+    """Cluster `rank` of a ring of views_per_cluster x world views: target image numbers
+    [vpc*rank - ov, vpc*(rank+1) + ov) mod V (every view once at world 1), rendered alone; seeds = the
+    synthetic seed candidates of the whole ring whose two images lie in the cluster, refined."""
+    vpc, ov = args.c4_views_per_cluster, (args.c4_overlap if world > 1 else 0)
+    V = vpc * world
+    first = (vpc * rank - ov) % V
+    ids = [(first + k) % V for k in range(vpc + 2 * ov)]
+    sp = P.synth_params(V, args.width, args.height, level=args.level, supersample=2)
+    sp.render_first, sp.render_count = first, len(ids)
+    rgb, proj = P.synth_ring(sp, nthreads=16)
+    inp = P.SceneInputs(images=[rgb[k] for k in range(len(ids))], projections=proj[ids], num_targets=len(ids),
+                        level=args.level)
+    return inp, sp, proj, ids
+
+
+def c4_seeds(P, scene, sp, proj, ids, n):
+    cands = P.synth_candidates(sp, proj, n, seed=0x5EED)
+    loc = {v: k for k, v in enumerate(ids)}
+    keep = [i for i in range(len(cands)) if int(cands["images"][i][0]) in loc and int(cands["images"][i][1]) in loc]
+    cs = cands[keep].copy()
+    for c in cs:
+        c["images"][0] = loc[int(c["images"][0])]
+        c["images"][1] = loc[int(c["images"][1])]
+    r, _ = scene.refine_batch(cs)
+    return P.patches_from_refined(r)
+
+
 def main():
     args = parse()
     import torch
@@ -339,6 +374,7 @@ def main():
         dist.init_process_group("nccl")
     dev = torch.device("cuda", local)
     shard = args.mode == "shard" and world > 1
+    c4 = args.mode == "c4"
     if args.only_c2:
         c2 = c2_refine(P, args, dev, rank)
         if rank == 0:
@@ -348,8 +384,12 @@ def main():
     # ---- scene: one cluster per rank (cluster mode) or one shared scene (shard mode)
     t0 = time.time()
     tex_seed = 0x504D5653 + (0 if (shard or world == 1) else 104729 * rank)
-    inp, sp = P.synth_scene(args.views, args.width, args.height, level=args.level, supersample=2, nthreads=16,
-                            seed=tex_seed)
+    if c4:
+        inp, sp, c4_proj, c4_ids = c4_cluster(P, args, rank, world)
+        args.views = len(c4_ids)
+    else:
+        inp, sp = P.synth_scene(args.views, args.width, args.height, level=args.level, supersample=2, nthreads=16,
+                                seed=tex_seed)
     t_synth = time.time() - t0
     log(f"scene rendered ({args.views} x {args.width}x{args.height}) in {t_synth:.1f} s")
     t0 = time.time()
@@ -357,7 +397,10 @@ def main():
     t_scene = time.time() - t0
     t0 = time.time()
     seed_info = {"mode": args.seed_mode}
-    if args.seed_mode == "features":
+    if c4:
+        seeds = c4_seeds(P, scene, sp, c4_proj, c4_ids, args.seeds * world)
+        seed_info.update(mode="synthetic (cluster)", seed_patches=int(len(seeds)))
+    elif args.seed_mode == "features":
         # CFindMatch::init's feature detection (findMatch.cpp:79-82, fcsize 16) and the seed phase
         # CSeed::run (findMatch.cpp:193) on the device
         points = [scene.detect_features(v) for v in range(args.views)]
@@ -376,11 +419,14 @@ def main():
     t_seed = time.time() - t0
     log(f"{len(seeds)} seed patches ({args.seed_mode}) in {t_seed:.1f} s")
     ex = None
-    if shard:  # native RCCL communicator (C++), records all-gathered device to device
+    if shard or (c4 and world > 1):  # native RCCL communicator (C++), records all-gathered device to device
         uid = [P.RcclExchange.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ex = P.RcclExchange(rank, world, uid[0], device=local)
-        ex.attach(scene)
+        if shard:
+            ex.attach(scene)
+        else:
+            ex.attach_cluster(scene, c4_ids)
 
     def step():
         return scene.run_loop(seeds, inp.threshold, iterations=args.iterations, wave=args.wave,
@@ -430,7 +476,7 @@ def main():
         checks = model_checks(last, inp, hashes)
         del last
         cpu = parity = None
-        if not args.no_cpu_baseline and not shard:
+        if not args.no_cpu_baseline and not shard and not c4:
             cpu, parity = loop_samples(P, scene, inp, seeds, args)
         first = logs[0][1]
         result = {
@@ -453,12 +499,14 @@ def main():
                             f"full expand->optim->filter loop ({args.iterations} iterations) from "
                             + (f"the device seed phase's {len(seeds)} seed patches" if args.seed_mode == "features" else
                                f"{args.seeds} synthetic seed candidates")
-                            + (", one scene sharded over all GPUs" if shard else ", one cluster per GPU"),
+                            + (", one scene sharded over all GPUs" if shard else
+                               f", C4: cluster {rank} of a {args.c4_views_per_cluster * world}-view ring, boundary "
+                               f"exchange over RCCL" if c4 else ", one cluster per GPU"),
                 "views": args.views, "width": args.width, "height": args.height, "level": args.level,
                 "seed_mode": args.seed_mode, "seed_patches": int(len(seeds)), "wave": args.wave,
                 "min_candidates": args.min_candidates, "iterations": args.iterations, "wsize": 7, "csize": 2,
                 "minImageNum": 3, "threshold": 0.7,
-                "parallelism": f"{'wave-sharded' if shard else 'cluster-per-GPU'} x{world}",
+                "parallelism": f"{'wave-sharded' if shard else 'CMVS clusters + RCCL boundary exchange' if c4 else 'cluster-per-GPU'} x{world}",
             },
             "ncc_evals_per_s": round(evals_all / elapsed_max, 1),
             "refined_candidates_per_s": round(refined_all / elapsed_max, 1),
@@ -469,7 +517,8 @@ def main():
             "iterations": [{"depth": it["depth"], "patches": it["patches"], "added": it["expand"]["added"],
                             "candidates": it["expand"]["candidates"], "waves": it["expand"]["waves"],
                             "expand_ms": round(it["expand"]["wall_ms"], 1),
-                            "filter_ms": round(it["filter"]["kernel_ms"], 1)} for it in first],
+                            "filter_ms": round(it["filter"]["kernel_ms"], 1),
+                            "boundary": it["boundary"]} for it in first],
             "refine_c2": c2,
             "cpu_baseline": cpu,
             "parity_c3_first_waves": None if parity is None else all(p["ok"] for p in parity),

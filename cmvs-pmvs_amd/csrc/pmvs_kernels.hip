@@ -816,10 +816,10 @@ __device__ void post_candidate(const DScene& s, WaveLds<WS>& L, const RefineJob&
     if (L.overflow) status = PMVS_FAIL_OVERFLOW;
   }
   const int nout = L.nimg;
-  for (int k = lane; k < nout; k += WAVE) {
-    cout.images[k] = L.images[k];
-    cout.grids[k][0] = (status == PMVS_ACCEPTED) ? L.grids[k][0] : 0;
-    cout.grids[k][1] = (status == PMVS_ACCEPTED) ? L.grids[k][1] : 0;
+  for (int k = lane; k < PMVS_MAX_IMAGES; k += WAVE) {  // the unused tail is zero: the record's bytes are defined
+    cout.images[k] = (k < nout) ? L.images[k] : 0;
+    cout.grids[k][0] = (k < nout && status == PMVS_ACCEPTED) ? L.grids[k][0] : 0;
+    cout.grids[k][1] = (k < nout && status == PMVS_ACCEPTED) ? L.grids[k][1] : 0;
   }
   if (lane == 0) {
     cout.status = status;

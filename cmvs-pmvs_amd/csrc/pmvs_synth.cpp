@@ -190,11 +190,17 @@ pmvs_status pmvs_synth_ring(const pmvs_synth_params* p, uint8_t* rgb, float* pro
   for (int i = 0; i < p->num_views; ++i) make_camera(*p, i, cams[i], proj + 12 * i);
   if (!rgb) return PMVS_OK;
   const size_t per = (size_t)p->width * p->height * 3;
-  int nt = std::max(1, std::min((int)nthreads, p->num_views));
+  const int first = p->render_count > 0 ? p->render_first : 0;
+  const int count = p->render_count > 0 ? p->render_count : p->num_views;
+  if (first < 0 || first >= p->num_views || count > p->num_views) return PMVS_EINVAL;
+  int nt = std::max(1, std::min((int)nthreads, count));
   std::vector<std::thread> th;
   for (int t = 0; t < nt; ++t)
     th.emplace_back([&, t]() {
-      for (int i = t; i < p->num_views; i += nt) render_view(*p, i, cams[i], rgb + per * i);
+      for (int i = t; i < count; i += nt) {
+        const int v = (first + i) % p->num_views;  // a cluster's views may wrap round the ring
+        render_view(*p, v, cams[v], rgb + per * i);
+      }
     });
   for (auto& t : th) t.join();
   return PMVS_OK;

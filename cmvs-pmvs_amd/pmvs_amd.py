@@ -125,7 +125,7 @@ class SynthParams(C.Structure):
                 ("seed", C.c_uint64), ("ring_radius", C.c_double), ("height_offset", C.c_double),
                 ("focal_scale", C.c_double), ("arc_step_deg", C.c_double), ("gain_sigma", C.c_double),
                 ("bias_sigma", C.c_double), ("noise_sigma", C.c_double), ("lowtex", C.c_double),
-                ("occluder_radius", C.c_double)]
+                ("occluder_radius", C.c_double), ("render_first", C.c_int32), ("render_count", C.c_int32)]
 
 
 # the photometrically hard synthetic mode (pmvs_synth_params): per-view gain / bias, sensor noise,
@@ -689,9 +689,11 @@ def synth_params(num_views: int, width: int, height: int, num_targets: Optional[
 
 
 def synth_ring(p: SynthParams, nthreads: int = 8, render: bool = True):
+    """(rgb of the rendered views -- all, or p.render_count from p.render_first --, every view's projection)."""
     lib = load_library()
     proj = np.zeros((p.num_views, 3, 4), np.float32)
-    rgb = np.zeros((p.num_views, p.height, p.width, 3), np.uint8) if render else None
+    count = p.render_count if p.render_count > 0 else p.num_views
+    rgb = np.zeros((count, p.height, p.width, 3), np.uint8) if render else None
     _check(lib.pmvs_synth_ring(C.byref(p), _ptr(rgb), _ptr(proj), nthreads))
     return rgb, proj
 

@@ -462,6 +462,9 @@ typedef struct pmvs_synth_params {
    * regions where a low-frequency noise field is below `lowtex` (texture contrast x 0.05), and a
    * textured occluding sphere of radius occluder_radius between the ring and the main sphere. */
   double gain_sigma, bias_sigma, noise_sigma, lowtex, occluder_radius;
+  /* render only the render_count views render_first, render_first + 1, ... (mod num_views) into rgb
+   * (count 0 = all views); projections are written for every view */
+  int32_t render_first, render_count;
 } pmvs_synth_params;
 
 /* Renders num_views RGB8 images (rgb: num_views*width*height*3 bytes, may be NULL to get only

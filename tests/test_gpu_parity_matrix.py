@@ -41,7 +41,10 @@ CONFIGS = {
     "hard_level1_masks": dict(views=8, w=480, h=360, level=1, hard=True, masks=True, edges=True,
                               opts=dict(threshold=0.6)),
 }
-HARD_NEAR_MIN = {"constraint_near": 20, "gains_near": 2}  # near-threshold decisions a hard loop must make
+# near-threshold decisions a hard loop must make (constraintImages within 0.02 of 1 - threshold,
+# filterOutside gains within 0.05 of 0); the level-1 masked scene has fewer patches
+HARD_NEAR_MIN = {"hard_level0": {"constraint_near": 20, "gains_near": 2},
+                 "hard_level1_masks": {"constraint_near": 10, "gains_near": 0}}
 
 
 def build(cfg):
@@ -161,9 +164,6 @@ def test_full_loop_matrix(gpu_available, oracle_mod, name):
     o.close()
     print(f"{name}: {[it['patches'] for it in log_o]} patches, ncc p1/p50 "
           f"{np.percentile(out_o['ncc'], [1, 50]).round(3).tolist()}, near-threshold decisions {near}")
-    if CONFIGS[name].get("hard"):
-        for k, v in HARD_NEAR_MIN.items():
-            assert near[k] >= v, (name, near)
     assert len(seeds) > 0 and len(out_o) > len(seeds)
     for a, b in zip(log_g, log_o):
         assert a["patches"] == b["patches"], (a, b)
@@ -171,6 +171,8 @@ def test_full_loop_matrix(gpu_available, oracle_mod, name):
         assert [a["filter"][k] for k in ("removed_outside", "removed_exact", "removed_neighbor",
                                          "removed_groups")] == b["filter"]
     assert out_g.tobytes() == out_o.tobytes() or _same_patches(out_g, out_o)
+    for k, v in HARD_NEAR_MIN.get(name, {}).items():  # the parity above is not vacuous near the thresholds
+        assert near[k] >= v, (name, near)
 
 
 def _same_patches(a, b):
