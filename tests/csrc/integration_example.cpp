@@ -84,19 +84,26 @@ int refine_seed_candidates(pmvs_scene* scene, std::vector<Patch::CPatch>& batch,
 
 // ---- §3 expansion call site: one CExpand::run (expand.cpp:17-72, whose expandSub at
 // expand.cpp:200-266 needs the organizer at depth >= 1) becomes one pmvs_expand_run
-static void to_pmvs(const Patch::CPatch& p, pmvs_patch& a) {
+// pmvs_patch keeps its lists as int16 (include/pmvs_amd.h): a cell coordinate outside the int16
+// range (a projection far outside the image) is stored as -32768, which no in-grid test accepts
+static int16_t cell16(int v) { return (v < -32767 || v > 32767) ? (int16_t)-32768 : (int16_t)v; }
+
+// returns false when a list is longer than PMVS_MAX_IMAGES (never truncated)
+static bool to_pmvs(const Patch::CPatch& p, pmvs_patch& a) {
   a = pmvs_patch{};
+  if (p._images.size() > PMVS_MAX_IMAGES || p._vimages.size() > PMVS_MAX_IMAGES) return false;
   for (int k = 0; k < 4; ++k) { a.coord[k] = p._coord[k]; a.normal[k] = p._normal[k]; }
   a.ncc = p._ncc;  a.dscale = p._dscale;  a.ascale = p._ascale;  a.tmp = p._tmp;
   a.timages = p._timages;  a.flag = p._flag;  a.fix = p._fix;  a.dflag = p._dflag;
-  a.num_images = (int)std::min<size_t>(p._images.size(), PMVS_MAX_IMAGES);
+  a.num_images = (int)p._images.size();
   for (int k = 0; k < a.num_images; ++k) {
-    a.images[k] = p._images[k];  a.grids[k][0] = p._grids[k][0];  a.grids[k][1] = p._grids[k][1];
+    a.images[k] = (int16_t)p._images[k];  a.grids[k][0] = cell16(p._grids[k][0]);  a.grids[k][1] = cell16(p._grids[k][1]);
   }
-  a.num_vimages = (int)std::min<size_t>(p._vimages.size(), PMVS_MAX_IMAGES);
+  a.num_vimages = (int)p._vimages.size();
   for (int k = 0; k < a.num_vimages; ++k) {
-    a.vimages[k] = p._vimages[k];  a.vgrids[k][0] = p._vgrids[k][0];  a.vgrids[k][1] = p._vgrids[k][1];
+    a.vimages[k] = (int16_t)p._vimages[k];  a.vgrids[k][0] = cell16(p._vgrids[k][0]);  a.vgrids[k][1] = cell16(p._vgrids[k][1]);
   }
+  return true;
 }
 
 static void from_pmvs(const pmvs_patch& a, Patch::CPatch& p) {
@@ -120,14 +127,15 @@ int seeds_on_device(PMVS3::CFindMatch& fm, pmvs_scene* scene, const std::vector<
     counts.push_back((int32_t)view.size());
     for (const PMVS3::CPoint& p : view) flat.push_back({p._icoord[0], p._icoord[1], p._response, p._type});
   }
-  std::vector<pmvs_patch> seeds(std::max<size_t>(flat.size(), 1024));
   int32_t n = 0;
   pmvs_seed_stats st{};
-  if (pmvs_seed_run(scene, flat.data(), counts.data(), /*batch*/ 0, seeds.data(), (int32_t)seeds.size(), &n,
-                    &st) != PMVS_OK) {
+  // out = NULL, cap = 0: the scene keeps the seeds until pmvs_seed_fetch (sized from n)
+  if (pmvs_seed_run(scene, flat.data(), counts.data(), /*batch*/ 0, nullptr, 0, &n, &st) != PMVS_OK) {
     std::cerr << "pmvs_seed_run: " << pmvs_last_error() << std::endl;
     return 1;
   }
+  std::vector<pmvs_patch> seeds(std::max(n, 1));
+  if (pmvs_seed_fetch(scene, seeds.data(), n) != PMVS_OK) return 1;
   for (int i = 0; i < n; ++i) {                // addPatch order of the reference's CPU 1 run
     Patch::PPatch pp(new Patch::CPatch());
     from_pmvs(seeds[i], *pp);
@@ -141,7 +149,8 @@ int expand_on_device(PMVS3::CFindMatch& fm, pmvs_scene* scene, bool after_seeds)
   const int n = (int)fm._pos._ppatches.size();
   std::vector<pmvs_patch> model(n);
   std::vector<int32_t> alive(n, 1);
-  for (int i = 0; i < n; ++i) to_pmvs(*fm._pos._ppatches[i], model[i]);
+  for (int i = 0; i < n; ++i)
+    if (!to_pmvs(*fm._pos._ppatches[i], model[i])) return 1;  // list > PMVS_MAX_IMAGES
   pmvs_set_thresholds(scene, fm._nccThreshold, fm._nccThresholdBefore, fm._depth);
   int32_t n_out = 0;
   pmvs_expand_stats st{};
@@ -170,7 +179,8 @@ int expand_on_device(PMVS3::CFindMatch& fm, pmvs_scene* scene, bool after_seeds)
 int run_loop_on_device(PMVS3::CFindMatch& fm, pmvs_scene* scene, std::vector<pmvs_patch>& model) {
   fm._pos.collectPatches();
   std::vector<pmvs_patch> seeds(fm._pos._ppatches.size());
-  for (size_t i = 0; i < seeds.size(); ++i) to_pmvs(*fm._pos._ppatches[i], seeds[i]);
+  for (size_t i = 0; i < seeds.size(); ++i)
+    if (!to_pmvs(*fm._pos._ppatches[i], seeds[i])) return 1;
   std::vector<pmvs_loop_iter> it(3);
   int32_t n = 0;
   if (pmvs_run_loop(scene, seeds.data(), (int)seeds.size(), fm._nccThreshold, /*iterations*/ 3,
