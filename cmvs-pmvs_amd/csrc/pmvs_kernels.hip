@@ -891,76 +891,77 @@ __device__ __forceinline__ int wave_excl_scan(int v) {
   } while (0)
 #endif
 
-template <int WS, int TSLOTS, int NC>
-__device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS, NC>& C, int njobs, unsigned long long* prof,
-                           unsigned long long& tprev) {
-  constexpr int S = WS * WS;
-  constexpr int NB = 4;  // samples per lane whose loads are in flight together
-  const int lane = lane_id();
-  // --- setup: one lane per texture (grabTex optim.cpp:818-846 + grabSafe :783-805)
-  if (lane < njobs) {
-    const int t = lane;
-    const int r = C.jreq[t];
-    const int index = C.views[r][C.jidx[t]];
-    const float* g = C.geo[r];
-    const float coord[4] = {g[0], g[1], g[2], g[3]}, pz[4] = {g[4], g[5], g[6], g[7]};
-    const float px[4] = {g[8], g[9], g[10], g[11]}, py[4] = {g[12], g[13], g[14], g[15]};
-    const DView& v = s.views[index];
-    int ok = 1;
-    float ray[4] = {v.center[0] - coord[0], v.center[1] - coord[1], v.center[2] - coord[2], v.center[3] - coord[3]};
-    unitize4(ray);
-    const float weight = smax(0.0f, dot4(ray, pz));
-    if ((double)weight < s.cosAngle1) ok = 0;
-    float center[3], c1[3], c2[3], tt[4];
-    project(v, coord, s.level, center);
-    for (int i = 0; i < 4; ++i) tt[i] = coord[i] + px[i];
-    project(v, tt, s.level, c1);
-    for (int i = 0; i < 4; ++i) tt[i] = coord[i] + py[i];
-    project(v, tt, s.level, c2);
-    float dx[3] = {c1[0] - center[0], c1[1] - center[1], c1[2] - center[2]};
-    float dy[3] = {c2[0] - center[0], c2[1] - center[1], c2[2] - center[2]};
-    const float ratio = __fdiv_rn(norm3(dx) + norm3(dy), 2.0f);
-    int leveldif = cvt_int_x86(floor(log((double)ratio) / (double)s.log2f + (double)0.5f));
-    leveldif = imax(-s.level, imin(2, leveldif));
-    const float scale = (leveldif >= 0) ? (float)(1 << leveldif) : __fdiv_rn(1.0f, (float)(1 << (-leveldif)));
-    const int newlevel = s.level + leveldif;
-    for (int i = 0; i < 3; ++i) {
-      center[i] = __fdiv_rn(center[i], scale);
-      dx[i] = __fdiv_rn(dx[i], scale);
-      dy[i] = __fdiv_rn(dy[i], scale);
-    }
-    const float fm = (float)(WS / 2);
-    const float dxm[2] = {dx[0] * fm, dx[1] * fm}, dym[2] = {dy[0] * fm, dy[1] * fm};
-    const float tl0 = (center[0] - dxm[0]) - dym[0], tl1 = (center[1] - dxm[1]) - dym[1];
-    const float tr0 = (center[0] + dxm[0]) - dym[0], tr1 = (center[1] + dxm[1]) - dym[1];
-    const float bl0 = (center[0] - dxm[0]) + dym[0], bl1 = (center[1] - dxm[1]) + dym[1];
-    const float br0 = (center[0] + dxm[0]) + dym[0], br1 = (center[1] + dxm[1]) + dym[1];
-    const float minx = smin(tl0, smin(tr0, smin(bl0, br0)));
-    const float maxx = smax(tl0, smax(tr0, smax(bl0, br0)));
-    const float miny = smin(tl1, smin(tr1, smin(bl1, br1)));
-    const float maxy = smax(tl1, smax(tr1, smax(bl1, br1)));
-    if (ok && (minx < 3.0f || (float)(v.w[newlevel] - 1 - 3) <= maxx || miny < 3.0f ||
-               (float)(v.h[newlevel] - 1 - 3) <= maxy))
-      ok = 0;
-    C.jvalid[t] = ok;
-    C.jW[t] = v.w[newlevel];
-    C.jbase[t] = v.pyr_off[newlevel];
-    C.jleft[t][0] = tl0; C.jleft[t][1] = tl1;
-    C.jdx[t][0] = dx[0]; C.jdx[t][1] = dx[1];
-    C.jdy[t][0] = dy[0]; C.jdy[t][1] = dy[1];
+// Per-texture steps of the cooperative objective evaluation, shared by the wavefront form
+// (refine_v2_kernel) and the workgroup form (refine_wg_kernel).  L is the kernel's LDS layout
+// (jreq / jidx / views / geo name the slot's request, tex / ave / j* hold the slot).
+// setup, one thread per texture: grabTex optim.cpp:818-846 + grabSafe :783-805
+template <int WS, class L>
+__device__ __forceinline__ void tex_setup(const DScene& s, L& C, int t) {
+  const int r = C.jreq[t];
+  const int index = C.views[r][C.jidx[t]];
+  const float* g = C.geo[r];
+  const float coord[4] = {g[0], g[1], g[2], g[3]}, pz[4] = {g[4], g[5], g[6], g[7]};
+  const float px[4] = {g[8], g[9], g[10], g[11]}, py[4] = {g[12], g[13], g[14], g[15]};
+  const DView& v = s.views[index];
+  int ok = 1;
+  float ray[4] = {v.center[0] - coord[0], v.center[1] - coord[1], v.center[2] - coord[2], v.center[3] - coord[3]};
+  unitize4(ray);
+  const float weight = smax(0.0f, dot4(ray, pz));
+  if ((double)weight < s.cosAngle1) ok = 0;
+  float center[3], c1[3], c2[3], tt[4];
+  project(v, coord, s.level, center);
+  for (int i = 0; i < 4; ++i) tt[i] = coord[i] + px[i];
+  project(v, tt, s.level, c1);
+  for (int i = 0; i < 4; ++i) tt[i] = coord[i] + py[i];
+  project(v, tt, s.level, c2);
+  float dx[3] = {c1[0] - center[0], c1[1] - center[1], c1[2] - center[2]};
+  float dy[3] = {c2[0] - center[0], c2[1] - center[1], c2[2] - center[2]};
+  const float ratio = __fdiv_rn(norm3(dx) + norm3(dy), 2.0f);
+  int leveldif = cvt_int_x86(floor(log((double)ratio) / (double)s.log2f + (double)0.5f));
+  leveldif = imax(-s.level, imin(2, leveldif));
+  const float scale = (leveldif >= 0) ? (float)(1 << leveldif) : __fdiv_rn(1.0f, (float)(1 << (-leveldif)));
+  const int newlevel = s.level + leveldif;
+  for (int i = 0; i < 3; ++i) {
+    center[i] = __fdiv_rn(center[i], scale);
+    dx[i] = __fdiv_rn(dx[i], scale);
+    dy[i] = __fdiv_rn(dy[i], scale);
   }
-  __syncthreads();
-  PROF_MARK(3);
-  // --- gather: NB samples per lane at a time, all 4*NB texel loads issued before use
+  const float fm = (float)(WS / 2);
+  const float dxm[2] = {dx[0] * fm, dx[1] * fm}, dym[2] = {dy[0] * fm, dy[1] * fm};
+  const float tl0 = (center[0] - dxm[0]) - dym[0], tl1 = (center[1] - dxm[1]) - dym[1];
+  const float tr0 = (center[0] + dxm[0]) - dym[0], tr1 = (center[1] + dxm[1]) - dym[1];
+  const float bl0 = (center[0] - dxm[0]) + dym[0], bl1 = (center[1] - dxm[1]) + dym[1];
+  const float br0 = (center[0] + dxm[0]) + dym[0], br1 = (center[1] + dxm[1]) + dym[1];
+  const float minx = smin(tl0, smin(tr0, smin(bl0, br0)));
+  const float maxx = smax(tl0, smax(tr0, smax(bl0, br0)));
+  const float miny = smin(tl1, smin(tr1, smin(bl1, br1)));
+  const float maxy = smax(tl1, smax(tr1, smax(bl1, br1)));
+  if (ok && (minx < 3.0f || (float)(v.w[newlevel] - 1 - 3) <= maxx || miny < 3.0f ||
+             (float)(v.h[newlevel] - 1 - 3) <= maxy))
+    ok = 0;
+  C.jvalid[t] = ok;
+  C.jW[t] = v.w[newlevel];
+  C.jbase[t] = v.pyr_off[newlevel];
+  C.jleft[t][0] = tl0; C.jleft[t][1] = tl1;
+  C.jdx[t][0] = dx[0]; C.jdx[t][1] = dx[1];
+  C.jdy[t][0] = dy[0]; C.jdy[t][1] = dy[1];
+}
+
+// gather: thread `tid` of `NT` takes samples tid, tid + NT, ...; NB samples per thread at a time,
+// all 4*NB texel loads issued before use
+template <int WS, int NT, class L>
+__device__ __forceinline__ void tex_gather(const DScene& s, L& C, int njobs, int tid) {
+  constexpr int S = WS * WS;
+  constexpr int NB = 4;
   const int total = njobs * S;
-  for (int u0 = 0; u0 < total; u0 += WAVE * NB) {
+  for (int u0 = 0; u0 < total; u0 += NT * NB) {
     uint32_t a0[NB], a1[NB], b0[NB], b1[NB];
     float fx[NB], fy[NB];
     int lxs[NB], lys[NB];
     bool live[NB];
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
-      const int u = u0 + q * WAVE + lane;
+      const int u = u0 + q * NT + tid;
       const int t = u / S, k = u - t * S;
       live[q] = (u < total) && C.jvalid[t < njobs ? t : 0];
       long long idx = 0;
@@ -985,7 +986,7 @@ __device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS, NC>& C, int njobs
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
       if (!live[q]) continue;
-      const int u = u0 + q * WAVE + lane;
+      const int u = u0 + q * NT + tid;
       const int t = u / S, k = u - t * S;
       const float dx1 = fx[q] - (float)lxs[q], dx0 = 1.0f - dx1;
       const float dy1 = fy[q] - (float)lys[q], dy0 = 1.0f - dy1;
@@ -1000,42 +1001,49 @@ __device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS, NC>& C, int njobs
       C.tex[t][0][k] = r; C.tex[t][1][k] = g; C.tex[t][2][k] = b;
     }
   }
-  __syncthreads();
-  PROF_MARK(4);
-  // --- normalize (optim.cpp:1031-1067), one lane per texture
-  if (lane < njobs && C.jvalid[lane]) {
-    const int t = lane;
-    const float *X = C.tex[t][0], *Y = C.tex[t][1], *Z = C.tex[t][2];
-    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;  // each channel summed in sample order
-    int i = 0;
-    for (; i + 4 <= S; i += 4) {
-      const float4 x = *reinterpret_cast<const float4*>(X + i), y = *reinterpret_cast<const float4*>(Y + i),
-                   z = *reinterpret_cast<const float4*>(Z + i);
-      a0 += x.x; a1 += y.x; a2 += z.x;
-      a0 += x.y; a1 += y.y; a2 += z.y;
-      a0 += x.z; a1 += y.z; a2 += z.z;
-      a0 += x.w; a1 += y.w; a2 += z.w;
-    }
-    for (; i < S; ++i) { a0 += X[i]; a1 += Y[i]; a2 += Z[i]; }
-    const float fs3 = (float)S;
-    a0 = __fdiv_rn(a0, fs3); a1 = __fdiv_rn(a1, fs3); a2 = __fdiv_rn(a2, fs3);
-    float ave2 = 0.0f;
-    auto sq = [&](float x, float y, float z) {
-      const float f0 = a0 - x, f1 = a1 - y, f2 = a2 - z;
-      ave2 += f0 * f0 + f1 * f1 + f2 * f2;
-    };
-    for (i = 0; i + 4 <= S; i += 4) {
-      const float4 x = *reinterpret_cast<const float4*>(X + i), y = *reinterpret_cast<const float4*>(Y + i),
-                   z = *reinterpret_cast<const float4*>(Z + i);
-      sq(x.x, y.x, z.x); sq(x.y, y.y, z.y); sq(x.z, y.z, z.z); sq(x.w, y.w, z.w);
-    }
-    for (; i < S; ++i) sq(X[i], Y[i], Z[i]);
-    ave2 = fsqrt_rn(__fdiv_rn(ave2, (float)(3 * S)));
-    if (ave2 == 0.0f) ave2 = 1.0f;
-    C.ave[t][0] = a0; C.ave[t][1] = a1; C.ave[t][2] = a2; C.ave[t][3] = ave2;
+}
+
+// normalize (optim.cpp:1031-1067) part 1, one thread per valid texture: channel means and ave2,
+// each sum in sample order
+template <int WS, class L>
+__device__ __forceinline__ void tex_moments(L& C, int t) {
+  constexpr int S = WS * WS;
+  const float *X = C.tex[t][0], *Y = C.tex[t][1], *Z = C.tex[t][2];
+  float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+  int i = 0;
+  for (; i + 4 <= S; i += 4) {
+    const float4 x = *reinterpret_cast<const float4*>(X + i), y = *reinterpret_cast<const float4*>(Y + i),
+                 z = *reinterpret_cast<const float4*>(Z + i);
+    a0 += x.x; a1 += y.x; a2 += z.x;
+    a0 += x.y; a1 += y.y; a2 += z.y;
+    a0 += x.z; a1 += y.z; a2 += z.z;
+    a0 += x.w; a1 += y.w; a2 += z.w;
   }
-  __syncthreads();
-  for (int u = lane; u < total; u += WAVE) {
+  for (; i < S; ++i) { a0 += X[i]; a1 += Y[i]; a2 += Z[i]; }
+  const float fs3 = (float)S;
+  a0 = __fdiv_rn(a0, fs3); a1 = __fdiv_rn(a1, fs3); a2 = __fdiv_rn(a2, fs3);
+  float ave2 = 0.0f;
+  auto sq = [&](float x, float y, float z) {
+    const float f0 = a0 - x, f1 = a1 - y, f2 = a2 - z;
+    ave2 += f0 * f0 + f1 * f1 + f2 * f2;
+  };
+  for (i = 0; i + 4 <= S; i += 4) {
+    const float4 x = *reinterpret_cast<const float4*>(X + i), y = *reinterpret_cast<const float4*>(Y + i),
+                 z = *reinterpret_cast<const float4*>(Z + i);
+    sq(x.x, y.x, z.x); sq(x.y, y.y, z.y); sq(x.z, y.z, z.z); sq(x.w, y.w, z.w);
+  }
+  for (; i < S; ++i) sq(X[i], Y[i], Z[i]);
+  ave2 = fsqrt_rn(__fdiv_rn(ave2, (float)(3 * S)));
+  if (ave2 == 0.0f) ave2 = 1.0f;
+  C.ave[t][0] = a0; C.ave[t][1] = a1; C.ave[t][2] = a2; C.ave[t][3] = ave2;
+}
+
+// normalize part 2, element-wise over all threads
+template <int WS, int NT, class L>
+__device__ __forceinline__ void tex_scale(L& C, int njobs, int tid) {
+  constexpr int S = WS * WS;
+  const int total = njobs * S;
+  for (int u = tid; u < total; u += NT) {
     const int t = u / S, k = u - t * S;
     if (!C.jvalid[t]) continue;
     const float a2 = C.ave[t][3];
@@ -1043,35 +1051,97 @@ __device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS, NC>& C, int njobs
     C.tex[t][1][k] = __fdiv_rn(C.tex[t][1][k] - C.ave[t][1], a2);
     C.tex[t][2][k] = __fdiv_rn(C.tex[t][2][k] - C.ave[t][2], a2);
   }
+}
+
+// robust INCC of slot t against its request's reference slot (optim.cpp:561-567, 919-929)
+template <int WS, class L>
+__device__ __forceinline__ void tex_dot(L& C, int t) {
+  constexpr int S = WS * WS;
+  const int ref = C.rfirst[C.jreq[t]];
+  float r = 0.0f;
+  if (C.jvalid[ref] && C.jvalid[t]) {
+    float ans = 0.0f;  // per sample R, G, B products, in sample order
+    const float *PX = C.tex[ref][0], *PY = C.tex[ref][1], *PZ = C.tex[ref][2];
+    const float *QX = C.tex[t][0], *QY = C.tex[t][1], *QZ = C.tex[t][2];
+    int i = 0;
+    for (; i + 4 <= S; i += 4) {
+      const float4 px = *reinterpret_cast<const float4*>(PX + i), py = *reinterpret_cast<const float4*>(PY + i),
+                   pz = *reinterpret_cast<const float4*>(PZ + i), qx = *reinterpret_cast<const float4*>(QX + i),
+                   qy = *reinterpret_cast<const float4*>(QY + i), qz = *reinterpret_cast<const float4*>(QZ + i);
+      ans += px.x * qx.x; ans += py.x * qy.x; ans += pz.x * qz.x;
+      ans += px.y * qx.y; ans += py.y * qy.y; ans += pz.y * qz.y;
+      ans += px.z * qx.z; ans += py.z * qy.z; ans += pz.z * qz.z;
+      ans += px.w * qx.w; ans += py.w * qy.w; ans += pz.w * qz.w;
+    }
+    for (; i < S; ++i) {
+      ans += PX[i] * QX[i];
+      ans += PY[i] * QY[i];
+      ans += PZ[i] * QZ[i];
+    }
+    r = robustincc((float)(1.0 - (double)__fdiv_rn(ans, (float)(3 * S))));
+  }
+  C.jres[t] = r;
+}
+
+// The objective value of one request from its slots [off, off + sz): COptim::my_f
+// (optim.cpp:527-577, need 1) or the robust weighted computeINCC (optim.cpp:875-938, need 2).
+template <class L>
+__device__ __forceinline__ double request_value(const DScene& s, const L& C, int off, int sz, int need,
+                                                const RefineJob& J, unsigned long long& tex_valid) {
+  const int ref = off;
+  int nv = 0;
+  for (int i = 0; i < sz; ++i) nv += C.jvalid[off + i];
+  double f;
+  if (need == 1) {
+    const int mininum = imin(s.minImageNum, sz);
+    tex_valid += nv;
+    if (!C.jvalid[ref]) {
+      f = 2.0;
+    } else {
+      double ans = 0.0f;
+      int denom = 0;
+      for (int i = 1; i < sz; ++i) {
+        if (!C.jvalid[off + i]) continue;
+        ans += (double)C.jres[off + i];
+        denom++;
+      }
+      f = (denom < mininum - 1) ? 2.0f : ans / denom;
+    }
+  } else {
+    if (!C.jvalid[ref]) {
+      f = 2.0;
+    } else {
+      double score = 0.0;
+      float totalweight = 0.0f;
+      for (int i = 1; i < sz; ++i) {
+        if (C.jvalid[off + i]) {
+          const float w = J.weights[i];
+          totalweight += w;
+          score += (double)(C.jres[off + i] * w);
+        }
+      }
+      f = (totalweight == 0.0f) ? 2.0 : score / (double)totalweight;
+    }
+  }
+  return f;
+}
+
+template <int WS, int TSLOTS, int NC>
+__device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS, NC>& C, int njobs, unsigned long long* prof,
+                           unsigned long long& tprev) {
+  const int lane = lane_id();
+  if (lane < njobs) tex_setup<WS>(s, C, lane);
+  __syncthreads();
+  PROF_MARK(3);
+  tex_gather<WS, WAVE>(s, C, njobs, lane);
+  __syncthreads();
+  PROF_MARK(4);
+  if (lane < njobs && C.jvalid[lane]) tex_moments<WS>(C, lane);
+  __syncthreads();
+  tex_scale<WS, WAVE>(C, njobs, lane);
   __syncthreads();
   PROF_MARK(5);
-  // --- robust INCC against the request's reference texture (optim.cpp:561-567, 919-929)
-  if (lane < njobs && C.jidx[lane] >= 1) {
-    const int t = lane, ref = C.rfirst[C.jreq[t]];
-    float r = 0.0f;
-    if (C.jvalid[ref] && C.jvalid[t]) {
-      float ans = 0.0f;  // per sample R, G, B products, in sample order
-      const float *PX = C.tex[ref][0], *PY = C.tex[ref][1], *PZ = C.tex[ref][2];
-      const float *QX = C.tex[t][0], *QY = C.tex[t][1], *QZ = C.tex[t][2];
-      int i = 0;
-      for (; i + 4 <= S; i += 4) {
-        const float4 px = *reinterpret_cast<const float4*>(PX + i), py = *reinterpret_cast<const float4*>(PY + i),
-                     pz = *reinterpret_cast<const float4*>(PZ + i), qx = *reinterpret_cast<const float4*>(QX + i),
-                     qy = *reinterpret_cast<const float4*>(QY + i), qz = *reinterpret_cast<const float4*>(QZ + i);
-        ans += px.x * qx.x; ans += py.x * qy.x; ans += pz.x * qz.x;
-        ans += px.y * qx.y; ans += py.y * qy.y; ans += pz.y * qz.y;
-        ans += px.z * qx.z; ans += py.z * qy.z; ans += pz.z * qz.z;
-        ans += px.w * qx.w; ans += py.w * qy.w; ans += pz.w * qz.w;
-      }
-      for (; i < S; ++i) {
-        ans += PX[i] * QX[i];
-        ans += PY[i] * QY[i];
-        ans += PZ[i] * QZ[i];
-      }
-      r = robustincc((float)(1.0 - (double)__fdiv_rn(ans, (float)(3 * S))));
-    }
-    C.jres[t] = r;
-  }
+  if (lane < njobs && C.jidx[lane] >= 1) tex_dot<WS>(C, lane);
   __syncthreads();
   PROF_MARK(6);
 }
@@ -1210,43 +1280,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(REFINE_WPE(N
       if (lane == 0) grabs += njobs;
       if (in) {
         // reduce this request's per-texture results in the reference's order
-        const int ref = off;
-        int nv = 0;
-        for (int i = 0; i < sz; ++i) nv += C.jvalid[off + i];
-        double f;
-        if (need == 1) {  // COptim::my_f (optim.cpp:527-577)
-          const int mininum = imin(s.minImageNum, sz);
-          tex_valid += nv;
-          if (!C.jvalid[ref]) {
-            f = 2.0;
-          } else {
-            double ans = 0.0f;
-            int denom = 0;
-            for (int i = 1; i < sz; ++i) {
-              if (!C.jvalid[off + i]) continue;
-              ans += (double)C.jres[off + i];
-              denom++;
-            }
-            f = (denom < mininum - 1) ? 2.0f : ans / denom;
-          }
-        } else {  // COptim::computeINCC robust weighted (optim.cpp:875-938)
-          const RefineJob& J = jobs[cand];
-          if (!C.jvalid[ref]) {
-            f = 2.0;
-          } else {
-            double score = 0.0;
-            float totalweight = 0.0f;
-            for (int i = 1; i < sz; ++i) {
-              if (C.jvalid[off + i]) {
-                const float w = J.weights[i];
-                totalweight += w;
-                score += (double)(C.jres[off + i] * w);
-              }
-            }
-            f = (totalweight == 0.0f) ? 2.0 : score / (double)totalweight;
-          }
-        }
-        fv = f;
+        fv = request_value(s, C, off, sz, need, jobs[cand], tex_valid);
         pending = false;
       }
       __syncthreads();
@@ -1281,6 +1315,229 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(REFINE_WPE(N
     atomicAdd(&st->rounds, rounds);
     atomicAdd(&st->chunks, chunks);
     for (int i = 0; i < 8; ++i) atomicAdd(&st->prof[i], prof[i]);
+  }
+}
+
+// ---------------------------------------------------------------- refinePatchBFGS, workgroup form
+// One 256-thread workgroup (4 wavefronts, one per SIMD) owns NC chains whose optimizer states
+// live in the workgroup's LDS.  Chain c is stepped by lane c % (NC/OW) of wavefront c / (NC/OW):
+// with OW = 1 a single wavefront advances all NC chains in one instruction stream (NC lanes per
+// f64 instruction instead of the wavefront form's 6), with OW = 4 every SIMD steps NC/4 of them.
+// The requests of a round are packed, in chain order, into chunks of <= TS texture slots, and all
+// 256 threads evaluate a chunk: thread-per-texture setup / moments / dot spread over the four
+// wavefronts (consecutive slots per wavefront: conflict-free LDS rows), thread-per-sample gather
+// and scaling.  Results, optimizer trajectories and counters equal the wavefront form's.
+constexpr int WG_THREADS = 256;
+constexpr int WG_LDS_BYTES = 160 * 1024;
+
+template <int WS, int NC, int WGPC>
+struct RefWgFit {  // texture slots (<= 64) that fit next to NC optimizer states, WGPC workgroups per CU
+  static constexpr int SP = (WS * WS + 3) & ~3;
+  static constexpr int per_slot = 3 * SP * 4 + 4 * 4 + 8 + 4 * 4 + 6 * 4 + 4;
+  static constexpr int fixed = NC * ((int)sizeof(BqState) + 16 * 4 + PMVS_MAX_TAU * 2 + 4 * 4) + 4 * (NC + 1) + 64;
+  static constexpr int fit = (WG_LDS_BYTES / WGPC - fixed) / per_slot - 1;
+  static constexpr int slots = fit < 64 ? fit : 64;
+};
+
+template <int WS, int NC, int TS>
+struct RefWgLds {
+  static constexpr int S = WS * WS;
+  static constexpr int SP = (S + 3) & ~3;
+  BqState bq[NC];                          // chain c's optimizer state
+  alignas(16) float tex[TS][3][SP];       // slot: R, G, B rows of the S samples
+  float ave[TS][4];
+  long long jbase[TS];
+  int jvalid[TS], jW[TS], jreq[TS], jidx[TS];
+  float jleft[TS][2], jdx[TS][2], jdy[TS][2];
+  float jres[TS];
+  float geo[NC][16];                       // requesting chain: coord, normal, pxaxis, pyaxis
+  unsigned short views[NC][PMVS_MAX_TAU];  // chain: first size images
+  int rsize[NC];                           // this round's request size (0: none)
+  int rfirst[NC], rchunk[NC];              // its first slot and chunk
+  int alive[NC];                           // chain holds a candidate or may still get one
+  int chunk_jobs[NC + 1];
+  int nchunk, live;
+};
+
+template <int WS, int NC, int TS, int OW>
+__global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(REFINE_WPE(NC)))) void refine_wg_kernel(
+    DScene s, RefineJob* __restrict__ jobs, int n, int nc_active, DevStats* st) {
+  constexpr int CPW = NC / OW;
+  static_assert(NC % OW == 0 && NC <= WAVE && OW >= 1 && OW <= WG_THREADS / WAVE, "chain layout");
+  static_assert(TS >= PMVS_MAX_TAU, "a request must fit one chunk");
+  static_assert(sizeof(RefWgLds<WS, NC, TS>) <= WG_LDS_BYTES, "LDS");
+  __shared__ RefWgLds<WS, NC, TS> C;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & (WAVE - 1);
+  // chain c = lane * OW + wave: the first nc_active chains (small batches spread over more
+  // workgroups) fall on every optimizer wavefront
+  const int cidx = lane * OW + wave;
+  const bool owner = wave < OW && lane < CPW && cidx < nc_active;
+  const int c = owner ? cidx : 0;
+  BQ_AS BqState& bq = *(BQ_AS BqState*)&C.bq[c];
+  RefineSetup R;
+  int cand = -1, need = 0, evals = 0, size = 0, nimg = 0, rc = 0;
+  bool exhausted = !owner;
+  double fv = 0.0;
+  float fcoord[4], fnormal[4];
+  unsigned long long tex_valid = 0, grabs = 0, nevals = 0, rounds = 0, chunks = 0;
+  const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999};
+  const double ub[3] = {HUGE_VAL, 23.99999, 23.99999};
+  for (;;) {
+    bool req = false;
+    if (owner) {
+      // (a) refill an idle chain from the queue (skipping candidates that failed preProcess)
+      while (cand < 0 && !exhausted) {
+        const unsigned long long q = atomicAdd(&st->queue2, 1ull);
+        if (q >= (unsigned long long)n) {
+          exhausted = true;
+          break;
+        }
+        const RefineJob& J = jobs[q];
+        if (J.status != PMVS_ACCEPTED) continue;
+        cand = (int)q;
+        for (int i = 0; i < 4; ++i) { R.center[i] = J.center[i]; R.ray[i] = J.ray[i]; }
+        R.dscale = J.dscale;
+        R.ascale = s.ascale;
+        R.ref = J.images[0];
+        nimg = J.nimg;
+        size = imin(s.tau, nimg);
+        for (int i = 0; i < size; ++i) C.views[c][i] = J.images[i];
+        evals = 0;
+        const double x0[3] = {J.x0[0], J.x0[1], J.x0[2]};
+        bq_begin(bq, x0, lb, ub, 1.e-7, 1000);
+        fv = 0.0;
+        need = 0;
+      }
+      // (b) advance BOBYQA when it holds an objective value (or just started)
+      if (cand >= 0 && need == 0) {
+        const int r = (bq.resume < 0) ? BQ_DONE : bq_step(bq, fv);
+        if (r == BQ_NEED_F) {
+          need = 1;
+          const double xe[3] = {bq.xeval[0], bq.xeval[1], bq.xeval[2]};
+          decode(s, R, xe, fcoord, fnormal);
+        } else {
+          rc = bq.rc;
+          const bool success = (rc == BQR_SUCCESS || rc == 2 || rc == 3 || rc == BQR_XTOL);
+          RefineJob& J = jobs[cand];
+          J.refine_code = rc;
+          J.evals = evals;
+          if (success) {
+            const double xo[3] = {bq.xout[0], bq.xout[1], bq.xout[2]};
+            decode(s, R, xo, fcoord, fnormal);
+            if (nimg < 2) {  // computeINCC returns 2.0 without grabbing (optim.cpp:866)
+              J.ncc = (float)(1.0 - (double)unrobustincc(2.0f));
+              for (int i = 0; i < 4; ++i) { J.rcoord[i] = fcoord[i]; J.rnormal[i] = fnormal[i]; }
+              cand = -1;
+            } else {
+              need = 2;  // final computeINCC (robust, weighted) at the refined geometry
+            }
+          } else {
+            cand = -1;  // geometry and _ncc stay unrefined (optim.cpp:649-655)
+          }
+        }
+      }
+      // (c) publish the request
+      req = (cand >= 0 && need != 0);
+      if (req) {
+        float px[4], py[4];
+        get_paxes(s, s.views[R.ref], fcoord, fnormal, px, py);
+        for (int i = 0; i < 4; ++i) {
+          C.geo[c][i] = fcoord[i]; C.geo[c][4 + i] = fnormal[i];
+          C.geo[c][8 + i] = px[i]; C.geo[c][12 + i] = py[i];
+        }
+      }
+      C.rsize[c] = req ? size : 0;
+      C.alive[c] = (cand >= 0 || !exhausted) ? 1 : 0;
+    }
+    __syncthreads();
+    // (d) pack the round's requests into chunks of <= TS slots, in chain order
+    if (wave == 0) {
+      const int sz = lane < NC ? C.rsize[lane] : 0;
+      bool pending = sz > 0;
+      int k = 0;
+      while (__ballot(pending) != 0ull) {
+        const int off = wave_excl_scan(pending ? sz : 0);
+        const bool in = pending && (off + sz <= TS);
+        const int nj = __shfl(off + sz, 63 - __clzll(__ballot(in)));
+        if (in) {
+          C.rfirst[lane] = off;
+          C.rchunk[lane] = k;
+        }
+        if (lane == 0) C.chunk_jobs[k] = nj;
+        pending = pending && !in;
+        ++k;
+      }
+      const bool al = lane < NC && C.alive[lane] != 0;
+      if (lane == 0) {
+        C.nchunk = k;
+        C.live = __ballot(al) != 0ull ? 1 : 0;
+      }
+    }
+    __syncthreads();
+    const int nchunk = C.nchunk;
+    rounds++;
+    if (nchunk == 0) {  // (nchunk / live are rewritten only after the next round's first barrier)
+      if (!C.live) break;
+      continue;
+    }
+    const int my_chunk = req ? C.rchunk[c] : -1;
+    const int my_off = req ? C.rfirst[c] : 0;
+    // (e) evaluate chunk by chunk
+    for (int k = 0; k < nchunk; ++k) {
+      if (my_chunk == k) {
+        for (int i = 0; i < size; ++i) {
+          C.jreq[my_off + i] = c;
+          C.jidx[my_off + i] = i;
+        }
+      }
+      __syncthreads();
+      const int njobs = C.chunk_jobs[k];
+      const int per = (njobs + 3) >> 2;  // slots per wavefront in the per-texture steps
+      const int t = wave * per + lane;
+      const bool mine = lane < per && t < njobs;
+      if (mine) tex_setup<WS>(s, C, t);
+      __syncthreads();
+      tex_gather<WS, WG_THREADS>(s, C, njobs, tid);
+      __syncthreads();
+      if (mine && C.jvalid[t]) tex_moments<WS>(C, t);
+      __syncthreads();
+      tex_scale<WS, WG_THREADS>(C, njobs, tid);
+      __syncthreads();
+      if (mine && C.jidx[t] >= 1) tex_dot<WS>(C, t);
+      __syncthreads();
+      chunks++;
+      grabs += njobs;
+      if (my_chunk == k) fv = request_value(s, C, my_off, size, need, jobs[cand], tex_valid);
+      __syncthreads();
+    }
+    // (f) consume the results
+    if (req) {
+      if (need == 1) {
+        evals++;
+        nevals++;
+        need = 0;
+      } else {
+        RefineJob& J = jobs[cand];
+        J.ncc = (float)(1.0 - (double)unrobustincc((float)fv));
+        for (int i = 0; i < 4; ++i) { J.rcoord[i] = fcoord[i]; J.rnormal[i] = fnormal[i]; }
+        cand = -1;
+        need = 0;
+      }
+    }
+  }
+  // per-wavefront reduction of the chain counters, one atomic each
+  for (int d = 32; d >= 1; d >>= 1) {
+    tex_valid += __shfl_xor(tex_valid, d);
+    nevals += __shfl_xor(nevals, d);
+  }
+  if (lane == 0 && wave < OW) {
+    atomicAdd(&st->evals, nevals);
+    atomicAdd(&st->tex_valid, tex_valid);
+  }
+  if (tid == 0) {
+    atomicAdd(&st->tex_grabs, grabs);
+    atomicAdd(&st->rounds, rounds);
+    atomicAdd(&st->chunks, chunks);
   }
 }
 
@@ -1543,6 +1800,7 @@ void RefineHost::release() {
 bool refine_config_supported(int tslots) {
   switch (tslots) {
     case 804: case 807: case 808: case 1204: case 1206: case 1608: case 2408: return true;
+    case 164011: case 164021: case 164041: case 148041: case 132022: case 132042: case 116042: return true;
 #if defined(BQ_PRIVATE)
     case 1264: case 2464: case 1232: case 2432: case 1216: case 2448: case 3232: case 3248: case 3264: case 4832:
     case 4864: return true;
@@ -1577,6 +1835,38 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
   }
   const int nc = tslots % 100;
   const int rg = refine_grid < (n + nc - 1) / nc ? refine_grid : (n + nc - 1) / nc;
+  if (tslots >= 100000) {  // workgroup form: 100000 + chains * 1000 + optimizer wavefronts * 10 + workgroups per CU
+    const int ncw = (tslots / 1000) % 100, wgpc = tslots % 10;
+    int dev = 0, cus = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess ||
+        (e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
+      return e;
+    cus = cus > 0 ? cus : 1;
+    // every CU gets a workgroup while the batch has candidates for them; a small batch runs fewer
+    // chains per workgroup (nc_active) rather than fewer workgroups: its length is one chain's latency
+    const int wgrid = cus * wgpc < n ? cus * wgpc : n;
+    const int nca = (n + wgrid - 1) / wgrid < ncw ? (n + wgrid - 1) / wgrid : ncw;
+#define PMVS_WG(NCc, OWc, WGPCc)                                                                                    \
+  case 100000 + NCc * 1000 + OWc * 10 + WGPCc:                                                                       \
+    hipLaunchKernelGGL((refine_wg_kernel<WS, NCc, RefWgFit<WS, NCc, WGPCc>::slots, OWc>), dim3(wgrid), dim3(WG_THREADS), \
+                       0, stream, s, d_jobs, n, nca, d_st);                                                           \
+    break;
+    switch (tslots) {
+      PMVS_WG(64, 1, 1)
+      PMVS_WG(64, 2, 1)
+      PMVS_WG(64, 4, 1)
+      PMVS_WG(48, 4, 1)
+      PMVS_WG(32, 2, 2)
+      PMVS_WG(32, 4, 2)
+      PMVS_WG(16, 4, 2)
+      default: return hipErrorInvalidValue;
+    }
+#undef PMVS_WG
+    (void)hipEventRecord(ev[2], stream);
+    hipLaunchKernelGGL((post_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_jobs, d_out, n, d_st);
+    (void)hipEventRecord(ev[3], stream);
+    return hipGetLastError();
+  }
   // tslots = texture slots per objective chunk * 100 + optimizer chains per wavefront
   switch (tslots) {
     case 804: hipLaunchKernelGGL((refine_v2_kernel<WS, 8, 4>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;

@@ -197,14 +197,19 @@ pmvs_status pmvs_incc_eval(pmvs_scene* scene, const pmvs_eval_query* q, int32_t 
                            pmvs_stats* stats);
 
 /* Batched preProcess -> refinePatch -> postProcess (optim.cpp:95-190, 496-658) for n candidates
- * at the scene's current thresholds and depth (depth must be 0 in this release: the
- * depth >= 1 organizer steps setVImagesVGrids/check are not part of this call). */
+ * at the scene's current thresholds, as the seed phase calls them (CSeed at _depth 0,
+ * findMatch.cpp:187-194; seed.cpp:385-395).  The expansion's calls (expand.cpp:225-237, _depth >= 1)
+ * also run postProcess's organizer steps (setVImagesVGrids, check(); optim.cpp:178-188) against the
+ * model, so they run inside pmvs_expand_run / pmvs_run_loop, where the organizer lives on the
+ * device; this call returns PMVS_EUNSUPPORTED when the scene's depth is >= 1. */
 pmvs_status pmvs_refine_batch(pmvs_scene* scene, const pmvs_candidate* in, int32_t n,
                               pmvs_refined* out, pmvs_stats* stats);
 
 /* Device-resident variant for benchmarking: candidates/results already on the device
- * (pointers from hipMalloc / torch).  Launches on the scene stream, does not synchronise;
- * call pmvs_scene_sync() and read stats afterwards. */
+ * (pointers from hipMalloc / torch).  Runs on the scene stream and waits once mid-call (after
+ * preProcess, for the start points' angles, which the host's libm computes as the reference's
+ * encode does); returns with the refine and postProcess kernels queued: call pmvs_scene_sync()
+ * and read stats afterwards. */
 pmvs_status pmvs_refine_batch_device(pmvs_scene* scene, const pmvs_candidate* d_in, int32_t n,
                                      pmvs_refined* d_out);
 pmvs_status pmvs_scene_sync(pmvs_scene* scene, pmvs_stats* stats);

@@ -108,6 +108,30 @@ def test_refine_batch_bit_exact(scenes):
         assert sg[k] == so[k], k
 
 
+REFINE_CONFIGS = [1206, 2408, 164011, 164021, 164041, 148041, 132022, 132042, 116042]
+
+
+@pytest.mark.parametrize("config", REFINE_CONFIGS)
+def test_refine_configs_bit_exact(scenes, monkeypatch, config):
+    """Every refine-kernel layout (PMVS_REFINE_CONFIG: the wavefront form's texture slots * 100 +
+    chains, the workgroup form's 100000 + chains * 1000 + optimizer wavefronts * 10 + workgroups per
+    CU) gives the oracle's records, for a batch that fills the chip and for a 5-candidate one."""
+    import pmvs_amd as P
+    inp, p, g, o = scenes
+    monkeypatch.setenv("PMVS_REFINE_CONFIG", str(config))
+    gc = P.Scene(inp)
+    try:
+        for n, seed in ((3000, 21), (5, 22)):
+            cands = P.synth_candidates(p, inp.projections, n, seed=seed)
+            rg, sg = gc.refine_batch(cands)
+            ro, so = o.refine_batch(cands, nthreads=8)
+            compare_refined(rg, ro)
+            for k in ("accepted", "fail_pre", "fail_post", "refine_failed", "evals", "tex_valid"):
+                assert sg[k] == so[k], (n, k)
+    finally:
+        gc.close()
+
+
 def test_full_size_c2_batch_parity(gpu_available, oracle_mod):
     """BASELINE configs[1] at full size (8 views 1920x1080, level 1, 100k seed candidates):
     every record of the HIP path equals the oracle's."""
