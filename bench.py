@@ -3,16 +3,18 @@
 
 Workload (default, BASELINE.json configs[2] "C3" -- the metric's "50-view 4K synthetic"): a
 synthetic 50-view 3840x2160 textured-sphere ring, level 0, csize 2, wsize 7, minImageNum 3,
-threshold 0.7.  Setup (untimed): render the views, build the scene on the device, refine 5000
-seed-path candidates into the seed model (the seed phase, SURVEY.md §8(f) f1, is not on this
-path).  One step = CFindMatch::run after the seeds: 3 x (CExpand::run -> COptim refine ->
+threshold 0.7.  Setup (untimed): render the views, build the scene on the device, and make the
+seed model: --seed-mode features runs the seed phase on the device (Harris/DoG features +
+CSeed::run, SURVEY.md §8(f) f1); --seed-mode synthetic (default) refines --seeds synthetic
+seed-path candidates instead.  One step = CFindMatch::run after the seeds: 3 x (CExpand::run -> COptim refine ->
 CFilter::run, updateThreshold) through pmvs_run_loop, with the model resident in HBM.
 
 value = refined patches/s: patches the expansion refined and committed to the model
 (preProcess -> refinePatch -> postProcess passed, expand.cpp:238) over all ranks / step time.
 Also: NCC evals/s (my_f + computeINCC evaluations), refined candidates/s.
-roofline: the loop's dominant kernel, refine_v2_kernel: algorithmic bytes = 588 B x valid
-textures per my_f evaluation over its HIP-event time, against 8 TB/s HBM.
+roofline: the loop's dominant kernel, refine_v2_kernel (the refine batches of >= 10000 candidates):
+algorithmic bytes = 588 B x valid textures per my_f evaluation over its HIP-event
+time, against 8 TB/s HBM; the smaller batches' workgroup-form kernel in roofline.small_batches.
 refine_c2: the refine kernel alone on configs[1] (8-view 1920x1080, level 1, 100k candidates).
 cpu_baseline: the same metric on the host CPU -- the oracle (CPU restatement) runs the first
 expansion of the same rank-0 C3 scene from the same seeds with the same wave schedule
@@ -54,6 +56,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 BYTES_PER_TEXTURE = 49 * 4 * 3  # wsize^2 samples x 4 texels x 3 B
 _RCFG = int(os.environ.get("PMVS_REFINE_CONFIG", "1206"))  # texture slots * 100 + chains per wavefront
 REFINE_KERNEL = f"refine_v2_kernel<7,{_RCFG // 100},{_RCFG % 100}>"
+SMALL_KERNEL = "refine_wg_kernel<7,32,31,4>"  # batches below 10000 candidates (pmvs_api.cpp refine_cfg)
 
 
 _T0 = time.time()
@@ -466,7 +469,15 @@ def main():
                                                                          dev)
     launches = tot("refine_launches")
     traffic, traffic_launches, traffic_src = pmc_traffic("c3")
-    roof = refine_roofline(tex_valid, refine_ms, launches, traffic, traffic_launches, traffic_src)
+    # the dominant kernel: the wavefront form, which runs the waves of >= 10k candidates; the
+    # workgroup form's small batches (iterations 2-3) are reported beside it
+    tv_s, ms_s, l_s = tot("tex_valid_small"), tot("refine_ms_small"), tot("refine_launches_small")
+    roof = refine_roofline(tex_valid - tv_s, refine_ms - ms_s, launches - l_s, traffic, traffic_launches, traffic_src)
+    small = refine_roofline(tv_s, ms_s, l_s, None, None, None)
+    small["kernel"] = SMALL_KERNEL
+    for k in ("traffic", "traffic_source", "traffic_launches", "bound", "peak", "unit"):
+        small.pop(k)
+    roof["small_batches"] = small
 
     result = None
     c2 = None

@@ -42,6 +42,23 @@
 
 #include <math.h>
 
+// The routines' array arguments are distinct BqState members (no two alias), so ALTMOV's and
+// UPDATE's are declared restrict: loads of read-only arrays (xpt, bmat, zmat, ...) may then stay in
+// registers across the stores to xnew / xalt / w instead of being re-read from LDS after each of
+// them (UPDATE: 132 -> 40 LDS reads, ALTMOV: 206 -> 127, gfx950 ISA).  TRSBOX keeps plain pointers:
+// hoisting its xpt / hq / pq reads out of the Hessian-product loops overflows its 256 registers
+// (944 B of scratch per lane) -- BQ_RST is empty unless -DBQ_TRSBOX_RESTRICT.
+#if defined(BQ_NO_RESTRICT)
+#define BQ_RS
+#else
+#define BQ_RS __restrict__
+#endif
+#if defined(BQ_TRSBOX_RESTRICT)
+#define BQ_RST __restrict__
+#else
+#define BQ_RST
+#endif
+
 namespace pmvsdev {
 
 // Diagnostic build only (-DBQ_PROFILE, tools/bq_profile.sh): wave-time spent in the optimizer's
@@ -114,10 +131,10 @@ struct BqState {
   BQ_A2(xpt, BQN); BQ_A2(bmat, BQN); BQ_A2(zmat, BQNPTM); BQ_A2(ptsaux, BQN)
 
 // ---------------------------------------------------------------- TRSBOX
-BQ_NI void bq_trsbox(const BQ_AS double (*xpt)[BQN], const BQ_AS double* xopt, const BQ_AS double* gopt,
-                     const BQ_AS double* hq, const BQ_AS double* pq, const BQ_AS double* sl, const BQ_AS double* su,
-                     double delta, BQ_AS double* xnew, BQ_AS double* d, BQ_AS double* gnew, BQ_AS double* dsq_out,
-                     BQ_AS double* crvmin_out) {
+BQ_NI void bq_trsbox(const BQ_AS double (*BQ_RST xpt)[BQN], const BQ_AS double* BQ_RST xopt, const BQ_AS double* BQ_RST gopt,
+                     const BQ_AS double* BQ_RST hq, const BQ_AS double* BQ_RST pq, const BQ_AS double* BQ_RST sl, const BQ_AS double* BQ_RST su,
+                     double delta, BQ_AS double* BQ_RST xnew, BQ_AS double* BQ_RST d, BQ_AS double* BQ_RST gnew, BQ_AS double* BQ_RST dsq_out,
+                     BQ_AS double* BQ_RST crvmin_out) {
   const double half = 0.5, one = 1.0, onemin = -1.0, zero = 0.0;
   double xbdi[BQN + 1], s[BQN + 1], hs[BQN + 1], hred[BQN + 1];
   int iterc = 0, nact = 0, itermax = 0, itcsav = 0, iact = 0, isav = 0, iu = 0;
@@ -379,10 +396,10 @@ L210: {
 }
 
 // ---------------------------------------------------------------- ALTMOV
-BQ_NI void bq_altmov(const BQ_AS double (*xpt)[BQN], const BQ_AS double* xopt, const BQ_AS double (*bmat)[BQN],
-                     const BQ_AS double (*zmat)[BQNPTM], const BQ_AS double* sl, const BQ_AS double* su, int kopt,
-                     int knew, double adelt, BQ_AS double* xnew, BQ_AS double* xalt, BQ_AS double* alpha,
-                     BQ_AS double* cauchy) {
+BQ_NI void bq_altmov(const BQ_AS double (*BQ_RS xpt)[BQN], const BQ_AS double* BQ_RS xopt, const BQ_AS double (*BQ_RS bmat)[BQN],
+                     const BQ_AS double (*BQ_RS zmat)[BQNPTM], const BQ_AS double* BQ_RS sl, const BQ_AS double* BQ_RS su, int kopt,
+                     int knew, double adelt, BQ_AS double* BQ_RS xnew, BQ_AS double* BQ_RS xalt, BQ_AS double* BQ_RS alpha,
+                     BQ_AS double* BQ_RS cauchy) {
   const double half = 0.5, one = 1.0, zero = 0.0;
   const double cnst = one + sqrt(2.0);
   double glag[BQN + 1], hcol[BQNPT + 1], w[2 * BQN + 1];
@@ -585,8 +602,8 @@ L120:
 }
 
 // ---------------------------------------------------------------- UPDATE
-BQ_NI void bq_update(BQ_AS double (*bmat)[BQN], BQ_AS double (*zmat)[BQNPTM], BQ_AS double* vlag, double beta,
-                     double denom, int knew, BQ_AS double* w) {
+BQ_NI void bq_update(BQ_AS double (*BQ_RS bmat)[BQN], BQ_AS double (*BQ_RS zmat)[BQNPTM], BQ_AS double* BQ_RS vlag, double beta,
+                     double denom, int knew, BQ_AS double* BQ_RS w) {
   const double one = 1.0, zero = 0.0;
   double ztest = zero, temp, tempa, tempb, alpha, tau;
   for (int k = 1; k <= BQNPT; ++k)

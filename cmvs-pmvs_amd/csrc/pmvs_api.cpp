@@ -203,6 +203,10 @@ struct pmvs_scene {
   DBuf<pmvs_patch> fpatches;
   DBuf<int> fkeep;
   int grid = 0, refine_grid = 0, tslots = 1206;
+  // batches below small_n candidates run the workgroup form spread over every CU (tslots_small):
+  // their length is one chain's latency, not the chip's throughput
+  int tslots_small = 132042, small_n = 10000;
+  int refine_cfg(int n) const { return n < small_n ? tslots_small : tslots; }
   // expansion sharding (pmvs_scene_set_shard) and the kept result of pmvs_expand_run(out = NULL)
   int shard_rank = 0, shard_world = 1;
   pmvs_allgather_fn shard_fn = nullptr;
@@ -445,8 +449,12 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
   // number of texture slots one cooperative objective chunk packs
   int wpc = 8;  // 1206: 19.5 KB LDS, <= 256 registers -> 8 resident per CU
   if (const char* e = getenv("PMVS_REFINE_WAVES_PER_CU")) wpc = std::max(1, std::min(32, atoi(e)));
-  if (const char* e = getenv("PMVS_REFINE_CONFIG")) sc->tslots = atoi(e);
-  if (!refine_config_supported(sc->tslots)) sc->tslots = 1206;
+  if (const char* e = getenv("PMVS_REFINE_CONFIG")) {  // one layout for every batch size
+    sc->tslots = atoi(e);
+    if (!refine_config_supported(sc->tslots)) sc->tslots = 1206;
+    sc->tslots_small = sc->tslots;
+  }
+  if (const char* e = getenv("PMVS_REFINE_SMALL_N")) sc->small_n = std::max(0, atoi(e));
   sc->refine_grid = std::max(1, prop.multiProcessorCount) * wpc;
   if (sc->scratch.alloc((size_t)sc->grid * PMVS_MAX_IMAGES * PMVS_MAX_IMAGES) != hipSuccess)
     return bail(fail(PMVS_ENOMEM, "scratch"));
@@ -645,12 +653,16 @@ pmvs_status pmvs_seed_run(pmvs_scene* sc, const pmvs_point* points, const int32_
   in.batch = batch > 0 ? batch : 16384;
   in.per_cell = 4;
   if (const char* e = getenv("PMVS_SEED_PER_CELL")) in.per_cell = std::max(1, atoi(e));
+  in.lookahead = 1;  // speculation into the next images: measured no fewer rounds
+  if (const char* e = getenv("PMVS_SEED_LOOKAHEAD")) in.lookahead = std::max(1, atoi(e));
+  in.spec_near = 2048;
+  if (const char* e = getenv("PMVS_SEED_NEAR")) in.spec_near = std::max(1, atoi(e));
   HIPCHK(hipMemsetAsync(sc->stats.p, 0, sizeof(DevStats), sc->stream));
   RefineFn refine = [&](const pmvs_candidate* d_in, int m, pmvs_refined* d_out) -> hipError_t {
     if (ensure(sc->jobs, m)) return hipErrorOutOfMemory;
     hipError_t e = hipMemsetAsync(&sc->stats.p->queue, 0, 3 * sizeof(unsigned long long), sc->stream);
     if (e != hipSuccess) return e;
-    return launch_refine(sc->ds, d_in, sc->jobs.p, d_out, m, sc->stats.p, sc->grid, sc->refine_grid, sc->tslots,
+    return launch_refine(sc->ds, d_in, sc->jobs.p, d_out, m, sc->stats.p, sc->grid, sc->refine_grid, sc->refine_cfg(m),
                          sc->stream, sc->kev, sc->rhost);
   };
   SeedOutput so;
@@ -768,7 +780,7 @@ pmvs_status pmvs_refine_batch_device(pmvs_scene* sc, const pmvs_candidate* d_in,
   if ((st = ensure(sc->jobs, n))) return st;
   HIPCHK(hipMemsetAsync(sc->stats.p, 0, sizeof(DevStats), sc->stream));
   HIPCHK(hipEventRecord(sc->ev0, sc->stream));
-  HIPCHK(launch_refine(sc->ds, d_in, sc->jobs.p, d_out, n, sc->stats.p, sc->grid, sc->refine_grid, sc->tslots, sc->stream,
+  HIPCHK(launch_refine(sc->ds, d_in, sc->jobs.p, d_out, n, sc->stats.p, sc->grid, sc->refine_grid, sc->refine_cfg(n), sc->stream,
                        sc->kev, sc->rhost));
   HIPCHK(hipEventRecord(sc->ev1, sc->stream));
   sc->last_refine = true;
@@ -1050,13 +1062,16 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
   // refine-work accounting: device counters accumulate over the run (only the work-queue heads
   // are reset per launch); the refine-kernel time of each launch is read at the next one, when
   // the host has synchronised in between.
-  double refine_ms = 0.0;
-  int64_t refined = 0, launches = 0;
-  bool pending = false;
+  double refine_ms = 0.0, refine_ms_small = 0.0;
+  int64_t refined = 0, launches = 0, launches_small = 0;
+  bool pending = false, pending_small = false;
   auto take_time = [&]() {
     if (!pending) return;
     float ms = 0.0f;
-    if (hipEventElapsedTime(&ms, sc->kev[1], sc->kev[2]) == hipSuccess) refine_ms += ms;
+    if (hipEventElapsedTime(&ms, sc->kev[1], sc->kev[2]) == hipSuccess) {
+      refine_ms += ms;
+      if (pending_small) refine_ms_small += ms;
+    }
     pending = false;
   };
   HIPCHK(hipMemsetAsync(sc->stats.p, 0, sizeof(DevStats), sc->stream));
@@ -1068,8 +1083,11 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
     refined += m;
     ++launches;
     pending = true;
-    return launch_refine(sc->ds, d_in, sc->jobs.p, d_out, m, sc->stats.p, sc->grid, sc->refine_grid, sc->tslots,
-                         sc->stream, sc->kev, sc->rhost);
+    const int cfg = sc->refine_cfg(m);
+    pending_small = cfg >= 100000;  // the workgroup form
+    launches_small += pending_small ? 1 : 0;
+    return launch_refine(sc->ds, d_in, sc->jobs.p, d_out, m, sc->stats.p, sc->grid, sc->refine_grid, cfg, sc->stream,
+                         sc->kev, sc->rhost);
   };
   const Shard sh = make_shard(sc);
   long long sv[8];
@@ -1101,6 +1119,9 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
     stats->tex_valid = (int64_t)ds.tex_valid;
     stats->refine_ms = refine_ms;
     stats->refine_launches = launches;
+    stats->tex_valid_small = (int64_t)ds.tex_valid_wg;
+    stats->refine_ms_small = refine_ms_small;
+    stats->refine_launches_small = launches_small;
   }
   sc->last_refine = false;
   return PMVS_OK;

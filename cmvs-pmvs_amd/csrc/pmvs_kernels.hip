@@ -1382,6 +1382,13 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(REFI
   unsigned long long tex_valid = 0, grabs = 0, nevals = 0, rounds = 0, chunks = 0;
   const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999};
   const double ub[3] = {HUGE_VAL, 23.99999, 23.99999};
+  // chains beyond nc_active never publish: they read as idle and dead (the packing and the loop's
+  // exit test read every chain's entry)
+  if (tid < NC) {
+    C.rsize[tid] = 0;
+    C.alive[tid] = 0;
+  }
+  __syncthreads();
   for (;;) {
     bool req = false;
     if (owner) {
@@ -1533,6 +1540,7 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(REFI
   if (lane == 0 && wave < OW) {
     atomicAdd(&st->evals, nevals);
     atomicAdd(&st->tex_valid, tex_valid);
+    atomicAdd(&st->tex_valid_wg, tex_valid);
   }
   if (tid == 0) {
     atomicAdd(&st->tex_grabs, grabs);

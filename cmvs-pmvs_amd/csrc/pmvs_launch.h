@@ -193,6 +193,8 @@ struct SeedInput {
   float angle0;              // _angleThreshold0
   std::vector<const uint8_t*> mask_level;  // per view: binary mask at the scene level (host), or null
   int batch, per_cell;       // speculative refine batch size / unknown candidates requested per cell
+  int lookahead;             // images (current + next) the speculation may request candidates of
+  int spec_near;             // cells from the replay cursor every speculation walk re-visits
 };
 struct SeedOutput {
   std::vector<pmvs_patch> seeds;  // addPatch order

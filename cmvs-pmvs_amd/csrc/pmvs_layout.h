@@ -93,6 +93,7 @@ struct DevStats {
   unsigned long long queue3;
   unsigned long long cyc_opt, cyc_eval, rounds, chunks;  // refine-kernel phase profile (lane 0 of each wave)
   unsigned long long prof[8];  // refill, step, publish, chunk setup, gather, normalize, dot, reduce
+  unsigned long long tex_valid_wg;  // the part of tex_valid the workgroup-form kernel evaluated
 };
 
 }  // namespace pmvsdev

@@ -32,6 +32,8 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
+#include <deque>
+#include <memory>
 #include <random>
 #include <vector>
 
@@ -448,16 +450,39 @@ hipError_t seed_pass(const DScene& s, const std::vector<DView>& hv, const SeedIn
   std::vector<pmvs_refined> hres;
   const int budget = std::max(1, in.batch);
   const int per_cell = std::max(1, in.per_cell);
+  const int lookahead = std::max(1, in.lookahead);
+  const int spec_near = std::max(1, in.spec_near);
   long long refined = 0, rounds = 0;
   double gen_ms = 0.0, refine_wall_ms = 0.0;
+  // ---- per target image: its epipolar candidates (gen) and its exact-replay state.  Images are
+  // replayed one after the other in `order`; the speculation may already request candidates of the
+  // next `lookahead - 1` images while the current one drains: a refine result is a pure function of
+  // the candidate, and which results the replay will read depends only on the occupancy / counts,
+  // which only grow -- a request made against the current state is a superset of the later need.
+  struct Img {
+    int index = -1;
+    std::vector<int> p0pts, p0cell, cellstart, sorted, soff, accepted_slot, creq, vcp;
+    std::vector<unsigned char> drained;  // per cell: a full walk found no unknown candidate left
+    std::vector<Cand> cands;
+    std::vector<unsigned char> state;  // per candidate: 0 unknown, 1 requested, 2 failed in preProcess,
+                                       // 3 failed in postProcess, 4 accepted
+    std::vector<pmvs_refined> accepted;
+    int ci = 0, pi = 0, vi = 0, count = 0, best = -1;  // replay cursor
+    int frontier = 0;                                   // first cell no speculation walk reached
+    bool in_point = false;
+    float best_score = 0.0f;
+    int ncells() const { return (int)cellstart.size() - 1; }
+  };
   std::vector<int> idx;
-  for (const int index : order) {
+  auto gen = [&](int index, Img& w) -> hipError_t {  // w.index stays -1 for an image without work
     collect_images(index, idx);
     if ((int)idx.size() > s.tau) idx.resize(s.tau);
-    if (idx.empty()) continue;
+    if (idx.empty()) return hipSuccess;
     const int nidx = (int)idx.size();
     // replay order: cells with points in raster order, their points in cell order
-    std::vector<int> p0pts, p0cell, cellstart;
+    std::vector<int>& p0pts = w.p0pts;
+    std::vector<int>& p0cell = w.p0cell;
+    std::vector<int>& cellstart = w.cellstart;
     {
       const int* off = coff.data() + cbase[index] + index;
       const long long ncell = (long long)gw[index] * gh[index];
@@ -472,7 +497,7 @@ hipError_t seed_pass(const DScene& s, const std::vector<DView>& hv, const SeedIn
       cellstart.push_back((int)p0pts.size());
     }
     const int np0 = (int)p0pts.size();
-    if (np0 == 0) continue;
+    if (np0 == 0) return hipSuccess;
     const auto tg0 = std::chrono::steady_clock::now();
     // ---- epipolar candidates of every point of this image (device), sorted per point
     std::vector<double> F(9 * nidx);
@@ -500,9 +525,11 @@ hipError_t seed_pass(const DScene& s, const std::vector<DView>& hv, const SeedIn
     std::vector<long long> hoff(npairs + 1, 0);
     for (long long k = 0; k < npairs; ++k) hoff[k + 1] = hoff[k] + hcnt[k];
     const long long nc = hoff[npairs];
-    std::vector<int> sorted;  // candidate ids per point in _response order (valid ones), CSR by p0
-    std::vector<int> soff(np0 + 1, 0);
-    std::vector<Cand> cands(std::max<long long>(nc, 1));
+    std::vector<int>& sorted = w.sorted;  // candidate ids per point in _response order (valid ones), CSR by p0
+    std::vector<int>& soff = w.soff;
+    soff.assign(np0 + 1, 0);
+    std::vector<Cand>& cands = w.cands;
+    cands.resize(std::max<long long>(nc, 1));
     if (nc > 0) {
       if (nc > INT_MAX / 2) return hipErrorOutOfMemory;
       SCHK(hipMemcpyAsync(doff.p, hoff.data(), (npairs + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
@@ -555,177 +582,219 @@ hipError_t seed_pass(const DScene& s, const std::vector<DView>& hv, const SeedIn
     }
     gen_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tg0).count();
     out.stats[6] += nc;
-    // ---- speculative refinement + exact replay of initialMatch (seed.cpp:133-205)
-    // per candidate: 0 unknown, 1 requested, 2 failed in preProcess, 3 failed in postProcess, 4 accepted
-    std::vector<unsigned char> state(std::max<long long>(nc, 1), 0);
-    std::vector<int> accepted_slot(std::max<long long>(nc, 1), -1);
-    std::vector<pmvs_refined> accepted;
-    auto filtered = [&](int p, std::vector<int>& v) {  // canAdd filter of collectCandidates at this moment
-      v.clear();
-      for (int k = soff[p]; k < soff[p + 1]; ++k) {
-        const Cand& c = cands[sorted[k]];
-        const int x = c.cell % gw[c.view], y = c.cell / gw[c.view];
-        if (can_add(c.view, x, y)) v.push_back(sorted[k]);
-      }
-    };
-    auto make_candidate = [&](int cid, pmvs_candidate& pc) {  // seed.cpp:167-173
-      const Cand& c = cands[cid];
-      std::memset(&pc, 0, sizeof(pc));
-      float n[4] = {hv[index].center[0] - c.coord[0], hv[index].center[1] - c.coord[1],
-                    hv[index].center[2] - c.coord[2], hv[index].center[3] - c.coord[3]};
-      const float l = hdot4(n, n);
-      if (l != 1.0 && l != 0.0) {
-        const float d = (float)std::sqrt((double)l);
-        for (int k = 0; k < 4; ++k) n[k] /= d;
-      }
-      n[3] = 0.0f;
-      for (int k = 0; k < 4; ++k) { pc.coord[k] = c.coord[k]; pc.normal[k] = n[k]; }
-      pc.dscale = 0.0f;
-      pc.num_images = 2;
-      pc.images[0] = index;
-      pc.images[1] = c.view;
-    };
-    // cursor of the exact replay
-    int ci = 0, pi = 0, vi = 0, count = 0, best = -1;
-    bool in_point = false;
-    float best_score = 0.0f;
-    std::vector<int> vcp, tmpv;
-    const int ncells_p = (int)cellstart.size() - 1;
-    auto score = [&](const pmvs_refined& r) { return std::max(0.0f, r.ncc - s.nccThreshold) * r.num_images; };
-    auto finish_point = [&]() {  // seed.cpp:194-199
-      if (count != 0) {
-        if (best >= 0) {
-          const pmvs_refined& r = accepted[best];
-          pmvs_patch pp;
-          std::memset(&pp, 0, sizeof(pp));
-          for (int k = 0; k < 4; ++k) { pp.coord[k] = r.coord[k]; pp.normal[k] = r.normal[k]; }
-          pp.ncc = r.ncc; pp.dscale = r.dscale; pp.ascale = r.ascale; pp.tmp = r.tmp; pp.timages = r.timages;
-          pp.num_images = r.num_images;
-          for (int k = 0; k < r.num_images; ++k) {
-            pp.images[k] = (int16_t)r.images[k];
-            pp.grids[k][0] = grid16(r.grids[k][0]);
-            pp.grids[k][1] = grid16(r.grids[k][1]);
-            const int t = r.images[k];
-            if (t < tnum && 0 <= r.grids[k][0] && r.grids[k][0] < gw[t] && 0 <= r.grids[k][1] && r.grids[k][1] < gh[t])
-              occupied[t][(size_t)r.grids[k][1] * gw[t] + r.grids[k][0]] = 1;  // addPatch at depth 0
-          }
-          out.seeds.push_back(pp);
-        }
-        ++ci;  // break out of the point loop: next cell
-        pi = 0;
-      } else {
-        ++pi;
-      }
-      in_point = false;
-    };
-    // returns -1 when the image is done, else the candidate whose result is needed
-    auto replay = [&]() -> int {
-      while (ci < ncells_p) {
-        if (!in_point) {
-          const int npts_cell = cellstart[ci + 1] - cellstart[ci];
-          if (pi == 0) {
-            const int c = p0cell[cellstart[ci]];
-            if (!can_add(index, c % gw[index], c / gw[index])) { ++ci; continue; }
-          }
-          if (pi >= npts_cell) { ++ci; pi = 0; continue; }
-          filtered(cellstart[ci] + pi, vcp);
-          vi = 0; count = 0; best = -1; best_score = 0.0f;
-          in_point = true;
-        }
-        if (vi >= (int)vcp.size()) { finish_point(); continue; }
-        const int cid = vcp[vi];
-        if (state[cid] < 2) return cid;
-        const Cand& c = cands[cid];
-        const int cell = p0cell[cellstart[ci]];
-        ++counts[index][cell];
-        if (c.view < tnum) ++counts[c.view][c.cell];
-        out.stats[0]++;  // trial
-        if (state[cid] == 2) { out.stats[2]++; ++vi; continue; }
-        if (state[cid] == 3) { out.stats[3]++; ++vi; continue; }
-        out.stats[1]++;  // pass
-        ++count;
-        const float sc = score(accepted[accepted_slot[cid]]);
-        if (best_score < sc) { best_score = sc; best = accepted_slot[cid]; }
-        if (2 <= count) { finish_point(); continue; }
-        ++vi;
-      }
-      return -1;
-    };
-    // requests for the cells from the cursor on, against the current state (read-only).  A cell
-    // whose earlier requests all failed gets twice as many the next time (creq: requests so far), so
-    // a point that tries many epipolar candidates before two succeed costs O(log) rounds, not one
-    // round per per_cell candidates; the replay is exact whatever was requested.
-    std::vector<int> creq(std::max(ncells_p, 1), 0);
-    auto speculate = [&](std::vector<int>& req) {
-      req.clear();
-      int c2 = ci, p2 = pi;
-      bool first = true;
-      while (c2 < ncells_p && (int)req.size() < budget) {
-        int unknown = 0;
-        const int quota = std::min(4096, std::max(per_cell, creq[c2]));
-        bool cell_done = false;
-        const int npts_cell = cellstart[c2 + 1] - cellstart[c2];
-        if (!(first && in_point) && p2 == 0) {
-          const int c = p0cell[cellstart[c2]];
-          if (!can_add(index, c % gw[index], c / gw[index])) { ++c2; p2 = 0; first = false; continue; }
-        }
-        for (; p2 < npts_cell && !cell_done && unknown < quota; ++p2) {
-          int v0 = 0, cnt = 0;
-          const std::vector<int>* list;
-          if (first && in_point) { list = &vcp; v0 = vi; cnt = count; }
-          else { filtered(cellstart[c2] + p2, tmpv); list = &tmpv; }
-          first = false;
-          for (int k = v0; k < (int)list->size(); ++k) {
-            const int cid = (*list)[k];
-            if (state[cid] == 4) {
-              if (2 <= ++cnt) break;
-            } else if (state[cid] == 0) {
-              state[cid] = 1;
-              req.push_back(cid);
-              if (++unknown >= quota) break;
-            }
-          }
-          if (cnt > 0) cell_done = true;  // this point adds a patch: the cell is finished
-        }
-        creq[c2] += unknown;
-        first = false;
-        ++c2;
-        p2 = 0;
-      }
-    };
-    std::vector<int> req;
-    while (true) {
-      const int need = replay();
-      if (need < 0) break;
-      speculate(req);
-      if (req.empty()) return hipErrorUnknown;  // cannot happen: `need` is unknown at the cursor
-      const int m = (int)req.size();
-      hcand.resize(m);
-      for (int k = 0; k < m; ++k) make_candidate(req[k], hcand[k]);
-      SCHK(dcand.need(m));
-      SCHK(dres.need(m));
-      const auto tr0 = std::chrono::steady_clock::now();
-      SCHK(hipMemcpyAsync(dcand.p, hcand.data(), m * sizeof(pmvs_candidate), hipMemcpyHostToDevice, st));
-      SCHK(refine(dcand.p, m, dres.p));
-      hres.resize(m);
-      SCHK(hipMemcpyAsync(hres.data(), dres.p, m * sizeof(pmvs_refined), hipMemcpyDeviceToHost, st));
-      SCHK(hipStreamSynchronize(st));
-      refine_wall_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
-      for (int k = 0; k < m; ++k) {
-        const int cid = req[k];
-        const pmvs_refined& r = hres[k];
-        if (r.status == PMVS_ACCEPTED) {
-          state[cid] = 4;
-          accepted_slot[cid] = (int)accepted.size();
-          accepted.push_back(r);
-        } else {
-          if (r.status == PMVS_FAIL_OVERFLOW) return hipErrorNotSupported;  // list capacity: an error, not a reject
-          state[cid] = (r.status == PMVS_FAIL_PRE) ? 2 : 3;
-        }
-      }
-      refined += m;
-      ++rounds;
+    w.state.assign(std::max<long long>(nc, 1), 0);
+    w.accepted_slot.assign(std::max<long long>(nc, 1), -1);
+    w.creq.assign(std::max(w.ncells(), 1), 0);
+    w.drained.assign(std::max(w.ncells(), 1), 0);
+    w.index = index;
+    return hipSuccess;
+  };
+  auto filtered = [&](const Img& w, int p, std::vector<int>& v) {  // canAdd filter of collectCandidates now
+    v.clear();
+    for (int k = w.soff[p]; k < w.soff[p + 1]; ++k) {
+      const Cand& c = w.cands[w.sorted[k]];
+      const int x = c.cell % gw[c.view], y = c.cell / gw[c.view];
+      if (can_add(c.view, x, y)) v.push_back(w.sorted[k]);
     }
+  };
+  auto make_candidate = [&](const Img& w, int cid, pmvs_candidate& pc) {  // seed.cpp:167-173
+    const Cand& c = w.cands[cid];
+    std::memset(&pc, 0, sizeof(pc));
+    float n[4] = {hv[w.index].center[0] - c.coord[0], hv[w.index].center[1] - c.coord[1],
+                  hv[w.index].center[2] - c.coord[2], hv[w.index].center[3] - c.coord[3]};
+    const float l = hdot4(n, n);
+    if (l != 1.0 && l != 0.0) {
+      const float d = (float)std::sqrt((double)l);
+      for (int k = 0; k < 4; ++k) n[k] /= d;
+    }
+    n[3] = 0.0f;
+    for (int k = 0; k < 4; ++k) { pc.coord[k] = c.coord[k]; pc.normal[k] = n[k]; }
+    pc.dscale = 0.0f;
+    pc.num_images = 2;
+    pc.images[0] = w.index;
+    pc.images[1] = c.view;
+  };
+  auto score = [&](const pmvs_refined& r) { return std::max(0.0f, r.ncc - s.nccThreshold) * r.num_images; };
+  auto finish_point = [&](Img& w) {  // seed.cpp:194-199
+    if (w.count != 0) {
+      if (w.best >= 0) {
+        const pmvs_refined& r = w.accepted[w.best];
+        pmvs_patch pp;
+        std::memset(&pp, 0, sizeof(pp));
+        for (int k = 0; k < 4; ++k) { pp.coord[k] = r.coord[k]; pp.normal[k] = r.normal[k]; }
+        pp.ncc = r.ncc; pp.dscale = r.dscale; pp.ascale = r.ascale; pp.tmp = r.tmp; pp.timages = r.timages;
+        pp.num_images = r.num_images;
+        for (int k = 0; k < r.num_images; ++k) {
+          pp.images[k] = (int16_t)r.images[k];
+          pp.grids[k][0] = grid16(r.grids[k][0]);
+          pp.grids[k][1] = grid16(r.grids[k][1]);
+          const int t = r.images[k];
+          if (t < tnum && 0 <= r.grids[k][0] && r.grids[k][0] < gw[t] && 0 <= r.grids[k][1] && r.grids[k][1] < gh[t])
+            occupied[t][(size_t)r.grids[k][1] * gw[t] + r.grids[k][0]] = 1;  // addPatch at depth 0
+        }
+        out.seeds.push_back(pp);
+      }
+      ++w.ci;  // break out of the point loop: next cell
+      w.pi = 0;
+    } else {
+      ++w.pi;
+    }
+    w.in_point = false;
+  };
+  // the exact replay of image w (the current one); returns -1 when the image is done, else the
+  // candidate whose result is needed
+  auto replay = [&](Img& w) -> int {
+    const int index = w.index;
+    while (w.ci < w.ncells()) {
+      if (!w.in_point) {
+        const int npts_cell = w.cellstart[w.ci + 1] - w.cellstart[w.ci];
+        if (w.pi == 0) {
+          const int c = w.p0cell[w.cellstart[w.ci]];
+          if (!can_add(index, c % gw[index], c / gw[index])) { ++w.ci; continue; }
+        }
+        if (w.pi >= npts_cell) { ++w.ci; w.pi = 0; continue; }
+        filtered(w, w.cellstart[w.ci] + w.pi, w.vcp);
+        w.vi = 0; w.count = 0; w.best = -1; w.best_score = 0.0f;
+        w.in_point = true;
+      }
+      if (w.vi >= (int)w.vcp.size()) { finish_point(w); continue; }
+      const int cid = w.vcp[w.vi];
+      if (w.state[cid] < 2) return cid;
+      const Cand& c = w.cands[cid];
+      const int cell = w.p0cell[w.cellstart[w.ci]];
+      ++counts[index][cell];
+      if (c.view < tnum) ++counts[c.view][c.cell];
+      out.stats[0]++;  // trial
+      if (w.state[cid] == 2) { out.stats[2]++; ++w.vi; continue; }
+      if (w.state[cid] == 3) { out.stats[3]++; ++w.vi; continue; }
+      out.stats[1]++;  // pass
+      ++w.count;
+      const float sc = score(w.accepted[w.accepted_slot[cid]]);
+      if (w.best_score < sc) { w.best_score = sc; w.best = w.accepted_slot[cid]; }
+      if (2 <= w.count) { finish_point(w); continue; }
+      ++w.vi;
+    }
+    return -1;
+  };
+  // requests for image w's cells from its cursor on, against the current state (read-only), until
+  // `limit` requests.  A cell whose earlier requests all failed gets twice as many the next time
+  // (creq: requests so far), so a point that tries many epipolar candidates before two succeed
+  // costs O(log) rounds, not one round per per_cell candidates; the replay is exact whatever was
+  // requested.
+  std::vector<int> tmpv;
+  // The walk covers the `near` cells from the cursor on (where the replay will block next, so their
+  // doubling quotas matter) and then continues from the frontier, the first cell no walk has reached
+  // yet: the cells in between were requested once and are re-walked when the cursor nears them,
+  // which keeps a round's host work O(near + new cells) instead of O(cells left in the image).
+  auto speculate = [&](Img& w, std::vector<int>& req, int limit) {
+    req.clear();
+    int c2 = w.ci, p2 = w.pi;
+    bool first = true;
+    const int index = w.index;
+    const int near_end = (int)std::min<long long>(w.ncells(), (long long)w.ci + spec_near);
+    while (c2 < w.ncells() && (int)req.size() < limit) {
+      if (c2 == near_end && c2 < w.frontier) c2 = w.frontier;
+      if (c2 >= w.ncells()) break;
+      // a cell whose walk went through every point and found every candidate requested or
+      // resolved stays so (states never return to unknown, and canAdd only removes candidates):
+      // later walks skip it
+      if (w.drained[c2] && !(first && w.in_point)) { ++c2; p2 = 0; first = false; continue; }
+      const bool full_walk = !(first && w.in_point) && p2 == 0;
+      int unknown = 0;
+      const int quota = std::min(4096, std::max(per_cell, w.creq[c2]));
+      bool cell_done = false;
+      const int npts_cell = w.cellstart[c2 + 1] - w.cellstart[c2];
+      if (!(first && w.in_point) && p2 == 0) {
+        const int c = w.p0cell[w.cellstart[c2]];
+        if (!can_add(index, c % gw[index], c / gw[index])) { ++c2; p2 = 0; first = false; continue; }
+      }
+      for (; p2 < npts_cell && !cell_done && unknown < quota; ++p2) {
+        int v0 = 0, cnt = 0;
+        const std::vector<int>* list;
+        if (first && w.in_point) { list = &w.vcp; v0 = w.vi; cnt = w.count; }
+        else { filtered(w, w.cellstart[c2] + p2, tmpv); list = &tmpv; }
+        first = false;
+        for (int k = v0; k < (int)list->size(); ++k) {
+          const int cid = (*list)[k];
+          if (w.state[cid] == 4) {
+            if (2 <= ++cnt) break;
+          } else if (w.state[cid] == 0) {
+            w.state[cid] = 1;
+            req.push_back(cid);
+            if (++unknown >= quota) break;
+          }
+        }
+        if (cnt > 0) cell_done = true;  // this point adds a patch: the cell is finished
+      }
+      // (not after a point with an accepted candidate ended the walk: canAdd may still drop that
+      // candidate before the replay gets there, and the cell's later points then matter)
+      if (full_walk && unknown == 0 && !cell_done) w.drained[c2] = 1;
+      w.creq[c2] += unknown;
+      first = false;
+      ++c2;
+      p2 = 0;
+    }
+    w.frontier = std::max(w.frontier, c2);
+  };
+  std::deque<std::unique_ptr<Img>> win;  // the current image and the look-ahead ones, in `order`
+  size_t next = 0;
+  auto fill = [&](size_t k) -> hipError_t {
+    while (win.size() < k && next < order.size()) {
+      auto w = std::make_unique<Img>();
+      SCHK(gen(order[next++], *w));
+      if (w->index >= 0) win.push_back(std::move(w));
+    }
+    return hipSuccess;
+  };
+  std::vector<int> req;
+  std::vector<std::pair<Img*, int>> reqs;
+  while (true) {
+    SCHK(fill(1));
+    if (win.empty()) break;
+    Img& cur = *win.front();
+    const int need = replay(cur);
+    if (need < 0) {
+      win.pop_front();
+      continue;
+    }
+    reqs.clear();
+    speculate(cur, req, budget);
+    if (req.empty()) return hipErrorUnknown;  // cannot happen: `need` is unknown at the cursor
+    for (const int cid : req) reqs.emplace_back(&cur, cid);
+    if ((int)reqs.size() < budget && lookahead > 1) {
+      SCHK(fill((size_t)lookahead));
+      for (size_t k = 1; k < win.size() && (int)reqs.size() < budget; ++k) {
+        speculate(*win[k], req, budget - (int)reqs.size());
+        for (const int cid : req) reqs.emplace_back(win[k].get(), cid);
+      }
+    }
+    const int m = (int)reqs.size();
+    hcand.resize(m);
+    for (int k = 0; k < m; ++k) make_candidate(*reqs[k].first, reqs[k].second, hcand[k]);
+    SCHK(dcand.need(m));
+    SCHK(dres.need(m));
+    const auto tr0 = std::chrono::steady_clock::now();
+    SCHK(hipMemcpyAsync(dcand.p, hcand.data(), m * sizeof(pmvs_candidate), hipMemcpyHostToDevice, st));
+    SCHK(refine(dcand.p, m, dres.p));
+    hres.resize(m);
+    SCHK(hipMemcpyAsync(hres.data(), dres.p, m * sizeof(pmvs_refined), hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
+    refine_wall_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
+    for (int k = 0; k < m; ++k) {
+      Img& w = *reqs[k].first;
+      const int cid = reqs[k].second;
+      const pmvs_refined& r = hres[k];
+      if (r.status == PMVS_ACCEPTED) {
+        w.state[cid] = 4;
+        w.accepted_slot[cid] = (int)w.accepted.size();
+        w.accepted.push_back(r);
+      } else {
+        if (r.status == PMVS_FAIL_OVERFLOW) return hipErrorNotSupported;  // list capacity: an error, not a reject
+        w.state[cid] = (r.status == PMVS_FAIL_PRE) ? 2 : 3;
+      }
+    }
+    refined += m;
+    ++rounds;
   }
   out.stats[4] = refined;
   out.stats[5] = rounds;

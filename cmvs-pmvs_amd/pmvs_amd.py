@@ -82,9 +82,11 @@ class ExpandStats(C.Structure):
     _fields_ = [(k, C.c_int64) for k in ("parents", "candidates", "fail_prep", "fail_pre", "fail_post",
                                           "fail_commit", "added", "waves")] + [("wall_ms", C.c_double)] + \
                [(k, C.c_int64) for k in ("refined", "evals", "tex_valid")] + [("refine_ms", C.c_double)] + \
-               [("refine_launches", C.c_int64)]
+               [("refine_launches", C.c_int64), ("tex_valid_small", C.c_int64), ("refine_ms_small", C.c_double),
+                ("refine_launches_small", C.c_int64)]
 
-    WORK = ("wall_ms", "refined", "evals", "tex_valid", "refine_ms", "refine_launches")  # timing / per-rank work fields
+    WORK = ("wall_ms", "refined", "evals", "tex_valid", "refine_ms", "refine_launches", "tex_valid_small",
+            "refine_ms_small", "refine_launches_small")  # timing / per-rank work fields
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

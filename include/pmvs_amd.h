@@ -291,6 +291,11 @@ typedef struct pmvs_expand_stats {
   int64_t refined, evals, tex_valid;
   double refine_ms;
   int64_t refine_launches;
+  /* the part of tex_valid / refine_ms / refine_launches that ran the small-batch refine layout
+   * (batches below the scene's small-batch size: the workgroup-form kernel) */
+  int64_t tex_valid_small;
+  double refine_ms_small;
+  int64_t refine_launches_small;
 } pmvs_expand_stats;
 pmvs_status pmvs_expand_run(pmvs_scene* scene, const pmvs_patch* patches, const int32_t* alive, int32_t n,
                             int32_t wave, int32_t min_candidates, int32_t count_threshold, int32_t flags, pmvs_patch* out, int32_t* alive_out,
