@@ -357,7 +357,8 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
   if (hipMalloc((void**)&sc->pyr.p, words * sizeof(uint32_t)) != hipSuccess)
     return bail(fail(PMVS_ENOMEM, "pyramid: %lld words", words));
   sc->pyr.n = words;
-  (void)hipMemsetAsync(sc->pyr.p, 0, words * sizeof(uint32_t), sc->stream);
+  if (memset_big(sc->pyr.p, 0, words * sizeof(uint32_t), sc->stream) != hipSuccess)
+    return bail(fail(PMVS_EDEVICE, "pyramid: clearing %lld words", words));
 
   // ---- pyramids on device: RGB level chain (CImage::buildImage) then RGBA packing
   {
@@ -372,17 +373,22 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
     for (int i = 0; i < num && st == PMVS_OK; ++i) {
       const DView& v = sc->hviews[i];
       const size_t bytes0 = (size_t)v.w[0] * v.h[0] * 3;
+      const char* step = "upload";
+      int lv = 0;
       hipError_t e = hipMemcpyAsync(a, d->views[i].rgb, bytes0, hipMemcpyHostToDevice, sc->stream);
-      if (e == hipSuccess) e = launch_pack_rgba(a, sc->pyr.p + v.pyr_off[0], (long long)v.w[0] * v.h[0], sc->stream);
+      if (e == hipSuccess && (step = "pack")) e = launch_pack_rgba(a, sc->pyr.p + v.pyr_off[0], (long long)v.w[0] * v.h[0], sc->stream);
       uint8_t* src = a;
       uint8_t* dst = b;
       for (int l = 1; l < maxLevel && e == hipSuccess; ++l) {
+        lv = l;
+        step = "downsample";
         e = launch_build_level(src, v.w[l - 1], v.h[l - 1], dst, v.w[l], v.h[l], sc->stream);
-        if (e == hipSuccess) e = launch_pack_rgba(dst, sc->pyr.p + v.pyr_off[l], (long long)v.w[l] * v.h[l], sc->stream);
+        if (e == hipSuccess && (step = "pack")) e = launch_pack_rgba(dst, sc->pyr.p + v.pyr_off[l], (long long)v.w[l] * v.h[l], sc->stream);
         std::swap(src, dst);
       }
-      if (e == hipSuccess) e = hipStreamSynchronize(sc->stream);  // staging reused per view
-      if (e != hipSuccess) st = fail(PMVS_EDEVICE, "pyramid build: %s", hipGetErrorString(e));
+      if (e == hipSuccess && (step = "sync")) e = hipStreamSynchronize(sc->stream);  // staging reused per view
+      if (e != hipSuccess)
+        st = fail(PMVS_EDEVICE, "pyramid build (view %d, level %d, %s): %s", i, lv, step, hipGetErrorString(e));
     }
     (void)hipFree(a);
     (void)hipFree(b);

@@ -1975,7 +1975,7 @@ static hipError_t build_lists(Ctx& c, int vis) {
                      B.keys);
   tb = B.temp_bytes;
   if (e > 0) FCHK(hipcub::DeviceRadixSort::SortKeys(B.temp, tb, B.keys, B.keys2, e, 0, 64, c.st));
-  FCHK(hipMemsetAsync(B.cellcnt, 0, (c.ncells + 1) * sizeof(int), c.st));
+  FCHK(memset_big(B.cellcnt, 0, (c.ncells + 1) * sizeof(int), c.st));
   if (e > 0) {
     hipLaunchKernelGGL(cell_hist_kernel, dim3(nblk(e)), dim3(256), 0, c.st, B.keys2, e, B.cellcnt);
     hipLaunchKernelGGL(items_kernel, dim3(nblk(e)), dim3(256), 0, c.st, B.keys2, e, items);
@@ -2074,7 +2074,7 @@ static hipError_t set_dm_vgrids(Ctx& c, int additive) {
   dbg(c.st, "  lists");
   FCHK(collect(c));
   dbg(c.st, "  collect");
-  FCHK(hipMemsetAsync(B.dpkey, 0xff, c.ncells * sizeof(unsigned long long), c.st));
+  FCHK(memset_big(B.dpkey, 0xff, c.ncells * sizeof(unsigned long long), c.st));
   if (c.nalive > 0)
     hipLaunchKernelGGL(coordc_kernel, dim3(nblk(c.nalive)), dim3(256), 0, c.st, c.P, B.order, c.nalive, B.coordc);
   if (c.nalive > 0)
@@ -3047,7 +3047,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   hipLaunchKernelGGL(alive_reg_kernel, dim3(nblk(n0)), dim3(256), 0, st, n0, d_alive, B.preg, B.vreg, dP);
   FCHK(build_lists(c, 0));
   FCHK(collect(c));
-  FCHK(hipMemsetAsync(B.dpkey, 0xff, ncells * sizeof(unsigned long long), st));
+  FCHK(memset_big(B.dpkey, 0xff, ncells * sizeof(unsigned long long), st));
   if (c.nalive > 0 && !(flags & 1))  // after the seed phase the depth maps are still empty
   {
     hipLaunchKernelGGL(coordc_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, dP, B.order, c.nalive, B.coordc);
@@ -3058,8 +3058,8 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   // ---- registrations committed by this run: per-cell chains (no per-wave rebuild of the CSR)
   FCHK(grow(X.pg_head, X.cap_pghead, (size_t)ncells));
   FCHK(grow(X.vp_head, X.cap_vphead, (size_t)ncells));
-  FCHK(hipMemsetAsync(X.pg_head, 0xff, ncells * sizeof(int), st));
-  FCHK(hipMemsetAsync(X.vp_head, 0xff, ncells * sizeof(int), st));
+  FCHK(memset_big(X.pg_head, 0xff, ncells * sizeof(int), st));
+  FCHK(memset_big(X.vp_head, 0xff, ncells * sizeof(int), st));
   size_t pool_need = 0;
   X.pool_host = 0;
   auto set_delta = [&]() {
@@ -3105,7 +3105,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
     FCHK(hipMemcpyAsync(qforeign, B.need, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
   }
   FCHK(grow(X.counts, X.cap_cnt, (size_t)ncells));
-  FCHK(hipMemsetAsync(X.counts, 0, ncells, st));
+  FCHK(memset_big(X.counts, 0, ncells, st));
   FCHK(hipStreamSynchronize(st));
   // The max-_tmp queue (P_compare; ties: earlier push first): the collected patches as a sorted
   // run, the patches pushed during the run in a heap, popped by merging the two.

@@ -6,6 +6,19 @@
 #include <vector>
 
 namespace pmvsdev {
+
+// hipMemsetAsync in pieces of at most 1 GiB: the C5-scale buffers (a 70-view 8K pyramid is 12 GB,
+// its cell tables 2-5 GB) exceed what one fill launch takes (a 12 GB pyramid clear failed with
+// "invalid resource handle", gpurun r03p).
+inline hipError_t memset_big(void* p, int value, size_t bytes, hipStream_t st) {
+  constexpr size_t kPiece = size_t(1) << 30;
+  char* c = static_cast<char*>(p);
+  for (size_t off = 0; off < bytes; off += kPiece) {
+    const hipError_t e = hipMemsetAsync(c + off, value, bytes - off < kPiece ? bytes - off : kPiece, st);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
 bool refine_config_supported(int tslots);  // PMVS_REFINE_CONFIG values this build instantiates
 // Host staging of the refine batches' start-point angles (encode_angles_host, pmvs_kernels.hip).
 struct RefineHost {
