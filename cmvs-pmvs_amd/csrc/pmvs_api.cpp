@@ -315,6 +315,7 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
   if (device < 0 || device >= ndev) return fail(PMVS_EINVAL, "device %d of %d", device, ndev);
   HIPCHK(hipSetDevice(device));
 
+  (void)hipGetLastError();  // launches below are checked with hipGetLastError: start from a clean slate
   pmvs_scene* sc = new pmvs_scene();
   sc->device = device;
   const int num = d->num_views;
@@ -364,18 +365,46 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
   {
     size_t maxrgb = 0;
     for (int i = 0; i < num; ++i) maxrgb = std::max(maxrgb, (size_t)d->views[i].width * d->views[i].height * 3);
-    uint8_t *a = nullptr, *b = nullptr;
-    if (hipMalloc((void**)&a, maxrgb) != hipSuccess || hipMalloc((void**)&b, maxrgb) != hipSuccess) {
+    uint8_t *a = nullptr, *b = nullptr, *pin = nullptr;
+    // host images go up through a pinned bounce buffer, in pieces: a direct pageable copy out of a
+    // multi-GB host array (70 views x 8K = 7 GB, sliced per view) failed with "invalid resource
+    // handle" (gpurun r03q), and pinned pieces also keep the copy at full PCIe rate
+    constexpr size_t kPin = size_t(32) << 20;
+    if (hipMalloc((void**)&a, maxrgb) != hipSuccess || hipMalloc((void**)&b, maxrgb) != hipSuccess ||
+        hipHostMalloc((void**)&pin, 2 * kPin, hipHostMallocDefault) != hipSuccess) {
       if (a) (void)hipFree(a);
+      if (b) (void)hipFree(b);
       return bail(fail(PMVS_ENOMEM, "pyramid staging"));
     }
+    hipEvent_t piece_done[2];
+    bool ev_ok = hipEventCreate(&piece_done[0]) == hipSuccess;
+    ev_ok = hipEventCreate(&piece_done[1]) == hipSuccess && ev_ok;
+    // double-buffered: piece k is copied into half k % 2 once that half's previous upload finished
+    auto upload = [&](uint8_t* dst, const uint8_t* src, size_t bytes) -> hipError_t {
+      if (!ev_ok) return hipErrorOutOfMemory;
+      bool used[2] = {false, false};
+      for (size_t off = 0, k = 0; off < bytes; off += kPin, ++k) {
+        const int h = (int)(k & 1);
+        const size_t m = bytes - off < kPin ? bytes - off : kPin;
+        if (used[h]) {
+          const hipError_t e = hipEventSynchronize(piece_done[h]);
+          if (e != hipSuccess) return e;
+        }
+        std::memcpy(pin + h * kPin, src + off, m);
+        hipError_t e = hipMemcpyAsync(dst + off, pin + h * kPin, m, hipMemcpyHostToDevice, sc->stream);
+        if (e == hipSuccess) e = hipEventRecord(piece_done[h], sc->stream);
+        if (e != hipSuccess) return e;
+        used[h] = true;
+      }
+      return hipSuccess;
+    };
     pmvs_status st = PMVS_OK;
     for (int i = 0; i < num && st == PMVS_OK; ++i) {
       const DView& v = sc->hviews[i];
       const size_t bytes0 = (size_t)v.w[0] * v.h[0] * 3;
       const char* step = "upload";
       int lv = 0;
-      hipError_t e = hipMemcpyAsync(a, d->views[i].rgb, bytes0, hipMemcpyHostToDevice, sc->stream);
+      hipError_t e = upload(a, d->views[i].rgb, bytes0);
       if (e == hipSuccess && (step = "pack")) e = launch_pack_rgba(a, sc->pyr.p + v.pyr_off[0], (long long)v.w[0] * v.h[0], sc->stream);
       uint8_t* src = a;
       uint8_t* dst = b;
@@ -390,8 +419,14 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
       if (e != hipSuccess)
         st = fail(PMVS_EDEVICE, "pyramid build (view %d, level %d, %s): %s", i, lv, step, hipGetErrorString(e));
     }
+    (void)hipStreamSynchronize(sc->stream);
     (void)hipFree(a);
     (void)hipFree(b);
+    (void)hipHostFree(pin);
+    if (ev_ok) {
+      (void)hipEventDestroy(piece_done[0]);
+      (void)hipEventDestroy(piece_done[1]);
+    }
     if (st != PMVS_OK) return bail(st);
   }
 

@@ -1,6 +1,7 @@
 #!/bin/bash
 # tools/gpu_round.sh -- GPU steps of one round, each under its own time limit, chained with &&.
 #   bash tools/gpu_round.sh test <tag>      pytest -m gpu, smoke(), the default bench line
+#   bash tools/gpu_round.sh tests <tag>     pytest -m gpu alone;  bench <tag>: smoke() + the bench line
 #   bash tools/gpu_round.sh prof <tag>      rocprofv3 kernel-trace stats of the bench, and the
 #                                           HBM-traffic PMC passes (FETCH_SIZE, WRITE_SIZE in
 #                                           separate runs, kernel-trace only) for the C3 loop and
@@ -11,10 +12,19 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
+# a line every 50 s under gpurun_out: a long single test or the bench's setup is not taken for a hang
+( while true; do sleep 50; echo "alive $(date +%T)" >> $O/heartbeat.txt; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 if [ "$WHAT" = test ]; then
   timeout -k 10 700 python3 -u -m pytest $R/tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && \
   timeout -k 10 300 python3 -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
   timeout -k 10 400 python3 -u $R/bench.py > $O/bench.json 2> $O/bench.err
+elif [ "$WHAT" = tests ]; then  # the GPU suite alone (no -x: every failure is listed)
+  timeout -k 10 1100 python3 -u -m pytest $R/tests -m gpu -v --timeout 400 --timeout-method thread > $O/pytest_gpu.log 2>&1
+elif [ "$WHAT" = bench ]; then  # smoke() and the default bench line
+  timeout -k 10 300 python3 -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
+  timeout -k 10 500 python3 -u $R/bench.py > $O/bench.json 2> $O/bench.err
 else
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/kt.log 2>&1 && \
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-c2 > $O/pmc_fetch.log 2>&1 && \
