@@ -1763,16 +1763,21 @@ static void encode_angles_host(const float4* enc, int n, float ascale, double2* 
     }
     ang[i] = make_double2(v1, v2);
   };
-  const int nt = (n >= 32768) ? std::min(8, (int)std::max(1u, std::thread::hardware_concurrency())) : 1;
-  if (nt == 1) {
+  // ~0.1 us of libm per candidate: a C3 expansion wave's 15-20 k candidates would hold the GPU for
+  // 2-3 ms on one thread, so from 2048 on the work is split into contiguous ranges over <= 8 threads
+  const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+  const int nt = (n >= 2048) ? std::min({8, hw, n / 1024}) : 1;
+  if (nt <= 1) {
     for (int i = 0; i < n; ++i) one(i);
     return;
   }
   std::vector<std::thread> th;
-  for (int t = 0; t < nt; ++t)
+  const int per = (n + nt - 1) / nt;
+  for (int t = 1; t < nt; ++t)
     th.emplace_back([&, t]() {
-      for (int i = t; i < n; i += nt) one(i);
+      for (int i = t * per; i < std::min(n, (t + 1) * per); ++i) one(i);
     });
+  for (int i = 0; i < std::min(n, per); ++i) one(i);
   for (auto& t : th) t.join();
 }
 
