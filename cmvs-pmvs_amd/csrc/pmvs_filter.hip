@@ -58,6 +58,9 @@ constexpr int NB_CAP = 1024;  // neighbours per patch in filterNeighbor (overflo
 // (5 NB_CAP), its right-hand side r (NB_CAP), then the filterQuad coordinates fx, fy, fz as floats
 // (1.5 NB_CAP).  Kept out of LDS so NbLds stays ~8 KB (occupancy of the latency-bound walks).
 constexpr int NB_SCR = NB_CAP * 8;
+// gather_neighbors: cell slots per lane per round, entries per lane per test round
+constexpr int NB_SK = 2;
+constexpr int NB_NE = 2;
 // Persistent workgroups per CU-grid unit for the NbLds kernels (neighbor_kernel, depth_post_kernel,
 // empty_blocks_kernel): twice the organizer grid, since ~8 KB of LDS and <= 107 VGPRs leave room.
 constexpr int NB_GRID_MULT = 2;
@@ -117,7 +120,7 @@ struct FilterDev {
   const int* order;  // collect order -> patch
   const int* rank;   // patch -> collect rank or -1
   int nalive;
-  const float* unit0;  // getUnit(images[0], coord) per patch
+  const PHot* hot;     // per patch: coord, normal, dscale, ncc, getUnit(images[0], coord)
   long long ncells;
   int npg, nvp;        // entries in the pgrids / vpgrids lists
   int* err;            // [0] count, [1] first code (defensive bounds checks)
@@ -161,8 +164,8 @@ __device__ __forceinline__ int gwidth(const DScene& s, int t) { return (s.views[
 __device__ __forceinline__ int gheight(const DScene& s, int t) { return (s.views[t].h[s.level] + s.csize - 1) / s.csize; }
 
 // CFindMatch::isNeighbor / isNeighborRadius (findMatch.cpp:125-185).
-__device__ int is_neighbor_h(const pmvs_patch& l, const pmvs_patch& r, float hunit, float thr, float radius,
-                             bool use_radius) {
+template <class PL, class PR>
+__device__ int is_neighbor_h(const PL& l, const PR& r, float hunit, float thr, float radius, bool use_radius) {
   if ((double)dot4(l.normal, r.normal) < cos(120.0 * M_PI / 180.0)) return 0;
   float diff[4];
   for (int k = 0; k < 4; ++k) diff[k] = r.coord[k] - l.coord[k];
@@ -178,13 +181,14 @@ __device__ int is_neighbor_h(const pmvs_patch& l, const pmvs_patch& r, float hun
   return ftmp < thr ? 1 : 0;
 }
 __device__ int is_neighbor(const DScene& s, const FilterDev& F, int a, int b, float thr) {
-  const float hunit = (float)((double)(F.unit0[a] + F.unit0[b]) / 2.0 * s.csize);
-  return is_neighbor_h(F.P[a], F.P[b], hunit, thr, 0.0f, false);
+  const PHot &ha = F.hot[a], &hb = F.hot[b];
+  const float hunit = (float)((double)(ha.unit0 + hb.unit0) / 2.0 * s.csize);
+  return is_neighbor_h(ha, hb, hunit, thr, 0.0f, false);
 }
 
 // CPatchOrganizerS::isVisible (patchOrganizerS.cpp:500-525).
-__device__ int is_visible_q(const DScene& s, const FilterDev& F, const pmvs_patch& q, int t, int ix, int iy,
-                             float strict) {
+template <class PQ>
+__device__ int is_visible_q(const DScene& s, const FilterDev& F, const PQ& q, int t, int ix, int iy, float strict) {
   if (!in_grid(s, t, ix, iy)) return 0;
   if (s.depth == 0) return 1;
   const unsigned long long key = F.dpkey[F.tgoff[t] + (long long)iy * gwidth(s, t) + ix];
@@ -209,7 +213,7 @@ __device__ int is_visible_q(const DScene& s, const FilterDev& F, const pmvs_patc
   return diff < get_unit(s, v, q.coord) * (float)s.csize * strict * factor ? 1 : 0;
 }
 __device__ int is_visible(const DScene& s, const FilterDev& F, int p, int t, int ix, int iy, float strict) {
-  return is_visible_q(s, F, F.P[p], t, ix, iy, strict);
+  return is_visible_q(s, F, F.hot[p], t, ix, iy, strict);
 }
 
 // --------------------------------------------------------------------------- organizer build
@@ -297,10 +301,19 @@ __global__ void rank_kernel(const unsigned long long* __restrict__ keys, int nal
   rank[p] = i;
 }
 
-__global__ void unit0_kernel(DScene s, const pmvs_patch* __restrict__ P, int n, float* __restrict__ unit0) {
+__device__ inline void write_hot(const DScene& s, const pmvs_patch& q, PHot& h) {
+  PHot v;
+  for (int k = 0; k < 4; ++k) { v.coord[k] = q.coord[k]; v.normal[k] = q.normal[k]; }
+  v.dscale = q.dscale;
+  v.ncc = q.ncc;
+  v.unit0 = q.num_images > 0 ? get_unit(s, s.views[q.images[0]], q.coord) : 0.0f;
+  for (int k = 0; k < 5; ++k) v.pad[k] = 0.0f;
+  h = v;
+}
+__global__ void hot_kernel(DScene s, const pmvs_patch* __restrict__ P, int n, PHot* __restrict__ hot) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
-  unit0[p] = P[p].num_images > 0 ? get_unit(s, s.views[P[p].images[0]], P[p].coord) : 0.0f;
+  write_hot(s, P[p], hot[p]);
 }
 
 // CFilter::setDepthMapsThread (filter.cpp:689-725): one thread per (collected patch, target).
@@ -393,7 +406,7 @@ __global__ void gain_kernel(DScene s, FilterDev F, int* __restrict__ remove) {
     float maxp = 0.0f;
     for (int e = F.pg_off[c]; e < F.pg_off[c + 1]; ++e) {
       const int j = F.pg_items[e];
-      if (!is_neighbor(s, F, p, j, 1.0f)) maxp = smax(maxp, F.P[j].ncc - s.nccThreshold);
+      if (!is_neighbor(s, F, p, j, 1.0f)) maxp = smax(maxp, F.hot[j].ncc - s.nccThreshold);
     }
     gain -= maxp;
   }
@@ -405,8 +418,8 @@ __global__ void gain_kernel(DScene s, FilterDev F, int* __restrict__ remove) {
     float maxp = 0.0f;
     for (int e = F.pg_off[c]; e < F.pg_off[c + 1]; ++e) {
       const int j = F.pg_items[e];
-      const float bdepth = depth_of(s.views[t], F.P[j].coord);
-      if (pdepth < bdepth && !is_neighbor(s, F, p, j, 1.0f)) maxp = smax(maxp, F.P[j].ncc - s.nccThreshold);
+      const float bdepth = depth_of(s.views[t], F.hot[j].coord);
+      if (pdepth < bdepth && !is_neighbor(s, F, p, j, 1.0f)) maxp = smax(maxp, F.hot[j].ncc - s.nccThreshold);
     }
     gain -= maxp;
   }
@@ -540,7 +553,7 @@ __global__ void exact_after_ref_kernel(DScene s, const pmvs_patch* __restrict__ 
 
 // --------------------------------------------------------------------------- filterNeighbor
 struct NbLds {
-  int sb[64], so[64], sl[64];  // gather_neighbors: per-slot list start, flattened offset, list kind
+  int sb[64 * NB_SK], so[64 * NB_SK];  // gather_neighbors: per-slot list start (bit 31: vpgrids), flattened offset
   alignas(8) int nb[NB_CAP];   // nb and seq are adjacent: filterQuad's lls rows reuse them
   float seq[NB_CAP];  // values summed in the reference's order by one lane (filterQuad)
   float units[PMVS_MAX_IMAGES];
@@ -934,78 +947,114 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, c
   const int side = 2 * margin + 1;
   const int per_list = side * side * 2;
   const int nslots = nlists * per_list;
-  for (int base = 0; base < nslots; base += 64) {
-    const int slot = base + lane;
-    int b = 0, e = 0, lst = 0, head = -1;
-    if (slot < nslots) {
-      const int k = slot / per_list;
-      int r = slot - k * per_list;
-      const int dyi = r / (2 * side);
-      r -= dyi * 2 * side;
-      const int dxi = r >> 1;
-      lst = r & 1;
-      const bool vis = k >= ni;
-      const int t = vis ? q.vimages[k - ni] : q.images[k];
-      if (t < s.tnum) {
-        const int gw = gwidth(s, t), gh = gheight(s, t);
-        const int yt = (vis ? q.vgrids[k - ni][1] : q.grids[k][1]) + dyi - margin;
-        const int xt = (vis ? q.vgrids[k - ni][0] : q.grids[k][0]) + dxi - margin;
-        if (0 <= yt && yt < gh && 0 <= xt && xt < gw) {
-          const long long c = F.tgoff[t] + (long long)yt * gw + xt;
-          const int* off = lst ? F.vp_off : F.pg_off;
-          const int lim = lst ? F.nvp : F.npg;
-          b = off[c];
-          e = off[c + 1];
-          if (b < 0 || e > lim || b > e) {
-            atomicAdd(&F.err[0], 1);
-            atomicExch(&F.err[1], 12 + lst);
-            b = 0;
-            e = 0;
+  // NB_SK cells per lane per round (their list bounds load together), then the round's entries
+  // NB_NE per lane at a time (their item and patch loads in flight together): fewer dependent
+  // global-memory round trips per patch than one cell / one entry per lane.
+  for (int base = 0; base < nslots; base += 64 * NB_SK) {
+    int bk[NB_SK], ck[NB_SK], hk[NB_SK];
+#pragma unroll
+    for (int k = 0; k < NB_SK; ++k) {
+      const int slot = base + k * 64 + lane;
+      int b = 0, e = 0, lst = 0, head = -1;
+      if (slot < nslots) {
+        const int li = slot / per_list;
+        int r = slot - li * per_list;
+        const int dyi = r / (2 * side);
+        r -= dyi * 2 * side;
+        const int dxi = r >> 1;
+        lst = r & 1;
+        const bool vis = li >= ni;
+        const int t = vis ? q.vimages[li - ni] : q.images[li];
+        if (t < s.tnum) {
+          const int gw = gwidth(s, t), gh = gheight(s, t);
+          const int yt = (vis ? q.vgrids[li - ni][1] : q.grids[li][1]) + dyi - margin;
+          const int xt = (vis ? q.vgrids[li - ni][0] : q.grids[li][0]) + dxi - margin;
+          if (0 <= yt && yt < gh && 0 <= xt && xt < gw) {
+            const long long c = F.tgoff[t] + (long long)yt * gw + xt;
+            const int* off = lst ? F.vp_off : F.pg_off;
+            const int lim = lst ? F.nvp : F.npg;
+            b = off[c];
+            e = off[c + 1];
+            if (b < 0 || e > lim || b > e) {
+              atomicAdd(&F.err[0], 1);
+              atomicExch(&F.err[1], 12 + lst);
+              b = 0;
+              e = 0;
+            }
+            if (F.pg_dhead) head = (lst ? F.vp_dhead : F.pg_dhead)[c];
           }
-          if (F.pg_dhead) head = (lst ? F.vp_dhead : F.pg_dhead)[c];
         }
       }
+      bk[k] = b | (lst << 31);  // list start, list kind in bit 31
+      ck[k] = e - b;
+      hk[k] = head;
     }
-    // the round's CSR entries, flattened in slot order
-    const int cntc = e - b;
-    const int offc = wave_excl_scan_w(cntc);
-    const int tot = uni(__shfl(offc + cntc, 63));
-    L.sb[lane] = b;
-    L.so[lane] = offc;
-    L.sl[lane] = lst;
-    __syncthreads();
-    for (int ib = 0; ib < tot; ib += 64) {
-      const int idx = ib + lane;
-      bool hit = false;
-      int j = 0;
-      if (idx < tot) {
-        int sidx = 0;
-        for (int step = 32; step >= 1; step >>= 1)
-          if (sidx + step < 64 && L.so[sidx + step] <= idx) sidx += step;
-        const int* items = L.sl[sidx] ? F.vp_items : F.pg_items;
-        j = items[L.sb[sidx] + idx - L.so[sidx]];
-        if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 14); j = 0; }
-        else hit = is_neighbor_h(q, F.P[j], unit, thr, radius, true) != 0;
+    // the round's CSR entries, flattened in (lane, k) order
+    int mine = 0;
+#pragma unroll
+    for (int k = 0; k < NB_SK; ++k) mine += ck[k];
+    const int offl = wave_excl_scan_w(mine);
+    const int tot = uni(__shfl(offl + mine, 63));
+    {
+      int o = offl;
+#pragma unroll
+      for (int k = 0; k < NB_SK; ++k) {
+        L.sb[lane * NB_SK + k] = bk[k];
+        L.so[lane * NB_SK + k] = o;
+        o += ck[k];
       }
-      nb_append(L, hit, j);
+    }
+    __syncthreads();
+    for (int ib = 0; ib < tot; ib += 64 * NB_NE) {
+      int jv[NB_NE];
+      bool hv[NB_NE];
+#pragma unroll
+      for (int u = 0; u < NB_NE; ++u) {
+        const int idx = ib + u * 64 + lane;
+        jv[u] = -1;
+        if (idx < tot) {
+          int sidx = 0;  // the last slot whose offset is <= idx (it holds idx)
+          for (int step = 64 * NB_SK / 2; step >= 1; step >>= 1)
+            if (sidx + step < 64 * NB_SK && L.so[sidx + step] <= idx) sidx += step;
+          const int sb = L.sb[sidx];
+          const int* items = (sb < 0) ? F.vp_items : F.pg_items;
+          jv[u] = items[(sb & 0x7fffffff) + idx - L.so[sidx]];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < NB_NE; ++u) {
+        const int j = jv[u];
+        hv[u] = false;
+        if (ib + u * 64 + lane < tot) {
+          if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 14); jv[u] = 0; }
+          else hv[u] = is_neighbor_h(q, F.hot[j], unit, thr, radius, true) != 0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < NB_NE; ++u)
+        if (ib + u * 64 < tot) nb_append(L, hv[u], jv[u] < 0 ? 0 : jv[u]);
     }
     // entries committed by earlier expansion waves (short chains, walked per lane)
-    if (F.pg_dhead && __ballot(head >= 0) != 0ull) {
-      if (uni(L.cnt) > NB_CAP / 2 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(uni(L.cnt), NB_CAP), &L.cnt);
-      for (int ent = head; ent >= 0; ent = F.d_next[ent]) {
-        const int j = F.d_item[ent];
-        if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 15); continue; }
-        if (is_neighbor_h(q, F.P[j], unit, thr, radius, true)) {
-          const int pos = atomicAdd(&L.cnt, 1);
-          if (pos < NB_CAP) L.nb[pos] = j;
-          else L.overflow = 1;
+#pragma unroll
+    for (int k = 0; k < NB_SK; ++k) {
+      const int head = hk[k];
+      if (F.pg_dhead && __ballot(head >= 0) != 0ull) {
+        if (uni(L.cnt) > NB_CAP / 2 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(uni(L.cnt), NB_CAP), &L.cnt);
+        for (int ent = head; ent >= 0; ent = F.d_next[ent]) {
+          const int j = F.d_item[ent];
+          if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 15); continue; }
+          if (is_neighbor_h(q, F.hot[j], unit, thr, radius, true)) {
+            const int pos = atomicAdd(&L.cnt, 1);
+            if (pos < NB_CAP) L.nb[pos] = j;
+            else L.overflow = 1;
+          }
         }
+        __syncthreads();
+        if (lane == 0 && L.cnt > NB_CAP) L.cnt = NB_CAP;
+        __syncthreads();
+        const int cnt = uni(L.cnt);
+        if (cnt > NB_CAP - 64 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(cnt, NB_CAP), &L.cnt);
       }
-      __syncthreads();
-      if (lane == 0 && L.cnt > NB_CAP) L.cnt = NB_CAP;
-      __syncthreads();
-      const int cnt = uni(L.cnt);
-      if (cnt > NB_CAP - 64 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(cnt, NB_CAP), &L.cnt);
     }
     __syncthreads();
   }
@@ -1725,9 +1774,10 @@ __global__ __launch_bounds__(64) void depth_post_kernel(DScene s, FilterDev F, c
                 int j;
                 if (e < ee) j = F.pg_items[e++];
                 else { j = F.d_item[ent]; ent = F.d_next[ent]; }
-                if (vis && !(pdepth < depth_of(s.views[t], F.P[j].coord))) continue;
-                const float hunit = (float)((double)(u0 + F.unit0[j]) / 2.0 * s.csize);
-                if (!is_neighbor_h(q, F.P[j], hunit, 1.0f, 0.0f, false)) maxp = smax(maxp, F.P[j].ncc - s.nccThreshold);
+                const PHot& hj = F.hot[j];
+                if (vis && !(pdepth < depth_of(s.views[t], hj.coord))) continue;
+                const float hunit = (float)((double)(u0 + hj.unit0) / 2.0 * s.csize);
+                if (!is_neighbor_h(q, hj, hunit, 1.0f, 0.0f, false)) maxp = smax(maxp, hj.ncc - s.nccThreshold);
               }
             }
           }
@@ -1773,7 +1823,7 @@ struct DeltaLists {  // the per-cell chains of FilterDev (expansion), writable
 
 __global__ void add_patches_kernel(DScene s, FilterDev F, int first, int count, int rank0, Reg* __restrict__ preg,
                                    Reg* __restrict__ vreg, int* __restrict__ order,
-                                   unsigned long long* __restrict__ dpkey, float* __restrict__ unit0) {
+                                   unsigned long long* __restrict__ dpkey, PHot* __restrict__ hot) {
   const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= (long long)count * s.tnum) return;
   const int k = (int)(g / s.tnum), t = (int)(g - (long long)k * s.tnum);
@@ -1786,7 +1836,7 @@ __global__ void add_patches_kernel(DScene s, FilterDev F, int first, int count, 
     preg[p] = m;
     vreg[p] = reg_first(q.num_vimages);
     order[rank0 + k] = p;
-    unit0[p] = get_unit(s, s.views[q.images[0]], q.coord);
+    write_hot(s, q, hot[p]);
   }
   if (s.depth == 0) return;  // addPatch keeps no depth maps at depth 0 (patchOrganizerS.cpp:331)
   const DView& v = s.views[t];
@@ -1855,7 +1905,7 @@ static hipError_t dalloc(T*& p, size_t n) {
 
 FilterBuffers::~FilterBuffers() {
   void* ps[] = {preg, vreg, tgoff, cnt, off, keys, keys2, cellcnt, pg_off, pg_items, vp_off, vp_items, dpkey,
-                order, rank, unit0, flags, safe, need, list, scratch, counters, temp, edge_off, edges, rbits, coordc,
+                order, rank, hot, flags, safe, need, list, scratch, counters, temp, edge_off, edges, rbits, coordc,
                 qf, qrows, qjobs, qctr, qkeys, qkeys2, qcrows, qoff};
   for (void* p : ps)
     if (p) (void)hipFree(p);
@@ -1877,7 +1927,7 @@ hipError_t FilterBuffers::reserve(int n_, long long ncells_, int tnum_, int grid
   FCHK(dalloc(cellcnt, cap_cells + 1)); FCHK(dalloc(pg_off, cap_cells + 1)); FCHK(dalloc(vp_off, cap_cells + 1));
   FCHK(dalloc(pg_items, ne)); FCHK(dalloc(vp_items, ne)); FCHK(dalloc(dpkey, cap_cells));
   FCHK(dalloc(coordc, cap_n));
-  FCHK(dalloc(order, cap_n)); FCHK(dalloc(rank, cap_n)); FCHK(dalloc(unit0, cap_n)); FCHK(dalloc(flags, cap_n));
+  FCHK(dalloc(order, cap_n)); FCHK(dalloc(rank, cap_n)); FCHK(dalloc(hot, cap_n)); FCHK(dalloc(flags, cap_n));
   FCHK(dalloc(safe, cap_n)); FCHK(dalloc(need, cap_n)); FCHK(dalloc(list, cap_n));
   FCHK(dalloc(scratch, (size_t)cap_grid * NB_SCR)); FCHK(dalloc(counters, 16));
   FCHK(dalloc(edge_off, cap_n + 1));
@@ -1943,7 +1993,7 @@ struct Ctx {
     FilterDev F{};
     F.P = P; F.n = n; F.preg = B.preg; F.vreg = B.vreg; F.tgoff = B.tgoff; F.tnum = s.tnum;
     F.pg_off = B.pg_off; F.pg_items = B.pg_items; F.vp_off = B.vp_off; F.vp_items = B.vp_items;
-    F.dpkey = B.dpkey; F.order = B.order; F.rank = B.rank; F.nalive = nalive; F.unit0 = B.unit0;
+    F.dpkey = B.dpkey; F.order = B.order; F.rank = B.rank; F.nalive = nalive; F.hot = B.hot;
     F.ncells = ncells; F.npg = npg; F.nvp = nvp; F.err = B.counters + 6; F.lovf = B.counters + 8;
     F.pg_dhead = pg_dhead; F.vp_dhead = vp_dhead; F.d_item = d_item; F.d_next = d_next;
     F.coordc = coordc;
@@ -2007,31 +2057,39 @@ __global__ void unpack_bits_kernel(const unsigned* __restrict__ bits, int n, int
 }
 
 // filterSmallGroups labels on the device (filter_pass): see the comment at the call.
-__global__ void lab_init_kernel(int* __restrict__ lab, int na) {
+__global__ void lab_init_kernel(int* __restrict__ lab, int* __restrict__ active, int na) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < na) lab[i] = i;
+  if (i < na) {
+    lab[i] = i;
+    active[i] = 1;
+  }
 }
+// One relaxation sweep over the vertices whose label dropped since they were last relaxed
+// (active[i] != 0), or over every vertex (all = 1: the verifying sweep).  A lowered target is
+// re-activated; the sweep's reads of other vertices' labels may already see this sweep's updates
+// (labels only decrease, so any interleaving converges to the same fixpoint).
 __global__ void lab_relax_kernel(const int* __restrict__ eoff, const int* __restrict__ edges, int na, int* lab,
-                                 int* changed) {
+                                 int* active, int all, int* changed) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= na) return;
-  const int li = lab[i];
+  if (atomicExch(&active[i], 0) == 0 && !all) return;
+  const int li = atomicAdd(&lab[i], 0);
   bool any = false;
   for (int e = eoff[i]; e < eoff[i + 1]; ++e) {
     const int j = edges[e];
-    if (li < lab[j]) {
-      atomicMin(&lab[j], li);
+    if (li < lab[j] && atomicMin(&lab[j], li) > li) {
+      atomicOr(&active[j], 1);
       any = true;
     }
   }
   if (any) atomicOr(changed, 1);
 }
-__global__ void lab_jump_kernel(int* lab, int na, int* changed) {
+__global__ void lab_jump_kernel(int* lab, int na, int* active, int* changed) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= na) return;
   const int l = lab[i], ll = lab[l];
-  if (ll < l) {
-    atomicMin(&lab[i], ll);
+  if (ll < l && atomicMin(&lab[i], ll) > ll) {
+    atomicOr(&active[i], 1);
     atomicOr(changed, 1);
   }
 }
@@ -2063,7 +2121,7 @@ static hipError_t collect(Ctx& c) {
   FCHK(hipMemsetAsync(B.rank, 0xff, c.n * sizeof(int), c.st));
   if (c.nalive > 0)
     hipLaunchKernelGGL(rank_kernel, dim3(nblk(c.nalive)), dim3(256), 0, c.st, B.keys2, c.nalive, B.order, B.rank);
-  hipLaunchKernelGGL(unit0_kernel, dim3(nblk(c.n)), dim3(256), 0, c.st, c.s, c.P, c.n, B.unit0);
+  hipLaunchKernelGGL(hot_kernel, dim3(nblk(c.n)), dim3(256), 0, c.st, c.s, c.P, c.n, B.hot);
   return hipGetLastError();
 }
 
@@ -2278,17 +2336,25 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
     int* lab = B.need;   // free after filterExact
     int* csize = B.list;
     int* changed = B.counters + 5;
-    hipLaunchKernelGGL(lab_init_kernel, dim3(nblk(na)), dim3(256), 0, st, lab, na);
+    // Relaxation sweeps visit only the vertices whose label dropped since their last sweep (the
+    // late sweeps, a few thousand vertices, cost a launch instead of a pass over every edge); the
+    // loop ends after a sweep over EVERY vertex changes nothing, i.e. at the fixpoint itself.
+    int* active = B.list;  // csize's buffer, free until the counting below
+    hipLaunchKernelGGL(lab_init_kernel, dim3(nblk(na)), dim3(256), 0, st, lab, active, na);
     for (int it = 0;; ++it) {
+      const bool verify = (it % 9) == 8;  // a full sweep after each 8 rounds of active sweeps that changed something
       FCHK(hipMemsetAsync(changed, 0, sizeof(int), st));
-      for (int r = 0; r < 4; ++r) {
-        if (ne) hipLaunchKernelGGL(lab_relax_kernel, dim3(nblk(na)), dim3(256), 0, st, B.edge_off, B.edges, na, lab, changed);
-        hipLaunchKernelGGL(lab_jump_kernel, dim3(nblk(na)), dim3(256), 0, st, lab, na, changed);
+      for (int r = 0; r < (verify ? 1 : 8); ++r) {
+        if (ne)
+          hipLaunchKernelGGL(lab_relax_kernel, dim3(nblk(na)), dim3(256), 0, st, B.edge_off, B.edges, na, lab, active,
+                             verify ? 1 : 0, changed);
+        if (verify || (r & 1)) hipLaunchKernelGGL(lab_jump_kernel, dim3(nblk(na)), dim3(256), 0, st, lab, na, active, changed);
       }
       int ch = 0;
       FCHK(read_int(changed, &ch, st));
-      if (!ch) break;
-      if (it > na) return hipErrorIllegalState;  // cannot happen: every round lowers some label
+      if (verify && !ch) break;
+      if (!verify && !ch) it = 9 * (it / 9) + 7;  // nothing moved: verify next
+      if (it > 9 * (na + 1)) return hipErrorIllegalState;  // cannot happen: every round lowers some label
     }
     FCHK(hipMemsetAsync(csize, 0, na * sizeof(int), st));
     hipLaunchKernelGGL(lab_count_kernel, dim3(nblk(na)), dim3(256), 0, st, lab, na, csize);
@@ -3328,7 +3394,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
           FCHK(grow_keep(B.preg, c1, ncap, (size_t)first, st));
           FCHK(grow_keep(B.vreg, c2, ncap, (size_t)first, st));
           FCHK(grow_keep(B.order, c3, ncap, (size_t)rank_next, st));
-          FCHK(grow_keep(B.unit0, c4, ncap, (size_t)first, st));
+          FCHK(grow_keep(B.hot, c4, ncap, (size_t)first, st));
           B.cap_n = 0;  // the other per-patch buffers are re-reserved by the next pass
           pcap = ncap;
           c.P = dP;
@@ -3340,7 +3406,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
         hipLaunchKernelGGL(register_kernel, dim3(added), dim3(64), 0, st, D, X.acc, X.acc + added, added, first, X.crec,
                            kRecInts);
         hipLaunchKernelGGL(add_patches_kernel, dim3(nblk((long long)added * s.tnum)), dim3(256), 0, st, s, c.dev(), first,
-                           added, rank_next, B.preg, B.vreg, B.order, B.dpkey, B.unit0);
+                           added, rank_next, B.preg, B.vreg, B.order, B.dpkey, B.hot);
         X.pool_host = pool_need;
         rank_next += added;
       }

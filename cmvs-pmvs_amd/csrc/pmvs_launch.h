@@ -69,6 +69,15 @@ struct PinnedBuf {
     if (p) (void)hipHostFree(p);
   }
 };
+// The fields of a patch that neighbour and visibility tests read from OTHER patches (isNeighbor,
+// computeGain, isVisible), one 64-B line per patch instead of 2-3 lines of its 1.6-KB record;
+// rebuilt by every collect and written by the expansion's commit (coord / normal / dscale / ncc
+// never change after a patch is created; unit0 = getUnit(images[0], coord) follows setRefImage).
+struct alignas(64) PHot {
+  float coord[4];
+  float normal[4];
+  float dscale, ncc, unit0, pad[5];
+};
 struct FilterBuffers {
   PinnedBuf pin;  // host staging of the small-groups BFS inputs
   Reg *preg = nullptr, *vreg = nullptr, *safe = nullptr;  // per patch: registered / filterExact-safe list entries
@@ -77,7 +86,7 @@ struct FilterBuffers {
   int *cnt = nullptr, *off = nullptr, *cellcnt = nullptr, *pg_off = nullptr, *pg_items = nullptr, *vp_off = nullptr,
       *vp_items = nullptr, *order = nullptr, *rank = nullptr, *flags = nullptr, *need = nullptr, *list = nullptr,
       *counters = nullptr, *edge_off = nullptr, *edges = nullptr;
-  float* unit0 = nullptr;
+  PHot* hot = nullptr;
   double* scratch = nullptr;
   void* temp = nullptr;
   size_t temp_bytes = 0, edges_cap = 0;
