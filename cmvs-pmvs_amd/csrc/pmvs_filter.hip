@@ -213,7 +213,7 @@ __device__ int is_visible_q(const DScene& s, const FilterDev& F, const PQ& q, in
   return diff < get_unit(s, v, q.coord) * (float)s.csize * strict * factor ? 1 : 0;
 }
 __device__ int is_visible(const DScene& s, const FilterDev& F, int p, int t, int ix, int iy, float strict) {
-  return is_visible_q(s, F, F.hot[p], t, ix, iy, strict);
+  return is_visible_q(s, F, F.P[p], t, ix, iy, strict);  // the caller reads this record anyway
 }
 
 // --------------------------------------------------------------------------- organizer build
@@ -3086,8 +3086,9 @@ struct PhaseTimer {
 // header exchange with its error (expand_pass), which its peers receive in place of their next
 // batch header or of their own terminal exchange -- so all ranks return the error together
 // instead of blocking in the next all-gather.  `agreed` = the pass ended on a header every rank saw.
-// Test hook (tests/test_gpu_expand.py): PMVS_TEST_SHARD_FAIL="rank:wave:b|a" fails that rank at the
-// given wave before its batch exchange (b) or right after it (a).
+// Test hook (tests/test_gpu_expand.py): PMVS_TEST_SHARD_FAIL="rank:wave:b|e|a" fails that rank at the
+// given wave before its batch exchange (b), at its findEmptyBlocks candidate exchange (e) or right after
+// its batch exchange (a).
 static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs_patch*& dP, size_t& dP_cap,
                                    int n0, const int* d_alive, int cap, long long ncells, const long long* h_tgoff,
                                    int wave, int cthr, int flags, int grid, hipStream_t st, const RefineFn& refine,
@@ -3216,8 +3217,64 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
       FCHK(grow_keep(X.cand_ok, X.cap_ok, parents.size() * 6, (size_t)off * 6, st));
       FCHK(hipMemcpyAsync(X.parents + off, parents.data() + off, nc * sizeof(int), hipMemcpyHostToDevice, st));
       FCHK(hipMemsetAsync(B.counters + 3, 0, 5 * sizeof(int), st));
-      hipLaunchKernelGGL(empty_blocks_kernel, dim3(std::min(grid * NB_GRID_MULT, nc)), dim3(64), 0, st, s, c.dev(), X.parents + off, nc,
-                         X.cand_coord + (size_t)off * 24, X.cand_ok + (size_t)off * 6, B.counters + 4, B.counters + 3);
+      // Sharded (G > 1): findEmptyBlocks of a contiguous share of the chunk's parents per rank, the
+      // candidates (24 floats + 6 flags per parent) all-gathered, so every rank holds the chunk's.
+      const int pch = (nc + G - 1) / G;
+      const int plo = (G > 1) ? std::min(nc, R * pch) : 0, phi = (G > 1) ? std::min(nc, plo + pch) : nc;
+      if (phi > plo)
+        hipLaunchKernelGGL(empty_blocks_kernel, dim3(std::min(grid * NB_GRID_MULT, phi - plo)), dim3(64), 0, st, s, c.dev(),
+                           X.parents + off + plo, phi - plo, X.cand_coord + (size_t)(off + plo) * 24,
+                           X.cand_ok + (size_t)(off + plo) * 6, B.counters + 4, B.counters + 3);
+      if (G > 1) {
+        hipError_t lerr = hipPeekAtLastError();
+        int ovf = 0;
+        if (lerr == hipSuccess) lerr = read_int(B.counters + 3, &ovf, st);
+        if (inject && inj_where == 'e' && stats[7] == inj_wave) lerr = hipErrorOutOfMemory;
+        const size_t pb = (size_t)pch * (24 * sizeof(float) + 6 * sizeof(int));
+        const bool dev = (bool)sh.exchange_dev;
+        auto pack = [&](char* dst, hipMemcpyKind kind) -> hipError_t {  // this rank's share: coords, then flags
+          if (phi <= plo) return hipSuccess;
+          hipError_t e = hipMemcpyAsync(dst, X.cand_coord + (size_t)(off + plo) * 24, (size_t)(phi - plo) * 24 * sizeof(float),
+                                        kind, st);
+          if (e == hipSuccess)
+            e = hipMemcpyAsync(dst + (size_t)pch * 24 * sizeof(float), X.cand_ok + (size_t)(off + plo) * 6,
+                               (size_t)(phi - plo) * 6 * sizeof(int), kind, st);
+          return e;
+        };
+        if (dev) {
+          if (lerr == hipSuccess) lerr = grow(X.xsd, X.cap_xsd, std::max<size_t>(pb, 1));
+          if (lerr == hipSuccess) lerr = grow(X.xrd, X.cap_xrd, std::max<size_t>(pb * G, 1));
+          if (lerr == hipSuccess) lerr = pack(X.xsd, hipMemcpyDeviceToDevice);
+        } else {
+          xsend.assign(pb, 0);
+          xrecv.assign(pb * G, 0);
+          if (lerr == hipSuccess) lerr = pack(xsend.data(), hipMemcpyDeviceToHost);
+          if (lerr == hipSuccess) lerr = hipStreamSynchronize(st);
+        }
+        int hdr[2] = {(int)lerr, ovf};
+        std::vector<int> hall(2 * (size_t)G, 0);
+        agreed = true;  // the header below is this chunk's terminal exchange for a failing rank
+        if (sh.exchange(hdr, sizeof(hdr), hall.data()) != 0) return hipErrorUnknown;
+        for (int r = 0; r < G; ++r) {
+          if (hall[2 * r] != 0 && lerr == hipSuccess) lerr = hipErrorUnknown;  // another rank failed
+          ovf |= hall[2 * r + 1];
+        }
+        FCHK(lerr);
+        if (ovf) return hipErrorOutOfMemory;  // more than NB_CAP neighbours (reported by the API)
+        if (dev ? sh.exchange_dev(X.xsd, pb, X.xrd, st) != 0 : sh.exchange(xsend.data(), pb, xrecv.data()) != 0)
+          return hipErrorUnknown;
+        agreed = false;
+        for (int r = 0; r < G; ++r) {
+          const int rlo = std::min(nc, r * pch), rhi = std::min(nc, rlo + pch);
+          if (r == R || rhi <= rlo) continue;
+          const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+          const char* b = dev ? X.xrd + (size_t)r * pb : xrecv.data() + (size_t)r * pb;
+          FCHK(hipMemcpyAsync(X.cand_coord + (size_t)(off + rlo) * 24, b, (size_t)(rhi - rlo) * 24 * sizeof(float), kind, st));
+          FCHK(hipMemcpyAsync(X.cand_ok + (size_t)(off + rlo) * 6, b + (size_t)pch * 24 * sizeof(float),
+                              (size_t)(rhi - rlo) * 6 * sizeof(int), kind, st));
+        }
+        if (!dev) FCHK(hipStreamSynchronize(st));  // xrecv is reused by the next exchange
+      }
       if (W > 1 && min_cands > 0) {
         okh.resize((size_t)nc * 6);
         FCHK(hipMemcpyAsync(okh.data(), X.cand_ok + (size_t)off * 6, (size_t)nc * 6 * sizeof(int), hipMemcpyDeviceToHost, st));

@@ -189,11 +189,12 @@ def test_sharded_expand_matches_single_rank(gpu_available, world, wave):
     assert all(r[2]["refined"] > 0 for r in res)
 
 
-@pytest.mark.parametrize("where", ["b", "a"])
+@pytest.mark.parametrize("where", ["b", "e", "a"])
 def test_sharded_expand_rank_failure_fails_all_ranks(gpu_available, monkeypatch, where):
     """A failure on ONE rank of a sharded expansion (advice r01: an allocation failure between
     exchanges used to leave the peers blocked in the next all-gather) makes every rank return an
-    error: injected on rank 1 at wave 2 before its batch exchange (b) or right after it (a)."""
+    error: injected on rank 1 at wave 2 before the wave (b), at its findEmptyBlocks candidate
+    exchange (e), or right after its refine batch exchange (a)."""
     import pmvs_amd as P
     inp, p = P.synth_scene(6, 480, 360, level=1, supersample=2)
     g = P.Scene(inp)
