@@ -2425,6 +2425,56 @@ static inline unsigned long long qkey(float tmp, long long seq) {
 struct QCmp {  // max-heap on key
   bool operator()(const QItem& a, const QItem& b) const { return a.key < b.key; }
 };
+// CExpand's max-_tmp queue as sorted runs: the collected patches (one run, sorted on the device)
+// and one run per wave (the patches that wave pushed, in key order); a pop takes the largest run
+// head through a max-heap over the runs (at most a few hundred: log2 of them per pop instead of a
+// binary heap over every queued patch).  Keys are unique (seq), so the pops are the same sequence
+// a single heap over all items gives.
+class RunQueue {
+ public:
+  bool empty() const { return heads_.empty(); }
+  // r sorted by key, descending
+  void add_run(std::vector<QItem>&& r) {
+    if (r.empty()) return;
+    const int id = (int)runs_.size();
+    runs_.push_back(std::move(r));
+    pos_.push_back(0);
+    heads_.push_back({runs_[id][0].key, id});
+    std::push_heap(heads_.begin(), heads_.end());
+  }
+  int pop() {
+    std::pop_heap(heads_.begin(), heads_.end());
+    const int id = heads_.back().second;
+    heads_.pop_back();
+    std::vector<QItem>& r = runs_[id];
+    const int p = r[pos_[id]].p;
+    if (++pos_[id] < r.size()) {
+      heads_.push_back({r[pos_[id]].key, id});
+      std::push_heap(heads_.begin(), heads_.end());
+    } else {
+      std::vector<QItem>().swap(r);
+    }
+    return p;
+  }
+  // a wave's pushes, in push order (seq ascending = low key bits descending): a stable LSD radix sort
+  // on the high 32 key bits (the _tmp order bits), descending, gives the run's key order
+  static void sort_run(std::vector<QItem>& v, std::vector<QItem>& tmp) {
+    const size_t n = v.size();
+    tmp.resize(n);
+    for (int sh = 32; sh < 64; sh += 8) {
+      size_t cnt[257] = {0};
+      for (const QItem& q : v) cnt[255 - ((q.key >> sh) & 0xff) + 1]++;
+      for (int b = 0; b < 256; ++b) cnt[b + 1] += cnt[b];
+      for (const QItem& q : v) tmp[cnt[255 - ((q.key >> sh) & 0xff)]++] = q;
+      v.swap(tmp);
+    }
+  }
+
+ private:
+  std::vector<std::vector<QItem>> runs_;
+  std::vector<size_t> pos_;
+  std::vector<std::pair<unsigned long long, int>> heads_;
+};
 
 __global__ void gather_slots_kernel(const int* __restrict__ slots, int m, const pmvs_candidate* __restrict__ cin,
                                     const pmvs_patch* __restrict__ prep, pmvs_candidate* __restrict__ cout,
@@ -3180,17 +3230,12 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   initial.reserve(c.nalive);
   for (int j = 0; j < c.nalive; ++j)  // collectPatches(queue) without other clusters' boundary patches
     if (!qforeign[srank[j]]) initial.push_back({qkey(qtmp[j], srank[j]), order[srank[j]]});
-  const QCmp less;  // less(a, b): a has lower priority than b
-  size_t ihead = 0;
-  std::priority_queue<QItem, std::vector<QItem>, QCmp> queue;
+  RunQueue queue;
+  queue.add_run(std::move(initial));
+  std::vector<QItem> wave_run, sort_tmp;
   long long seq = c.nalive;
-  auto q_empty = [&]() { return ihead >= initial.size() && queue.empty(); };
-  auto q_pop = [&]() -> int {
-    if (ihead < initial.size() && (queue.empty() || !less(initial[ihead], queue.top()))) return initial[ihead++].p;
-    const int p = queue.top().p;
-    queue.pop();
-    return p;
-  };
+  auto q_empty = [&]() { return queue.empty(); };
+  auto q_pop = [&]() -> int { return queue.pop(); };
   int rank_next = c.nalive;
   int nmodel = n0;
   const int G = std::max(1, sh.world), R = std::min(std::max(0, sh.rank), G - 1);
@@ -3437,7 +3482,10 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
       const int added = co.nacc;
       if (added > 0 && nmodel + added > cap) return hipErrorOutOfMemory;
       stats[6] += added;
-      for (const int2& u : co.push) queue.push({qkey(__int_as_float_h(u.x), seq++), u.y});
+      wave_run.clear();
+      for (const int2& u : co.push) wave_run.push_back({qkey(__int_as_float_h(u.x), seq++), u.y});
+      RunQueue::sort_run(wave_run, sort_tmp);
+      queue.add_run(std::vector<QItem>(wave_run));
       T.mark(7);
       if (added > 0) {
         pool_need = X.pool_host + (size_t)co.entries;
