@@ -1150,6 +1150,12 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   DevStats ds{};
   HIPCHK(hipMemcpy(&ds, sc->stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));
+  if (getenv("PMVS_REFINE_TAIL"))  // diagnostics: the refine launches' tails (s_memrealtime: 100 MHz)
+    for (int f = 0; f < 2; ++f)
+      if (ds.tail_launches[f])
+        fprintf(stderr, "[refine tail] form=%s launches=%llu span_ms=%.2f tail_ms=%.2f tail_frac=%.3f\n",
+                f ? "workgroup" : "wavefront", ds.tail_launches[f], ds.span_t[f] / 1e5, ds.tail_t[f] / 1e5,
+                ds.span_t[f] ? (double)ds.tail_t[f] / (double)ds.span_t[f] : 0.0);
   if (stats) {
     std::memset(stats, 0, sizeof(*stats));
     stats->parents = sv[0]; stats->candidates = sv[1]; stats->fail_prep = sv[2]; stats->fail_pre = sv[3];

@@ -1184,6 +1184,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(REFINE_WPE(N
   unsigned long long tprev = 0;
   const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999};
   const double ub[3] = {HUGE_VAL, 23.99999, 23.99999};
+  if (lane == 0) atomicMax(&st->t_first_inv, ~__builtin_amdgcn_s_memrealtime());
   for (;;) {
     const unsigned long long t0 = PROF_NOW();
     tprev = t0;
@@ -1192,6 +1193,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(REFINE_WPE(N
       const unsigned long long c = atomicAdd(&st->queue2, 1ull);
       if (c >= (unsigned long long)n) {
         exhausted = true;
+        atomicMax(&st->t_drain_inv, ~__builtin_amdgcn_s_memrealtime());
         break;
       }
       const RefineJob& J = jobs[c];
@@ -1318,6 +1320,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(REFINE_WPE(N
     atomicAdd(&st->rounds, rounds);
     atomicAdd(&st->chunks, chunks);
     for (int i = 0; i < 8; ++i) atomicAdd(&st->prof[i], prof[i]);
+    atomicMax(&st->t_last, __builtin_amdgcn_s_memrealtime());
   }
 }
 
@@ -1391,6 +1394,7 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(REFI
     C.rsize[tid] = 0;
     C.alive[tid] = 0;
   }
+  if (tid == 0) atomicMax(&st->t_first_inv, ~__builtin_amdgcn_s_memrealtime());
   __syncthreads();
   for (;;) {
     bool req = false;
@@ -1400,6 +1404,7 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(REFI
         const unsigned long long q = atomicAdd(&st->queue2, 1ull);
         if (q >= (unsigned long long)n) {
           exhausted = true;
+          atomicMax(&st->t_drain_inv, ~__builtin_amdgcn_s_memrealtime());
           break;
         }
         const RefineJob& J = jobs[q];
@@ -1549,7 +1554,24 @@ __global__ __launch_bounds__(WG_THREADS) __attribute__((amdgpu_waves_per_eu(REFI
     atomicAdd(&st->tex_grabs, grabs);
     atomicAdd(&st->rounds, rounds);
     atomicAdd(&st->chunks, chunks);
+    atomicMax(&st->t_last, __builtin_amdgcn_s_memrealtime());
   }
+}
+
+// PMVS_REFINE_TAIL=1 (diagnostics): after each refine launch, its span (first wavefront start -> last
+// end) and tail (first empty refill -> last end: chains still running while no new candidate
+// starts) are added to DevStats' sums and the per-launch stamps cleared.
+__global__ void refine_tail_kernel(DevStats* st, int form) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const unsigned long long last = st->t_last, first = ~st->t_first_inv, drain = ~st->t_drain_inv;
+  if (st->t_last != 0 && st->t_first_inv != 0) {
+    st->span_t[form] += last - first;
+    st->tail_t[form] += (st->t_drain_inv != 0 && drain < last) ? last - drain : 0ull;
+    st->tail_launches[form] += 1;
+  }
+  st->t_first_inv = 0;
+  st->t_drain_inv = 0;
+  st->t_last = 0;
 }
 
 }  // namespace pmvsdev
@@ -1892,6 +1914,11 @@ bool refine_config_supported(int tslots) {
   }
 }
 
+static bool refine_tail_on() {
+  static const bool on = getenv("PMVS_REFINE_TAIL") != nullptr;
+  return on;
+}
+
 template <int WS>
 static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out,
                                    int n, DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream,
@@ -1945,6 +1972,7 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
       default: return hipErrorInvalidValue;
     }
 #undef PMVS_WG
+    if (refine_tail_on()) hipLaunchKernelGGL(refine_tail_kernel, dim3(1), dim3(64), 0, stream, d_st, 1);
     (void)hipEventRecord(ev[2], stream);
     hipLaunchKernelGGL((post_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_jobs, d_out, n, d_st);
     (void)hipEventRecord(ev[3], stream);
@@ -1973,6 +2001,7 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
 #endif
     default: hipLaunchKernelGGL((refine_v2_kernel<WS, 12, 6>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
   }
+  if (refine_tail_on()) hipLaunchKernelGGL(refine_tail_kernel, dim3(1), dim3(64), 0, stream, d_st, 0);
   (void)hipEventRecord(ev[2], stream);
   hipLaunchKernelGGL((post_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_jobs, d_out, n, d_st);
   (void)hipEventRecord(ev[3], stream);

@@ -94,6 +94,11 @@ struct DevStats {
   unsigned long long cyc_opt, cyc_eval, rounds, chunks;  // refine-kernel phase profile (lane 0 of each wave)
   unsigned long long prof[8];  // refill, step, publish, chunk setup, gather, normalize, dot, reduce
   unsigned long long tex_valid_wg;  // the part of tex_valid the workgroup-form kernel evaluated
+  // launch tail (s_memrealtime, 100 MHz): per launch the first wavefront's start (as ~t, so atomicMax
+  // keeps the minimum), the first refill that found the queue empty (~t) and the last wavefront's
+  // end; refine_tail_kernel folds them into the sums below ([0] wavefront form, [1] workgroup form)
+  unsigned long long t_first_inv, t_drain_inv, t_last;
+  unsigned long long tail_t[2], span_t[2], tail_launches[2];
 };
 
 }  // namespace pmvsdev
