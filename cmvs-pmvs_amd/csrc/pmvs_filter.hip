@@ -37,6 +37,7 @@
 #include "pmvs_device.h"
 #include "pmvs_launch.h"
 #include "pmvs_layout.h"
+#include "pmvs_queue.h"
 
 namespace pmvsdev {
 
@@ -906,6 +907,28 @@ __device__ __forceinline__ int wave_excl_scan_w(int v) {
   return x - v;
 }
 
+// The candidates a findNeighbors walk has already tested, as an open-addressing set over NbLds.seq
+// (free during the walk; filterQuad writes it afterwards).  A patch registered in several of the
+// walked images' cells is met once per image; isNeighbor(patch, j) does not depend on the cell it
+// was found in, so only the first meeting is tested (the hit list's final sort + unique removes
+// duplicates either way).  A crowded probe sequence just tests again.
+__device__ __forceinline__ void nb_seen_clear(NbLds& L) {
+  int* tab = reinterpret_cast<int*>(L.seq);
+  for (int i = lane_id_w(); i < NB_CAP; i += 64) tab[i] = -1;
+}
+__device__ __forceinline__ bool nb_first_visit(NbLds& L, int j) {
+  int* tab = reinterpret_cast<int*>(L.seq);
+  unsigned h = ((unsigned)j * 2654435761u) >> 22;  // 10 bits: NB_CAP slots
+  for (int probe = 0; probe < 16; ++probe) {
+    const int old = atomicCAS(&tab[h], -1, j);
+    if (old == -1) return true;
+    if (old == j) return false;
+    h = (h + 1) & (NB_CAP - 1);
+  }
+  return true;
+}
+static_assert(NB_CAP == 1024, "nb_first_visit hashes to 10 bits");
+
 // Appends the hits of one 64-lane round in lane order (ballot), compacting the buffer (sort +
 // unique) when it nears capacity, as the reference's final sort/unique would (same set).
 __device__ __forceinline__ void nb_append(NbLds& L, bool hit, int j) {
@@ -942,6 +965,7 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, c
   unit *= (float)s.csize;
   const float thr = 0.5f * scale;
   if (lane == 0) { L.cnt = 0; L.overflow = 0; }
+  nb_seen_clear(L);
   __syncthreads();
   const int nlists = skipvis ? ni : ni + uni(q.num_vimages);
   const int side = 2 * margin + 1;
@@ -1027,7 +1051,7 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, c
         hv[u] = false;
         if (ib + u * 64 + lane < tot) {
           if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 14); jv[u] = 0; }
-          else hv[u] = is_neighbor_h(q, F.hot[j], unit, thr, radius, true) != 0;
+          else if (nb_first_visit(L, j)) hv[u] = is_neighbor_h(q, F.hot[j], unit, thr, radius, true) != 0;
         }
       }
 #pragma unroll
@@ -1043,7 +1067,7 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, c
         for (int ent = head; ent >= 0; ent = F.d_next[ent]) {
           const int j = F.d_item[ent];
           if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 15); continue; }
-          if (is_neighbor_h(q, F.hot[j], unit, thr, radius, true)) {
+          if (nb_first_visit(L, j) && is_neighbor_h(q, F.hot[j], unit, thr, radius, true)) {
             const int pos = atomicAdd(&L.cnt, 1);
             if (pos < NB_CAP) L.nb[pos] = j;
             else L.overflow = 1;
@@ -1087,7 +1111,7 @@ __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, d
   float* gz = gy + (fout ? n : NB_CAP);
   for (int a = lane; a < n; a += 64) {  // the distances in parallel, their sum in order below
     float d[4];
-    for (int k = 0; k < 4; ++k) d[k] = F.P[L.nb[a]].coord[k] - q.coord[k];
+    for (int k = 0; k < 4; ++k) d[k] = F.hot[L.nb[a]].coord[k] - q.coord[k];
     L.seq[a] = norm4(d);
   }
   __syncthreads();
@@ -1100,7 +1124,7 @@ __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, d
   const float h = (float)L.f[1];
   for (int a = lane; a < n; a += 64) {
     float d[4];
-    for (int k = 0; k < 4; ++k) d[k] = F.P[L.nb[a]].coord[k] - q.coord[k];
+    for (int k = 0; k < 4; ++k) d[k] = F.hot[L.nb[a]].coord[k] - q.coord[k];
     const float fx = __fdiv_rn(dot4(d, xdir), h), fy = __fdiv_rn(dot4(d, ydir), h), fz = dot4(d, q.normal);
     gx[a] = fx; gy[a] = fy; gz[a] = fz;
   }
@@ -1562,7 +1586,7 @@ __global__ __launch_bounds__(64) void empty_blocks_kernel(DScene s, FilterDev F,
     unsigned pos = 0u, nan = 0u;
     for (int a = lane; a < n; a += 64) {
       float d[4];
-      for (int c = 0; c < 4; ++c) d[c] = F.P[L.nb[a]].coord[c] - q.coord[c];
+      for (int c = 0; c < 4; ++c) d[c] = F.hot[L.nb[a]].coord[c] - q.coord[c];
       float f0 = dot4(d, xdir), f1 = dot4(d, ydir);
       const float len = (float)sqrt((double)(f0 * f0 + f1 * f1));
       if (len < radiuslow || radiushigh < len) continue;
@@ -2411,71 +2435,6 @@ static inline float __int_as_float_h(int v) {
 
 // Queue entry: key = order-preserving bits of _tmp (-0 as +0) << 32 | ~seq, so that one unsigned
 // compare is P_compare (patchOrganizerS.hpp:10-15: max _tmp) with ties to the earlier push.
-struct QItem {
-  unsigned long long key;
-  int p;
-};
-static inline unsigned long long qkey(float tmp, long long seq) {
-  if (tmp == 0.0f) tmp = 0.0f;
-  unsigned u;
-  std::memcpy(&u, &tmp, sizeof(u));
-  u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-  return ((unsigned long long)u << 32) | (0xffffffffull - (unsigned long long)seq);
-}
-struct QCmp {  // max-heap on key
-  bool operator()(const QItem& a, const QItem& b) const { return a.key < b.key; }
-};
-// CExpand's max-_tmp queue as sorted runs: the collected patches (one run, sorted on the device)
-// and one run per wave (the patches that wave pushed, in key order); a pop takes the largest run
-// head through a max-heap over the runs (at most a few hundred: log2 of them per pop instead of a
-// binary heap over every queued patch).  Keys are unique (seq), so the pops are the same sequence
-// a single heap over all items gives.
-class RunQueue {
- public:
-  bool empty() const { return heads_.empty(); }
-  // r sorted by key, descending
-  void add_run(std::vector<QItem>&& r) {
-    if (r.empty()) return;
-    const int id = (int)runs_.size();
-    runs_.push_back(std::move(r));
-    pos_.push_back(0);
-    heads_.push_back({runs_[id][0].key, id});
-    std::push_heap(heads_.begin(), heads_.end());
-  }
-  int pop() {
-    std::pop_heap(heads_.begin(), heads_.end());
-    const int id = heads_.back().second;
-    heads_.pop_back();
-    std::vector<QItem>& r = runs_[id];
-    const int p = r[pos_[id]].p;
-    if (++pos_[id] < r.size()) {
-      heads_.push_back({r[pos_[id]].key, id});
-      std::push_heap(heads_.begin(), heads_.end());
-    } else {
-      std::vector<QItem>().swap(r);
-    }
-    return p;
-  }
-  // a wave's pushes, in push order (seq ascending = low key bits descending): a stable LSD radix sort
-  // on the high 32 key bits (the _tmp order bits), descending, gives the run's key order
-  static void sort_run(std::vector<QItem>& v, std::vector<QItem>& tmp) {
-    const size_t n = v.size();
-    tmp.resize(n);
-    for (int sh = 32; sh < 64; sh += 8) {
-      size_t cnt[257] = {0};
-      for (const QItem& q : v) cnt[255 - ((q.key >> sh) & 0xff) + 1]++;
-      for (int b = 0; b < 256; ++b) cnt[b + 1] += cnt[b];
-      for (const QItem& q : v) tmp[cnt[255 - ((q.key >> sh) & 0xff)]++] = q;
-      v.swap(tmp);
-    }
-  }
-
- private:
-  std::vector<std::vector<QItem>> runs_;
-  std::vector<size_t> pos_;
-  std::vector<std::pair<unsigned long long, int>> heads_;
-};
-
 __global__ void gather_slots_kernel(const int* __restrict__ slots, int m, const pmvs_candidate* __restrict__ cin,
                                     const pmvs_patch* __restrict__ prep, pmvs_candidate* __restrict__ cout,
                                     pmvs_patch* __restrict__ pout, const int* __restrict__ cidx) {
