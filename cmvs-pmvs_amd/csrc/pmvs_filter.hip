@@ -328,12 +328,22 @@ __global__ void coordc_kernel(const pmvs_patch* __restrict__ P, const int* __res
   coordc[i] = make_float4(c[0], c[1], c[2], c[3]);
 }
 
+// XCD-aware block order: the hardware deals workgroups to the 8 XCDs round-robin (block b on XCD
+// b % 8), each XCD with its own L2.  Remapping b to the logical block (b % 8) * (grid / 8) + b / 8
+// (grid a multiple of 8: xcd_grid) gives each XCD one contiguous range of logical blocks, so
+// threads that touch neighbouring cells share an L2.
+constexpr int kXcds = 8;
+__device__ __forceinline__ long long xcd_block() {
+  const unsigned b = blockIdx.x, per = gridDim.x / kXcds;
+  return (long long)(b % kXcds) * per + b / kXcds;
+}
+
 // setDepthMaps: one thread per (target, collected patch), target-major so that neighbouring
 // threads hold neighbouring patches (collect order is by image and cell) and their atomics hit
 // nearby cells of the same map.
 __global__ void depth_map_kernel(DScene s, FilterDev F, const float4* __restrict__ coordc,
                                  unsigned long long* __restrict__ dpkey) {
-  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long g = xcd_block() * blockDim.x + threadIdx.x;
   if (g >= (long long)F.nalive * F.tnum) return;
   const int t = (int)(g / F.nalive), i = (int)(g - (long long)t * F.nalive);
   const float4 c4 = coordc[i];
@@ -360,7 +370,7 @@ __global__ void depth_map_kernel(DScene s, FilterDev F, const float4* __restrict
 // vreg = every vimages entry (addPatchVThread registers the first entry per image, and the
 // list never holds an image twice).
 __global__ void vimages_kernel(DScene s, FilterDev F, int additive, Reg* __restrict__ vreg) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = (int)(xcd_block() * blockDim.x + threadIdx.x);
   if (i >= F.nalive) return;
   const int p = F.order[i];
   pmvs_patch& q = F.P[p];
@@ -1909,6 +1919,8 @@ __global__ void flag_rank_kernel(pmvs_patch* __restrict__ P, const int* __restri
   } while (0)
 
 static inline unsigned nblk(long long n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+// a grid for the XCD-remapped kernels (xcd_block): nblk rounded up to a multiple of the XCD count
+static inline unsigned xcd_grid(long long n, int b = 256) { return (nblk(n, b) + kXcds - 1) / kXcds * kXcds; }
 
 static void dbg(hipStream_t st, const char* what) {
   static const bool on = getenv("PMVS_FILTER_DEBUG") != nullptr;
@@ -1937,7 +1949,9 @@ FilterBuffers::~FilterBuffers() {
 
 hipError_t FilterBuffers::reserve(int n_, long long ncells_, int tnum_, int grid_) {
   if (n_ <= cap_n && ncells_ <= cap_cells && grid_ <= cap_grid) return hipSuccess;
-  cap_n = std::max(n_, cap_n);
+  // 25 % headroom: the next loop iteration's expansion reserves its model plus a few waves, so an exact
+  // capacity would free and reallocate every per-patch buffer (GBs) once per iteration
+  cap_n = std::max(n_ + n_ / 4, cap_n);
   cap_cells = std::max(ncells_, cap_cells);
   cap_grid = std::max(grid_, cap_grid);
   // cell-list entries: about 16 per patch to start with (a C3 patch registers ~10-17), grown by
@@ -2160,12 +2174,12 @@ static hipError_t set_dm_vgrids(Ctx& c, int additive) {
   if (c.nalive > 0)
     hipLaunchKernelGGL(coordc_kernel, dim3(nblk(c.nalive)), dim3(256), 0, c.st, c.P, B.order, c.nalive, B.coordc);
   if (c.nalive > 0)
-    hipLaunchKernelGGL(depth_map_kernel, dim3(nblk((long long)c.nalive * c.s.tnum)), dim3(256), 0, c.st, c.s, c.dev(), B.coordc,
+    hipLaunchKernelGGL(depth_map_kernel, dim3(xcd_grid((long long)c.nalive * c.s.tnum)), dim3(256), 0, c.st, c.s, c.dev(), B.coordc,
                        B.dpkey);
   dbg(c.st, "  depth");
-  FCHK(hipMemsetAsync(B.vreg, 0, c.n * sizeof(unsigned long long), c.st));
+  FCHK(hipMemsetAsync(B.vreg, 0, c.n * sizeof(Reg), c.st));
   if (c.nalive > 0)
-    hipLaunchKernelGGL(vimages_kernel, dim3(nblk(c.nalive)), dim3(256), 0, c.st, c.s, c.dev(), additive, B.vreg);
+    hipLaunchKernelGGL(vimages_kernel, dim3(xcd_grid(c.nalive)), dim3(256), 0, c.st, c.s, c.dev(), additive, B.vreg);
   dbg(c.st, "  vimages");
   FCHK(build_lists(c, 1));
   dbg(c.st, "  vlists");
@@ -2435,6 +2449,13 @@ static inline float __int_as_float_h(int v) {
 
 // Queue entry: key = order-preserving bits of _tmp (-0 as +0) << 32 | ~seq, so that one unsigned
 // compare is P_compare (patchOrganizerS.hpp:10-15: max _tmp) with ties to the earlier push.
+// sum of n 0/1 flags into *out (one atomic per wavefront)
+__global__ void count_ok_kernel(const int* __restrict__ ok, int n, int* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned long long m = __ballot(i < n && ok[i] != 0);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(out, (int)__popcll(m));
+}
+
 __global__ void gather_slots_kernel(const int* __restrict__ slots, int m, const pmvs_candidate* __restrict__ cin,
                                     const pmvs_patch* __restrict__ prep, pmvs_candidate* __restrict__ cout,
                                     pmvs_patch* __restrict__ pout, const int* __restrict__ cidx) {
@@ -3127,7 +3148,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   if (c.nalive > 0 && !(flags & 1))  // after the seed phase the depth maps are still empty
   {
     hipLaunchKernelGGL(coordc_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, dP, B.order, c.nalive, B.coordc);
-    hipLaunchKernelGGL(depth_map_kernel, dim3(nblk((long long)c.nalive * s.tnum)), dim3(256), 0, st, s, c.dev(), B.coordc,
+    hipLaunchKernelGGL(depth_map_kernel, dim3(xcd_grid((long long)c.nalive * s.tnum)), dim3(256), 0, st, s, c.dev(), B.coordc,
                        B.dpkey);
   }
   FCHK(build_lists(c, 1));
@@ -3201,7 +3222,6 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   std::vector<char> xsend, xrecv;
   CommitOut co;
   T.mark(0);
-  std::vector<int> okh;
   const long long max_waves = (long long)((unsigned)flags >> 8);  // PMVS_EXPAND_MAX_WAVES (0 = unbounded)
   while (!q_empty() && (max_waves <= 0 || stats[7] < max_waves)) {
     stats[7]++;
@@ -3279,11 +3299,13 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
         }
         if (!dev) FCHK(hipStreamSynchronize(st));  // xrecv is reused by the next exchange
       }
-      if (W > 1 && min_cands > 0) {
-        okh.resize((size_t)nc * 6);
-        FCHK(hipMemcpyAsync(okh.data(), X.cand_ok + (size_t)off * 6, (size_t)nc * 6 * sizeof(int), hipMemcpyDeviceToHost, st));
-        FCHK(hipStreamSynchronize(st));
-        for (int v : okh) ndirs += v;
+      if (W > 1 && min_cands > 0) {  // the chunk's free directions, summed on the device
+        FCHK(hipMemsetAsync(B.counters + 9, 0, sizeof(int), st));
+        hipLaunchKernelGGL(count_ok_kernel, dim3(nblk((long long)nc * 6)), dim3(256), 0, st, X.cand_ok + (size_t)off * 6,
+                           nc * 6, B.counters + 9);
+        int nfree = 0;
+        FCHK(read_int(B.counters + 9, &nfree, st));
+        ndirs += nfree;
       }
       T.mark(2);
     } while (W > 1 && ndirs < min_cands && !q_empty());

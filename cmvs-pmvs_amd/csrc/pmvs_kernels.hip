@@ -21,6 +21,7 @@
 #include <functional>
 #include <mutex>
 #include <thread>
+#include <unistd.h>
 #include <vector>
 
 #include "bobyqa_dev.h"
@@ -1756,85 +1757,13 @@ __global__ void unpack_rgba_kernel(const uint32_t* __restrict__ in, uint8_t* __r
 
 // ==================================================================== launchers
 #include "pmvs_launch.h"
+#include "pmvs_hostpool.h"
 
 namespace pmvsdev {
 
 // The optimizer start point's angles (encode's transcendental tail, see encode_dev) with the host's
 // libm, exactly as COptim::encode (optim.cpp:671-686) evaluates them, then std::max(std::min(x,
 // ub), lb) with the angle bounds (optim.cpp:629-634).  Threads for large batches.
-// A persistent pool of host threads for the per-batch host work of the refine (the start-point
-// angles below).  run(nt, f) calls f(t, nt') for t in [0, nt') (nt' = nt capped by the pool, t = 0 on
-// the caller's thread) and returns after every call returned; false (nothing run) when another
-// thread is using the pool.
-class HostPool {
- public:
-  static HostPool& get() {
-    static HostPool pool;
-    return pool;
-  }
-  template <class F>
-  bool run(int nt, F&& f) {
-    std::unique_lock<std::mutex> use(use_, std::try_to_lock);
-    if (!use.owns_lock()) return false;
-    nt = std::max(1, std::min(nt, (int)workers_.size() + 1));
-    std::function<void(int, int)> job = [&f](int t, int k) { f(t, k); };
-    {
-      std::lock_guard<std::mutex> g(m_);
-      job_ = &job;
-      nt_ = nt;
-      pending_ = nt - 1;
-      ++gen_;
-    }
-    cv_.notify_all();
-    job(0, nt);
-    std::unique_lock<std::mutex> g(m_);
-    done_.wait(g, [&] { return pending_ == 0; });
-    job_ = nullptr;
-    return true;
-  }
-  ~HostPool() {
-    {
-      std::lock_guard<std::mutex> g(m_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& w : workers_) w.join();
-  }
-
- private:
-  HostPool() {
-    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
-    for (int t = 1; t < std::min(8, hw); ++t) workers_.emplace_back([this, t] { loop(t); });
-  }
-  void loop(int t) {
-    unsigned long long seen = 0;
-    for (;;) {
-      std::function<void(int, int)>* job;
-      int nt;
-      {
-        std::unique_lock<std::mutex> g(m_);
-        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
-        if (stop_) return;
-        seen = gen_;
-        job = job_;
-        nt = nt_;
-      }
-      if (t < nt) {
-        (*job)(t, nt);
-        std::lock_guard<std::mutex> g(m_);
-        if (--pending_ == 0) done_.notify_one();
-      }
-    }
-  }
-  std::vector<std::thread> workers_;
-  std::mutex use_, m_;
-  std::condition_variable cv_, done_;
-  std::function<void(int, int)>* job_ = nullptr;
-  int nt_ = 0, pending_ = 0;
-  unsigned long long gen_ = 0;
-  bool stop_ = false;
-};
-
 static void encode_angles_host(const float4* enc, int n, float ascale, double2* ang) {
   auto one = [&](int i) {
     const float4 e = enc[i];
