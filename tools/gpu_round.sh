@@ -6,6 +6,11 @@
 #                                           HBM-traffic PMC passes (FETCH_SIZE, WRITE_SIZE in
 #                                           separate runs, kernel-trace only) for the C3 loop and
 #                                           the C2 refine batch
+#   bash tools/gpu_round.sh loop <tag>      filter / expansion / loop / sharding GPU tests, the
+#                                           expansion phase profile (PMVS_EXPAND_PROFILE=1) and the
+#                                           refine launch tails (PMVS_REFINE_TAIL=1) of one C3 step,
+#                                           and the bench line
+#   bash tools/gpu_round.sh kt <tag>        rocprofv3 kernel-trace stats of one C3 step only
 set -o pipefail
 WHAT=${1:-test}; TAG=${2:-r01}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -25,6 +30,14 @@ elif [ "$WHAT" = tests ]; then  # the GPU suite alone (no -x: every failure is l
 elif [ "$WHAT" = bench ]; then  # smoke() and the default bench line
   timeout -k 10 300 python3 -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
   timeout -k 10 500 python3 -u $R/bench.py > $O/bench.json 2> $O/bench.err
+elif [ "$WHAT" = loop ]; then
+  T=""; for t in test_gpu_filter.py test_gpu_expand.py test_gpu_loop_scale.py test_gpu_dist.py test_gpu_poison.py; do T="$T $R/tests/$t"; done
+  timeout -k 10 800 python3 -u -m pytest $T -m gpu -x -v --timeout 400 --timeout-method thread > $O/pytest_gpu.log 2>&1 && \
+  PMVS_EXPAND_PROFILE=1 timeout -k 10 300 python3 -u $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-c2 > $O/phase.json 2> $O/phase.err && \
+  PMVS_REFINE_TAIL=1 timeout -k 10 300 python3 -u $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-c2 > $O/tail.json 2> $O/tail.err && \
+  timeout -k 10 500 python3 -u $R/bench.py --steps 2 --warmup 1 > $O/bench.json 2> $O/bench.err
+elif [ "$WHAT" = kt ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-c2 > $O/kt.log 2>&1
 else
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/kt.log 2>&1 && \
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-c2 > $O/pmc_fetch.log 2>&1 && \
