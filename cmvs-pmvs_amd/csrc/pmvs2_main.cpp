@@ -9,6 +9,14 @@
 // pyramids) -> pmvs_detect_features (Harris + DoG on the device) -> pmvs_seed_run (seed phase) ->
 // pmvs_run_loop (3 x expand / filter, model resident in HBM) -> writers (colours on the device).
 //
+// Multi-rank jobs (CMVS cluster per GPU): with WORLD_SIZE > 1 in the environment
+// (torchrun-style: RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR, MASTER_PORT; genOption --gpus N writes
+// the script that sets them) the WORLD_SIZE pmvs2 processes of one job -- one cluster option file
+// each -- find each other over TCP (pmvs_tcp), and their loops exchange the clusters' boundary
+// patches after every iteration (pmvs_scene_set_cluster): device to device over RCCL on GPU LOCAL_RANK
+// (the unique id travels on the TCP channel), or over the TCP channel itself with
+// PMVS_EXCHANGE=tcp (several ranks on one GPU).  Each rank writes its own cluster's outputs.
+//
 // Expansion schedule: option `CPU 1` selects the reference's single-thread schedule exactly
 // (wave = 1); any other value the production wave schedule (the reference's own
 // multi-threaded schedule is nondeterministic).  PMVS_WAVE / PMVS_MIN_CANDIDATES override it.
@@ -55,6 +63,33 @@ int env_int(const char* name, int dflt) {
   const char* e = std::getenv(name);
   return e ? std::atoi(e) : dflt;
 }
+
+const char* env_str(const char* name, const char* dflt) {
+  const char* e = std::getenv(name);
+  return (e && *e) ? e : dflt;
+}
+
+// The job's channels (WORLD_SIZE > 1): TCP between the processes, and RCCL unless PMVS_EXCHANGE=tcp.
+struct Job {
+  int rank = 0, world = 1, device = 0;
+  bool rccl = true;
+  pmvs_tcp* tcp = nullptr;
+  pmvs_rccl* comm = nullptr;
+  ~Job() {
+    pmvs_rccl_destroy(comm);
+    pmvs_tcp_destroy(tcp);
+  }
+  // every rank's `ok` flag; false when some rank failed (or has exited: its connection is closed)
+  bool all_ok(bool ok) {
+    if (world == 1) return ok;
+    int32_t mine = ok ? 1 : 0;
+    std::vector<int32_t> all(world, 0);
+    if (pmvs_tcp_allgather(tcp, &mine, sizeof(mine), all.data()) != 0) return false;
+    for (int32_t a : all)
+      if (!a) return false;
+    return true;
+  }
+};
 
 // CImage::completeName (image.cpp:40-84): the first existing extension, else the bare name.
 std::string complete_name(const std::string& base, bool color) {
@@ -110,6 +145,23 @@ int main(int argc, char* argv[]) {
     if (std::string(argv[i]) == "PSET") export_pset = true;
   }
   const double t0 = now_s();
+
+  // ---- the job (WORLD_SIZE > 1: one rank per cluster option file)
+  Job job;
+  job.world = env_int("WORLD_SIZE", 1);
+  job.rank = env_int("RANK", 0);
+  job.device = env_int("PMVS_DEVICE", env_int("LOCAL_RANK", 0));
+  job.rccl = std::string(env_str("PMVS_EXCHANGE", "rccl")) != "tcp";
+  if (job.world < 1 || job.rank < 0 || job.rank >= job.world) {
+    std::cerr << "pmvs2: RANK " << job.rank << " / WORLD_SIZE " << job.world << " out of range" << std::endl;
+    return 1;
+  }
+  if (job.world > 1) {
+    CHECK("job", pmvs_tcp_create(job.rank, job.world, env_str("MASTER_ADDR", "127.0.0.1"), env_int("MASTER_PORT", 29533),
+                                 env_int("PMVS_JOIN_TIMEOUT_MS", 600000), &job.tcp));
+    std::cerr << "pmvs2: rank " << job.rank << " of " << job.world << ", GPU " << job.device << ", exchange "
+              << (job.rccl ? "rccl" : "tcp") << std::endl;
+  }
 
   // ---- SOption::init (option.cpp:30-160)
   pmvs_options* opt = nullptr;
@@ -220,7 +272,28 @@ int main(int argc, char* argv[]) {
   d.bindexes = opt->bindexes;
   d.views = vd.data();
   pmvs_scene* sc = nullptr;
-  CHECK("scene", pmvs_scene_create(&d, env_int("PMVS_DEVICE", 0), &sc));
+  CHECK("scene", pmvs_scene_create(&d, job.device, &sc));
+  // every rank has its scene before any collective (a rank that failed has exited, which its
+  // peers see here instead of blocking in the RCCL bootstrap)
+  if (!job.all_ok(true)) {
+    std::cerr << "pmvs2: another rank of the job failed before the cluster exchange was set up" << std::endl;
+    return 1;
+  }
+  if (job.world > 1) {
+    if (job.rccl) {
+      uint8_t id[128] = {0};
+      if (job.rank == 0) CHECK("rccl", pmvs_rccl_unique_id(id));
+      std::vector<uint8_t> ids((size_t)128 * job.world);
+      if (pmvs_tcp_allgather(job.tcp, id, 128, ids.data()) != 0) {
+        std::cerr << "pmvs2: the RCCL id exchange failed" << std::endl;
+        return 1;
+      }
+      CHECK("rccl", pmvs_rccl_create(job.device, job.rank, job.world, ids.data(), &job.comm));
+      CHECK("cluster", pmvs_scene_set_cluster_rccl(sc, job.rank, job.world, images.data(), job.comm));
+    } else {
+      CHECK("cluster", pmvs_scene_set_cluster(sc, job.rank, job.world, images.data(), &pmvs_tcp_allgather, job.tcp));
+    }
+  }
   std::vector<int> gwidth(num);  // _gwidths (patchOrganizerS.cpp:54-87)
   for (int i = 0; i < num; ++i) {
     int w = views[i].w;
@@ -259,6 +332,14 @@ int main(int argc, char* argv[]) {
             << sst.fail1 << ' ' << sst.pass + sst.fail1 << std::endl;
   const double t_seed = now_s();
 
+  // every rank reaches the loop (a rank whose features or seeds failed has exited, which its peers
+  // see on the TCP channel here rather than inside an RCCL collective); failures inside the loop
+  // reach every rank through the loop's error headers
+  if (!job.all_ok(true)) {
+    std::cerr << "pmvs2: another rank of the job failed before the loop" << std::endl;
+    return 1;
+  }
+
   // ---- expansion / filtering (findMatch.cpp:196-217)
   const int wave = env_int("PMVS_WAVE", opt->cpu == 1 ? 1 : 32768);
   const int min_cands = env_int("PMVS_MIN_CANDIDATES", wave == 1 ? 0 : 131072);
@@ -272,6 +353,10 @@ int main(int argc, char* argv[]) {
   model.resize(nmodel);
   for (int t = 0; t < iterations; ++t)
     std::cerr << "depth " << it[t].depth << ": expanded " << it[t].expand.added << ", kept " << it[t].patches
+              << (job.world > 1 ? ", boundary sent " + std::to_string(it[t].boundary_sent) + " received " +
+                                      std::to_string(it[t].boundary_received) + " inserted " +
+                                      std::to_string(it[t].boundary_inserted)
+                                : std::string())
               << std::endl;
   const double t_loop = now_s();
 

@@ -1091,7 +1091,8 @@ bool test_local_fail(const pmvs_scene* sc, char where) {
   const char* e = getenv("PMVS_TEST_SHARD_FAIL");
   int r = -1, w = -1;
   char c = 0;
-  return e && sc->shard_world > 1 && sscanf(e, "%d:%d:%c", &r, &w, &c) == 3 && r == sc->shard_rank && c == where;
+  if (!e || sscanf(e, "%d:%d:%c", &r, &w, &c) != 3 || c != where) return false;
+  return (sc->shard_world > 1 && r == sc->shard_rank) || (sc->cl_world > 1 && r == sc->cl_rank);
 }
 
 // *handled (sharded loop): whether the peers already know of a failure returned here -- true only
@@ -1314,12 +1315,15 @@ pmvs_status pmvs_run_loop(pmvs_scene* sc, const pmvs_patch* seeds, int32_t n, fl
     pmvs_loop_iter li{};
     li.depth = depth;
     int nn = cur;
+    // expand_device / filter_device report failures their own exchanges announced (*handled); those
+    // exchanges run on the shard channel, so in a cluster scene (loop headers on the cluster
+    // channel) no peer has seen them and the loop header must carry them
     bool xhandled = true;
-    if (cur > 0 && (st = expand_device(sc, cur, wave, min_candidates, cthr, (it == 0 && (flags & PMVS_EXPAND_AFTER_SEEDS)) ? 1 : 0, cap,
-                                       &nn, &li.expand, &xhandled)))
-      return fail_loop(st, xhandled);
+    const int xflags = (flags & ~PMVS_EXPAND_AFTER_SEEDS) | ((it == 0 && (flags & PMVS_EXPAND_AFTER_SEEDS)) ? 1 : 0);
+    if (cur > 0 && (st = expand_device(sc, cur, wave, min_candidates, cthr, xflags, cap, &nn, &li.expand, &xhandled)))
+      return fail_loop(st, xhandled && &hsh == &lsh);
     bool handled = true;
-    if ((st = filter_device(sc, nn, &li.filter, &handled))) return fail_loop(st, handled);
+    if ((st = filter_device(sc, nn, &li.filter, &handled))) return fail_loop(st, handled && &hsh == &lsh);
     int kept = 0;
     if (nn > 0) {
       if ((st = ensure_keep_data(sc, sc->fpatches2, sc->fpatches.n))) return fail_loop(st, false);
@@ -1394,24 +1398,34 @@ pmvs_status pmvs_scene_set_cluster(pmvs_scene* sc, int32_t rank, int32_t world, 
   sc->cl_rccl = nullptr;
   if (world == 1) return PMVS_OK;
   const int num = sc->ds.num, tnum = sc->ds.tnum;
+  // Local validation first; its outcome travels in the all-gather (mine[0] < 0), so a rank with a
+  // bad argument fails together with its peers instead of leaving them in the collective.
+  pmvs_status bad = PMVS_OK;
   int maxid = -1;
-  for (int i = 0; i < num; ++i) {
-    if (image_ids[i] < 0) return fail(PMVS_EINVAL, "image_ids[%d] = %d", i, image_ids[i]);
+  std::vector<int> id2idx;
+  if (tnum > PMVS_MAX_TARGETS) bad = fail(PMVS_EUNSUPPORTED, "cluster: more than %d target images", PMVS_MAX_TARGETS);
+  for (int i = 0; i < num && !bad; ++i) {
+    if (image_ids[i] < 0) bad = fail(PMVS_EINVAL, "image_ids[%d] = %d", i, image_ids[i]);
     maxid = std::max(maxid, image_ids[i]);
   }
-  if (maxid > (1 << 26)) return fail(PMVS_EUNSUPPORTED, "image number %d", maxid);
-  std::vector<int> id2idx((size_t)maxid + 1, -1);
-  for (int i = 0; i < num; ++i) {
-    if (id2idx[image_ids[i]] >= 0) return fail(PMVS_EINVAL, "image number %d appears twice", image_ids[i]);
-    id2idx[image_ids[i]] = i;
+  if (!bad && maxid > (1 << 26)) bad = fail(PMVS_EUNSUPPORTED, "image number %d", maxid);
+  if (!bad) {
+    id2idx.assign((size_t)maxid + 1, -1);
+    for (int i = 0; i < num && !bad; ++i) {
+      if (id2idx[image_ids[i]] >= 0) bad = fail(PMVS_EINVAL, "image number %d appears twice", image_ids[i]);
+      id2idx[image_ids[i]] = i;
+    }
   }
   // all-gather of the target image numbers (collective): a target is shared when another cluster
   // has it as a target too
   std::vector<int> mine(1 + PMVS_MAX_TARGETS, -1), all((size_t)(1 + PMVS_MAX_TARGETS) * world, -1);
-  mine[0] = tnum;
-  for (int t = 0; t < tnum; ++t) mine[1 + t] = image_ids[t];
+  mine[0] = bad ? -1 : tnum;
+  for (int t = 0; t < tnum && !bad; ++t) mine[1 + t] = image_ids[t];
   if (fn(ctx, mine.data(), (int64_t)(mine.size() * sizeof(int)), all.data()) != 0)
     return fail(PMVS_EDEVICE, "cluster setup: the all-gather failed");
+  if (bad) return bad;
+  for (int r = 0; r < world; ++r)
+    if (all[(size_t)r * (1 + PMVS_MAX_TARGETS)] < 0) return fail(PMVS_EINVAL, "cluster setup: rank %d failed its validation", r);
   std::vector<unsigned char> shared(std::max(tnum, 1), 0);
   for (int r = 0; r < world; ++r) {
     if (r == rank) continue;

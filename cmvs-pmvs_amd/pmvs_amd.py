@@ -146,7 +146,7 @@ EXPORTS = ["pmvs_last_error", "pmvs_device_count", "pmvs_scene_create", "pmvs_sc
            "pmvs_expand_run", "pmvs_expand_fetch", "pmvs_run_loop", "pmvs_loop_fetch", "pmvs_scene_set_shard", "pmvs_scene_set_shard_rccl", "pmvs_scene_set_cluster",
            "pmvs_scene_set_cluster_rccl", "pmvs_rccl_unique_id",
            "pmvs_rccl_create", "pmvs_rccl_destroy", "pmvs_rccl_allgather", "pmvs_rccl_allgather_device",
-           "pmvs_thread_exchange_create",
+           "pmvs_tcp_create", "pmvs_tcp_allgather", "pmvs_tcp_destroy", "pmvs_thread_exchange_create",
            "pmvs_thread_exchange_ctx", "pmvs_thread_allgather", "pmvs_thread_exchange_destroy", "pmvs_detect_features",
            "pmvs_seed_run", "pmvs_seed_fetch", "pmvs_selftest_lls", "pmvs_image_load", "pmvs_pnm_mask_load", "pmvs_set_edge"]
 
@@ -218,6 +218,10 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.pmvs_rccl_allgather.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
     lib.pmvs_rccl_allgather.restype = C.c_int
     lib.pmvs_scene_set_shard_rccl.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]
+    lib.pmvs_tcp_create.argtypes = [C.c_int32, C.c_int32, C.c_char_p, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]
+    lib.pmvs_tcp_allgather.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
+    lib.pmvs_tcp_destroy.argtypes = [C.c_void_p]
+    lib.pmvs_tcp_destroy.restype = None
     lib.pmvs_thread_exchange_create.argtypes = [C.c_int32]
     lib.pmvs_thread_exchange_create.restype = C.c_void_p
     lib.pmvs_thread_exchange_ctx.argtypes = [C.c_void_p, C.c_int32]
@@ -234,6 +238,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.pmvs_thread_exchange_create.restype = C.c_void_p
     lib.pmvs_thread_exchange_ctx.restype = C.c_void_p
     lib.pmvs_thread_exchange_destroy.restype = None
+    lib.pmvs_tcp_destroy.restype = None
     _lib = lib
     return lib
 
@@ -470,19 +475,22 @@ class Scene:
         _check(self.lib.pmvs_scene_set_cluster(self.handle, rank, world, _ptr(ids), ptr, ctx))
 
     def run_loop(self, seeds: np.ndarray, threshold: float, iterations: int = 3, wave: int = 4096, cap=None,
-                 after_seeds: bool = True, native: bool = True, min_candidates: int = 0):
+                 after_seeds: bool = True, native: bool = True, min_candidates: int = 0, max_waves: int = 0):
         """CFindMatch::run after the seed phase (findMatch.cpp:196-217): depth 1, then `iterations` x
         (CExpand::run, CFilter::run, updateThreshold, ++depth).  Thresholds follow the reference's
         float arithmetic: before = threshold - 0.3f (findMatch.cpp:104), -= 0.05f per iteration and
         _countThreshold1 4 -> 2 (findMatch.cpp:23-28).  native=True runs the whole loop in the
         library with the model resident in HBM (pmvs_run_loop); native=False composes expand_run
-        and filter_run through host memory (same result).  Returns (patches, per-iteration stats)."""
+        and filter_run through host memory (same result).  max_waves > 0 bounds every iteration's
+        expansion to that many waves (PMVS_EXPAND_MAX_WAVES: bounded full-size parity samples).
+        Returns (patches, per-iteration stats)."""
         model = np.ascontiguousarray(seeds, PATCH_DTYPE)
         if native:
             iters = (LoopIter * max(1, iterations))()
             n_out = C.c_int32(0)
             _check(self.lib.pmvs_run_loop(self.handle, _ptr(model), len(model), float(np.float32(threshold)),
-                                          iterations, wave, min_candidates, 1 if after_seeds else 0, int(cap or (1 << 30)),
+                                          iterations, wave, min_candidates,
+                                          (1 if after_seeds else 0) | (int(max_waves) << 8), int(cap or (1 << 30)),
                                           C.byref(n_out), iters))
             out = np.empty(n_out.value, PATCH_DTYPE)
             _check(self.lib.pmvs_loop_fetch(self.handle, _ptr(out), n_out.value))
@@ -494,7 +502,8 @@ class Scene:
         for t in range(iterations):
             self.set_thresholds(float(ncc), float(before), depth)
             model, alive, st_e = self.expand_run(model, wave=wave, count_threshold=cthr, cap=cap,
-                                                 after_seeds=after_seeds and t == 0, min_candidates=min_candidates)
+                                                 after_seeds=after_seeds and t == 0, min_candidates=min_candidates,
+                                                 max_waves=max_waves)
             model, keep, st_f = self.filter_run(model)
             model = model[keep == 1]
             log.append({"depth": depth, "expand": st_e, "filter": st_f, "patches": len(model)})

@@ -308,7 +308,9 @@ pmvs_status pmvs_expand_fetch(pmvs_scene* scene, pmvs_patch* out, int32_t* alive
  * model resident in HBM between the passes (only the final model crosses PCIe).  Thresholds as
  * the reference: depth 1 upwards, ncc = threshold and before = threshold - 0.3f, both -= 0.05f
  * and _countThreshold1 4 -> 2 after each iteration (findMatch.cpp:23-28, 104).  flags:
- * PMVS_EXPAND_AFTER_SEEDS for the first expansion.  cap bounds the model size.  *n_out = the final
+ * PMVS_EXPAND_AFTER_SEEDS for the first expansion; PMVS_EXPAND_MAX_WAVES(n) bounds every
+ * iteration's expansion to n waves (not a reference behaviour: full-size parity samples of the
+ * whole loop against the CPU oracle, which has the same bound).  cap bounds the model size.  *n_out = the final
  * model's size; pmvs_loop_fetch copies it out.  iters (may be NULL) receives per-iteration stats.
  * Collective when a shard is set. */
 typedef struct pmvs_loop_iter {
@@ -389,6 +391,17 @@ pmvs_status pmvs_scene_set_cluster(pmvs_scene* scene, int32_t rank, int32_t worl
                                    pmvs_allgather_fn fn, void* ctx);
 pmvs_status pmvs_scene_set_cluster_rccl(pmvs_scene* scene, int32_t rank, int32_t world, const int32_t* image_ids,
                                         pmvs_rccl* comm);
+
+/* A host all-gather over TCP among `world` processes (pmvs_hostcomm.cpp): rank 0 listens on addr:port,
+ * the other ranks connect (retrying until timeout_ms); pmvs_tcp_allgather is a pmvs_allgather_fn with
+ * ctx = the pmvs_tcp.  The multi-rank pmvs2 job's bootstrap (the RCCL unique id travels on it) and its
+ * exchange channel when the ranks share one GPU (PMVS_EXCHANGE=tcp).  A rank that exits closes its
+ * connection, so its peers' exchanges fail instead of blocking. */
+typedef struct pmvs_tcp pmvs_tcp;
+pmvs_status pmvs_tcp_create(int32_t rank, int32_t world, const char* addr, int32_t port, int32_t timeout_ms,
+                            pmvs_tcp** out);
+int pmvs_tcp_allgather(void* ctx, const void* send, int64_t bytes, void* recv);
+void pmvs_tcp_destroy(pmvs_tcp* comm);
 
 /* An in-process all-gather among `world` threads (one scene per thread, e.g. several scenes on
  * one GPU): pmvs_thread_allgather with ctx = pmvs_thread_exchange_ctx(group, rank). */

@@ -223,7 +223,7 @@ class OracleScene:
         return out[:m].copy(), alo[:m].copy(), stats
 
     def run_loop(self, seeds, threshold, iterations=3, wave=4096, cap=None, after_seeds=True, min_candidates=0,
-                 nthreads=1):
+                 nthreads=1, max_waves=0):
         """findMatch.cpp:196-217 after the seed phase, restated: returns (patches, per-iteration counts)."""
         ncc = np.float32(threshold)
         before = np.float32(ncc - np.float32(0.3))  # findMatch.cpp:104
@@ -234,7 +234,7 @@ class OracleScene:
             self.set_thresholds(float(ncc), float(before), depth)
             model, _, st_e = self.expand_run(model, wave=wave, count_threshold=cthr, cap=cap,
                                              after_seeds=after_seeds and t == 0, min_candidates=min_candidates,
-                                             nthreads=nthreads)
+                                             nthreads=nthreads, max_waves=max_waves)
             model, keep, counts = self.filter_run(model)
             model = model[keep == 1]
             log.append({"depth": depth, "expand": st_e, "filter": counts.tolist(), "patches": len(model)})

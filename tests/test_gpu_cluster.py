@@ -176,3 +176,74 @@ def test_cluster_exchange_single_rank_is_a_no_op(gpu_available):
     g.close()
     assert out.tobytes() == ref.tobytes()
     assert all(it["boundary"]["sent"] == 0 for it in log)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("where", ["x", "s"], ids=["after_expansion", "after_filter"])
+def test_cluster_local_failure_fails_all_ranks(gpu_available, monkeypatch, where):
+    """A failure local to one cluster rank (injected after its expansion, or after its filter pass,
+    as an asynchronous fault surfacing at the stream synchronisation would) is announced on the
+    cluster channel: every rank returns an error and none is left blocked in the boundary
+    exchange or the final loop header (the expansion / filter exchanges of a cluster
+    scene run at world 1, so their failures are never known to the peers)."""
+    import pmvs_amd as P
+    full, p = P.synth_scene(12, 320, 240, level=1, supersample=2, nthreads=8)
+    cands = P.synth_candidates(p, full.projections, 300, seed=13)
+    inps = [_cluster_scene(P, full, ids) for ids in CLUSTERS]
+    scenes = [P.Scene(inp) for inp in inps]
+    seeds = [_cluster_seeds(P, g, cands, ids) for g, ids in zip(scenes, CLUSTERS)]
+    monkeypatch.setenv("PMVS_TEST_SHARD_FAIL", f"1:0:{where}")
+    ex = P.ThreadExchange(len(CLUSTERS))
+    errs = [None] * len(CLUSTERS)
+
+    def work(r):
+        try:
+            scenes[r].set_cluster(r, len(CLUSTERS), CLUSTERS[r], *ex.endpoint(r))
+            scenes[r].run_loop(seeds[r], inps[r].threshold, cap=1 << 20, **PROD)
+        except P.PmvsError as e:
+            errs[r] = str(e)
+
+    th = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(len(CLUSTERS))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=200)
+    assert not any(t.is_alive() for t in th), "a rank is blocked after a peer's local failure"
+    for g in scenes:
+        g.close()
+    ex.close()
+    print(errs)
+    assert all(errs), errs
+    assert "injected" in errs[1]
+
+
+def test_cluster_setup_validation_fails_all_ranks(gpu_available):
+    """pmvs_scene_set_cluster validates after the collective: a rank with a bad image list (a
+    duplicate image number) makes every rank fail, instead of returning before the all-gather and
+    leaving its peers blocked in it."""
+    import pmvs_amd as P
+    full, p = P.synth_scene(8, 160, 120, level=1, supersample=1, nthreads=8)
+    ids = [[0, 1, 2, 3, 4], [4, 5, 6, 7, 0]]
+    inps = [_cluster_scene(P, full, c) for c in ids]
+    scenes = [P.Scene(inp) for inp in inps]
+    bad = [list(ids[0]), [4, 5, 6, 6, 0]]  # rank 1 names image 6 twice
+    ex = P.ThreadExchange(2)
+    errs = [None, None]
+
+    def work(r):
+        try:
+            scenes[r].set_cluster(r, 2, bad[r], *ex.endpoint(r))
+        except P.PmvsError as e:
+            errs[r] = str(e)
+
+    th = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=60)
+    assert not any(t.is_alive() for t in th), "cluster setup deadlock"
+    for g in scenes:
+        g.close()
+    ex.close()
+    assert errs[0] and errs[1], errs
+    assert "twice" in errs[1] and "rank 1" in errs[0], errs

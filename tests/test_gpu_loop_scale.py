@@ -1,9 +1,11 @@
 """The full expand -> optimise -> filter loop (pmvs_run_loop, CFindMatch::run after the seeds,
 findMatch.cpp:196-217) at the C3 view count.
 
-1. Parity: a 50-view ring (C3's view count and level 0, at 640x360 so the CPU oracle finishes in
-   tens of seconds) with the production schedule (wave 32768, min_candidates 131072, as bench.py
-   runs C3) equals the oracle's loop patch for patch.
+1. Parity: a 50-view ring (C3's view count and level 0) with the production schedule (wave 32768,
+   min_candidates 131072, as bench.py runs C3) equals the oracle's whole loop -- every wave of the
+   three expansions and all three filter passes -- patch for patch: the plain scene at 1920x1080
+   (about 1 M patches, a quarter of C3's cells per view) and the photometrically hard scene at
+   640x360.
 2. Schedule gap: the production schedule against wave = 1, the reference's single-thread
    (CPU 1) schedule (expand.cpp:17-72).  Wave = 1 is the schedule the reference
    produces when it is deterministic; the production schedule expands against start-of-wave
@@ -12,6 +14,7 @@ findMatch.cpp:196-217) at the C3 view count.
    the NCC distribution, with the tolerances below (DESIGN.md §6 records the measured values).
 """
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -19,6 +22,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 PROD = dict(wave=32768, min_candidates=131072)
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # bench.py
 # Schedule-gap tolerances (DESIGN.md §6 records the measured values):
 TOL_COUNT = 0.04          # |patches_prod / patches_ref - 1|
 TOL_WITHIN1 = 0.99        # covered target cells lying within one cell of the other run's coverage
@@ -51,14 +55,14 @@ def _seeds(g, cands):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("hard", [False, True], ids=["plain", "hard"])
-def test_loop_50_views_matches_oracle(gpu_available, oracle_mod, hard):
+@pytest.mark.parametrize("w,h,hard", [(1920, 1080, False), (640, 360, True)], ids=["plain_1080p", "hard_640x360"])
+def test_loop_50_views_matches_oracle(gpu_available, oracle_mod, w, h, hard):
     import pmvs_amd as P
-    from test_gpu_parity_matrix import _same_patches
-    inp, p, cands = _scene(50, 640, 360, 300, hard=hard)
+    from bench import patch_mismatches
+    inp, p, cands = _scene(50, w, h, 300, hard=hard)
     g = P.Scene(inp)
     seeds = _seeds(g, cands)
-    cap = 1 << 20
+    cap = (3 << 20) if w >= 1920 else (1 << 20)
     out_g, log_g = g.run_loop(seeds, inp.threshold, cap=cap, **PROD)
     g.close()
     o = oracle_mod.OracleScene(inp)
@@ -76,7 +80,7 @@ def test_loop_50_views_matches_oracle(gpu_available, oracle_mod, hard):
         assert {k: v for k, v in a["expand"].items() if k not in P.ExpandStats.WORK} == b["expand"]
         assert [a["filter"][k] for k in ("removed_outside", "removed_exact", "removed_neighbor",
                                          "removed_groups")] == b["filter"]
-    assert out_g.tobytes() == out_o.tobytes() or _same_patches(out_g, out_o)
+    assert out_g.tobytes() == out_o.tobytes() or patch_mismatches(out_g, out_o) == 0
 
 
 @pytest.mark.timeout(900)

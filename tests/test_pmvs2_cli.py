@@ -45,9 +45,59 @@ def test_genoption_gpu_script(product_lib, tmp_path):
     write_ske(tmp_path / "ske.dat", [([0, 1], [2]), ([2, 3], []), ([4], [5]), ([6], [])])
     subprocess.run([os.path.join(PKG, "genOption"), str(tmp_path) + "/", "--gpus", "2"], check=True)
     s = (tmp_path / "pmvs_gpus.sh").read_text()
-    assert "PMVS_DEVICE=0 pmvs2 pmvs/ option-0000 && PMVS_DEVICE=0 pmvs2 pmvs/ option-0002" in s
-    assert "PMVS_DEVICE=1 pmvs2 pmvs/ option-0001 && PMVS_DEVICE=1 pmvs2 pmvs/ option-0003" in s
+    # clusters in jobs of 2 ranks: {0, 1} on GPUs 0, 1, then {2, 3}; each job's ranks exchange
+    assert "MASTER_PORT=$((PORT+0)) WORLD_SIZE=2 RANK=0 LOCAL_RANK=0 pmvs2 pmvs/ option-0000 &" in s
+    assert "MASTER_PORT=$((PORT+0)) WORLD_SIZE=2 RANK=1 LOCAL_RANK=1 pmvs2 pmvs/ option-0001 &" in s
+    assert "MASTER_PORT=$((PORT+1)) WORLD_SIZE=2 RANK=1 LOCAL_RANK=1 pmvs2 pmvs/ option-0003 &" in s
+    assert s.index("option-0001") < s.index("wait $p") < s.index("option-0002")
     assert (tmp_path / "option-0003").exists() and (tmp_path / "pmvs.sh").exists()
+    # a job of one rank for an odd cluster count
+    write_ske(tmp_path / "ske.dat", [([0, 1], [2]), ([2, 3], []), ([4], [5])])
+    subprocess.run([os.path.join(PKG, "genOption"), str(tmp_path) + "/", "--gpus", "2"], check=True)
+    s = (tmp_path / "pmvs_gpus.sh").read_text()
+    assert "WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 pmvs2 pmvs/ option-0002 &" in s
+    assert subprocess.run(["sh", "-n", str(tmp_path / "pmvs_gpus.sh")]).returncode == 0
+
+
+def test_tcp_allgather_processes(product_lib, tmp_path):
+    """pmvs_tcp (the multi-rank pmvs2 job's host channel): three processes all-gather their blocks in
+    rank order, a size mismatch fails the exchange on every rank, and a rank that exits makes its
+    peers' next exchange fail instead of blocking."""
+    import socket
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    prog = f"""
+import ctypes as C, sys
+sys.path.insert(0, {os.path.join(ROOT, 'cmvs-pmvs_amd')!r})
+import pmvs_amd as P
+lib = P.load_library()
+rank, world = int(sys.argv[1]), 3
+h = C.c_void_p()
+assert lib.pmvs_tcp_create(rank, world, b"127.0.0.1", {port}, 20000, C.byref(h)) == 0, lib.pmvs_last_error()
+send = bytes([rank + 1] * 5)
+recv = C.create_string_buffer(15)
+assert lib.pmvs_tcp_allgather(h, send, 5, recv) == 0
+assert recv.raw == bytes([1] * 5 + [2] * 5 + [3] * 5), recv.raw
+n = 4 if rank == 2 else 5                      # rank 2 sends a different size: every rank fails
+assert lib.pmvs_tcp_allgather(h, send, n, recv) == -1
+assert lib.pmvs_tcp_allgather(h, send, 5, recv) == 0  # and the channel still works afterwards
+if rank == 1:
+    sys.exit(0)                                 # rank 1 leaves: the others' next exchange fails
+r = lib.pmvs_tcp_allgather(h, send, 5, recv)
+assert r == -1, r
+print("ok", rank)
+"""
+    f = tmp_path / "tcp_rank.py"
+    f.write_text(prog)
+    ps = [subprocess.Popen([sys.executable, str(f), str(r)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+          for r in range(3)]
+    outs = [p.communicate(timeout=60) for p in ps]
+    for r, (p, (o, e)) in enumerate(zip(ps, outs)):
+        assert p.returncode == 0, (r, o, e)
+    assert "ok 0" in outs[0][0] and "ok 2" in outs[2][0]
 
 
 def test_jpeg_matches_libjpeg(product_lib, tmp_path):
