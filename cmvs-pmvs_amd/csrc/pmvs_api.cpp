@@ -699,6 +699,7 @@ pmvs_status pmvs_seed_run(pmvs_scene* sc, const pmvs_point* points, const int32_
   in.spec_near = 2048;
   if (const char* e = getenv("PMVS_SEED_NEAR")) in.spec_near = std::max(1, atoi(e));
   HIPCHK(hipMemsetAsync(sc->stats.p, 0, sizeof(DevStats), sc->stream));
+  sc->rhost.prof = false;
   RefineFn refine = [&](const pmvs_candidate* d_in, int m, pmvs_refined* d_out) -> hipError_t {
     if (ensure(sc->jobs, m)) return hipErrorOutOfMemory;
     hipError_t e = hipMemsetAsync(&sc->stats.p->queue, 0, 3 * sizeof(unsigned long long), sc->stream);
@@ -1117,6 +1118,9 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
     pending = false;
   };
   HIPCHK(hipMemsetAsync(sc->stats.p, 0, sizeof(DevStats), sc->stream));
+  sc->rhost.prof = getenv("PMVS_EXPAND_PROFILE") != nullptr;
+  sc->rhost.trip_ms = 0.0;
+  sc->rhost.trips = 0;
   RefineFn refine = [&](const pmvs_candidate* d_in, int m, pmvs_refined* d_out) -> hipError_t {
     if (ensure(sc->jobs, m)) return hipErrorOutOfMemory;
     take_time();
@@ -1151,6 +1155,9 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   DevStats ds{};
   HIPCHK(hipMemcpy(&ds, sc->stats.p, sizeof(DevStats), hipMemcpyDeviceToHost));
+  if (sc->rhost.prof)
+    fprintf(stderr, "[refine round trip] batches=%lld device_ms=%.1f (pre_kernel end -> refine start: start points "
+                    "down, host libm asin/acos, angles up)\n", sc->rhost.trips, sc->rhost.trip_ms);
   if (getenv("PMVS_REFINE_TAIL"))  // diagnostics: the refine launches' tails (s_memrealtime: 100 MHz)
     for (int f = 0; f < 2; ++f)
       if (ds.tail_launches[f])

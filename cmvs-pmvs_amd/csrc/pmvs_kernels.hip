@@ -1822,6 +1822,8 @@ hipError_t RefineHost::ensure(size_t n) {
   return e;
 }
 void RefineHost::release() {
+  if (ev_pre) (void)hipEventDestroy(ev_pre);
+  ev_pre = nullptr;
   if (d_enc) (void)hipFree(d_enc);
   if (d_ang) (void)hipFree(d_ang);
   if (h_enc) (void)hipHostFree(h_enc);
@@ -1857,6 +1859,7 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
   if (e != hipSuccess) return e;
   (void)hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL((pre_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_in, d_jobs, rh.d_enc, n, d_st);
+  if (rh.prof && (rh.ev_pre || hipEventCreate(&rh.ev_pre) == hipSuccess)) (void)hipEventRecord(rh.ev_pre, stream);
   // the start point's angles with the host's libm (encode_angles_host): one round trip per batch
   if ((e = hipMemcpyAsync(rh.h_enc, rh.d_enc, (size_t)n * sizeof(float4), hipMemcpyDeviceToHost, stream)) != hipSuccess ||
       (e = hipStreamSynchronize(stream)) != hipSuccess)
@@ -1866,6 +1869,11 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
     return e;
   hipLaunchKernelGGL(angles_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_jobs, rh.d_ang, rh.d_enc, n);
   (void)hipEventRecord(ev[1], stream);
+  if (rh.prof && rh.ev_pre && hipEventSynchronize(ev[1]) == hipSuccess) {  // diagnostics only: one more wait
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, rh.ev_pre, ev[1]) == hipSuccess) rh.trip_ms += ms;
+    ++rh.trips;
+  }
   // a request's textures must fit one chunk (TSLOTS >= tau, tau <= PMVS_MAX_TAU = 16): smaller
   // chunk configs are only valid for small tau, otherwise the default 24-slot kernel runs
   if (tslots / 100 < s.tau) {

@@ -27,6 +27,12 @@ struct RefineHost {
   float4* h_enc = nullptr;   // pinned
   double2* h_ang = nullptr;  // pinned
   size_t cap = 0;
+  // PMVS_EXPAND_PROFILE: the round trip's share of the device timeline (pre_kernel's end to the
+  // refine kernel's start: start points down, host libm, angles up), summed over the batches
+  bool prof = false;
+  hipEvent_t ev_pre = nullptr;
+  double trip_ms = 0.0;
+  long long trips = 0;
   hipError_t ensure(size_t n);
   void release();
   ~RefineHost() { release(); }

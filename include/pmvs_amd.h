@@ -376,8 +376,10 @@ pmvs_status pmvs_scene_set_shard_rccl(pmvs_scene* scene, int32_t rank, int32_t w
  * (bundle.cpp:1003-1160, ske.dat).  With a cluster set, pmvs_run_loop on this scene (one rank of
  * `world`, one scene per GPU) all-gathers after every iteration but the last, through `fn` (or the
  * native RCCL communicator, device to device), the patches it holds in target images that another
- * rank also has as targets -- a {error, count} header per rank first (the images' visibility counts),
- * then the records with image NUMBERS.  Every rank inserts the other ranks' records whose reference
+ * rank also has as targets -- a {error, record count} header per rank first, then the records with
+ * image NUMBERS.  (CExpand's per-cell _counts are not exchanged: every expansion run starts by clearing
+ * them, expand.cpp:32, and the exchange happens between runs; the inserted patches carry the cell
+ * occupancy the next run's checkCounts reads.)  Every rank inserts the other ranks' records whose reference
  * image is one of its views as the reference's readPatches inserts another run's patches
  * (patchOrganizerS.cpp:133-197: image numbers mapped to indexes, _vimages cleared, setGrids, addPatch),
  * as fixed patches that are never expanded (fix = PMVS_FIX_FOREIGN): they fill their cells, so the

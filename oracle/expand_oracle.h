@@ -42,7 +42,8 @@ static void model_load(Model& m, std::vector<FPatch>& P, const std::vector<int>&
     if (alive[p]) add_patch_p(m.o, P, p);
   collect_patches(m.o, P, 0);
   if (depth_maps) set_depth_maps(m.o, P);  // none after the seed phase (addPatch at depth 0)
-  for (int t = 0; t < m.s.tnum; ++t)
+  parallel_for(g_threads, (size_t)m.s.tnum, [&](int, size_t tt) {  // one target image per job
+    const int t = (int)tt;
     for (int p : m.o.ppatches) {
       const FPatch& q = P[p];
       for (size_t i = 0; i < q.vimages.size(); ++i)
@@ -52,6 +53,7 @@ static void model_load(Model& m, std::vector<FPatch>& P, const std::vector<int>&
           break;
         }
     }
+  });
 }
 
 // CPatchOrganizerS::updateDepthMaps (patchOrganizerS.cpp:348-381).

@@ -84,18 +84,27 @@ static void remove_patch(Organizer& o, const std::vector<FPatch>& P, int p) {
   }
 }
 
-// CPatchOrganizerS::collectPatches(target) (patchOrganizerS.cpp:218-248).
+template <class F>
+static void parallel_for(int nthreads, size_t n, F&& f);
+static int g_threads = 1;
+
+// CPatchOrganizerS::collectPatches(target) (patchOrganizerS.cpp:218-248).  The cell walk of each
+// target image runs in parallel (its entries in cell order); the first-occurrence numbering then
+// walks those entries in target order, as the serial walk does.
 static void collect_patches(Organizer& o, std::vector<FPatch>& P, int target) {
   o.ppatches.clear();
   for (auto& q : P) q.id = -1;
+  std::vector<std::vector<int>> ent(o.s.tnum);
+  parallel_for(g_threads, (size_t)o.s.tnum, [&](int, size_t t) {
+    for (auto& cellv : o.pgrids[t]) ent[t].insert(ent[t].end(), cellv.begin(), cellv.end());
+  });
   int count = 0;
   for (int t = 0; t < o.s.tnum; ++t)
-    for (auto& cellv : o.pgrids[t])
-      for (int p : cellv)
-        if (P[p].id == -1) {
-          P[p].id = count++;
-          if (target == 0 || P[p].fix == 0) o.ppatches.push_back(p);
-        }
+    for (int p : ent[t])
+      if (P[p].id == -1) {
+        P[p].id = count++;
+        if (target == 0 || P[p].fix == 0) o.ppatches.push_back(p);
+      }
 }
 
 static inline float depth_of(const OScene& s, int t, const V4& c) { return dot4(s.views[t].oaxis, c); }
@@ -103,7 +112,8 @@ static inline float depth_of(const OScene& s, int t, const V4& c) { return dot4(
 // CFilter::setDepthMaps / setDepthMapsThread (filter.cpp:668-725).
 static void set_depth_maps(Organizer& o, const std::vector<FPatch>& P) {
   const OScene& s = o.s;
-  for (int t = 0; t < s.tnum; ++t) {
+  parallel_for(g_threads, (size_t)s.tnum, [&](int, size_t tt) {  // setDepthMapsThread: one image per job
+    const int t = (int)tt;
     std::fill(o.dpgrids[t].begin(), o.dpgrids[t].end(), -1);
     for (int p : o.ppatches) {
       const V3 ic = project(s, t, P[p].coord, s.level);
@@ -119,7 +129,7 @@ static void set_depth_maps(Organizer& o, const std::vector<FPatch>& P) {
           else if (depth < depth_of(s, t, P[d].coord)) d = p;
         }
     }
-  }
+  });
 }
 
 // CPatchOrganizerS::isVisible (patchOrganizerS.cpp:500-525).
@@ -160,7 +170,6 @@ static void set_vimages_vgrids(const Organizer& o, const std::vector<FPatch>& P,
 // Thread pool for the per-patch stages (the reference runs them on _CPU threads, filter.cpp:
 // filterOutsideThread / filterExactThread / filterNeighborThread / setVImagesVGrids threads).  Each
 // task writes only its own slot, so results do not depend on the thread count.
-static int g_threads = 1;
 template <class F>
 static void parallel_for(int nthreads, size_t n, F&& f) {
   if (nthreads <= 1 || n < 2) {
@@ -186,15 +195,17 @@ static void parallel_for(int nthreads, size_t n, F&& f) {
 static void set_dm_vgrids(Organizer& o, std::vector<FPatch>& P, int additive) {
   collect_patches(o, P, 0);
   set_depth_maps(o, P);
-  for (auto& img : o.vpgrids)
-    for (auto& c : img) c.clear();
+  parallel_for(g_threads, o.vpgrids.size(), [&](int, size_t t) {
+    for (auto& c : o.vpgrids[t]) c.clear();
+  });
   if (additive == 0)
     for (int p : o.ppatches) {
       P[p].vimages.clear();
       P[p].vgrids.clear();
     }
   parallel_for(g_threads, o.ppatches.size(), [&](int, size_t k) { set_vimages_vgrids(o, P, P[o.ppatches[k]]); });
-  for (int t = 0; t < o.s.tnum; ++t)  // addPatchVThread: first matching entry only
+  parallel_for(g_threads, (size_t)o.s.tnum, [&](int, size_t tt) {  // addPatchVThread: one image per job,
+    const int t = (int)tt;                                         // first matching entry only
     for (int p : o.ppatches) {
       const FPatch& q = P[p];
       for (size_t i = 0; i < q.vimages.size(); ++i)
@@ -203,6 +214,7 @@ static void set_dm_vgrids(Organizer& o, std::vector<FPatch>& P, int additive) {
           break;
         }
     }
+  });
 }
 
 // CFindMatch::isNeighbor / isNeighborRadius (findMatch.cpp:125-185).
@@ -740,19 +752,38 @@ static int filter_small_groups(Organizer& o, std::vector<FPatch>& P) {
 
 // CFilter::run (filter.cpp:13-27).  counts[0..3] = removed by outside/exact/neighbor/groups.
 static void filter_run(const OScene& s, std::vector<FPatch>& P, std::vector<int>& keep, int counts[4]) {
+  // ORACLE_PROFILE=1: wall time of each stage on stderr (diagnostics of the checker's own cost)
+  const bool prof = getenv("ORACLE_PROFILE") != nullptr;
+  auto t = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    if (!prof) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[oracle filter] %s %.2f s\n", what, std::chrono::duration<double>(now - t).count());
+    t = now;
+  };
   Organizer o(s);
   std::vector<OCtx> ctxs(std::max(1, g_threads));
   for (auto& c : ctxs) init_ctx(s, c);
   for (int p = 0; p < (int)P.size(); ++p) add_patch_p(o, P, p);
+  mark("organizer");
   set_dm_vgrids(o, P, 0);
+  mark("set_dm_vgrids");
   counts[0] = filter_outside(o, P);
+  mark("outside");
   set_dm_vgrids(o, P, 1);
+  mark("set_dm_vgrids");
   counts[1] = filter_exact(o, P, ctxs);
+  mark("exact");
   set_dm_vgrids(o, P, 1);
+  mark("set_dm_vgrids");
   counts[2] = filter_neighbor(o, P);
+  mark("neighbor");
   set_dm_vgrids(o, P, 1);
+  mark("set_dm_vgrids");
   counts[3] = filter_small_groups(o, P);
+  mark("groups");
   set_dm_vgrids(o, P, 1);
+  mark("set_dm_vgrids");
   collect_patches(o, P, 0);
   keep.assign(P.size(), 0);
   for (int p : o.ppatches) keep[p] = 1;

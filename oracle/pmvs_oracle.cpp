@@ -21,6 +21,8 @@
 #include <climits>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -1179,7 +1181,7 @@ void oracle_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
 void oracle_filter_run(void* h, pmvs_patch* patches, int n, int* keep, int* counts) {
   const OScene& s = *static_cast<const OScene*>(h);
   std::vector<FPatch> P(n);
-  for (int i = 0; i < n; ++i) {
+  parallel_for(g_threads, (size_t)n, [&](int, size_t i) {
     const pmvs_patch& a = patches[i];
     FPatch& q = P[i];
     for (int k = 0; k < 4; ++k) { q.coord[k] = a.coord[k]; q.normal[k] = a.normal[k]; }
@@ -1187,10 +1189,11 @@ void oracle_filter_run(void* h, pmvs_patch* patches, int n, int* keep, int* coun
     q.timages = a.timages; q.flag = a.flag; q.fix = a.fix; q.dflag = a.dflag;
     for (int k = 0; k < a.num_images; ++k) { q.images.push_back(a.images[k]); q.grids.push_back({a.grids[k][0], a.grids[k][1]}); }
     for (int k = 0; k < a.num_vimages; ++k) { q.vimages.push_back(a.vimages[k]); q.vgrids.push_back({a.vgrids[k][0], a.vgrids[k][1]}); }
-  }
+  });
   std::vector<int> kp;
   filter_run(s, P, kp, counts);
-  for (int i = 0; i < n; ++i) {
+  parallel_for(g_threads, (size_t)n, [&](int, size_t ii) {
+    const int i = (int)ii;
     pmvs_patch& a = patches[i];
     const FPatch& q = P[i];
     a.timages = q.timages;
@@ -1204,7 +1207,7 @@ void oracle_filter_run(void* h, pmvs_patch* patches, int n, int* keep, int* coun
       a.vimages[k] = (int16_t)q.vimages[k]; a.vgrids[k][0] = cell16(q.vgrids[k].first); a.vgrids[k][1] = cell16(q.vgrids[k].second);
     }
     keep[i] = kp[i];
-  }
+  });
 }
 
 // Diagnostic: filterNeighbor's neighbour-list sizes (raw with duplicates, unique) on the
@@ -1262,16 +1265,23 @@ int oracle_expand_run(void* h, const pmvs_patch* patches, const int* alive, int 
                       int min_cands, pmvs_patch* out, int* alive_out, int cap, int64_t* stats, int nthreads,
                       int64_t max_waves) {
   const OScene& s = *static_cast<const OScene*>(h);
+  // the organizer's per-target loops (collect, depth maps, vpgrids) use the same pool size
+  const int saved = g_threads;
+  g_threads = std::max(g_threads, nthreads);
   std::vector<FPatch> P(n);
   std::vector<int> al(alive, alive + n);
-  for (int i = 0; i < n; ++i) to_fpatch(patches[i], P[i]);
+  parallel_for(g_threads, (size_t)n, [&](int, size_t i) { to_fpatch(patches[i], P[i]); });
   ExpandStats st;
   expand_run(s, P, al, wave, cthr, flags, st, min_cands, nthreads, max_waves);
-  if ((int)P.size() > cap) return -1;
-  for (size_t i = 0; i < P.size(); ++i) {
+  if ((int)P.size() > cap) {
+    g_threads = saved;
+    return -1;
+  }
+  parallel_for(g_threads, P.size(), [&](int, size_t i) {
     from_fpatch(P[i], out[i]);
     alive_out[i] = al[i];
-  }
+  });
+  g_threads = saved;
   const int64_t v[9] = {st.parents, st.candidates, st.fail_prep, st.fail_pre, st.fail_post, st.fail_commit, st.added,
                         st.waves, st.wave_ns};
   for (int k = 0; k < 9; ++k) stats[k] = v[k];

@@ -14,6 +14,56 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
     config.addinivalue_line("markers", "slow: longer CPU tests")
+    _Heartbeat.start()
+
+
+class _Heartbeat:
+    """A line every 50 s while one test runs longer than that (the full-size parity tests run for
+    minutes): on the session's own stderr, which pytest's capture does not redirect, and appended to
+    gpurun_out/heartbeat.txt on the GPU box -- a command that prints nothing for minutes is taken
+    for a hung one there."""
+    current = None
+    since = 0.0
+
+    @classmethod
+    def start(cls):
+        import threading
+        import time
+        try:
+            fd = os.dup(2)
+        except OSError:
+            return
+        out = None
+        root = os.environ.get("GRAFT_REPO_ROOT")
+        if root:
+            os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+            out = os.path.join(root, "gpurun_out", "heartbeat.txt")
+
+        def run():
+            while True:
+                time.sleep(50)
+                cur, t0 = cls.current, cls.since
+                if cur is None or time.time() - t0 < 45:
+                    continue
+                line = f"[heartbeat] {cur}: {time.time() - t0:.0f} s\n"
+                try:
+                    os.write(fd, line.encode())
+                    if out:
+                        with open(out, "a") as f:
+                            f.write(line)
+                except OSError:
+                    pass
+
+        threading.Thread(target=run, daemon=True).start()
+
+
+def pytest_runtest_logstart(nodeid, location):
+    import time
+    _Heartbeat.current, _Heartbeat.since = nodeid, time.time()
+
+
+def pytest_runtest_logfinish(nodeid, location):
+    _Heartbeat.current = None
 
 
 def _newest(paths):
