@@ -343,11 +343,15 @@ __device__ __forceinline__ long long xcd_block() {
 // setDepthMaps: one thread per (target, collected patch), target-major so that neighbouring
 // threads hold neighbouring patches (collect order is by image and cell) and their atomics hit
 // nearby cells of the same map.
+// Owner-partitioned filter pass (world > 1): only the targets rank owns (t = rank + world j) -- the
+// other targets' maps are never read on this rank (its visibility tests are its own targets').
 __global__ void depth_map_kernel(DScene s, FilterDev F, const float4* __restrict__ coordc,
-                                 unsigned long long* __restrict__ dpkey) {
+                                 unsigned long long* __restrict__ dpkey, int rank = 0, int world = 1) {
   const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // hardware order (r03k3: the XCD
-  if (g >= (long long)F.nalive * F.tnum) return;                           // order made it 7.9 -> 10.6 ms)
-  const int t = (int)(g / F.nalive), i = (int)(g - (long long)t * F.nalive);
+  const int nown = (F.tnum - rank + world - 1) / world;                   // order made it 7.9 -> 10.6 ms)
+  if (g >= (long long)F.nalive * nown) return;
+  const int j = (int)(g / F.nalive), i = (int)(g - (long long)j * F.nalive);
+  const int t = rank + world * j;
   const float4 c4 = coordc[i];
   const float coord[4] = {c4.x, c4.y, c4.z, c4.w};
   const DView& v = s.views[t];
@@ -402,15 +406,79 @@ __global__ void vimages_kernel(DScene s, FilterDev F, int additive, Reg* __restr
   vreg[p] = reg_first(q.num_vimages);
 }
 
+// setVImagesVGrids, owner-partitioned (world > 1): the visibility of collected patch i
+// in the targets this rank owns (t = rank + world j, j < nown), as bit j of bits[i * W ..].  Every rank
+// then builds the lists from all ranks' bits (vis_merge_kernel), in target order as vimages_kernel.
+__global__ void vis_bits_kernel(DScene s, FilterDev F, int additive, int rank, int world, int W,
+                                unsigned* __restrict__ bits) {
+  const int i = (int)(xcd_block() * blockDim.x + threadIdx.x);
+  if (i >= F.nalive) return;
+  const int p = F.order[i];
+  const pmvs_patch& q = F.P[p];
+  unsigned long long used[PMVS_MAX_TARGETS / 64] = {};
+  for (int k = 0; k < q.num_images; ++k)
+    if (q.images[k] < s.tnum) used[q.images[k] >> 6] |= 1ull << (q.images[k] & 63);
+  if (additive)
+    for (int k = 0; k < q.num_vimages; ++k) used[q.vimages[k] >> 6] |= 1ull << (q.vimages[k] & 63);
+  unsigned* out = bits + (size_t)i * W;
+  for (int w = 0; w < W; ++w) out[w] = 0u;
+  for (int t = rank, j = 0; t < s.tnum; t += world, ++j) {
+    if (used[t >> 6] & (1ull << (t & 63))) continue;
+    const DView& v = s.views[t];
+    float ic[3];
+    project(v, q.coord, s.level, ic);
+    const int ix = ((int)floorf(ic[0] + 0.5f)) / s.csize;
+    const int iy = ((int)floorf(ic[1] + 0.5f)) / s.csize;
+    if (is_visible(s, F, p, t, ix, iy, 0.5f) == 0) continue;
+    if (get_edge(s, v, q.coord, s.level) == 0) continue;
+    out[j >> 5] |= 1u << (j & 31);
+  }
+}
+
+// The vimages lists from every rank's visibility bits (all: world blocks of nalive * W words).
+__global__ void vis_merge_kernel(DScene s, FilterDev F, int additive, int world, int W,
+                                 const unsigned* __restrict__ all, Reg* __restrict__ vreg) {
+  const int i = (int)(xcd_block() * blockDim.x + threadIdx.x);
+  if (i >= F.nalive) return;
+  const int p = F.order[i];
+  pmvs_patch& q = F.P[p];
+  if (!additive) q.num_vimages = 0;
+  const size_t stride = (size_t)F.nalive * W;
+  for (int t = 0; t < s.tnum; ++t) {
+    const int r = t % world, j = t / world;
+    if (!((all[(size_t)r * stride + (size_t)i * W + (j >> 5)] >> (j & 31)) & 1u)) continue;
+    float ic[3];
+    project(s.views[t], q.coord, s.level, ic);
+    if (q.num_vimages >= PMVS_MAX_IMAGES) {
+      atomicAdd(F.lovf, 1);
+      break;
+    }
+    q.vimages[q.num_vimages] = (int16_t)t;
+    q.vgrids[q.num_vimages][0] = grid16(((int)floorf(ic[0] + 0.5f)) / s.csize);
+    q.vgrids[q.num_vimages][1] = grid16(((int)floorf(ic[1] + 0.5f)) / s.csize);
+    q.num_vimages++;
+  }
+  vreg[p] = reg_first(q.num_vimages);
+}
+
+__global__ void or_bits_kernel(const unsigned* __restrict__ all, int world, size_t words, unsigned* __restrict__ out) {
+  const size_t w = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= words) return;
+  unsigned v = 0u;
+  for (int r = 0; r < world; ++r) v |= all[(size_t)r * words + w];
+  out[w] = v;
+}
+
 // --------------------------------------------------------------------------- filterOutside
-// CFilter::filterOutsideThread (filter.cpp:148-201), neighbourThreshold1 = 1.0.
-__global__ void gain_kernel(DScene s, FilterDev F, int* __restrict__ remove) {
+// CFilter::filterOutsideThread (filter.cpp:148-201), neighbourThreshold1 = 1.0.  Owner-partitioned
+// (world > 1): the patches whose reference image this rank owns; the flags are all-gathered.
+__global__ void gain_kernel(DScene s, FilterDev F, int* __restrict__ remove, int rank = 0, int world = 1) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= F.nalive) return;
   const int p = F.order[i];
   const pmvs_patch& q = F.P[p];
   remove[p] = 0;
-  if (q.fix) return;
+  if (q.fix || q.images[0] % world != rank) return;
   float gain = smax(0.0f, q.ncc - s.nccThreshold) * (float)q.timages;
   for (int k = 0; k < q.num_images; ++k) {
     const int t = q.images[k];
@@ -459,13 +527,17 @@ __global__ void apply_remove_kernel(int n, const int* __restrict__ remove, Reg* 
 // --------------------------------------------------------------------------- filterExact
 // filterExactThread (filter.cpp:291-340): one thread per registered pgrids entry; marks the
 // patch's images[] positions that are safe (visible at the cell or one of its 4 neighbours).
-__global__ void exact_entries_kernel(DScene s, FilterDev F, long long ncells, Reg* __restrict__ safe) {
+// Owner-partitioned (world > 1): the cells of the targets this rank owns; the safe bits are OR-merged
+// over the ranks afterwards.
+__global__ void exact_entries_kernel(DScene s, FilterDev F, long long ncells, Reg* __restrict__ safe, int rank = 0,
+                                     int world = 1) {
   const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= ncells) return;
   const int b = F.pg_off[c], e = F.pg_off[c + 1];
   if (b == e) return;
   int t = 0;
   while (F.tgoff[t + 1] <= c) ++t;
+  if (t % world != rank) return;
   const int gw = gwidth(s, t), h = gheight(s, t);
   const long long local = c - F.tgoff[t];
   const int y = (int)(local / gw), x = (int)(local - (long long)y * gw);
@@ -1944,7 +2016,7 @@ static hipError_t dalloc(T*& p, size_t n) {
 FilterBuffers::~FilterBuffers() {
   void* ps[] = {preg, vreg, tgoff, cnt, off, keys, keys2, cellcnt, pg_off, pg_items, vp_off, vp_items, dpkey,
                 order, rank, hot, flags, safe, need, list, scratch, counters, temp, edge_off, edges, rbits, coordc,
-                qf, qrows, qjobs, qctr, qkeys, qkeys2, qcrows, qoff};
+                qf, qrows, qjobs, qctr, qkeys, qkeys2, qcrows, qoff, vbits, refpos, xr};
   for (void* p : ps)
     if (p) (void)hipFree(p);
 }
@@ -2016,7 +2088,19 @@ hipError_t FilterBuffers::ensure_entries(size_t e, int vis) {
   return hipSuccess;
 }
 
+template <class T>
+static hipError_t fgrow(T*& p, size_t& cap, size_t need) {  // grown, contents not kept
+  if (need <= cap && p) return hipSuccess;
+  need = std::max(need, cap + cap / 4);
+  FCHK(dalloc(p, need));
+  cap = need;
+  return hipSuccess;
+}
+
 namespace {
+
+// All-gather of one owner-partitioned filter stage (see filter_pass_impl).
+using FilterXchg = std::function<hipError_t(int value, const void* dsend, size_t bytes, void* drecv, long long* vsum)>;
 
 struct Ctx {
   const DScene& s;
@@ -2026,6 +2110,8 @@ struct Ctx {
   long long ncells;
   int grid;
   hipStream_t st;
+  int rank = 0, world = 1;  // owner partition of the target images (world > 1: xchg is set)
+  FilterXchg xchg;
   int nalive = 0, npg = 0, nvp = 0;
   const int *pg_dhead = nullptr, *vp_dhead = nullptr, *d_item = nullptr, *d_next = nullptr;
   const float4* coordc = nullptr;
@@ -2175,13 +2261,30 @@ static hipError_t set_dm_vgrids(Ctx& c, int additive) {
   FCHK(memset_big(B.dpkey, 0xff, c.ncells * sizeof(unsigned long long), c.st));
   if (c.nalive > 0)
     hipLaunchKernelGGL(coordc_kernel, dim3(nblk(c.nalive)), dim3(256), 0, c.st, c.P, B.order, c.nalive, B.coordc);
-  if (c.nalive > 0)
-    hipLaunchKernelGGL(depth_map_kernel, dim3(nblk((long long)c.nalive * c.s.tnum)), dim3(256), 0, c.st, c.s, c.dev(), B.coordc,
-                       B.dpkey);
+  // owner-partitioned: this rank's targets only (t = rank + world j)
+  const int nown = (c.s.tnum - c.rank + c.world - 1) / c.world;
+  if (c.nalive > 0 && nown > 0)
+    hipLaunchKernelGGL(depth_map_kernel, dim3(nblk((long long)c.nalive * nown)), dim3(256), 0, c.st, c.s, c.dev(), B.coordc,
+                       B.dpkey, c.rank, c.world);
   dbg(c.st, "  depth");
   FCHK(hipMemsetAsync(B.vreg, 0, c.n * sizeof(Reg), c.st));
-  if (c.nalive > 0)
+  if (c.world > 1) {
+    // setVImagesVGrids by target owner: each rank tests its targets, the bits are all-gathered and
+    // every rank appends the visible targets in target order (vis_merge_kernel)
+    const int W = ((c.s.tnum + c.world - 1) / c.world + 31) / 32;
+    const size_t words = (size_t)c.nalive * W;
+    FCHK(fgrow(B.vbits, B.cap_vbits, std::max(words, (size_t)1)));
+    FCHK(fgrow(B.xr, B.cap_xr, std::max(words, (size_t)1) * 4 * c.world));
+    if (c.nalive > 0)
+      hipLaunchKernelGGL(vis_bits_kernel, dim3(xcd_grid(c.nalive)), dim3(256), 0, c.st, c.s, c.dev(), additive, c.rank,
+                         c.world, W, B.vbits);
+    FCHK(c.xchg(0, B.vbits, words * 4, B.xr, nullptr));
+    if (c.nalive > 0)
+      hipLaunchKernelGGL(vis_merge_kernel, dim3(xcd_grid(c.nalive)), dim3(256), 0, c.st, c.s, c.dev(), additive, c.world, W,
+                         reinterpret_cast<const unsigned*>(B.xr), B.vreg);
+  } else if (c.nalive > 0) {
     hipLaunchKernelGGL(vimages_kernel, dim3(xcd_grid(c.nalive)), dim3(256), 0, c.st, c.s, c.dev(), additive, B.vreg);
+  }
   dbg(c.st, "  vimages");
   FCHK(build_lists(c, 1));
   dbg(c.st, "  vlists");
@@ -2198,13 +2301,28 @@ static hipError_t apply_flags(Ctx& c, int* removed) {
 
 }  // namespace
 
+// Owner-partitioned pass (sh->world > 1): rank g owns the target images t with
+// t mod world = g and the patches whose reference image it owns.  The per-target stages run on the
+// owner and their results are all-gathered, so every rank ends the pass with the same model:
+//   setDepthMaps          the owned targets' maps only (no other rank reads them);
+//   setVImagesVGrids      visibility bits in the owned targets -> all-gather -> every rank appends the
+//                         visible targets in target order (5 times per pass);
+//   filterOutside         gains of the owned patches -> reject bits all-gathered;
+//   filterExact           isVisible over the owned targets' cells -> safe bits all-gathered (OR);
+//                         setRefImage of the owned patches -> the chosen swap all-gathered;
+//   filterNeighbor        the owned patches' neighbour walks and fits -> reject bits all-gathered;
+//   filterSmallGroups     replicated (O(edges) label fixpoint).
+// Every exchange is an 8-byte header {error, value} all-gathered first, then (all fine) the payload,
+// device to device over RCCL when the shard has it.  A rank that fails between exchanges leaves the
+// pass and sends one header with its error (filter_pass), which its peers receive at their next
+// header -- this pass's next exchange, or the loop's next one -- so every rank returns the error.
 static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n, long long ncells,
                                    const long long* h_tgoff, int grid, hipStream_t st, int counts[4], int* overflow,
-                                   int* keep_dev, const Shard* sh, int& phase) {
+                                   int* keep_dev, const Shard* sh, bool& agreed) {
   const bool part = sh && sh->world > 1;
-  phase = 0;  // 0: before the flag exchange, 1: at it (every rank sees the outcome), 2: after it
+  agreed = false;
   // test hook (tests/test_gpu_expand.py): PMVS_TEST_SHARD_FAIL="rank:0:f|g" fails that rank's
-  // filter pass before (f) or after (g) its flag exchange
+  // filter pass before (f) or after (g) its filterNeighbor exchange
   int inj_rank = -1, inj_wave = -1;
   char inj_where = 0;
   if (const char* e = getenv("PMVS_TEST_SHARD_FAIL")) (void)sscanf(e, "%d:%d:%c", &inj_rank, &inj_wave, &inj_where);
@@ -2215,6 +2333,51 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
   FCHK(hipMemcpyAsync(B.tgoff, h_tgoff, (s.tnum + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
   Ctx c{s, B, dP, n, ncells, grid, st};
   c.coordc = B.coordc;  // written with every depth map of this pass (set_dm_vgrids)
+  const int G = part ? sh->world : 1, R = part ? sh->rank : 0;
+  if (part) {
+    c.rank = R;
+    c.world = G;
+    c.xchg = [&](int value, const void* dsend, size_t bytes, void* drecv, long long* vsum) -> hipError_t {
+      int h[2] = {0, value};
+      std::vector<int> all(2 * (size_t)G, 0);
+      agreed = true;  // a failure from here to the payload's end is every rank's
+      if (sh->exchange(h, sizeof(h), all.data()) != 0) return hipErrorUnknown;
+      long long sum = 0;
+      for (int r = 0; r < G; ++r) {
+        if (all[2 * r] != 0) return hipErrorUnknown;  // a peer failed since the last exchange
+        sum += all[2 * r + 1];
+      }
+      if (vsum) *vsum = sum;
+      if (bytes) {
+        if (sh->exchange_dev) {
+          if (sh->exchange_dev(dsend, bytes, drecv, st) != 0) return hipErrorUnknown;
+        } else {
+          std::vector<char> hs(bytes), hr(bytes * G);
+          FCHK(hipMemcpyAsync(hs.data(), dsend, bytes, hipMemcpyDeviceToHost, st));
+          FCHK(hipStreamSynchronize(st));
+          if (sh->exchange(hs.data(), bytes, hr.data()) != 0) return hipErrorUnknown;
+          FCHK(hipMemcpyAsync(drecv, hr.data(), bytes * G, hipMemcpyHostToDevice, st));
+          FCHK(hipStreamSynchronize(st));
+        }
+      }
+      agreed = false;
+      return hipSuccess;
+    };
+  }
+  // flags[0, n) of the patches this rank decided -> every rank's, OR-merged (one exchange)
+  auto merge_flags = [&](int value, long long* vsum) -> hipError_t {
+    const size_t nw = (size_t)(n + 31) / 32;
+    FCHK(fgrow(B.rbits, B.cap_rbits, nw + 1));
+    FCHK(fgrow(B.xr, B.cap_xr, (nw + 1) * 4 * G));
+    if (nw) hipLaunchKernelGGL(pack_bits_kernel, dim3(nblk((long long)nw)), dim3(256), 0, st, B.flags, n, B.rbits);
+    FCHK(c.xchg(value, B.rbits, nw * 4, B.xr, vsum));
+    if (nw) {
+      hipLaunchKernelGGL(or_bits_kernel, dim3(nblk((long long)nw)), dim3(256), 0, st, reinterpret_cast<const unsigned*>(B.xr),
+                         G, nw, B.rbits);
+      hipLaunchKernelGGL(unpack_bits_kernel, dim3(nblk(n)), dim3(256), 0, st, B.rbits, n, B.flags);
+    }
+    return hipGetLastError();
+  };
   for (int k = 0; k < 4; ++k) counts[k] = 0;
   *overflow = 0;
   FCHK(hipMemsetAsync(B.counters + 8, 0, sizeof(int), st));  // vimages list overflows (vimages_kernel)
@@ -2223,14 +2386,22 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
   dbg(st, "set_dm_vgrids(0)");
   // ---- filterOutside
   FCHK(hipMemsetAsync(B.flags, 0, n * sizeof(int), st));
-  if (c.nalive) hipLaunchKernelGGL(gain_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, s, c.dev(), B.flags);
+  if (c.nalive) hipLaunchKernelGGL(gain_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, s, c.dev(), B.flags, R, G);
+  if (part) FCHK(merge_flags(0, nullptr));
   FCHK(apply_flags(c, &counts[0]));
   dbg(st, "outside");
   FCHK(set_dm_vgrids(c, 1));
   // ---- filterExact
   FCHK(hipMemsetAsync(B.safe, 0, n * sizeof(Reg), st));
   FCHK(hipMemsetAsync(B.counters + 2, 0, sizeof(int), st));
-  hipLaunchKernelGGL(exact_entries_kernel, dim3(nblk(ncells)), dim3(256), 0, st, s, c.dev(), ncells, B.safe);
+  hipLaunchKernelGGL(exact_entries_kernel, dim3(nblk(ncells)), dim3(256), 0, st, s, c.dev(), ncells, B.safe, R, G);
+  if (part) {  // safe bits of every rank's targets, OR-merged
+    const size_t words = (size_t)n * (sizeof(Reg) / 4);
+    FCHK(fgrow(B.xr, B.cap_xr, words * 4 * G));
+    FCHK(c.xchg(0, B.safe, words * 4, B.xr, nullptr));
+    hipLaunchKernelGGL(or_bits_kernel, dim3(nblk((long long)words)), dim3(256), 0, st, reinterpret_cast<const unsigned*>(B.xr), G,
+                       words, reinterpret_cast<unsigned*>(B.safe));
+  }
   FCHK(hipMemsetAsync(B.need, 0, n * sizeof(int), st));
   if (c.nalive)
     hipLaunchKernelGGL(exact_patch_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, s, c.dev(), B.safe, B.preg, B.vreg,
@@ -2244,11 +2415,18 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
     hipLaunchKernelGGL(scatter_index_kernel, dim3(nblk(n)), dim3(256), 0, st, B.cnt, B.off, n, B.list);
     int m = 0;
     FCHK(read_int(B.off + n, &m, st));
-    if (m) {
+    if (part) {  // the owners' setRefImage outcomes (m is the same on every rank)
+      FCHK(fgrow(B.refpos, B.cap_refpos, (size_t)std::max(m, 1)));
+      FCHK(fgrow(B.xr, B.cap_xr, (size_t)std::max(m, 1) * 4 * G));
+      FCHK(launch_filter_refimage(s, dP, B.list, m, grid, st, B.refpos, R, G));
+      FCHK(c.xchg(0, B.refpos, (size_t)m * 4, B.xr, nullptr));
+      FCHK(launch_apply_refpos(s, dP, B.list, m, reinterpret_cast<const int*>(B.xr), G, st));
+    } else if (m) {
       FCHK(launch_filter_refimage(s, dP, B.list, m, grid, st));
+    }
+    if (m)
       hipLaunchKernelGGL(exact_after_ref_kernel, dim3(nblk(m)), dim3(256), 0, st, s, dP, B.list, m, B.preg, B.vreg,
                          B.counters + 2);
-    }
     FCHK(read_int(B.counters + 2, &counts[1], st));
   }
   dbg(st, "exact");
@@ -2265,8 +2443,7 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
     if (qj.cap_rows == 0) qj.f = nullptr;
     FCHK(hipMemsetAsync(B.qctr, 0, 2 * sizeof(unsigned long long), st));
     hipLaunchKernelGGL(neighbor_kernel, dim3(std::min(grid * NB_GRID_MULT, c.nalive)), dim3(64), 0, st, s, c.dev(), B.scratch, B.flags,
-                       B.counters + 3, B.counters + 4, getenv("PMVS_FILTER_DEBUG") ? B.need : nullptr, part ? sh->rank : 0,
-                       part ? sh->world : 1, qj);
+                       B.counters + 3, B.counters + 4, getenv("PMVS_FILTER_DEBUG") ? B.need : nullptr, R, G, qj);
     if (qj.f) {
       int nj = 0;
       FCHK(read_int(qj.njobs, &nj, st));
@@ -2306,38 +2483,11 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
             cnts[ord[0]], c.nalive > 1 ? cnts[ord[1]] : 0, c.nalive > 2 ? cnts[ord[2]] : 0);
   }
   FCHK(read_int(B.counters + 3, overflow, st));
-  if (part) {
-    // all-gather of {error, overflow, reject bits} per rank; a rank's bits cover the patches it owns
-    const int nw = (n + 31) / 32;
-    if ((size_t)nw + 1 > B.cap_rbits) {
-      if (B.rbits) (void)hipFree(B.rbits);
-      B.rbits = nullptr;
-      B.cap_rbits = 0;
-      FCHK(hipMalloc((void**)&B.rbits, ((size_t)nw + 1) * sizeof(unsigned)));
-      B.cap_rbits = (size_t)nw + 1;
-    }
-    if (nw) hipLaunchKernelGGL(pack_bits_kernel, dim3(nblk(nw)), dim3(256), 0, st, B.flags, n, B.rbits);
-    std::vector<unsigned> mine(2 + (size_t)nw, 0u), all((2 + (size_t)nw) * sh->world, 0u);
-    if (nw) FCHK(hipMemcpyAsync(mine.data() + 2, B.rbits, (size_t)nw * sizeof(unsigned), hipMemcpyDeviceToHost, st));
-    FCHK(hipStreamSynchronize(st));
-    mine[1] = (unsigned)*overflow;
-    phase = 1;
-    if (sh->exchange(mine.data(), mine.size() * sizeof(unsigned), all.data()) != 0) return hipErrorUnknown;
-    int ovf = 0;
-    for (int r = 0; r < sh->world; ++r) {
-      const unsigned* a = all.data() + (size_t)r * mine.size();
-      if (a[0] != 0) return hipErrorUnknown;  // a peer failed before the exchange
-      ovf += (int)a[1];
-      if (r != sh->rank)
-        for (int w = 0; w < nw; ++w) mine[2 + w] |= a[2 + w];
-    }
-    *overflow = ovf;
-    phase = 2;
+  if (part) {  // reject flags of every rank's patches; the overflow counts summed in the header
+    long long ovf = 0;
+    FCHK(merge_flags(*overflow, &ovf));
+    *overflow = (int)ovf;
     if (inject && inj_where == 'g') return hipErrorOutOfMemory;
-    if (nw) {
-      FCHK(hipMemcpyAsync(B.rbits, mine.data() + 2, (size_t)nw * sizeof(unsigned), hipMemcpyHostToDevice, st));
-      hipLaunchKernelGGL(unpack_bits_kernel, dim3(nblk(n)), dim3(256), 0, st, B.rbits, n, B.flags);
-    }
   }
   {
     int errs[2] = {0, 0};
@@ -2417,24 +2567,18 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
   return hipGetLastError();
 }
 
-// Sharded (world > 1): filter_pass makes exactly one all-gather (the filterNeighbor flags).  A rank
-// that fails before it still sends its {error} payload, so its peers fail with it; *handled says
-// whether the peers have seen this rank's failure (else the caller sends an abort header).
+// Owner-partitioned (world > 1): a rank that fails outside an exchange sends one 8-byte error header
+// here (see filter_pass_impl), so its peers fail at their next header instead of blocking.
 hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n, long long ncells, const long long* h_tgoff,
                        int grid, hipStream_t st, int counts[4], int* overflow, int* keep_dev, const Shard* sh,
                        bool* handled) {
-  int phase = 0;
-  hipError_t e = filter_pass_impl(s, B, dP, n, ncells, h_tgoff, grid, st, counts, overflow, keep_dev, sh, phase);
+  bool agreed = false;
+  hipError_t e = filter_pass_impl(s, B, dP, n, ncells, h_tgoff, grid, st, counts, overflow, keep_dev, sh, agreed);
   if (handled) *handled = true;
-  if (e != hipSuccess && sh && sh->world > 1 && n > 0) {
-    if (phase == 0) {  // the peers wait in the flag exchange: send them this rank's error there
-      const size_t words = 2 + (size_t)(n + 31) / 32;
-      std::vector<unsigned> mine(words, 0u), all(words * sh->world, 0u);
-      mine[0] = 1u;
-      (void)sh->exchange(mine.data(), words * sizeof(unsigned), all.data());
-    } else if (phase == 2 && handled) {
-      *handled = false;  // failed after the exchange: the caller announces it (loop header)
-    }
+  if (e != hipSuccess && sh && sh->world > 1 && n > 0 && !agreed) {
+    int h[2] = {1, 0};
+    std::vector<int> all(2 * (size_t)sh->world, 0);
+    (void)sh->exchange(h, sizeof(h), all.data());
   }
   return e;
 }

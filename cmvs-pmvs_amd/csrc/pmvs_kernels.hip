@@ -2006,9 +2006,24 @@ namespace pmvsdev {
 // filterExact's "setRefImage(patch, 0); setGrids(patch)" (filter.cpp:340-343) for the listed
 // patches: one wavefront per patch, the refine path's set_ref_image (pairwise INCC in the
 // workgroup's global scratch), then CPatchOrganizerS::setGrids (patchOrganizerS.cpp:417-426).
+// setRefImage's outcome applied to the record: the list as set_ref_image left it (images[0] swapped with
+// the chosen reference, or emptied) and setGrids over it.
+__device__ __forceinline__ void apply_ref_list(const DScene& s, pmvs_patch& q, const float* coord, int j, int img) {
+  float ic[3];
+  project(s.views[img], coord, s.level, ic);
+  q.images[j] = (int16_t)img;
+  q.grids[j][0] = grid16(((int)floorf(ic[0] + 0.5f)) / s.csize);
+  q.grids[j][1] = grid16(((int)floorf(ic[1] + 0.5f)) / s.csize);
+}
+
+// refpos == nullptr: setRefImage + setGrids in place.  Otherwise (owner-partitioned filter pass) only
+// the list entries whose reference image this rank owns (images[0] % world == rank) are evaluated and
+// their outcome written to refpos[k] -- the list position swapped with position 0 (0: unchanged) or
+// -1 (no target image: list cleared); apply_refpos_kernel applies the all-gathered outcomes.
 template <int WS>
 __global__ __launch_bounds__(64) void filter_refimage_kernel(DScene s, pmvs_patch* __restrict__ P,
-                                                             const int* __restrict__ list, int m) {
+                                                             const int* __restrict__ list, int m, int* __restrict__ refpos,
+                                                             int rank, int world) {
   __shared__ WaveLds<WS> L;
   float* mat = s.scratch + (size_t)blockIdx.x * PMVS_MAX_IMAGES * PMVS_MAX_IMAGES;
   const int lane = lane_id();
@@ -2016,6 +2031,7 @@ __global__ __launch_bounds__(64) void filter_refimage_kernel(DScene s, pmvs_patc
   for (int k = blockIdx.x; k < m; k += gridDim.x) {
     pmvs_patch& q = P[list[k]];
     const int n = q.num_images;
+    if (refpos && __builtin_amdgcn_readfirstlane(q.images[0]) % world != rank) continue;  // wave-uniform
     for (int j = lane; j < n; j += WAVE) L.images[j] = q.images[j];
     if (lane == 0) { L.nimg = n; L.overflow = 0; }
     __syncthreads();
@@ -2023,28 +2039,63 @@ __global__ __launch_bounds__(64) void filter_refimage_kernel(DScene s, pmvs_patc
     for (int i = 0; i < 4; ++i) { coord[i] = q.coord[i]; normal[i] = q.normal[i]; }
     set_ref_image<WS>(s, L, coord, normal, mat, &grabs);
     const int nn = L.nimg;
-    for (int j = lane; j < nn; j += WAVE) {
-      const int img = L.images[j];
-      float ic[3];
-      project(s.views[img], coord, s.level, ic);
-      q.images[j] = (int16_t)img;
-      q.grids[j][0] = grid16(((int)floorf(ic[0] + 0.5f)) / s.csize);
-      q.grids[j][1] = grid16(((int)floorf(ic[1] + 0.5f)) / s.csize);
+    if (refpos) {
+      if (lane == 0) {
+        int pos = -1;
+        if (nn > 0) {
+          pos = 0;
+          for (int j = 1; j < n; ++j)
+            if (q.images[j] == L.images[0]) pos = j;
+        }
+        refpos[k] = pos;
+      }
+      __syncthreads();
+      continue;
     }
+    for (int j = lane; j < nn; j += WAVE) apply_ref_list(s, q, coord, j, L.images[j]);
     if (lane == 0) q.num_images = nn;
     __syncthreads();
   }
 }
 
-hipError_t launch_filter_refimage(const DScene& s, pmvs_patch* P, const int* list, int m, int grid, hipStream_t stream) {
+// The owner-partitioned setRefImage's outcomes (all ranks' refpos, rank-major m ints each) applied on
+// every rank: entry k's value comes from the rank owning its reference image.
+__global__ void apply_refpos_kernel(DScene s, pmvs_patch* __restrict__ P, const int* __restrict__ list, int m,
+                                    const int* __restrict__ allpos, int world) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= m) return;
+  pmvs_patch& q = P[list[k]];
+  const int pos = allpos[(size_t)(q.images[0] % world) * m + k];
+  if (pos < 0) {
+    q.num_images = 0;
+    return;
+  }
+  if (pos > 0) {
+    const int16_t t = q.images[0];
+    q.images[0] = q.images[pos];
+    q.images[pos] = t;
+  }
+  const float coord[4] = {q.coord[0], q.coord[1], q.coord[2], q.coord[3]};
+  for (int j = 0; j < q.num_images; ++j) apply_ref_list(s, q, coord, j, q.images[j]);
+}
+
+hipError_t launch_filter_refimage(const DScene& s, pmvs_patch* P, const int* list, int m, int grid, hipStream_t stream,
+                                  int* refpos, int rank, int world) {
   if (m <= 0) return hipSuccess;
   const int g = grid < m ? grid : m;
   switch (s.wsize) {
-    case 5: hipLaunchKernelGGL((filter_refimage_kernel<5>), dim3(g), dim3(64), 0, stream, s, P, list, m); break;
-    case 7: hipLaunchKernelGGL((filter_refimage_kernel<7>), dim3(g), dim3(64), 0, stream, s, P, list, m); break;
-    case 9: hipLaunchKernelGGL((filter_refimage_kernel<9>), dim3(g), dim3(64), 0, stream, s, P, list, m); break;
+    case 5: hipLaunchKernelGGL((filter_refimage_kernel<5>), dim3(g), dim3(64), 0, stream, s, P, list, m, refpos, rank, world); break;
+    case 7: hipLaunchKernelGGL((filter_refimage_kernel<7>), dim3(g), dim3(64), 0, stream, s, P, list, m, refpos, rank, world); break;
+    case 9: hipLaunchKernelGGL((filter_refimage_kernel<9>), dim3(g), dim3(64), 0, stream, s, P, list, m, refpos, rank, world); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_apply_refpos(const DScene& s, pmvs_patch* P, const int* list, int m, const int* allpos, int world,
+                               hipStream_t stream) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(apply_refpos_kernel, dim3((m + 255) / 256), dim3(256), 0, stream, s, P, list, m, allpos, world);
   return hipGetLastError();
 }
 }  // namespace pmvsdev

@@ -99,6 +99,12 @@ struct FilterBuffers {
   unsigned* rbits = nullptr;  // sharded filterNeighbor: packed reject flags
   float4* coordc = nullptr;   // collected patches' coordinates in collect order (depth maps)
   size_t cap_rbits = 0;
+  // owner-partitioned filter pass (world > 1): this rank's visibility bits, setRefImage outcomes, and
+  // the all-gathered payloads of every rank
+  unsigned* vbits = nullptr;
+  int* refpos = nullptr;
+  char* xr = nullptr;
+  size_t cap_vbits = 0, cap_refpos = 0, cap_xr = 0;
   // filterNeighbor's deferred quadric fits (pmvs_filter.hip QuadJobs)
   float* qf = nullptr;
   double* qrows = nullptr;
@@ -115,7 +121,12 @@ struct FilterBuffers {
   ~FilterBuffers();
 };
 
-hipError_t launch_filter_refimage(const DScene& s, pmvs_patch* P, const int* list, int m, int grid, hipStream_t stream);
+// setRefImage + setGrids for the patches list[0, m) (filterExact); with refpos, only the entries whose
+// reference image rank owns (of world) are evaluated, their outcomes written to refpos (see the kernel)
+hipError_t launch_filter_refimage(const DScene& s, pmvs_patch* P, const int* list, int m, int grid, hipStream_t stream,
+                                  int* refpos = nullptr, int rank = 0, int world = 1);
+hipError_t launch_apply_refpos(const DScene& s, pmvs_patch* P, const int* list, int m, const int* allpos, int world,
+                               hipStream_t stream);
 
 // ---- expansion run (pmvs_filter.hip)
 constexpr int kMaxWave = 65536;  // parents per expansion wave (device slot arrays are sized by it)
