@@ -331,8 +331,8 @@ __global__ void coordc_kernel(const pmvs_patch* __restrict__ P, const int* __res
 // XCD-aware block order: the hardware deals workgroups to the 8 XCDs round-robin (block b on XCD
 // b % 8), each XCD with its own L2.  Remapping b to the logical block (b % 8) * (grid / 8) + b / 8
 // (grid a multiple of 8: xcd_grid) gives each XCD one contiguous range of logical blocks, so
-// threads that touch neighbouring cells share an L2.  Used by vimages_kernel (8.6 -> 5.8 ms per
-// launch with its record reads); setDepthMaps keeps the hardware order, where this order measured
+// threads that touch neighbouring cells share an L2.  Used by the vimages lists (round 3's
+// patch-major vimages kernel: 8.6 -> 5.8 ms per launch); setDepthMaps keeps the hardware order, where this order measured
 // slower (7.9 -> 10.6 ms: a contiguous range is ~6 whole target maps of atomics on one L2).
 constexpr int kXcds = 8;
 __device__ __forceinline__ long long xcd_block() {
@@ -372,84 +372,79 @@ __global__ void depth_map_kernel(DScene s, FilterDev F, const float4* __restrict
     }
 }
 
-// CPatchOrganizerS::setVImagesVGrids (patchOrganizerS.cpp:429-459) per collected patch;
-// vreg = every vimages entry (addPatchVThread registers the first entry per image, and the
-// list never holds an image twice).
-__global__ void vimages_kernel(DScene s, FilterDev F, int additive, Reg* __restrict__ vreg) {
-  const int i = (int)(xcd_block() * blockDim.x + threadIdx.x);
-  if (i >= F.nalive) return;
-  const int p = F.order[i];
-  pmvs_patch& q = F.P[p];
-  if (!additive) q.num_vimages = 0;
-  unsigned long long used[PMVS_MAX_TARGETS / 64] = {};  // bit t: target t is already in a list
-  for (int k = 0; k < q.num_images; ++k)
-    if (q.images[k] < s.tnum) used[q.images[k] >> 6] |= 1ull << (q.images[k] & 63);
-  for (int k = 0; k < q.num_vimages; ++k) used[q.vimages[k] >> 6] |= 1ull << (q.vimages[k] & 63);
-  for (int t = 0; t < s.tnum; ++t) {
-    if (used[t >> 6] & (1ull << (t & 63))) continue;
-    const DView& v = s.views[t];
-    float ic[3];
-    project(v, q.coord, s.level, ic);
-    const int ix = ((int)floorf(ic[0] + 0.5f)) / s.csize;
-    const int iy = ((int)floorf(ic[1] + 0.5f)) / s.csize;
-    if (is_visible(s, F, p, t, ix, iy, 0.5f) == 0) continue;
-    if (get_edge(s, v, q.coord, s.level) == 0) continue;
-    if (q.num_vimages >= PMVS_MAX_IMAGES) {  // more than PMVS_MAX_IMAGES targets see the patch: the pass fails
-      atomicAdd(F.lovf, 1);
-      break;
-    }
-    q.vimages[q.num_vimages] = (int16_t)t;
-    q.vgrids[q.num_vimages][0] = grid16(ix);
-    q.vgrids[q.num_vimages][1] = grid16(iy);
-    q.num_vimages++;
-  }
-  vreg[p] = reg_first(q.num_vimages);
+// setVImagesVGrids (patchOrganizerS.cpp:429-459) in two steps, target-major:
+//   vis_rows_kernel   one thread per (target, collected patch), consecutive patches of one target per
+//                     wavefront: isVisible0 + the edge test (the tests vimages_kernel makes) and a ballot,
+//                     so row t holds one bit per collected patch -- while the grid works through target
+//                     t, t's depth map and edge map stay in L2 (vimages_kernel walks all targets per
+//                     patch, every wavefront in another map);
+//   vis_lists_kernel  one thread per patch: the visible targets appended in target order, their cells.
+// Owner-partitioned (world > 1): a rank computes the rows of the targets it owns
+// (t = rank + world j), the rows are all-gathered, and every rank builds the same lists.
+__global__ void normalc_kernel(const pmvs_patch* __restrict__ P, const int* __restrict__ order, int na,
+                               float4* __restrict__ normalc) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= na) return;
+  const float* c = P[order[i]].normal;
+  normalc[i] = make_float4(c[0], c[1], c[2], c[3]);
 }
 
-// setVImagesVGrids, owner-partitioned (world > 1): the visibility of collected patch i
-// in the targets this rank owns (t = rank + world j, j < nown), as bit j of bits[i * W ..].  Every rank
-// then builds the lists from all ranks' bits (vis_merge_kernel), in target order as vimages_kernel.
-__global__ void vis_bits_kernel(DScene s, FilterDev F, int additive, int rank, int world, int W,
-                                unsigned* __restrict__ bits) {
-  const int i = (int)(xcd_block() * blockDim.x + threadIdx.x);
+// per collected patch: the targets already in its lists (images; vimages too when additive)
+__global__ void used_kernel(DScene s, FilterDev F, int additive, unsigned long long* __restrict__ used) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= F.nalive) return;
-  const int p = F.order[i];
-  const pmvs_patch& q = F.P[p];
-  unsigned long long used[PMVS_MAX_TARGETS / 64] = {};
+  const pmvs_patch& q = F.P[F.order[i]];
+  unsigned long long u[PMVS_MAX_TARGETS / 64] = {};
   for (int k = 0; k < q.num_images; ++k)
-    if (q.images[k] < s.tnum) used[q.images[k] >> 6] |= 1ull << (q.images[k] & 63);
+    if (q.images[k] < s.tnum) u[q.images[k] >> 6] |= 1ull << (q.images[k] & 63);
   if (additive)
-    for (int k = 0; k < q.num_vimages; ++k) used[q.vimages[k] >> 6] |= 1ull << (q.vimages[k] & 63);
-  unsigned* out = bits + (size_t)i * W;
-  for (int w = 0; w < W; ++w) out[w] = 0u;
-  for (int t = rank, j = 0; t < s.tnum; t += world, ++j) {
-    if (used[t >> 6] & (1ull << (t & 63))) continue;
+    for (int k = 0; k < q.num_vimages; ++k) u[q.vimages[k] >> 6] |= 1ull << (q.vimages[k] & 63);
+  for (int w = 0; w < PMVS_MAX_TARGETS / 64; ++w) used[(size_t)i * (PMVS_MAX_TARGETS / 64) + w] = u[w];
+}
+
+struct PCN {  // the fields isVisible reads of the tested patch
+  float coord[4], normal[4];
+};
+
+__global__ __launch_bounds__(256) void vis_rows_kernel(DScene s, FilterDev F, const float4* __restrict__ coordc,
+                                                       const float4* __restrict__ normalc,
+                                                       const unsigned long long* __restrict__ used, int rank, int world,
+                                                       int nown, long long row_words, unsigned long long* __restrict__ rows) {
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long napad = row_words * 64;
+  if (g >= (long long)nown * napad) return;  // whole wavefronts: napad is a multiple of 64
+  const int j = (int)(g / napad), i = (int)(g - (long long)j * napad);
+  const int t = rank + world * j;
+  bool vis = false;
+  if (i < F.nalive && !((used[(size_t)i * (PMVS_MAX_TARGETS / 64) + (t >> 6)] >> (t & 63)) & 1ull)) {
+    const float4 c4 = coordc[i], n4 = normalc[i];
+    const PCN q{{c4.x, c4.y, c4.z, c4.w}, {n4.x, n4.y, n4.z, n4.w}};
     const DView& v = s.views[t];
     float ic[3];
     project(v, q.coord, s.level, ic);
     const int ix = ((int)floorf(ic[0] + 0.5f)) / s.csize;
     const int iy = ((int)floorf(ic[1] + 0.5f)) / s.csize;
-    if (is_visible(s, F, p, t, ix, iy, 0.5f) == 0) continue;
-    if (get_edge(s, v, q.coord, s.level) == 0) continue;
-    out[j >> 5] |= 1u << (j & 31);
+    vis = is_visible_q(s, F, q, t, ix, iy, 0.5f) != 0 && get_edge(s, v, q.coord, s.level) != 0;
   }
+  const unsigned long long b = __ballot(vis);
+  if ((threadIdx.x & 63) == 0) rows[(long long)j * row_words + i / 64] = b;
 }
 
-// The vimages lists from every rank's visibility bits (all: world blocks of nalive * W words).
-__global__ void vis_merge_kernel(DScene s, FilterDev F, int additive, int world, int W,
-                                 const unsigned* __restrict__ all, Reg* __restrict__ vreg) {
+// rows: world blocks (rank r: nown_max rows of row_words words; row j = target r + world j)
+__global__ void vis_lists_kernel(DScene s, FilterDev F, int additive, int world, int nown_max, long long row_words,
+                                 const unsigned long long* __restrict__ rows, Reg* __restrict__ vreg) {
   const int i = (int)(xcd_block() * blockDim.x + threadIdx.x);
   if (i >= F.nalive) return;
   const int p = F.order[i];
   pmvs_patch& q = F.P[p];
   if (!additive) q.num_vimages = 0;
-  const size_t stride = (size_t)F.nalive * W;
+  const long long blk = (long long)nown_max * row_words;
   for (int t = 0; t < s.tnum; ++t) {
-    const int r = t % world, j = t / world;
-    if (!((all[(size_t)r * stride + (size_t)i * W + (j >> 5)] >> (j & 31)) & 1u)) continue;
+    const unsigned long long w = rows[(long long)(t % world) * blk + (long long)(t / world) * row_words + i / 64];
+    if (!((w >> (i & 63)) & 1ull)) continue;
     float ic[3];
     project(s.views[t], q.coord, s.level, ic);
-    if (q.num_vimages >= PMVS_MAX_IMAGES) {
+    if (q.num_vimages >= PMVS_MAX_IMAGES) {  // more than PMVS_MAX_IMAGES targets see the patch: the pass fails
       atomicAdd(F.lovf, 1);
       break;
     }
@@ -2016,7 +2011,7 @@ static hipError_t dalloc(T*& p, size_t n) {
 FilterBuffers::~FilterBuffers() {
   void* ps[] = {preg, vreg, tgoff, cnt, off, keys, keys2, cellcnt, pg_off, pg_items, vp_off, vp_items, dpkey,
                 order, rank, hot, flags, safe, need, list, scratch, counters, temp, edge_off, edges, rbits, coordc,
-                qf, qrows, qjobs, qctr, qkeys, qkeys2, qcrows, qoff, vbits, refpos, xr};
+                qf, qrows, qjobs, qctr, qkeys, qkeys2, qcrows, qoff, vrows, used, normalc, refpos, xr};
   for (void* p : ps)
     if (p) (void)hipFree(p);
 }
@@ -2268,22 +2263,30 @@ static hipError_t set_dm_vgrids(Ctx& c, int additive) {
                        B.dpkey, c.rank, c.world);
   dbg(c.st, "  depth");
   FCHK(hipMemsetAsync(B.vreg, 0, c.n * sizeof(Reg), c.st));
-  if (c.world > 1) {
-    // setVImagesVGrids by target owner: each rank tests its targets, the bits are all-gathered and
-    // every rank appends the visible targets in target order (vis_merge_kernel)
-    const int W = ((c.s.tnum + c.world - 1) / c.world + 31) / 32;
-    const size_t words = (size_t)c.nalive * W;
-    FCHK(fgrow(B.vbits, B.cap_vbits, std::max(words, (size_t)1)));
-    FCHK(fgrow(B.xr, B.cap_xr, std::max(words, (size_t)1) * 4 * c.world));
-    if (c.nalive > 0)
-      hipLaunchKernelGGL(vis_bits_kernel, dim3(xcd_grid(c.nalive)), dim3(256), 0, c.st, c.s, c.dev(), additive, c.rank,
-                         c.world, W, B.vbits);
-    FCHK(c.xchg(0, B.vbits, words * 4, B.xr, nullptr));
-    if (c.nalive > 0)
-      hipLaunchKernelGGL(vis_merge_kernel, dim3(xcd_grid(c.nalive)), dim3(256), 0, c.st, c.s, c.dev(), additive, c.world, W,
-                         reinterpret_cast<const unsigned*>(B.xr), B.vreg);
-  } else if (c.nalive > 0) {
-    hipLaunchKernelGGL(vimages_kernel, dim3(xcd_grid(c.nalive)), dim3(256), 0, c.st, c.s, c.dev(), additive, B.vreg);
+  if (c.nalive > 0) {
+    // setVImagesVGrids: visibility rows of this rank's targets (all targets at world 1), all-gathered
+    // when the pass is owner-partitioned, then every rank's lists in target order
+    const long long row_words = (c.nalive + 63) / 64;
+    const int nown_max = (c.s.tnum + c.world - 1) / c.world;
+    const size_t rwords = (size_t)nown_max * row_words;
+    FCHK(fgrow(B.normalc, B.cap_normalc, (size_t)c.nalive));
+    FCHK(fgrow(B.used, B.cap_used, (size_t)c.nalive * (PMVS_MAX_TARGETS / 64)));
+    FCHK(fgrow(B.vrows, B.cap_vrows, rwords));
+    hipLaunchKernelGGL(normalc_kernel, dim3(nblk(c.nalive)), dim3(256), 0, c.st, c.P, B.order, c.nalive, B.normalc);
+    hipLaunchKernelGGL(used_kernel, dim3(nblk(c.nalive)), dim3(256), 0, c.st, c.s, c.dev(), additive, B.used);
+    if (nown > 0)
+      hipLaunchKernelGGL(vis_rows_kernel, dim3(nblk((long long)nown * row_words * 64)), dim3(256), 0, c.st, c.s, c.dev(),
+                         B.coordc, B.normalc, B.used, c.rank, c.world, nown, row_words, B.vrows);
+    const unsigned long long* rows = B.vrows;
+    if (c.world > 1) {
+      FCHK(fgrow(B.xr, B.cap_xr, rwords * 8 * c.world));
+      FCHK(c.xchg(0, B.vrows, rwords * 8, B.xr, nullptr));
+      rows = reinterpret_cast<const unsigned long long*>(B.xr);
+    }
+    hipLaunchKernelGGL(vis_lists_kernel, dim3(xcd_grid(c.nalive)), dim3(256), 0, c.st, c.s, c.dev(), additive, c.world,
+                       nown_max, row_words, rows, B.vreg);
+  } else if (c.world > 1) {
+    FCHK(c.xchg(0, nullptr, 0, nullptr, nullptr));  // the exchange every rank makes here
   }
   dbg(c.st, "  vimages");
   FCHK(build_lists(c, 1));
@@ -2380,7 +2383,7 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
   };
   for (int k = 0; k < 4; ++k) counts[k] = 0;
   *overflow = 0;
-  FCHK(hipMemsetAsync(B.counters + 8, 0, sizeof(int), st));  // vimages list overflows (vimages_kernel)
+  FCHK(hipMemsetAsync(B.counters + 8, 0, sizeof(int), st));  // vimages list overflows (vis_lists_kernel)
   hipLaunchKernelGGL(init_reg_kernel, dim3(nblk(n)), dim3(256), 0, st, s, dP, n, B.preg, B.vreg);
   FCHK(set_dm_vgrids(c, 0));
   dbg(st, "set_dm_vgrids(0)");

@@ -99,12 +99,13 @@ struct FilterBuffers {
   unsigned* rbits = nullptr;  // sharded filterNeighbor: packed reject flags
   float4* coordc = nullptr;   // collected patches' coordinates in collect order (depth maps)
   size_t cap_rbits = 0;
-  // owner-partitioned filter pass (world > 1): this rank's visibility bits, setRefImage outcomes, and
-  // the all-gathered payloads of every rank
-  unsigned* vbits = nullptr;
+  // setVImagesVGrids' visibility rows (target-major bits), the collected patches' normals and used
+  // targets; owner-partitioned pass (world > 1): setRefImage outcomes and the all-gathered payloads
+  unsigned long long *vrows = nullptr, *used = nullptr;
+  float4* normalc = nullptr;
   int* refpos = nullptr;
   char* xr = nullptr;
-  size_t cap_vbits = 0, cap_refpos = 0, cap_xr = 0;
+  size_t cap_vrows = 0, cap_used = 0, cap_normalc = 0, cap_refpos = 0, cap_xr = 0;
   // filterNeighbor's deferred quadric fits (pmvs_filter.hip QuadJobs)
   float* qf = nullptr;
   double* qrows = nullptr;

@@ -45,7 +45,8 @@ def test_c3_full_size_step_and_first_waves_match_oracle(c3):
     assert checks["ok"] and checks["sphere_residual_p99"] < 0.01, checks
     assert log[0]["expand"]["added"] > 3_000_000
     del model
-    args = argparse.Namespace(iterations=3, cpu_iterations=3, cpu_waves=2, cpu_seconds=1.0, cpu_threads=0,
+    # iteration 1 here (every bench.py run samples all three iterations: parity_c3_first_waves)
+    args = argparse.Namespace(iterations=3, cpu_iterations=1, cpu_waves=2, cpu_seconds=1.0, cpu_threads=0,
                               wave=32768, min_candidates=131072)
     _, parity = bench.loop_samples(P, scene, inp, seeds, args)
     print(f"first waves: {parity}")
