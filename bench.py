@@ -517,7 +517,9 @@ def main():
                 "seed_mode": args.seed_mode, "seed_patches": int(len(seeds)), "wave": args.wave,
                 "min_candidates": args.min_candidates, "iterations": args.iterations, "wsize": 7, "csize": 2,
                 "minImageNum": 3, "threshold": 0.7,
-                "parallelism": f"{'wave-sharded' if shard else 'CMVS clusters + RCCL boundary exchange' if c4 else 'cluster-per-GPU'} x{world}",
+                "parallelism": (f"one shared scene, wave-sharded refine/findEmptyBlocks + target-owned filter x{world}"
+                                if shard else f"CMVS clusters + RCCL boundary exchange x{world}" if c4 else
+                                f"independent CMVS-style clusters, one {args.views}-view ring per GPU (weak scaling) x{world}"),
             },
             "ncc_evals_per_s": round(evals_all / elapsed_max, 1),
             "refined_candidates_per_s": round(refined_all / elapsed_max, 1),

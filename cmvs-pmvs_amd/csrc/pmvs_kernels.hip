@@ -41,7 +41,7 @@ struct WaveLds {
   float ave[TEXCAP][4];     // per-texture channel means and ave2
   int valid[TEXCAP];
   int jview[TEXCAP], jlevel[TEXCAP];
-  float jleft[TEXCAP][2], jdx[TEXCAP][2], jdy[TEXCAP][2];
+  float jrow[TEXCAP][WS][2], jdx[TEXCAP][2], jdy[TEXCAP][2];  // jrow: each sample row's start (left)
   float res[TEXCAP];        // per-texture result (inccs)
   int images[PMVS_MAX_IMAGES];
   int nimg;
@@ -121,8 +121,11 @@ __device__ void grab_batch(const DScene& s, WaveLds<WS>& L, int cnt, const int* 
     L.valid[slot] = ok;
     L.jview[slot] = index;
     L.jlevel[slot] = newlevel;
-    L.jleft[slot][0] = tl0;
-    L.jleft[slot][1] = tl1;
+    float lx = tl0, ly = tl1;  // rows' starts: `left += dy` (optim.cpp:850-860), once per texture
+    for (int r = 0; r < WS; ++r) {
+      L.jrow[slot][r][0] = lx; L.jrow[slot][r][1] = ly;
+      lx = lx + dy[0]; ly = ly + dy[1];
+    }
     L.jdx[slot][0] = dx[0];
     L.jdx[slot][1] = dx[1];
     L.jdy[slot][0] = dy[0];
@@ -137,9 +140,7 @@ __device__ void grab_batch(const DScene& s, WaveLds<WS>& L, int cnt, const int* 
     const int slot = slot0 + j;
     if (!L.valid[slot]) continue;
     const int yy = k / WS, xx = k - yy * WS;
-    float lx = L.jleft[slot][0], ly = L.jleft[slot][1];
-    const float dyx = L.jdy[slot][0], dyy = L.jdy[slot][1];
-    for (int r = 0; r < yy; ++r) { lx = lx + dyx; ly = ly + dyy; }
+    float lx = L.jrow[slot][yy][0], ly = L.jrow[slot][yy][1];
     const float dxx = L.jdx[slot][0], dxy = L.jdx[slot][1];
     for (int c = 0; c < xx; ++c) { lx = lx + dxx; ly = ly + dxy; }
     float rgb[3];
@@ -861,7 +862,7 @@ struct RefLds {
   float ave[TSLOTS][4];
   long long jbase[TSLOTS];
   int jvalid[TSLOTS], jW[TSLOTS], jreq[TSLOTS], jidx[TSLOTS];
-  float jleft[TSLOTS][2], jdx[TSLOTS][2], jdy[TSLOTS][2];
+  float jrow[TSLOTS][WS][2], jdx[TSLOTS][2], jdy[TSLOTS][2];  // jrow: each sample row's start (left)
   float jres[TSLOTS];
   float geo[NC][16];                 // requesting lane: coord, normal, pxaxis, pyaxis
   unsigned short views[NC][PMVS_MAX_TAU];  // requesting lane: first size images
@@ -946,7 +947,13 @@ __device__ __forceinline__ void tex_setup(const DScene& s, L& C, int t) {
   C.jvalid[t] = ok;
   C.jW[t] = v.w[newlevel];
   C.jbase[t] = v.pyr_off[newlevel];
-  C.jleft[t][0] = tl0; C.jleft[t][1] = tl1;
+  // each row's start, by the reference's recurrence `left += dy` (optim.cpp:850-860), once per texture
+  // instead of once per sample in the gather
+  float lx = tl0, ly = tl1;
+  for (int r = 0; r < WS; ++r) {
+    C.jrow[t][r][0] = lx; C.jrow[t][r][1] = ly;
+    lx = lx + dy[0]; ly = ly + dy[1];
+  }
   C.jdx[t][0] = dx[0]; C.jdx[t][1] = dx[1];
   C.jdy[t][0] = dy[0]; C.jdy[t][1] = dy[1];
 }
@@ -972,9 +979,8 @@ __device__ __forceinline__ void tex_gather(const DScene& s, L& C, int njobs, int
       float lx = 0.f, ly = 0.f;
       if (live[q]) {
         const int yy = k / WS, xx = k - yy * WS;
-        lx = C.jleft[t][0]; ly = C.jleft[t][1];
-        const float dyx = C.jdy[t][0], dyy = C.jdy[t][1], dxx = C.jdx[t][0], dxy = C.jdx[t][1];
-        for (int r = 0; r < yy; ++r) { lx = lx + dyx; ly = ly + dyy; }
+        lx = C.jrow[t][yy][0]; ly = C.jrow[t][yy][1];
+        const float dxx = C.jdx[t][0], dxy = C.jdx[t][1];
         for (int c = 0; c < xx; ++c) { lx = lx + dxx; ly = ly + dxy; }
         const int ix = (int)lx, iy = (int)ly;
         idx = C.jbase[t] + (long long)iy * C.jW[t] + ix;
@@ -1340,7 +1346,7 @@ constexpr int WG_LDS_BYTES = 160 * 1024;
 template <int WS, int NC, int WGPC>
 struct RefWgFit {  // texture slots (<= 64) that fit next to NC optimizer states, WGPC workgroups per CU
   static constexpr int SP = (WS * WS + 3) & ~3;
-  static constexpr int per_slot = 3 * SP * 4 + 4 * 4 + 8 + 4 * 4 + 6 * 4 + 4;
+  static constexpr int per_slot = 3 * SP * 4 + 4 * 4 + 8 + 4 * 4 + (2 * WS + 4) * 4 + 4;
   static constexpr int fixed = NC * ((int)sizeof(BqState) + 16 * 4 + PMVS_MAX_TAU * 2 + 4 * 4) + 4 * (NC + 1) + 64;
   static constexpr int fit = (WG_LDS_BYTES / WGPC - fixed) / per_slot - 1;
   static constexpr int slots = fit < 64 ? fit : 64;
@@ -1355,7 +1361,7 @@ struct RefWgLds {
   float ave[TS][4];
   long long jbase[TS];
   int jvalid[TS], jW[TS], jreq[TS], jidx[TS];
-  float jleft[TS][2], jdx[TS][2], jdy[TS][2];
+  float jrow[TS][WS][2], jdx[TS][2], jdy[TS][2];
   float jres[TS];
   float geo[NC][16];                       // requesting chain: coord, normal, pxaxis, pyaxis
   unsigned short views[NC][PMVS_MAX_TAU];  // chain: first size images
@@ -1684,8 +1690,7 @@ __global__ __launch_bounds__(64) void grab_tex_kernel(DScene s, const pmvs_tex_q
     if (L.valid[0]) {
       for (int t = lane; t < S; t += WAVE) {
         const int yy = t / WS, xx = t - yy * WS;
-        float lx = L.jleft[0][0], ly = L.jleft[0][1];
-        for (int r = 0; r < yy; ++r) { lx = lx + L.jdy[0][0]; ly = ly + L.jdy[0][1]; }
+        float lx = L.jrow[0][yy][0], ly = L.jrow[0][yy][1];
         for (int c = 0; c < xx; ++c) { lx = lx + L.jdx[0][0]; ly = ly + L.jdx[0][1]; }
         float rgb[3];
         get_color(s, s.views[L.jview[0]], lx, ly, L.jlevel[0], rgb);
