@@ -1840,7 +1840,7 @@ void RefineHost::release() {
 // refine_v2_kernel instantiations (texture slots * 100 + chains per wavefront)
 bool refine_config_supported(int tslots) {
   switch (tslots) {
-    case 804: case 807: case 808: case 1204: case 1206: case 1608: case 2408: return true;
+    case 804: case 807: case 808: case 1201: case 1202: case 1203: case 1204: case 1206: case 1608: case 2408: return true;
     case 164011: case 164021: case 164041: case 148041: case 132022: case 132042: case 116042: return true;
 #if defined(BQ_PRIVATE)
     case 1264: case 2464: case 1232: case 2432: case 1216: case 2448: case 3232: case 3248: case 3264: case 4832:
@@ -1928,6 +1928,9 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
     case 1608: hipLaunchKernelGGL((refine_v2_kernel<WS, 16, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     case 2408: hipLaunchKernelGGL((refine_v2_kernel<WS, 24, 8>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     case 1204: hipLaunchKernelGGL((refine_v2_kernel<WS, 12, 4>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 1201: hipLaunchKernelGGL((refine_v2_kernel<WS, 12, 1>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 1202: hipLaunchKernelGGL((refine_v2_kernel<WS, 12, 2>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
+    case 1203: hipLaunchKernelGGL((refine_v2_kernel<WS, 12, 3>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
 #if defined(BQ_PRIVATE)
     case 1264: hipLaunchKernelGGL((refine_v2_kernel<WS, 12, 64>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
     case 2464: hipLaunchKernelGGL((refine_v2_kernel<WS, 24, 64>), dim3(rg), dim3(64), 0, stream, s, d_jobs, n, d_st); break;
