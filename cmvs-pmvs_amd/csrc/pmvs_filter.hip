@@ -1328,11 +1328,16 @@ __global__ void quad_keys_kernel(const int4* __restrict__ jobs, int njobs, unsig
 __device__ inline void quad_lane_job(const DScene& s, const FilterDev& F, const QuadJobs& qj,
                                      const unsigned long long* __restrict__ qsorted, const int* __restrict__ qoff, int k,
                                      int* __restrict__ reject);
+__device__ inline void quad_solve(const DScene& s, const FilterDev& F, const double* M, const int* perm, double scale,
+                                  bool fin, int p, int n, const float* gx, const float* gy, const float* gz,
+                                  int* __restrict__ reject);
 __global__ __launch_bounds__(256) void quad_lane_kernel(DScene s, FilterDev F, QuadJobs qj, const unsigned long long* __restrict__ qsorted,
-                                                        const int* __restrict__ qoff, int njobs, int* __restrict__ reject) {
+                                                        const int* __restrict__ qoff, int njobs, int* __restrict__ reject,
+                                                        const int* __restrict__ klim) {
   // grid-stride over the jobs: a capped grid (PMVS_QUAD_WAVES_PER_CU) bounds the row working set
-  // of the resident wavefronts
-  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < njobs; k += gridDim.x * blockDim.x)
+  // of the resident wavefronts.  klim: the jobs [0, *klim) (the rest go to quad_qr_kernel)
+  const int kend = klim ? imin(njobs, *klim) : njobs;
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < kend; k += gridDim.x * blockDim.x)
     quad_lane_job(s, F, qj, qsorted, qoff, k, reject);
 }
 __device__ inline void quad_lane_job(const DScene& s, const FilterDev& F, const QuadJobs& qj,
@@ -1358,15 +1363,15 @@ __device__ inline void quad_lane_job(const DScene& s, const FilterDev& F, const 
     }
     M[(size_t)(6 * i + 5) * 64] = (double)gz[i];
   }
-  float x[N] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-  if (isfinite(scale)) {
+  const bool fin = isfinite(scale);
+  int perm[N] = {0, 1, 2, 3, 4};
+  if (fin) {
     if (scale == 0.0) scale = 1.0;
     for (int i = 0; i < n; ++i)
       for (int j = 0; j < N; ++j) M[(size_t)(6 * i + j) * 64] = M[(size_t)(6 * i + j) * 64] / scale;
     auto rr = [&](int i) -> double& { return M[(size_t)(6 * i + 5) * 64]; };
     auto at = [&](int i, int j) -> double& { return M[(size_t)(6 * i + j) * 64]; };
     // ---- column-pivoting Householder QR
-    int perm[N];
     double nu[N], nd[N], tau[N];
     for (int j = 0; j < N; ++j) {
       perm[j] = j;
@@ -1433,6 +1438,21 @@ __device__ inline void quad_lane_job(const DScene& s, const FilterDev& F, const 
       rr(kk) -= tau[kk] * t;
       for (int i = kk + 1; i < n; ++i) rr(i) -= (tau[kk] * at(i, kk)) * t;
     }
+  }
+  quad_solve(s, F, M, perm, scale, fin, p, n, gx, gy, gz, reject);
+}
+
+// The two-sided Jacobi stage on R, the rank-thresholded minimum-norm solve and filterQuad's residual
+// test, on a pivoted QR left in the lane layout (rows 0..4: R in the upper triangle, Q^T b in column 5).
+__device__ inline void quad_solve(const DScene& s, const FilterDev& F, const double* M, const int* perm, double scale,
+                                  bool fin, int p, int n, const float* gx, const float* gy, const float* gz,
+                                  int* __restrict__ reject) {
+  constexpr int N = 5;
+  const double eps = 2.220446049250313e-16, dmin = 2.2250738585072014e-308;
+  float x[N] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  if (fin) {
+    auto rr = [&](int i) -> double { return M[(size_t)(6 * i + 5) * 64]; };
+    auto at = [&](int i, int j) -> double { return M[(size_t)(6 * i + j) * 64]; };
     // ---- two-sided Jacobi on R
     double W[N][N], U[N][N], V[N][N];
     for (int i = 0; i < N; ++i)
@@ -1591,6 +1611,180 @@ __device__ inline void quad_lane_job(const DScene& s, const FilterDev& F, const 
   }
   residual = __fdiv_rn(residual, (float)(n - 5));
   reject[p] = (residual < s.quad ? 0 : 1);
+}
+
+// The fits with at most nq rows, eight lanes per job (QL) and the job's rows in LDS: the same
+// column-pivoting Householder steps as quad_lane_job, with every column sum still one lane's
+// in-order loop -- the lanes split the columns (the five norms, the five dot products with the
+// Householder vector, Q^T b's among them as column 5), and the row-wise scalings, swaps and rank-1
+// updates. Applying H_kk to b inside step kk is the same arithmetic as quad_lane_job's Q^T b loop
+// after the QR: column kk is final once step kk ends (later pivots and updates touch columns > kk).
+// The result (R, Q^T b, perm, scale) goes to rows 0..5 of the job's lane-layout chunk for
+// quad_solve_kernel.  Jobs are in descending row count, so the fits above nq rows are the prefix
+// [0, kb) (quad_split_kernel) left to quad_lane_kernel.
+constexpr int QL = 8;
+__global__ void quad_split_kernel(const unsigned long long* __restrict__ qsorted, int njobs, int nq, int* __restrict__ kb) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= njobs) return;
+  const unsigned thr = 2047u - (unsigned)nq;  // n > nq  <=>  key >> 32 < thr
+  const bool big = (unsigned)(qsorted[k] >> 32) < thr;
+  const bool next = k + 1 < njobs && (unsigned)(qsorted[k + 1] >> 32) < thr;
+  if (k == 0 && !big) *kb = 0;
+  if (big && !next) *kb = k + 1;
+}
+
+__global__ __launch_bounds__(64) void quad_qr_kernel(QuadJobs qj, const unsigned long long* __restrict__ qsorted,
+                                                     const int* __restrict__ qoff, const int* __restrict__ kb_ptr,
+                                                     int njobs, int nq) {
+  constexpr int N = 5;
+  const double dmin = 2.2250738585072014e-308;
+  const double downdate = sqrt(2.220446049250313e-16);
+  extern __shared__ double qlds[];  // (64 / QL) jobs x nq rows x 6
+  __shared__ double sh_nu[64 / QL][N], sh_nd[64 / QL][N], sh_t[64 / QL][N + 1], sh_c[64 / QL][3];
+  __shared__ int sh_perm[64 / QL][N];
+  const int lane = threadIdx.x, js = lane / QL, jl = lane % QL;
+  const int kb = *kb_ptr;
+  double* A = qlds + (size_t)js * nq * 6;  // at(i, j) = A[6 i + j], j = 5: b
+  for (int k0 = kb + blockIdx.x * (64 / QL); k0 < njobs; k0 += gridDim.x * (64 / QL)) {
+    const int k = k0 + js;
+    int n = 0;
+    const float* gx = nullptr;
+    if (k < njobs) {
+      const int4 jb = qj.jobs[(int)(qsorted[k] & 0xffffffffull)];
+      n = jb.z;
+      gx = qj.f + 3 * (size_t)jb.y;
+    }
+    const float* gy = gx + n;
+    const float* gz = gy + n;
+    double smax = 0.0;
+    for (int i = jl; i < n; i += QL) {
+      const float fx = gx[i], fy = gy[i];
+      const double a[5] = {(double)(fx * fx), (double)(fy * fy), (double)(fx * fy), (double)fx, (double)fy};
+      for (int j = 0; j < N; ++j) {
+        A[6 * i + j] = a[j];
+        smax = dmaxd2(smax, fabs(a[j]));  // the max of the non-NaN terms: any order gives it
+      }
+      A[6 * i + 5] = (double)gz[i];
+    }
+    for (int m = 1; m < QL; m <<= 1) smax = dmaxd2(smax, __shfl_xor(smax, m));
+    const bool fin = isfinite(smax);
+    const double scale = smax == 0.0 ? 1.0 : smax;
+    const int nn = fin ? n : 0;  // the rows this job's QR walks (none: x = 0, as quad_lane_job)
+    __syncthreads();
+    for (int i = jl; i < nn; i += QL)
+      for (int j = 0; j < N; ++j) A[6 * i + j] = A[6 * i + j] / scale;
+    __syncthreads();
+    if (jl < N) {
+      double sq = 0.0;
+      for (int i = 0; i < nn; ++i) sq += A[6 * i + jl] * A[6 * i + jl];
+      sh_nd[js][jl] = sh_nu[js][jl] = sqrt(sq);
+      sh_perm[js][jl] = jl;
+    }
+    __syncthreads();
+    for (int kk = 0; kk < N; ++kk) {
+      // pivot: the column of largest remaining norm (first on ties)
+      int big = kk;
+      for (int j = kk + 1; j < N; ++j)
+        if (sh_nu[js][j] > sh_nu[js][big]) big = j;
+      if (big != kk)
+        for (int i = jl; i < nn; i += QL) {
+          const double t = A[6 * i + kk];
+          A[6 * i + kk] = A[6 * i + big];
+          A[6 * i + big] = t;
+        }
+      __syncthreads();
+      if (jl == 0 && nn) {
+        if (big != kk) {
+          double t = sh_nu[js][kk]; sh_nu[js][kk] = sh_nu[js][big]; sh_nu[js][big] = t;
+          t = sh_nd[js][kk]; sh_nd[js][kk] = sh_nd[js][big]; sh_nd[js][big] = t;
+          const int pk = sh_perm[js][kk]; sh_perm[js][kk] = sh_perm[js][big]; sh_perm[js][big] = pk;
+        }
+        double tail = 0.0;
+        for (int i = kk + 1; i < nn; ++i) tail += A[6 * i + kk] * A[6 * i + kk];
+        const double c0 = A[6 * kk + kk];
+        double beta, tau = 0.0, den = 0.0;
+        if (tail <= dmin) {
+          beta = c0;
+        } else {
+          beta = sqrt(c0 * c0 + tail);
+          if (c0 >= 0.0) beta = -beta;
+          den = c0 - beta;
+          tau = (beta - c0) / beta;
+        }
+        A[6 * kk + kk] = beta;
+        sh_c[js][0] = tau;
+        sh_c[js][1] = den;
+        sh_c[js][2] = tail <= dmin ? 1.0 : 0.0;
+      }
+      __syncthreads();
+      const double tau = sh_c[js][0], den = sh_c[js][1];
+      const bool zero = sh_c[js][2] != 0.0;
+      for (int i = kk + 1 + jl; i < nn; i += QL) A[6 * i + kk] = zero ? 0.0 : A[6 * i + kk] / den;
+      __syncthreads();
+      const bool upd = nn && tau != 0.0;
+      if (upd && jl > kk && jl <= N) {  // column jl's dot product with the Householder vector
+        double t = 0.0;
+        for (int i = kk + 1; i < nn; ++i) t += A[6 * i + kk] * A[6 * i + jl];
+        t += A[6 * kk + jl];
+        A[6 * kk + jl] -= tau * t;
+        sh_t[js][jl] = t;
+      }
+      __syncthreads();
+      if (upd)
+        for (int i = kk + 1 + jl; i < nn; i += QL) {
+          const double v = tau * A[6 * i + kk];
+          for (int j = kk + 1; j <= N; ++j) A[6 * i + j] -= v * sh_t[js][j];
+        }
+      __syncthreads();
+      if (nn && jl > kk && jl < N) {  // norm downdate of column jl
+        const double nuj = sh_nu[js][jl];
+        if (nuj != 0.0) {
+          double t = fabs(A[6 * kk + jl]) / nuj;
+          t = (1.0 + t) * (1.0 - t);
+          if (t < 0.0) t = 0.0;
+          const double qq = nuj / sh_nd[js][jl];
+          const double t2 = t * (qq * qq);
+          if (t2 <= downdate) {
+            double sq = 0.0;
+            for (int i = kk + 1; i < nn; ++i) sq += A[6 * i + jl] * A[6 * i + jl];
+            sh_nd[js][jl] = sh_nu[js][jl] = sqrt(sq);
+          } else {
+            sh_nu[js][jl] = nuj * sqrt(t);
+          }
+        }
+      }
+      __syncthreads();
+    }
+    // R, Q^T b and (row 5) scale (non-finite: no fit) and perm, to the job's lane-layout chunk
+    if (k < njobs) {
+      double* M = qj.rows + 6 * (size_t)qoff[k >> 6] + (k & 63);
+      for (int e = jl; e < 36; e += QL) {
+        const int i = e / 6, j = e % 6;
+        double v;
+        if (i < N) v = A[e];
+        else if (j == 0) v = fin ? scale : smax;
+        else v = (double)sh_perm[js][j - 1];
+        M[(size_t)e * 64] = v;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void quad_solve_kernel(DScene s, FilterDev F, QuadJobs qj,
+                                                         const unsigned long long* __restrict__ qsorted,
+                                                         const int* __restrict__ qoff, const int* __restrict__ kb_ptr,
+                                                         int njobs, int* __restrict__ reject) {
+  const int k = *kb_ptr + blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= njobs) return;
+  const int4 jb = qj.jobs[(int)(qsorted[k] & 0xffffffffull)];
+  const int n = jb.z;
+  const float* gx = qj.f + 3 * (size_t)jb.y;
+  const double* M = qj.rows + 6 * (size_t)qoff[k >> 6] + (k & 63);
+  const double scale = M[(size_t)30 * 64];
+  int perm[5];
+  for (int j = 0; j < 5; ++j) perm[j] = (int)M[(size_t)(31 + j) * 64];
+  quad_solve(s, F, M, perm, scale, isfinite(scale), jb.x, n, gx, gx + n, gx + 2 * n, reject);
 }
 
 // --------------------------------------------------------------------------- filterSmallGroups
@@ -2044,7 +2238,7 @@ hipError_t FilterBuffers::reserve(int n_, long long ncells_, int tnum_, int grid
   // (64 x their first n) sum to at most every job's n plus 64 x NB_CAP
   cap_qrows = std::min((size_t)cap_n * 48, (size_t)1 << 27);
   FCHK(dalloc(qf, cap_qrows * 3)); FCHK(dalloc(qrows, (cap_qrows + 64 * (size_t)NB_CAP) * 6)); FCHK(dalloc(qjobs, cap_n));
-  FCHK(dalloc(qctr, 2)); FCHK(dalloc(qkeys, cap_n)); FCHK(dalloc(qkeys2, cap_n));
+  FCHK(dalloc(qctr, 3)); FCHK(dalloc(qkeys, cap_n)); FCHK(dalloc(qkeys2, cap_n));
   FCHK(dalloc(qcrows, cap_n / 64 + 2)); FCHK(dalloc(qoff, cap_n / 64 + 2));
   size_t t1 = 0, t2 = 0;
   FCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, t1, keys, keys2, (int)ne));
@@ -2458,16 +2652,29 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
         hipLaunchKernelGGL(quad_chunk_rows_kernel, dim3(nblk(nch)), dim3(256), 0, st, B.qkeys2, nj, B.qcrows);
         tb = B.temp_bytes;
         FCHK(hipcub::DeviceScan::ExclusiveSum(B.temp, tb, B.qcrows, B.qoff, nch, st));
+        int dev = 0, cus = 0;
+        FCHK(hipGetDevice(&dev));
+        FCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        // fits of at most nq rows: quad_qr_kernel (rows in LDS) + quad_solve_kernel; the rest (the
+        // sorted prefix [0, kb)) one lane per job.  PMVS_QUAD_LDS_ROWS=0: every fit one lane per job.
+        int nq = 96;
+        if (const char* e = getenv("PMVS_QUAD_LDS_ROWS")) nq = std::max(0, std::min(160, atoi(e)));
+        int* kb = reinterpret_cast<int*>(B.qctr + 2);
+        if (nq > 0) hipLaunchKernelGGL(quad_split_kernel, dim3(nblk(nj)), dim3(256), 0, st, B.qkeys2, nj, nq, kb);
         unsigned qgrid = nblk(nj);
         if (const char* e = getenv("PMVS_QUAD_WAVES_PER_CU"))  // 0 = one lane per job, no cap
-          if (atoi(e) > 0) {
-            int dev = 0, cus = 0;
-            FCHK(hipGetDevice(&dev));
-            FCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-            qgrid = std::min(qgrid, (unsigned)std::max(1, cus * atoi(e) / 4));  // 4 wavefronts per 256-lane block
-          }
+          if (atoi(e) > 0) qgrid = std::min(qgrid, (unsigned)std::max(1, cus * atoi(e) / 4));  // 4 wavefronts per 256-lane block
         hipLaunchKernelGGL(quad_lane_kernel, dim3(qgrid), dim3(256), 0, st, s, c.dev(), qj, B.qkeys2, B.qoff, nj,
-                           B.flags);
+                           B.flags, nq > 0 ? kb : nullptr);
+        if (nq > 0) {
+          int wpc = 4;
+          if (const char* e = getenv("PMVS_QUAD_QR_WAVES_PER_CU")) wpc = std::max(1, atoi(e));
+          const unsigned qrgrid = std::min((unsigned)(cus * wpc), (unsigned)((nj + 64 / QL - 1) / (64 / QL)));
+          const size_t lds = (size_t)(64 / QL) * nq * 6 * sizeof(double);
+          hipLaunchKernelGGL(quad_qr_kernel, dim3(qrgrid), dim3(64), lds, st, qj, B.qkeys2, B.qoff, kb, nj, nq);
+          hipLaunchKernelGGL(quad_solve_kernel, dim3(nblk(nj)), dim3(256), 0, st, s, c.dev(), qj, B.qkeys2, B.qoff, kb,
+                             nj, B.flags);
+        }
       }
     }
   }
@@ -2787,7 +2994,9 @@ static hipError_t grow_keep(T*& p, size_t& cap, size_t need, size_t used, hipStr
 struct CommitWork {
   int *stc = nullptr, *nacc = nullptr, *aoff = nullptr, *vals = nullptr, *vals2 = nullptr, *pos = nullptr,
       *head = nullptr, *segid = nullptr, *seghead = nullptr, *segptr = nullptr, *segfirst = nullptr,
-      *slot2 = nullptr, *flag = nullptr, *scan = nullptr, *ctr = nullptr, *pbits = nullptr;
+      *slot2 = nullptr, *flag = nullptr, *scan = nullptr, *ctr = nullptr, *pbits = nullptr,
+      *segmin = nullptr;  // cm_tail_kernel: per target cell, kSegFree between launches
+  size_t cap_seg = 0;
   unsigned long long *keys = nullptr, *keys2 = nullptr;
   unsigned char* dec = nullptr;
   int2* push = nullptr;
@@ -2795,7 +3004,7 @@ struct CommitWork {
   size_t cap_k = 0, cap_a = 0, temp_bytes = 0;
   ~CommitWork() {
     void* ps[] = {stc, nacc, aoff, vals, vals2, pos, head, segid, seghead, segptr, segfirst, slot2, flag, scan, ctr,
-                  pbits, keys, keys2, dec, push, temp};
+                  pbits, keys, keys2, dec, push, temp, segmin};
     for (void* p : ps)
       if (p) (void)hipFree(p);
   }
@@ -2885,21 +3094,13 @@ __global__ void cm_first_kernel(const unsigned long long* __restrict__ keys, con
   segfirst[s] = (p < end) ? (int)(keys[p] & 0xffffffffull) : -1;
 }
 
-// Decides every undecided candidate that is the first undecided one in all of its cells.
-// ctr: [0] decided this call, [1] fail_commit, [2] invalid.
-__global__ void cm_decide_kernel(DScene s, int nk, const int* __restrict__ slot2, const int* __restrict__ rec,
-                                 const int* __restrict__ aoff, const int* __restrict__ nacc, const int* __restrict__ pos,
-                                 const int* __restrict__ segid, const int* __restrict__ segfirst,
-                                 unsigned char* __restrict__ dec, int* __restrict__ stc, int* __restrict__ flag,
-                                 unsigned char* __restrict__ counts, unsigned char* __restrict__ occ, int cthr, int check,
-                                 int* __restrict__ ctr) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= nk || dec[k]) return;
-  for (int e = aoff[k], ee = aoff[k] + nacc[k]; e < ee; ++e)
-    if (segfirst[segid[pos[e]]] != k) return;
-  const int* r = rec + (size_t)slot2[k] * kRecInts;
+// The decision of candidate k (record r) once it is the first undecided candidate in all of its
+// cells: checkCounts with the committed state (expand.cpp:309-322), then updateCounts
+// (expand.cpp:325-406) + addPatch's pgrids registration.  ctr: [0] decided, [1] fail_commit.
+__device__ __forceinline__ void cm_apply(const DScene& s, int k, const int* r, unsigned char* dec, int* stc, int* flag,
+                                         unsigned char* counts, unsigned char* occ, int cthr, int check, int* ctr) {
   int st = 0;
-  if (check) {  // checkCounts with the committed state (expand.cpp:309-322)
+  if (check) {
     int full = 0, empty = 0;
     for (int i = 0; i < r[2]; ++i) {
       const int c = r[5 + i];
@@ -2910,7 +3111,7 @@ __global__ void cm_decide_kernel(DScene s, int nk, const int* __restrict__ slot2
     const bool fail = (s.depth <= 1) ? (empty < s.minImageNum && full != 0) : (empty < s.minImageNum - 1 && full != 0);
     if (fail) st = 4;
   }
-  if (st == 0) {  // updateCounts (expand.cpp:325-406) + addPatch's pgrids registration
+  if (st == 0) {
     int full = 0, empty = 0;
     auto touch = [&](int c) {
       const unsigned char cc = counts[c];
@@ -2929,6 +3130,92 @@ __global__ void cm_decide_kernel(DScene s, int nk, const int* __restrict__ slot2
   }
   dec[k] = 1;
   atomicAdd(&ctr[0], 1);
+}
+
+// Decides every undecided candidate that is the first undecided one in all of its cells.
+// ctr: [0] decided this call, [1] fail_commit, [2] invalid.
+__global__ void cm_decide_kernel(DScene s, int nk, const int* __restrict__ slot2, const int* __restrict__ rec,
+                                 const int* __restrict__ aoff, const int* __restrict__ nacc, const int* __restrict__ pos,
+                                 const int* __restrict__ segid, const int* __restrict__ segfirst,
+                                 unsigned char* __restrict__ dec, int* __restrict__ stc, int* __restrict__ flag,
+                                 unsigned char* __restrict__ counts, unsigned char* __restrict__ occ, int cthr, int check,
+                                 int* __restrict__ ctr) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nk || dec[k]) return;
+  for (int e = aoff[k], ee = aoff[k] + nacc[k]; e < ee; ++e)
+    if (segfirst[segid[pos[e]]] != k) return;
+  cm_apply(s, k, rec + (size_t)slot2[k] * kRecInts, dec, stc, flag, counts, occ, cthr, check, ctr);
+}
+
+// The commit's last rounds (or all of them, for a wave with few refined candidates) in one
+// workgroup, over the undecided candidates only: a round takes, per cell, the smallest undecided
+// k touching it (atomicMin into segmin, which holds kSegFree outside this kernel), decides every k
+// that is the smallest one in all of its cells -- the rule cm_first + cm_decide apply with the
+// sorted (cell, k) segments -- and keeps the others for the next round.  No launch or host sync
+// per round.  Winners of one round share no cell, so their updates do not interact.
+constexpr int kTailMax = 6144, kTailThreads = 1024;
+constexpr int kSegFree = 0x7f7f7f7f;  // hipMemset byte 0x7f
+__device__ __forceinline__ int cm_cell(const int* r, int i) {  // access i of a record, in cm_emit's order
+  if (i < r[2]) return r[5 + i];
+  i -= r[2];
+  if (i < r[3]) return r[5 + PMVS_MAX_IMAGES + i];
+  return r[5 + 2 * PMVS_MAX_IMAGES + (i - r[3])];
+}
+__global__ __launch_bounds__(kTailThreads) void cm_tail_kernel(DScene s, int nk, const int* __restrict__ slot2,
+                                                               const int* __restrict__ rec, unsigned char* dec, int* stc,
+                                                               int* flag, unsigned char* counts, unsigned char* occ,
+                                                               int cthr, int check, int* ctr, int* segmin) {
+  __shared__ int ua[kTailMax], ub[kTailMax];
+  __shared__ unsigned char win[kTailMax];
+  __shared__ int nu, nn;
+  const int tid = threadIdx.x;
+  if (tid == 0) nu = 0;
+  __syncthreads();
+  for (int k = tid; k < nk; k += kTailThreads)
+    if (!dec[k]) {
+      const int p = atomicAdd(&nu, 1);
+      if (p < kTailMax) ua[p] = k;  // the host launches this kernel with at most kTailMax undecided
+    }
+  __syncthreads();
+  int* cur = ua;
+  int* nxt = ub;
+  for (;;) {
+    const int m = imin(nu, kTailMax);
+    if (m == 0) break;
+    for (int u = tid; u < m; u += kTailThreads) {
+      const int k = cur[u];
+      const int* r = rec + (size_t)slot2[k] * kRecInts;
+      const int na = r[2] + r[3] + r[4];
+      for (int i = 0; i < na; ++i) atomicMin(&segmin[cm_cell(r, i)], k);
+    }
+    __syncthreads();
+    for (int u = tid; u < m; u += kTailThreads) {
+      const int k = cur[u];
+      const int* r = rec + (size_t)slot2[k] * kRecInts;
+      const int na = r[2] + r[3] + r[4];
+      unsigned char w = 1;
+      for (int i = 0; i < na && w; ++i)  // atomic loads: the minima live in L2, not in this CU's L1
+        if (__hip_atomic_load(&segmin[cm_cell(r, i)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != k) w = 0;
+      win[u] = w;
+    }
+    if (tid == 0) nn = 0;
+    __syncthreads();
+    for (int u = tid; u < m; u += kTailThreads) {
+      const int k = cur[u];
+      const int* r = rec + (size_t)slot2[k] * kRecInts;
+      const int na = r[2] + r[3] + r[4];
+      for (int i = 0; i < na; ++i)
+        __hip_atomic_store(&segmin[cm_cell(r, i)], kSegFree, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (win[u]) cm_apply(s, k, r, dec, stc, flag, counts, occ, cthr, check, ctr);
+      else nxt[atomicAdd(&nn, 1)] = k;
+    }
+    __syncthreads();
+    if (tid == 0) nu = nn;
+    int* t = cur;
+    cur = nxt;
+    nxt = t;
+    __syncthreads();
+  }
 }
 
 // flags of the non-refined candidates (0) and the outcome counters: ctr[3] fail_prep, [4] fail_pre,
@@ -3135,7 +3422,9 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
   FCHK(hipStreamSynchronize(st));
   const int na = hv[0], nlive = hv[1];
   int nseg = 0;
-  if (na > 0) {
+  const char* tail_env = getenv("PMVS_COMMIT_TAIL");  // tests: 0 = grid-wide rounds only, n = the last n
+  const int tail_max = tail_env ? std::max(0, std::min(kTailMax, atoi(tail_env))) : kTailMax;
+  if (na > 0 && nlive > tail_max) {  // the (cell, k) segments of the grid-wide rounds
     if ((size_t)na + 1 > W.cap_a) {
       const size_t c = std::max((size_t)na + 1, 2 * W.cap_a);
       FCHK(cm_grow(W.keys, c)); FCHK(cm_grow(W.keys2, c)); FCHK(cm_grow(W.vals, c)); FCHK(cm_grow(W.vals2, c));
@@ -3161,7 +3450,18 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
   }
   // rounds: every round decides at least the lowest undecided candidate
   int decided = 0;
+
   for (int round = 0; decided < nlive; ) {
+    if (nlive - decided <= tail_max) {  // the remaining rounds in one workgroup (cm_tail_kernel)
+      if (W.cap_seg < X.cap_cnt) {
+        FCHK(cm_grow(W.segmin, X.cap_cnt));
+        FCHK(memset_big(W.segmin, 0x7f, X.cap_cnt * sizeof(int), st));
+        W.cap_seg = X.cap_cnt;
+      }
+      hipLaunchKernelGGL(cm_tail_kernel, dim3(1), dim3(kTailThreads), 0, st, s, nk, W.slot2, X.crec, W.dec, W.stc, W.flag,
+                         X.counts, X.occ, cthr, check ? 1 : 0, W.ctr, W.segmin);
+      break;
+    }
     for (int r = 0; r < 4; ++r, ++round) {
       if (nseg > 0)
         hipLaunchKernelGGL(cm_first_kernel, dim3(nblk(nseg)), dim3(256), 0, st, W.keys2, W.dec, W.seghead, nseg, W.segptr,

@@ -110,7 +110,7 @@ struct FilterBuffers {
   float* qf = nullptr;
   double* qrows = nullptr;
   int4* qjobs = nullptr;
-  unsigned long long* qctr = nullptr;  // [0] rows used, [1] low 32 bits: jobs
+  unsigned long long* qctr = nullptr;  // [0] rows used, [1] low 32 bits: jobs, [2] low 32 bits: quad_split_kernel's kb
   unsigned long long *qkeys = nullptr, *qkeys2 = nullptr;  // jobs by descending row count
   int *qcrows = nullptr, *qoff = nullptr;                  // per 64-job chunk: pool rows, offsets
   size_t cap_qrows = 0;
