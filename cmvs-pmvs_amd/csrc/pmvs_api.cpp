@@ -989,7 +989,7 @@ pmvs_status pmvs_filter_run(pmvs_scene* sc, pmvs_patch* patches, int32_t n, int3
   HIPCHK(hipMemcpyAsync(patches, sc->fpatches.p, (size_t)n * sizeof(pmvs_patch), hipMemcpyDeviceToHost, sc->stream));
   HIPCHK(hipMemcpyAsync(keep, sc->fkeep.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, sc->stream));
   HIPCHK(hipStreamSynchronize(sc->stream));
-  if (overflow) return fail(PMVS_EUNSUPPORTED, "filterNeighbor: %d patches with more than 1024 neighbours", overflow);
+  if (overflow) return fail(PMVS_EUNSUPPORTED, "filterNeighbor: %d patches with more than 16384 neighbours", overflow);
   if (stats) {
     float ms = 0;
     (void)hipEventElapsedTime(&ms, sc->ev0, sc->ev1);
@@ -1144,7 +1144,7 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
   if (handled) *handled = e != hipSuccess;  // expand_pass ends every failure with a header all ranks see
   if (e == hipErrorOutOfMemory)
     return fail(PMVS_EUNSUPPORTED,
-                "expansion: capacity %d exceeded, a patch has more than 1024 neighbours, or a patch's image / "
+                "expansion: capacity %d exceeded, a patch has more than 16384 neighbours, or a patch's image / "
                 "visible-target list exceeds %d entries", cap, PMVS_MAX_IMAGES);
   if (e == hipErrorUnknown && sh.world > 1) return fail(PMVS_EDEVICE, "expansion: the shard exchange or another rank failed");
   HIPCHK(e);
@@ -1209,7 +1209,7 @@ pmvs_status filter_device(pmvs_scene* sc, int n, pmvs_filter_stats* stats, bool*
   if (test_local_fail(sc, 's')) return fail(PMVS_EDEVICE, "filter pass: injected local failure (test)");
   HIPCHK(hipStreamSynchronize(sc->stream));
   if (handled) *handled = true;  // overflow is all-gathered: every rank returns it together
-  if (overflow) return fail(PMVS_EUNSUPPORTED, "filterNeighbor: %d patches with more than 1024 neighbours", overflow);
+  if (overflow) return fail(PMVS_EUNSUPPORTED, "filterNeighbor: %d patches with more than 16384 neighbours", overflow);
   if (stats) {
     float ms = 0;
     (void)hipEventElapsedTime(&ms, sc->ev0, sc->ev1);

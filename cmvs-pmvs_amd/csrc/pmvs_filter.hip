@@ -54,19 +54,22 @@ inline void poison_alloc(void* p, size_t bytes) {
   }
 }
 
-constexpr int NB_CAP = 1024;  // neighbours per patch in filterNeighbor (overflow is reported)
+// Neighbours per patch the walks hold in LDS.  The NB_CAP form runs every walk; the few patches
+// with more unique neighbours are walked again by the NB_CAP_BIG form (NbLdsT<16384>, about 130 KB
+// of LDS, one workgroup per CU); only beyond NB_CAP_BIG is the run an error.
+constexpr int NB_CAP = 1024;
+constexpr int NB_CAP_BIG = 16384;
 // Global scratch per persistent workgroup of the neighbour walks (doubles): the lls rows M
-// (5 NB_CAP), its right-hand side r (NB_CAP), then the filterQuad coordinates fx, fy, fz as floats
-// (1.5 NB_CAP).  Kept out of LDS so NbLds stays ~8 KB (occupancy of the latency-bound walks).
+// (5 CAP), its right-hand side r (CAP), then the filterQuad coordinates fx, fy, fz as floats
+// (1.5 CAP).  Kept out of LDS so NbLds stays ~8 KB (occupancy of the latency-bound walks).
 constexpr int NB_SCR = NB_CAP * 8;
+constexpr int NB_GRID_BIG = 32;  // workgroups of the NB_CAP_BIG re-walks
 // gather_neighbors: cell slots per lane per round, entries per lane per test round
 constexpr int NB_SK = 2;
 constexpr int NB_NE = 2;
 // Persistent workgroups per CU-grid unit for the NbLds kernels (neighbor_kernel, depth_post_kernel,
 // empty_blocks_kernel): twice the organizer grid, since ~8 KB of LDS and <= 107 VGPRs leave room.
 constexpr int NB_GRID_MULT = 2;
-// doubles of NbLds.nb + NbLds.seq that filterQuad's lls rows (6 per neighbour) may use
-constexpr int NB_LLS_LDS = (NB_CAP * 2 * 4) / 8;
 __device__ __forceinline__ int lane_id_w() { return threadIdx.x & 63; }
 // Wave-uniform copies (SGPR) of values that are uniform by construction but loaded from memory:
 // every branch or loop around a barrier is driven by one of these, never by a VGPR value.
@@ -126,6 +129,7 @@ struct FilterDev {
   int npg, nvp;        // entries in the pgrids / vpgrids lists
   int* err;            // [0] count, [1] first code (defensive bounds checks)
   int* lovf;           // patches whose image / vimage list would exceed PMVS_MAX_IMAGES (an error, never a clamp)
+  int nb_softcap;      // tests (PMVS_NB_SOFTCAP): neighbour capacity of the NB_CAP walks, to exercise the re-walks
   // Expansion only: registrations committed since the CSR lists were built, as per-cell chains
   // (head per cell, -1 = empty; item/next in a shared entry pool).  Every expansion reader is
   // insensitive to the order inside a cell list (findNeighbors sorts and uniques, computeGain
@@ -632,10 +636,8 @@ __global__ void exact_after_ref_kernel(DScene s, const pmvs_patch* __restrict__ 
 }
 
 // --------------------------------------------------------------------------- filterNeighbor
-struct NbLds {
+struct NbSmall {
   int sb[64 * NB_SK], so[64 * NB_SK];  // gather_neighbors: per-slot list start (bit 31: vpgrids), flattened offset
-  alignas(8) int nb[NB_CAP];   // nb and seq are adjacent: filterQuad's lls rows reuse them
-  float seq[NB_CAP];  // values summed in the reference's order by one lane (filterQuad)
   float units[PMVS_MAX_IMAGES];
   int cnt, overflow;
   double f[5];
@@ -644,6 +646,15 @@ struct NbLds {
   float x[5];
   double jw[5][5], ju[5][5], jv[5][5], sv[5], jy[5];  // lls5_wave's Jacobi stage (lane 0)
 };
+template <int CAP>
+struct NbLdsT : NbSmall {
+  static_assert((CAP & (CAP - 1)) == 0 && CAP >= 64, "power of two");
+  static constexpr int kCap = CAP;
+  static constexpr int kLlsRows = (CAP * 2 * 4) / 8;  // doubles of nb + seq filterQuad's lls rows may use
+  alignas(8) int nb[CAP];  // nb and seq are adjacent: filterQuad's lls rows reuse them
+  float seq[CAP];          // values summed in the reference's order by one lane (filterQuad)
+};
+using NbLds = NbLdsT<NB_CAP>;
 
 // Cmylapack::lls (mylapack.cpp:102-149, Eigen JacobiSVD(ThinU | ThinV).solve) with Eigen's algorithm,
 // the same operation order as the oracle's lls5 (oracle/filter_oracle.h): column-pivoting
@@ -653,7 +664,7 @@ struct NbLds {
 typedef __attribute__((address_space(3))) double lds_f64;
 __device__ __forceinline__ double dmaxd(double a, double b) { return (a < b) ? b : a; }  // std::max
 // lls5_wave's 5 x 5 stage on lane 0 (two-sided Jacobi, signs, sort, rank-thresholded solve).
-__device__ __attribute__((noinline)) void lls5_jacobi(NbLds& L, const double* M, const double* r, double scale) {
+__device__ __attribute__((noinline)) void lls5_jacobi(NbSmall& L, const double* M, const double* r, double scale) {
   constexpr int N = 5;
   const double eps = 2.220446049250313e-16, dmin = 2.2250738585072014e-308;
     // L lives in LDS in every caller: LDS-typed pointers give 32-bit addresses with immediate offsets
@@ -777,7 +788,7 @@ __device__ __attribute__((noinline)) void lls5_jacobi(NbLds& L, const double* M,
 // occupancy is register-limited); M / r rows in global scratch, the 5 x 5 stage in NbLds.  The
 // one-lane row loops are unrolled by 8 so their (independent) row loads are in flight together;
 // the sums stay sequential in row order.
-__device__ __attribute__((noinline)) void lls5_wave(NbLds& L, double* M, double* r, int n) {
+__device__ __attribute__((noinline)) void lls5_wave(NbSmall& L, double* M, double* r, int n) {
   constexpr int N = 5;
   const double eps = 2.220446049250313e-16, dmin = 2.2250738585072014e-308;
   const int lane = lane_id_w();
@@ -950,7 +961,7 @@ __device__ int sort_unique_lds(int* a, int n, int* cnt_slot) {
 // (patchOrganizerS.cpp:527-631) + filterQuad (filter.cpp:387-446), one wavefront per patch.
 // CExpand::computeRadius (expand.cpp:182-198): second smallest of COptim::computeUnits
 // (optim.cpp:446-471) times csize.  All lanes call; result in every lane.
-__device__ float compute_radius_wave(const DScene& s, NbLds& L, const pmvs_patch& q) {
+__device__ float compute_radius_wave(const DScene& s, NbSmall& L, const pmvs_patch& q) {
   const int lane = lane_id_w();
   const int ni = uni(q.num_images);
   __syncthreads();
@@ -991,39 +1002,43 @@ __device__ __forceinline__ int wave_excl_scan_w(int v) {
 // walked images' cells is met once per image; isNeighbor(patch, j) does not depend on the cell it
 // was found in, so only the first meeting is tested (the hit list's final sort + unique removes
 // duplicates either way).  A crowded probe sequence just tests again.
-__device__ __forceinline__ void nb_seen_clear(NbLds& L) {
+template <int CAP>
+__device__ __forceinline__ void nb_seen_clear(NbLdsT<CAP>& L) {
   int* tab = reinterpret_cast<int*>(L.seq);
-  for (int i = lane_id_w(); i < NB_CAP; i += 64) tab[i] = -1;
+  for (int i = lane_id_w(); i < CAP; i += 64) tab[i] = -1;
 }
-__device__ __forceinline__ bool nb_first_visit(NbLds& L, int j) {
+template <int CAP>
+__device__ __forceinline__ bool nb_first_visit(NbLdsT<CAP>& L, int j) {
   int* tab = reinterpret_cast<int*>(L.seq);
-  unsigned h = ((unsigned)j * 2654435761u) >> 22;  // 10 bits: NB_CAP slots
+  constexpr int kBits = __builtin_ctz(CAP);
+  unsigned h = ((unsigned)j * 2654435761u) >> (32 - kBits);  // kBits bits: CAP slots
   for (int probe = 0; probe < 16; ++probe) {
     const int old = atomicCAS(&tab[h], -1, j);
     if (old == -1) return true;
     if (old == j) return false;
-    h = (h + 1) & (NB_CAP - 1);
+    h = (h + 1) & (CAP - 1);
   }
   return true;
 }
-static_assert(NB_CAP == 1024, "nb_first_visit hashes to 10 bits");
 
 // Appends the hits of one 64-lane round in lane order (ballot), compacting the buffer (sort +
 // unique) when it nears capacity, as the reference's final sort/unique would (same set).
-__device__ __forceinline__ void nb_append(NbLds& L, bool hit, int j) {
+// cap: the capacity in use (CAP, or less under PMVS_NB_SOFTCAP in tests).
+template <int CAP>
+__device__ __forceinline__ void nb_append(NbLdsT<CAP>& L, bool hit, int j, int cap) {
   const int lane = lane_id_w();
   const unsigned long long mask = __ballot(hit);
   const int before = __popcll(mask & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
   const int pos = L.cnt + before;
   if (hit) {
-    if (pos < NB_CAP) L.nb[pos] = j;
+    if (pos < cap) L.nb[pos] = j;
     else L.overflow = 1;
   }
   __syncthreads();
   if (lane == 0) L.cnt += __popcll(mask);
   __syncthreads();
   const int cnt = uni(L.cnt);
-  if (cnt > NB_CAP - 64 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(cnt, NB_CAP), &L.cnt);
+  if (cnt > cap - 64 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(cnt, cap), &L.cnt);
 }
 
 // CPatchOrganizerS::findNeighbors(patch, neighbors, lock, scale, margin, skipvis)
@@ -1033,9 +1048,12 @@ __device__ __forceinline__ void nb_append(NbLds& L, bool hit, int j) {
 // list bounds load in parallel); the cells' entries are then flattened and tested 64 per round.
 // Expansion-time chain entries (FilterDev delta) are walked per lane.  The neighbour SET is the
 // reference's; the visiting order only matters for the buffer's compaction points.
-__device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, const pmvs_patch& q, float scale,
+template <int CAP>
+__device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLdsT<CAP>& L, const pmvs_patch& q, float scale,
                                 int margin, int skipvis) {
   const int lane = lane_id_w();
+  // the capacity in use: CAP (a test soft cap, F.nb_softcap, applies to the NB_CAP form only)
+  const int cap = (CAP == NB_CAP && F.nb_softcap > 0) ? imin(CAP, F.nb_softcap) : CAP;
   const int ni = uni(q.num_images);
   const float radius = (float)(1.5 * margin * (double)compute_radius_wave(s, L, q));
   float unit = 0.0f;
@@ -1135,33 +1153,33 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, c
       }
 #pragma unroll
       for (int u = 0; u < NB_NE; ++u)
-        if (ib + u * 64 < tot) nb_append(L, hv[u], jv[u] < 0 ? 0 : jv[u]);
+        if (ib + u * 64 < tot) nb_append(L, hv[u], jv[u] < 0 ? 0 : jv[u], cap);
     }
     // entries committed by earlier expansion waves (short chains, walked per lane)
 #pragma unroll
     for (int k = 0; k < NB_SK; ++k) {
       const int head = hk[k];
       if (F.pg_dhead && __ballot(head >= 0) != 0ull) {
-        if (uni(L.cnt) > NB_CAP / 2 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(uni(L.cnt), NB_CAP), &L.cnt);
+        if (uni(L.cnt) > cap / 2 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(uni(L.cnt), cap), &L.cnt);
         for (int ent = head; ent >= 0; ent = F.d_next[ent]) {
           const int j = F.d_item[ent];
           if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 15); continue; }
           if (nb_first_visit(L, j) && is_neighbor_h(q, F.hot[j], unit, thr, radius, true)) {
             const int pos = atomicAdd(&L.cnt, 1);
-            if (pos < NB_CAP) L.nb[pos] = j;
+            if (pos < cap) L.nb[pos] = j;
             else L.overflow = 1;
           }
         }
         __syncthreads();
-        if (lane == 0 && L.cnt > NB_CAP) L.cnt = NB_CAP;
+        if (lane == 0 && L.cnt > cap) L.cnt = cap;
         __syncthreads();
         const int cnt = uni(L.cnt);
-        if (cnt > NB_CAP - 64 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(cnt, NB_CAP), &L.cnt);
+        if (cnt > cap - 64 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(cnt, cap), &L.cnt);
       }
     }
     __syncthreads();
   }
-  const int n = imin(uni(L.cnt), NB_CAP);
+  const int n = imin(uni(L.cnt), cap);
 #if defined(NBX_SKIP_SORT)  // timing experiment only (tools): the final sort skipped
   return n;
 #else
@@ -1172,7 +1190,8 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLds& L, c
 // CFilter::filterQuad (filter.cpp:387-446) on the neighbours in L.nb[0..n); returns 1 = reject.
 // fout != nullptr: the rows' fx[n], fy[n], fz[n] go there and the fit is left to quad_lane_kernel
 // (returns -1).
-__device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, double* M, double* r,
+template <int CAP>
+__device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLdsT<CAP>& L, double* M, double* r,
                                 const pmvs_patch& q, int n, float* fout = nullptr) {
   const int lane = lane_id_w();
   n = uni(n);
@@ -1185,9 +1204,9 @@ __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, d
   ydir[0] = z[1] * xdir[2] - z[2] * xdir[1];
   ydir[1] = z[2] * xdir[0] - z[0] * xdir[2];
   ydir[2] = z[0] * xdir[1] - z[1] * xdir[0];
-  float* gx = fout ? fout : reinterpret_cast<float*>(r + NB_CAP);  // fx, fy, fz (workgroup's global scratch)
-  float* gy = gx + (fout ? n : NB_CAP);
-  float* gz = gy + (fout ? n : NB_CAP);
+  float* gx = fout ? fout : reinterpret_cast<float*>(r + CAP);  // fx, fy, fz (workgroup's global scratch)
+  float* gy = gx + (fout ? n : CAP);
+  float* gz = gy + (fout ? n : CAP);
   for (int a = lane; a < n; a += 64) {  // the distances in parallel, their sum in order below
     float d[4];
     for (int k = 0; k < 4; ++k) d[k] = F.hot[L.nb[a]].coord[k] - q.coord[k];
@@ -1211,7 +1230,7 @@ __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, d
   // The lls rows: in LDS over the neighbour list and seq[] (free until the residuals) when they
   // fit -- the solver's many wave barriers then drain LDS traffic only -- else in global scratch.
   __syncthreads();
-  if (n * 6 <= NB_LLS_LDS) {
+  if (n * 6 <= NbLdsT<CAP>::kLlsRows) {
     M = reinterpret_cast<double*>(L.nb);
     r = M + (size_t)n * 5;
   }
@@ -1262,28 +1281,42 @@ __device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLds& L, d
 // Sharded loop (world > 1): a rank tests only the patches whose reference image it owns
 // (target t belongs to rank t mod world); the others are left to their owners
 // and the reject flags are all-gathered afterwards (filter_pass).
+// Overflow (more than CAP unique neighbours): with `ovf` (the NB_CAP form) the patch goes on the
+// re-walk list ovf.items and the NB_CAP_BIG form (ovf.only: walks that list) decides it; without,
+// it is counted in `overflow` (an error for the run).
+struct NbOverflow {
+  int* items = nullptr;        // NB_CAP form: the overflowed work items (patch / parent / candidate)
+  int* count = nullptr;        // their number
+  const int* only = nullptr;   // NB_CAP_BIG form: walk items only[0 .. *only_n)
+  const int* only_n = nullptr;
+};
+template <int CAP>
 __global__ __launch_bounds__(64) void neighbor_kernel(DScene s, FilterDev F, double* __restrict__ scratch,
                                                       int* __restrict__ reject, int* __restrict__ overflow,
                                                       int* __restrict__ queue, int* __restrict__ dbg_counts, int rank,
-                                                      int world, QuadJobs qj) {
-  __shared__ NbLds L;
+                                                      int world, QuadJobs qj, NbOverflow ov) {
+  __shared__ NbLdsT<CAP> L;
   const int lane = threadIdx.x;
-  double* M = scratch + (size_t)blockIdx.x * NB_SCR;
-  double* r = M + (size_t)NB_CAP * 5;
+  double* M = scratch + (size_t)blockIdx.x * (CAP * 8);
+  double* r = M + (size_t)CAP * 5;
   for (;;) {
     int i = 0;
     if (lane == 0) i = atomicAdd(queue, 1);
     i = __builtin_amdgcn_readfirstlane(i);  // work-queue index, wave-uniform (SGPR)
-    if (i >= F.nalive) break;
-    const int p = F.order[i];
+    if (i >= (ov.only ? *ov.only_n : F.nalive)) break;
+    const int p = __builtin_amdgcn_readfirstlane(ov.only ? ov.only[i] : F.order[i]);
     const pmvs_patch& q = F.P[p];
     int rej = 0;  // _fix patches are kept; no early `continue` (see depth_post_kernel)
     const bool mine = world <= 1 || uni(q.images[0]) % world == rank;
     if (mine && !uni(q.fix)) {
       const int n = gather_neighbors(s, F, L, q, 4.0f, 2, 1);
-      if (lane == 0 && L.overflow) atomicAdd(overflow, 1);
+      const bool rewalk = ov.items && uni(L.overflow);
+      if (lane == 0 && rewalk) ov.items[atomicAdd(ov.count, 1)] = p;
+      if (lane == 0 && L.overflow && !ov.items) atomicAdd(overflow, 1);
       if (lane == 0 && dbg_counts) dbg_counts[p] = L.overflow ? -n : n;
-      if (n < 6) {
+      if (rewalk) {
+        rej = 0;  // decided by the NB_CAP_BIG re-walk
+      } else if (n < 6) {
         rej = 1;
       } else {
         // room for the rows in the deferred-fit buffers? (else the fit runs here, same result)
@@ -1829,20 +1862,24 @@ __global__ void group_edges_kernel(DScene s, FilterDev F, int pass, const int* _
 // CExpand::findEmptyBlocks (expand.cpp:95-180), one wavefront per parent: the six angular
 // bins around the patch that hold no neighbour (findNeighbors(patch, ., 1, 4.0f), margin 1,
 // vimages included) and were not tried before (_dflag) get a candidate at `radius`.
+template <int CAP>
 __global__ __launch_bounds__(64) void empty_blocks_kernel(DScene s, FilterDev F, const int* __restrict__ parents, int np,
                                                           float* __restrict__ cand_coord, int* __restrict__ cand_ok,
-                                                          int* __restrict__ queue, int* __restrict__ overflow) {
-  __shared__ NbLds L;
+                                                          int* __restrict__ queue, int* __restrict__ overflow, NbOverflow ov) {
+  __shared__ NbLdsT<CAP> L;
   const int lane = threadIdx.x;
   for (;;) {
-    int k = 0;
-    if (lane == 0) k = atomicAdd(queue, 1);
-    k = __builtin_amdgcn_readfirstlane(k);
-    if (k >= np) break;
+    int i = 0;
+    if (lane == 0) i = atomicAdd(queue, 1);
+    i = __builtin_amdgcn_readfirstlane(i);
+    if (i >= (ov.only ? *ov.only_n : np)) break;
+    const int k = ov.only ? __builtin_amdgcn_readfirstlane(ov.only[i]) : i;
     const pmvs_patch& q = F.P[parents[k]];
     const float radius = compute_radius_wave(s, L, q);
     const int n = gather_neighbors(s, F, L, q, 4.0f, 1, 0);
-    if (lane == 0 && L.overflow) atomicAdd(overflow, 1);
+    // overflowed: this parent's bins are rewritten by the NB_CAP_BIG re-walk
+    if (lane == 0 && L.overflow && ov.items) ov.items[atomicAdd(ov.count, 1)] = k;
+    if (lane == 0 && L.overflow && !ov.items) atomicAdd(overflow, 1);
     float xdir[4] = {0, 0, 0, 0}, ydir[4] = {0, 0, 0, 0};
     const float* z = q.normal;
     if (fabs((double)z[0]) > 0.5) { xdir[0] = z[1]; xdir[1] = -z[0]; xdir[2] = 0; }
@@ -1978,20 +2015,22 @@ __global__ void prepare_kernel(DScene s, FilterDev F, const unsigned char* __res
 // each: setVImagesVGrids against the model's depth maps and, at depth >= 2, check() =
 // computeGain + findNeighbors(patch, ., 1, 4, 2) + filterQuad.  out_status: 0 accepted,
 // 2 preProcess failed, 3 postProcess failed.
+template <int CAP>
 __global__ __launch_bounds__(64) void depth_post_kernel(DScene s, FilterDev F, const pmvs_refined* __restrict__ res,
                                                         int m, pmvs_patch* __restrict__ outp, int* __restrict__ out_status,
                                                         double* __restrict__ scratch, int* __restrict__ queue,
-                                                        int* __restrict__ overflow) {
-  __shared__ NbLds L;
+                                                        int* __restrict__ overflow, NbOverflow ov) {
+  __shared__ NbLdsT<CAP> L;
   __shared__ pmvs_patch Q;  // the patch is built in LDS and stored once (no global read-back)
   const int lane = threadIdx.x;
-  double* M = scratch + (size_t)blockIdx.x * NB_SCR;
-  double* r = M + (size_t)NB_CAP * 5;
+  double* M = scratch + (size_t)blockIdx.x * (CAP * 8);
+  double* r = M + (size_t)CAP * 5;
   for (;;) {
-    int k = 0;
-    if (lane == 0) k = atomicAdd(queue, 1);
-    k = __builtin_amdgcn_readfirstlane(k);
-    if (k >= m) break;
+    int i = 0;
+    if (lane == 0) i = atomicAdd(queue, 1);
+    i = __builtin_amdgcn_readfirstlane(i);
+    if (i >= (ov.only ? *ov.only_n : m)) break;
+    const int k = ov.only ? __builtin_amdgcn_readfirstlane(ov.only[i]) : i;
     const pmvs_refined& rr = res[k];
     pmvs_patch& q = Q;
     // wave-uniform (SGPR) status: the branch below holds barriers, so it must not be divergent
@@ -2094,7 +2133,9 @@ __global__ __launch_bounds__(64) void depth_post_kernel(DScene s, FilterDev F, c
         } else {
           // ... findNeighbors(patch, neighbors, 1, 4, 2) + filterQuad when more than 6 neighbours
           const int n = gather_neighbors(s, F, L, q, 4.0f, 2, 0);
-          if (lane == 0 && L.overflow) atomicAdd(overflow, 1);
+          // overflowed: candidate k is rewritten by the NB_CAP_BIG re-walk
+          if (lane == 0 && L.overflow && ov.items) ov.items[atomicAdd(ov.count, 1)] = k;
+          if (lane == 0 && L.overflow && !ov.items) atomicAdd(overflow, 1);
           if (6 < n && filter_quad_wave(s, F, L, M, r, q, n)) st = 3;
         }
       }
@@ -2205,7 +2246,8 @@ static hipError_t dalloc(T*& p, size_t n) {
 FilterBuffers::~FilterBuffers() {
   void* ps[] = {preg, vreg, tgoff, cnt, off, keys, keys2, cellcnt, pg_off, pg_items, vp_off, vp_items, dpkey,
                 order, rank, hot, flags, safe, need, list, scratch, counters, temp, edge_off, edges, rbits, coordc,
-                qf, qrows, qjobs, qctr, qkeys, qkeys2, qcrows, qoff, vrows, used, normalc, refpos, xr};
+                qf, qrows, qjobs, qctr, qkeys, qkeys2, qcrows, qoff, vrows, used, normalc, refpos, xr, ovf_items,
+                scratch_big};
   for (void* p : ps)
     if (p) (void)hipFree(p);
 }
@@ -2286,6 +2328,22 @@ static hipError_t fgrow(T*& p, size_t& cap, size_t need) {  // grown, contents n
   return hipSuccess;
 }
 
+// The neighbour walks' re-walk lists (NbOverflow): the NB_CAP walk appends its overflowed items to
+// B.ovf_items (count at B.counters[10]); the NB_CAP_BIG form, launched right after it without a host
+// sync (its workgroups leave at once when the list is empty), walks them (queue B.counters[11]).
+static hipError_t nb_overflow_lists(FilterBuffers& B, size_t items, hipStream_t st, NbOverflow& walk, NbOverflow& rewalk) {
+  FCHK(fgrow(B.ovf_items, B.cap_ovf, std::max<size_t>(items, 1)));
+  if (!B.scratch_big) FCHK(hipMalloc((void**)&B.scratch_big, (size_t)NB_GRID_BIG * NB_CAP_BIG * 8 * sizeof(double)));
+  FCHK(hipMemsetAsync(B.counters + 10, 0, 2 * sizeof(int), st));
+  walk = NbOverflow{};
+  walk.items = B.ovf_items;
+  walk.count = B.counters + 10;
+  rewalk = NbOverflow{};
+  rewalk.only = B.ovf_items;
+  rewalk.only_n = B.counters + 10;
+  return hipSuccess;
+}
+
 namespace {
 
 // All-gather of one owner-partitioned filter stage (see filter_pass_impl).
@@ -2312,6 +2370,8 @@ struct Ctx {
     F.ncells = ncells; F.npg = npg; F.nvp = nvp; F.err = B.counters + 6; F.lovf = B.counters + 8;
     F.pg_dhead = pg_dhead; F.vp_dhead = vp_dhead; F.d_item = d_item; F.d_next = d_next;
     F.coordc = coordc;
+    const char* sc = getenv("PMVS_NB_SOFTCAP");
+    F.nb_softcap = sc ? atoi(sc) : 0;
     return F;
   }
 };
@@ -2639,8 +2699,11 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
     if (const char* e = getenv("PMVS_QUAD_ROWS")) qj.cap_rows = std::min(qj.cap_rows, (unsigned long long)atoll(e));
     if (qj.cap_rows == 0) qj.f = nullptr;
     FCHK(hipMemsetAsync(B.qctr, 0, 2 * sizeof(unsigned long long), st));
-    hipLaunchKernelGGL(neighbor_kernel, dim3(std::min(grid * NB_GRID_MULT, c.nalive)), dim3(64), 0, st, s, c.dev(), B.scratch, B.flags,
-                       B.counters + 3, B.counters + 4, getenv("PMVS_FILTER_DEBUG") ? B.need : nullptr, R, G, qj);
+    NbOverflow nbw, nbr;
+    FCHK(nb_overflow_lists(B, (size_t)c.nalive, st, nbw, nbr));
+    int* nbdbg = getenv("PMVS_FILTER_DEBUG") ? B.need : nullptr;
+    hipLaunchKernelGGL(neighbor_kernel<NB_CAP>, dim3(std::min(grid * NB_GRID_MULT, c.nalive)), dim3(64), 0, st, s, c.dev(),
+                       B.scratch, B.flags, B.counters + 3, B.counters + 4, nbdbg, R, G, qj, nbw);
     if (qj.f) {
       int nj = 0;
       FCHK(read_int(qj.njobs, &nj, st));
@@ -2677,6 +2740,14 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
         }
       }
     }
+  }
+  if (c.nalive) {  // the patches with more than NB_CAP neighbours, walked again (fits in the wavefront)
+    QuadJobs qnone{};
+    NbOverflow nbr;
+    nbr.only = B.ovf_items;
+    nbr.only_n = B.counters + 10;
+    hipLaunchKernelGGL(neighbor_kernel<NB_CAP_BIG>, dim3(NB_GRID_BIG), dim3(64), 0, st, s, c.dev(), B.scratch_big, B.flags,
+                       B.counters + 3, B.counters + 11, getenv("PMVS_FILTER_DEBUG") ? B.need : nullptr, R, G, qnone, nbr);
   }
   dbg(st, "neighbor kernel");
   if (getenv("PMVS_FILTER_DEBUG")) {
@@ -3154,6 +3225,9 @@ __global__ void cm_decide_kernel(DScene s, int nk, const int* __restrict__ slot2
 // sorted (cell, k) segments -- and keeps the others for the next round.  No launch or host sync
 // per round.  Winners of one round share no cell, so their updates do not interact.
 constexpr int kTailMax = 6144, kTailThreads = 1024;
+// one CU walks every undecided candidate's cells three times per round: cheaper than the grid-wide
+// rounds (two launches each, a host sync every four) only for the last few candidates
+constexpr int kTailDefault = 0;
 constexpr int kSegFree = 0x7f7f7f7f;  // hipMemset byte 0x7f
 __device__ __forceinline__ int cm_cell(const int* r, int i) {  // access i of a record, in cm_emit's order
   if (i < r[2]) return r[5 + i];
@@ -3422,8 +3496,10 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
   FCHK(hipStreamSynchronize(st));
   const int na = hv[0], nlive = hv[1];
   int nseg = 0;
-  const char* tail_env = getenv("PMVS_COMMIT_TAIL");  // tests: 0 = grid-wide rounds only, n = the last n
-  const int tail_max = tail_env ? std::max(0, std::min(kTailMax, atoi(tail_env))) : kTailMax;
+  // PMVS_COMMIT_TAIL=n: the rounds with at most n undecided candidates run in cm_tail_kernel
+  // (default kTailDefault; 0 = grid-wide rounds only)
+  const char* tail_env = getenv("PMVS_COMMIT_TAIL");
+  const int tail_max = tail_env ? std::max(0, std::min(kTailMax, atoi(tail_env))) : kTailDefault;
   if (na > 0 && nlive > tail_max) {  // the (cell, k) segments of the grid-wide rounds
     if ((size_t)na + 1 > W.cap_a) {
       const size_t c = std::max((size_t)na + 1, 2 * W.cap_a);
@@ -3694,10 +3770,16 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
       // candidates (24 floats + 6 flags per parent) all-gathered, so every rank holds the chunk's.
       const int pch = (nc + G - 1) / G;
       const int plo = (G > 1) ? std::min(nc, R * pch) : 0, phi = (G > 1) ? std::min(nc, plo + pch) : nc;
-      if (phi > plo)
-        hipLaunchKernelGGL(empty_blocks_kernel, dim3(std::min(grid * NB_GRID_MULT, phi - plo)), dim3(64), 0, st, s, c.dev(),
+      if (phi > plo) {  // the NB_CAP walk, then the NB_CAP_BIG re-walk of the parents it overflowed on
+        NbOverflow nbw, nbr;
+        FCHK(nb_overflow_lists(B, (size_t)(phi - plo), st, nbw, nbr));
+        hipLaunchKernelGGL(empty_blocks_kernel<NB_CAP>, dim3(std::min(grid * NB_GRID_MULT, phi - plo)), dim3(64), 0, st, s,
+                           c.dev(), X.parents + off + plo, phi - plo, X.cand_coord + (size_t)(off + plo) * 24,
+                           X.cand_ok + (size_t)(off + plo) * 6, B.counters + 4, B.counters + 3, nbw);
+        hipLaunchKernelGGL(empty_blocks_kernel<NB_CAP_BIG>, dim3(NB_GRID_BIG), dim3(64), 0, st, s, c.dev(),
                            X.parents + off + plo, phi - plo, X.cand_coord + (size_t)(off + plo) * 24,
-                           X.cand_ok + (size_t)(off + plo) * 6, B.counters + 4, B.counters + 3);
+                           X.cand_ok + (size_t)(off + plo) * 6, B.counters + 11, B.counters + 3, nbr);
+      }
       if (G > 1) {
         hipError_t lerr = hipPeekAtLastError();
         int ovf = 0;
@@ -3837,8 +3919,12 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
             FCHK(refine(X.cand2 + lo, mine, X.res + lo));
             T.mark(4);
             FCHK(hipMemsetAsync(B.counters + 4, 0, sizeof(int), st));
-            hipLaunchKernelGGL(depth_post_kernel, dim3(std::min(grid * NB_GRID_MULT, mine)), dim3(64), 0, st, s, c.dev(), X.res + lo, mine,
-                               X.outp + lo, X.ostatus + lo, B.scratch, B.counters + 4, B.counters + 3);
+            NbOverflow nbw, nbr;
+            FCHK(nb_overflow_lists(B, (size_t)mine, st, nbw, nbr));
+            hipLaunchKernelGGL(depth_post_kernel<NB_CAP>, dim3(std::min(grid * NB_GRID_MULT, mine)), dim3(64), 0, st, s, c.dev(),
+                               X.res + lo, mine, X.outp + lo, X.ostatus + lo, B.scratch, B.counters + 4, B.counters + 3, nbw);
+            hipLaunchKernelGGL(depth_post_kernel<NB_CAP_BIG>, dim3(NB_GRID_BIG), dim3(64), 0, st, s, c.dev(), X.res + lo, mine,
+                               X.outp + lo, X.ostatus + lo, B.scratch_big, B.counters + 11, B.counters + 3, nbr);
             FCHK(hipPeekAtLastError());
           }
         }

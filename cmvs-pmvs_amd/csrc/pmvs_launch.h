@@ -114,6 +114,11 @@ struct FilterBuffers {
   unsigned long long *qkeys = nullptr, *qkeys2 = nullptr;  // jobs by descending row count
   int *qcrows = nullptr, *qoff = nullptr;                  // per 64-job chunk: pool rows, offsets
   size_t cap_qrows = 0;
+  // the neighbour walks' NB_CAP_BIG re-walks (pmvs_filter.hip NbOverflow): overflowed work items
+  // and the big form's global scratch
+  int* ovf_items = nullptr;
+  double* scratch_big = nullptr;
+  size_t cap_ovf = 0;
   int cap_n = 0, cap_grid = 0;
   long long cap_cells = 0;
   size_t cap_e = 0, cap_pi = 0, cap_vi = 0;  // entries of keys/keys2, pg_items, vp_items: grown to the lists' size

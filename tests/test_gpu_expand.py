@@ -240,16 +240,19 @@ def test_sharded_full_loop_matches_single_rank(gpu_available):
         compare(out, np.ones(len(out), np.int32), {}, ref, np.ones(len(ref), np.int32), {})
 
 
-@pytest.mark.parametrize("depth,tail", [(1, None), (2, None), (1, "0"), (2, "8")],
-                         ids=["d1", "d2", "d1_grid_rounds", "d2_grid_then_tail"])
-def test_expand_min_candidates_matches_oracle(gpu_available, oracle_mod, monkeypatch, depth, tail):
+@pytest.mark.parametrize("depth,tail,softcap", [(1, None, None), (2, None, None), (1, "6144", None), (2, "8", None),
+                                               (1, None, "8"), (2, None, "8")],
+                         ids=["d1", "d2", "d1_tail_rounds", "d2_grid_then_tail", "d1_nb_rewalk", "d2_nb_rewalk"])
+def test_expand_min_candidates_matches_oracle(gpu_available, oracle_mod, monkeypatch, depth, tail, softcap):
     """Waves extended by further parent chunks until they hold min_candidates free directions
     (the schedule bench.py uses for C3): device and oracle run the same schedule.  The commit's
-    rounds run in one workgroup (cm_tail_kernel, the default for these wave sizes), grid-wide
-    (PMVS_COMMIT_TAIL=0) or grid-wide until 8 candidates are left (PMVS_COMMIT_TAIL=8)."""
+    rounds run grid-wide (the default), in one workgroup (cm_tail_kernel, PMVS_COMMIT_TAIL=6144: every
+    wave of this scene) or grid-wide until 8 candidates are left (PMVS_COMMIT_TAIL=8)."""
     import pmvs_amd as P
     if tail is not None:
         monkeypatch.setenv("PMVS_COMMIT_TAIL", tail)
+    if softcap is not None:  # findEmptyBlocks / depth >= 2 check() walks re-walked by the NB_CAP_BIG form
+        monkeypatch.setenv("PMVS_NB_SOFTCAP", softcap)
     inp, p = P.synth_scene(6, 480, 360, level=1, supersample=2)
     g = P.Scene(inp)
     o = oracle_mod.OracleScene(inp)
