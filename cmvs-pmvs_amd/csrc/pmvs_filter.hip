@@ -2216,10 +2216,23 @@ __global__ void flag_rank_kernel(pmvs_patch* __restrict__ P, const int* __restri
 }
 
 // ============================================================================ host orchestration
+// PMVS_TRACE_ERRORS=1: the first failing call of a pass is reported with its line and the free
+// device memory (diagnosis of capacity / allocation failures at full scale)
+static void trace_error(hipError_t e, int line) {
+  static const bool on = getenv("PMVS_TRACE_ERRORS") != nullptr;
+  if (!on) return;
+  size_t fr = 0, tot = 0;
+  (void)hipMemGetInfo(&fr, &tot);
+  fprintf(stderr, "[pmvs] pmvs_filter.hip:%d: %s (device memory free %.2f of %.2f GB)\n", line, hipGetErrorString(e),
+          fr / 1e9, tot / 1e9);
+}
 #define FCHK(x)                          \
   do {                                   \
     hipError_t e_ = (x);                 \
-    if (e_ != hipSuccess) return e_;     \
+    if (e_ != hipSuccess) {              \
+      trace_error(e_, __LINE__);         \
+      return e_;                         \
+    }                                    \
   } while (0)
 
 static inline unsigned nblk(long long n, int b = 256) { return (unsigned)((n + b - 1) / b); }
@@ -3822,7 +3835,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
           ovf |= hall[2 * r + 1];
         }
         FCHK(lerr);
-        if (ovf) return hipErrorOutOfMemory;  // more than NB_CAP neighbours (reported by the API)
+        if (ovf) { trace_error(hipErrorOutOfMemory, __LINE__); return hipErrorOutOfMemory; }  // more than NB_CAP neighbours (reported by the API)
         if (dev ? sh.exchange_dev(X.xsd, pb, X.xrd, st) != 0 : sh.exchange(xsend.data(), pb, xrecv.data()) != 0)
           return hipErrorUnknown;
         agreed = false;
@@ -3974,7 +3987,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
           ovf |= hall[2 * r + 1];
         }
         FCHK(lerr);
-        if (ovf) return hipErrorOutOfMemory;  // more than NB_CAP neighbours (reported by the API)
+        if (ovf) { trace_error(hipErrorOutOfMemory, __LINE__); return hipErrorOutOfMemory; }  // more than NB_CAP neighbours (reported by the API)
         if (dev ? sh.exchange_dev(X.xsd, bytes, X.xrd, st) != 0 : sh.exchange(xsend.data(), bytes, xrecv.data()) != 0)
           return hipErrorUnknown;
         agreed = false;
@@ -3990,7 +4003,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
         if (inject && inj_where == 'a' && stats[7] == inj_wave) return hipErrorOutOfMemory;
       }
       FCHK(lerr);
-      if (ovf) return hipErrorOutOfMemory;  // more than NB_CAP neighbours (reported by the API)
+      if (ovf) { trace_error(hipErrorOutOfMemory, __LINE__); return hipErrorOutOfMemory; }  // more than NB_CAP neighbours (reported by the API)
       if (m > 0) {
         FCHK(grow(X.crec, X.cap_crec, (size_t)m * kRecInts));
         hipLaunchKernelGGL(commit_rec_kernel, dim3(nblk(m)), dim3(256), 0, st, s, B.tgoff, X.outp, X.ostatus, X.prep2, m,
@@ -4003,7 +4016,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
       for (int q = 0; q < 4; ++q) stats[2 + q] += co.fail[q];
       if (W == 1) pbits |= co.pbits;
       const int added = co.nacc;
-      if (added > 0 && nmodel + added > cap) return hipErrorOutOfMemory;
+      if (added > 0 && nmodel + added > cap) { trace_error(hipErrorOutOfMemory, __LINE__); return hipErrorOutOfMemory; }
       stats[6] += added;
       wave_run.clear();
       for (const int2& u : co.push) wave_run.push_back({qkey(__int_as_float_h(u.x), seq++), u.y});
