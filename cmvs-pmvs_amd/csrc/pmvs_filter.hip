@@ -2685,21 +2685,14 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
     hipLaunchKernelGGL(scatter_index_kernel, dim3(nblk(n)), dim3(256), 0, st, B.cnt, B.off, n, B.list);
     int m = 0;
     FCHK(read_int(B.off + n, &m, st));
-    // several patches per wavefront (PMVS_REFIMAGE_PACKED=0: one per wavefront)
-    int* rwork = nullptr;
-    const char* pk = getenv("PMVS_REFIMAGE_PACKED");
-    if (!(pk && atoi(pk) == 0)) {
-      FCHK(fgrow(B.ovf_items, B.cap_ovf, (size_t)m + 2));
-      rwork = B.ovf_items;
-    }
     if (part) {  // the owners' setRefImage outcomes (m is the same on every rank)
       FCHK(fgrow(B.refpos, B.cap_refpos, (size_t)std::max(m, 1)));
       FCHK(fgrow(B.xr, B.cap_xr, (size_t)std::max(m, 1) * 4 * G));
-      FCHK(launch_filter_refimage(s, dP, B.list, m, grid, st, B.refpos, R, G, rwork));
+      FCHK(launch_filter_refimage(s, dP, B.list, m, grid, st, B.refpos, R, G));
       FCHK(c.xchg(0, B.refpos, (size_t)m * 4, B.xr, nullptr));
       FCHK(launch_apply_refpos(s, dP, B.list, m, reinterpret_cast<const int*>(B.xr), G, st));
     } else if (m) {
-      FCHK(launch_filter_refimage(s, dP, B.list, m, grid, st, nullptr, 0, 1, rwork));
+      FCHK(launch_filter_refimage(s, dP, B.list, m, grid, st));
     }
     if (m)
       hipLaunchKernelGGL(exact_after_ref_kernel, dim3(nblk(m)), dim3(256), 0, st, s, dP, B.list, m, B.preg, B.vreg,

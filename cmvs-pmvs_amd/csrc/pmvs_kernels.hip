@@ -2028,20 +2028,15 @@ __device__ __forceinline__ void apply_ref_list(const DScene& s, pmvs_patch& q, c
 // the list entries whose reference image this rank owns (images[0] % world == rank) are evaluated and
 // their outcome written to refpos[k] -- the list position swapped with position 0 (0: unchanged) or
 // -1 (no target image: list cleared); apply_refpos_kernel applies the all-gathered outcomes.
-// only != nullptr: the list entries only[0 .. *only_n) (the packed kernel's patches with more than
-// RefImgLds::kMaxTargets target images).
 template <int WS>
 __global__ __launch_bounds__(64) void filter_refimage_kernel(DScene s, pmvs_patch* __restrict__ P,
                                                              const int* __restrict__ list, int m, int* __restrict__ refpos,
-                                                             int rank, int world, const int* __restrict__ only,
-                                                             const int* __restrict__ only_n) {
+                                                             int rank, int world) {
   __shared__ WaveLds<WS> L;
   float* mat = s.scratch + (size_t)blockIdx.x * PMVS_MAX_IMAGES * PMVS_MAX_IMAGES;
   const int lane = lane_id();
   unsigned long long grabs = 0;
-  const int kend = only ? *only_n : m;
-  for (int i = blockIdx.x; i < kend; i += gridDim.x) {
-    const int k = only ? __builtin_amdgcn_readfirstlane(only[i]) : i;
+  for (int k = blockIdx.x; k < m; k += gridDim.x) {
     pmvs_patch& q = P[list[k]];
     const int n = q.num_images;
     if (refpos && __builtin_amdgcn_readfirstlane(q.images[0]) % world != rank) continue;  // wave-uniform
@@ -2071,176 +2066,6 @@ __global__ __launch_bounds__(64) void filter_refimage_kernel(DScene s, pmvs_patc
   }
 }
 
-// setRefImage + setGrids for several patches per wavefront: their target textures share one chunk
-// of kTexSlots LDS slots (the refine evaluation's tex_setup / tex_gather / tex_moments / tex_scale,
-// each patch with its own geometry), then every pair's robust INCC (spread over the lanes), the
-// rows' sums in j order and each patch's argmin -- the per-patch kernel's arithmetic and order.
-// Each wavefront takes kBlock consecutive list entries and packs them greedily (in list order) into
-// chunks; a patch with more than kMaxTargets target images goes to the per-patch kernel (big list).
-template <int WS>
-struct RefImgLds {
-  static constexpr int kTexSlots = 32, kBlock = 16, kMaxTargets = 16;
-  static constexpr int S = WS * WS;
-  static constexpr int SP = (S + 3) & ~3;
-  alignas(16) float tex[kTexSlots][3][SP];
-  float ave[kTexSlots][4];
-  long long jbase[kTexSlots];
-  int jvalid[kTexSlots], jW[kTexSlots], jreq[kTexSlots], jidx[kTexSlots];
-  float jrow[kTexSlots][WS][2], jdx[kTexSlots][2], jdy[kTexSlots][2];
-  float geo[kBlock][16];                      // patch: coord, normal, pxaxis, pyaxis
-  unsigned short views[kBlock][kMaxTargets];  // patch: its target images in list order (setRefImage's indexes)
-  int rfirst[kBlock], rsize[kBlock];
-  int pbase[kTexSlots + 1];                   // slot i's first pair (i, j > i of its patch)
-  float mat[kTexSlots][kMaxTargets];          // slot i: row i of its patch's INCC matrix
-  float rsum[kTexSlots];
-};
-
-template <int WS>
-__global__ __launch_bounds__(64) void filter_refimage_packed_kernel(DScene s, pmvs_patch* __restrict__ P,
-                                                                    const int* __restrict__ list, int m,
-                                                                    int* __restrict__ refpos, int rank, int world,
-                                                                    int* __restrict__ work, int maxt) {
-  using LT = RefImgLds<WS>;
-  __shared__ LT C;
-  const int lane = lane_id();
-  int* queue = work;
-  int* nbig = work + 1;
-  int* big = work + 2;
-  for (;;) {
-    int b = 0;
-    if (lane == 0) b = atomicAdd(queue, LT::kBlock);
-    b = __builtin_amdgcn_readfirstlane(b);
-    if (b >= m) break;
-    const int nb = imin(LT::kBlock, m - b);
-    // lane p < nb: list entry b + p -- its target images; mt = their number, or 0 (nothing to pack)
-    int mt = 0;
-    if (lane < nb) {
-      const int k = b + lane;
-      pmvs_patch& q = P[list[k]];
-      const int n = q.num_images;
-      if (!refpos || q.images[0] % world == rank) {
-        int c = 0;
-        for (int j = 0; j < n; ++j)
-          if (q.images[j] < s.tnum) {
-            if (c < LT::kMaxTargets) C.views[lane][c] = (unsigned short)q.images[j];
-            ++c;
-          }
-        if (c > maxt) {  // maxt = kMaxTargets (less in tests: PMVS_REFIMAGE_MAXT)
-          big[atomicAdd(nbig, 1)] = k;
-        } else if (c == 0) {  // no target image: setRefImage clears the list
-          if (refpos) refpos[k] = -1;
-          else q.num_images = 0;
-        } else {
-          mt = c;
-        }
-      }
-    }
-    __syncthreads();
-    for (int p0 = 0; p0 < nb;) {
-      // the chunk: entries [p0, p1) whose targets fit the slots together (uniform loop)
-      int tot = 0, p1 = p0;
-      for (; p1 < nb; ++p1) {
-        const int a = __shfl(mt, p1);
-        if (tot + a > LT::kTexSlots) break;
-        tot += a;
-      }
-      const int mine = (lane >= p0 && lane < p1) ? mt : 0;
-      const int off = wave_excl_scan(mine);
-      if (mine > 0) {
-        const pmvs_patch& q = P[list[b + lane]];
-        float coord[4], normal[4], px[4], py[4];
-        for (int i = 0; i < 4; ++i) { coord[i] = q.coord[i]; normal[i] = q.normal[i]; }
-        get_paxes(s, s.views[C.views[lane][0]], coord, normal, px, py);
-        for (int i = 0; i < 4; ++i) {
-          C.geo[lane][i] = coord[i]; C.geo[lane][4 + i] = normal[i];
-          C.geo[lane][8 + i] = px[i]; C.geo[lane][12 + i] = py[i];
-        }
-        C.rfirst[lane] = off;
-        C.rsize[lane] = mine;
-        for (int i = 0; i < mine; ++i) {
-          C.jreq[off + i] = lane;
-          C.jidx[off + i] = i;
-        }
-      }
-      __syncthreads();
-      if (lane < tot) tex_setup<WS>(s, C, lane);
-      __syncthreads();
-      tex_gather<WS, WAVE>(s, C, tot, lane);
-      __syncthreads();
-      if (lane < tot && C.jvalid[lane]) tex_moments<WS>(C, lane);
-      __syncthreads();
-      tex_scale<WS, WAVE>(C, tot, lane);
-      // pairs (i, j > i) of each patch, numbered slot by slot
-      int np = 0;
-      if (lane < tot) {
-        const int r = C.jreq[lane];
-        np = C.rfirst[r] + C.rsize[r] - lane - 1;
-        C.mat[lane][C.jidx[lane]] = 0.0f;  // the diagonal
-      }
-      const int pb = wave_excl_scan(np);
-      if (lane < tot) C.pbase[lane] = pb;
-      const int npairs = __shfl(pb + np, 63);
-      if (lane == 0) C.pbase[tot] = npairs;
-      __syncthreads();
-      for (int u = lane; u < npairs; u += WAVE) {
-        int i = 0;  // the last slot whose first pair is <= u
-        for (int step = LT::kTexSlots / 2; step >= 1; step >>= 1)
-          if (i + step < tot && C.pbase[i + step] <= u) i += step;
-        const int j = i + 1 + (u - C.pbase[i]);
-        float v = 2.0f;
-        if (C.jvalid[i] && C.jvalid[j]) {
-          float ans = 0.0f;  // COptim::dot: sample order, R G B
-          for (int k = 0; k < LT::S; ++k) {
-            ans += C.tex[i][0][k] * C.tex[j][0][k];
-            ans += C.tex[i][1][k] * C.tex[j][1][k];
-            ans += C.tex[i][2][k] * C.tex[j][2][k];
-          }
-          v = robustincc(1.0f - __fdiv_rn(ans, (float)(3 * LT::S)));
-        }
-        C.mat[i][C.jidx[j]] = v;
-        C.mat[j][C.jidx[i]] = v;
-      }
-      __syncthreads();
-      if (lane < tot) {  // row sums in j order (std::accumulate, float)
-        const int mp = C.rsize[C.jreq[lane]];
-        float sum = 0.0f;
-        for (int j = 0; j < mp; ++j) sum = sum + C.mat[lane][j];
-        C.rsum[lane] = sum;
-      }
-      __syncthreads();
-      if (mine > 0) {  // argmin (first on ties), the swap with position 0, setGrids
-        float refncc = 1073741824.0f;  // (float)(INT_MAX/2)
-        int refindex = -1;
-        for (int i = 0; i < mine; ++i)
-          if (C.rsum[off + i] < refncc) {
-            refncc = C.rsum[off + i];
-            refindex = i;
-          }
-        const int refimg = C.views[lane][refindex];
-        const int k = b + lane;
-        pmvs_patch& q = P[list[k]];
-        const int n = q.num_images;
-        int pos = 0;
-        for (int j = 1; j < n; ++j)
-          if (q.images[j] == refimg) pos = j;
-        if (refpos) {
-          refpos[k] = pos;
-        } else {
-          if (pos > 0) {
-            const int16_t t = q.images[0];
-            q.images[0] = q.images[pos];
-            q.images[pos] = t;
-          }
-          const float coord[4] = {C.geo[lane][0], C.geo[lane][1], C.geo[lane][2], C.geo[lane][3]};
-          for (int j = 0; j < n; ++j) apply_ref_list(s, q, coord, j, q.images[j]);
-        }
-      }
-      __syncthreads();
-      p0 = p1;
-    }
-  }
-}
-
 // The owner-partitioned setRefImage's outcomes (all ranks' refpos, rank-major m ints each) applied on
 // every rank: entry k's value comes from the rank owning its reference image.
 __global__ void apply_refpos_kernel(DScene s, pmvs_patch* __restrict__ P, const int* __restrict__ list, int m,
@@ -2262,31 +2087,14 @@ __global__ void apply_refpos_kernel(DScene s, pmvs_patch* __restrict__ P, const 
   for (int j = 0; j < q.num_images; ++j) apply_ref_list(s, q, coord, j, q.images[j]);
 }
 
-template <int WS>
-static void launch_refimage_ws(const DScene& s, pmvs_patch* P, const int* list, int m, int grid, hipStream_t stream,
-                               int* refpos, int rank, int world, int* work) {
-  if (work) {  // packed, then the entries with many target images one per wavefront
-    const int g = std::min(grid, (m + RefImgLds<WS>::kBlock - 1) / RefImgLds<WS>::kBlock);
-    const char* e = getenv("PMVS_REFIMAGE_MAXT");
-    const int maxt = e ? std::max(0, std::min(RefImgLds<WS>::kMaxTargets, atoi(e))) : RefImgLds<WS>::kMaxTargets;
-    hipLaunchKernelGGL((filter_refimage_packed_kernel<WS>), dim3(g), dim3(64), 0, stream, s, P, list, m, refpos, rank,
-                       world, work, maxt);
-    hipLaunchKernelGGL((filter_refimage_kernel<WS>), dim3(std::min(grid, 256)), dim3(64), 0, stream, s, P, list, m, refpos, rank,
-                       world, work + 2, work + 1);
-  } else {
-    hipLaunchKernelGGL((filter_refimage_kernel<WS>), dim3(grid < m ? grid : m), dim3(64), 0, stream, s, P, list, m, refpos,
-                       rank, world, nullptr, nullptr);
-  }
-}
-
 hipError_t launch_filter_refimage(const DScene& s, pmvs_patch* P, const int* list, int m, int grid, hipStream_t stream,
-                                  int* refpos, int rank, int world, int* work) {
+                                  int* refpos, int rank, int world) {
   if (m <= 0) return hipSuccess;
-  if (work && hipMemsetAsync(work, 0, 2 * sizeof(int), stream) != hipSuccess) return hipGetLastError();
+  const int g = grid < m ? grid : m;
   switch (s.wsize) {
-    case 5: launch_refimage_ws<5>(s, P, list, m, grid, stream, refpos, rank, world, work); break;
-    case 7: launch_refimage_ws<7>(s, P, list, m, grid, stream, refpos, rank, world, work); break;
-    case 9: launch_refimage_ws<9>(s, P, list, m, grid, stream, refpos, rank, world, work); break;
+    case 5: hipLaunchKernelGGL((filter_refimage_kernel<5>), dim3(g), dim3(64), 0, stream, s, P, list, m, refpos, rank, world); break;
+    case 7: hipLaunchKernelGGL((filter_refimage_kernel<7>), dim3(g), dim3(64), 0, stream, s, P, list, m, refpos, rank, world); break;
+    case 9: hipLaunchKernelGGL((filter_refimage_kernel<9>), dim3(g), dim3(64), 0, stream, s, P, list, m, refpos, rank, world); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -129,9 +129,8 @@ struct FilterBuffers {
 
 // setRefImage + setGrids for the patches list[0, m) (filterExact); with refpos, only the entries whose
 // reference image rank owns (of world) are evaluated, their outcomes written to refpos (see the kernel)
-// work (m + 2 device ints, or nullptr: one wavefront per patch): several patches per wavefront
 hipError_t launch_filter_refimage(const DScene& s, pmvs_patch* P, const int* list, int m, int grid, hipStream_t stream,
-                                  int* refpos = nullptr, int rank = 0, int world = 1, int* work = nullptr);
+                                  int* refpos = nullptr, int rank = 0, int world = 1);
 hipError_t launch_apply_refpos(const DScene& s, pmvs_patch* P, const int* list, int m, const int* allpos, int world,
                                hipStream_t stream);
 

@@ -87,22 +87,18 @@ def test_filter_depth0_and_empty(gpu_available, oracle_mod):
     o.close()
 
 
-@pytest.mark.parametrize("cap,qwaves,qlds,softcap,refimg", [("0", "0", "96", None, None), ("20000", "0", "96", None, None),
-                                                             ("-1", "1", "0", None, None), ("-1", "0", "12", None, None),
-                                                             ("-1", "0", "160", None, None), ("-1", "0", "96", "8", None),
-                                                             ("-1", "0", "96", None, "0"), ("-1", "0", "96", None, "3")],
-                         ids=["all_in_wave", "mixed", "lane_grid_stride", "lds_and_lane", "lds_160", "nb_rewalk",
-                              "refimage_per_patch", "refimage_packed_and_big"])
-def test_filter_quad_deferral_paths(gpu_available, oracle_mod, monkeypatch, cap, qwaves, qlds, softcap, refimg):
+@pytest.mark.parametrize("cap,qwaves,qlds,softcap", [("0", "0", "96", None), ("20000", "0", "96", None),
+                                                      ("-1", "1", "0", None), ("-1", "0", "12", None),
+                                                      ("-1", "0", "160", None), ("-1", "0", "96", "8")],
+                         ids=["all_in_wave", "mixed", "lane_grid_stride", "lds_and_lane", "lds_160", "nb_rewalk"])
+def test_filter_quad_deferral_paths(gpu_available, oracle_mod, monkeypatch, cap, qwaves, qlds, softcap):
     """filterNeighbor's quadric fits run after the neighbour walk -- eight lanes per fit with the
     rows in LDS (quad_qr_kernel + quad_solve_kernel) up to PMVS_QUAD_LDS_ROWS rows, one lane per fit
     (quad_lane_kernel) above -- or inside the walk's wavefront when the deferred-row buffer is
     full; PMVS_QUAD_ROWS caps that buffer so both paths (and a mix) meet the oracle.
     PMVS_QUAD_WAVES_PER_CU = 1 caps the lane kernel's grid, so each lane fits several jobs
     (the grid-stride path); PMVS_QUAD_LDS_ROWS = 12 splits the fits between the two kernels.
-    PMVS_NB_SOFTCAP = 8: the neighbour walk's overflow path (the NB_CAP_BIG re-walk).  filterExact's
-    setRefImage: packed (default), one patch per wavefront, or packed with the patches of more than 3
-    target images on the per-patch kernel."""
+    PMVS_NB_SOFTCAP = 8: the neighbour walk's overflow path (the NB_CAP_BIG re-walk)."""
     import pmvs_amd as P
     if cap != "-1":
         monkeypatch.setenv("PMVS_QUAD_ROWS", cap)
@@ -110,10 +106,6 @@ def test_filter_quad_deferral_paths(gpu_available, oracle_mod, monkeypatch, cap,
     monkeypatch.setenv("PMVS_QUAD_LDS_ROWS", qlds)
     if softcap:  # the NB_CAP walk holds 8 neighbours: nearly every patch is re-walked by the NB_CAP_BIG form
         monkeypatch.setenv("PMVS_NB_SOFTCAP", softcap)
-    if refimg == "0":  # filterExact's setRefImage one patch per wavefront
-        monkeypatch.setenv("PMVS_REFIMAGE_PACKED", "0")
-    elif refimg:  # packed, but the patches with more than 3 target images go to the per-patch kernel
-        monkeypatch.setenv("PMVS_REFIMAGE_MAXT", refimg)
     inp, p = P.synth_scene(8, 960, 540, level=1, supersample=2, nthreads=16)
     g = P.Scene(inp)
     o = oracle_mod.OracleScene(inp)
