@@ -3078,9 +3078,7 @@ static hipError_t grow_keep(T*& p, size_t& cap, size_t need, size_t used, hipStr
 struct CommitWork {
   int *stc = nullptr, *nacc = nullptr, *aoff = nullptr, *vals = nullptr, *vals2 = nullptr, *pos = nullptr,
       *head = nullptr, *segid = nullptr, *seghead = nullptr, *segptr = nullptr, *segfirst = nullptr,
-      *slot2 = nullptr, *flag = nullptr, *scan = nullptr, *ctr = nullptr, *pbits = nullptr,
-      *segmin = nullptr;  // cm_tail_kernel: per target cell, kSegFree between launches
-  size_t cap_seg = 0;
+      *slot2 = nullptr, *flag = nullptr, *scan = nullptr, *ctr = nullptr, *pbits = nullptr;
   unsigned long long *keys = nullptr, *keys2 = nullptr;
   unsigned char* dec = nullptr;
   int2* push = nullptr;
@@ -3088,7 +3086,7 @@ struct CommitWork {
   size_t cap_k = 0, cap_a = 0, temp_bytes = 0;
   ~CommitWork() {
     void* ps[] = {stc, nacc, aoff, vals, vals2, pos, head, segid, seghead, segptr, segfirst, slot2, flag, scan, ctr,
-                  pbits, keys, keys2, dec, push, temp, segmin};
+                  pbits, keys, keys2, dec, push, temp};
     for (void* p : ps)
       if (p) (void)hipFree(p);
   }
@@ -3229,80 +3227,6 @@ __global__ void cm_decide_kernel(DScene s, int nk, const int* __restrict__ slot2
   for (int e = aoff[k], ee = aoff[k] + nacc[k]; e < ee; ++e)
     if (segfirst[segid[pos[e]]] != k) return;
   cm_apply(s, k, rec + (size_t)slot2[k] * kRecInts, dec, stc, flag, counts, occ, cthr, check, ctr);
-}
-
-// The commit's last rounds (or all of them, for a wave with few refined candidates) in one
-// workgroup, over the undecided candidates only: a round takes, per cell, the smallest undecided
-// k touching it (atomicMin into segmin, which holds kSegFree outside this kernel), decides every k
-// that is the smallest one in all of its cells -- the rule cm_first + cm_decide apply with the
-// sorted (cell, k) segments -- and keeps the others for the next round.  No launch or host sync
-// per round.  Winners of one round share no cell, so their updates do not interact.
-constexpr int kTailMax = 6144, kTailThreads = 1024;
-// one CU walks every undecided candidate's cells three times per round: cheaper than the grid-wide
-// rounds (two launches each, a host sync every four) only for the last few candidates
-constexpr int kTailDefault = 0;
-constexpr int kSegFree = 0x7f7f7f7f;  // hipMemset byte 0x7f
-__device__ __forceinline__ int cm_cell(const int* r, int i) {  // access i of a record, in cm_emit's order
-  if (i < r[2]) return r[5 + i];
-  i -= r[2];
-  if (i < r[3]) return r[5 + PMVS_MAX_IMAGES + i];
-  return r[5 + 2 * PMVS_MAX_IMAGES + (i - r[3])];
-}
-__global__ __launch_bounds__(kTailThreads) void cm_tail_kernel(DScene s, int nk, const int* __restrict__ slot2,
-                                                               const int* __restrict__ rec, unsigned char* dec, int* stc,
-                                                               int* flag, unsigned char* counts, unsigned char* occ,
-                                                               int cthr, int check, int* ctr, int* segmin) {
-  __shared__ int ua[kTailMax], ub[kTailMax];
-  __shared__ unsigned char win[kTailMax];
-  __shared__ int nu, nn;
-  const int tid = threadIdx.x;
-  if (tid == 0) nu = 0;
-  __syncthreads();
-  for (int k = tid; k < nk; k += kTailThreads)
-    if (!dec[k]) {
-      const int p = atomicAdd(&nu, 1);
-      if (p < kTailMax) ua[p] = k;  // the host launches this kernel with at most kTailMax undecided
-    }
-  __syncthreads();
-  int* cur = ua;
-  int* nxt = ub;
-  for (;;) {
-    const int m = imin(nu, kTailMax);
-    if (m == 0) break;
-    for (int u = tid; u < m; u += kTailThreads) {
-      const int k = cur[u];
-      const int* r = rec + (size_t)slot2[k] * kRecInts;
-      const int na = r[2] + r[3] + r[4];
-      for (int i = 0; i < na; ++i) atomicMin(&segmin[cm_cell(r, i)], k);
-    }
-    __syncthreads();
-    for (int u = tid; u < m; u += kTailThreads) {
-      const int k = cur[u];
-      const int* r = rec + (size_t)slot2[k] * kRecInts;
-      const int na = r[2] + r[3] + r[4];
-      unsigned char w = 1;
-      for (int i = 0; i < na && w; ++i)  // atomic loads: the minima live in L2, not in this CU's L1
-        if (__hip_atomic_load(&segmin[cm_cell(r, i)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != k) w = 0;
-      win[u] = w;
-    }
-    if (tid == 0) nn = 0;
-    __syncthreads();
-    for (int u = tid; u < m; u += kTailThreads) {
-      const int k = cur[u];
-      const int* r = rec + (size_t)slot2[k] * kRecInts;
-      const int na = r[2] + r[3] + r[4];
-      for (int i = 0; i < na; ++i)
-        __hip_atomic_store(&segmin[cm_cell(r, i)], kSegFree, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (win[u]) cm_apply(s, k, r, dec, stc, flag, counts, occ, cthr, check, ctr);
-      else nxt[atomicAdd(&nn, 1)] = k;
-    }
-    __syncthreads();
-    if (tid == 0) nu = nn;
-    int* t = cur;
-    cur = nxt;
-    nxt = t;
-    __syncthreads();
-  }
 }
 
 // flags of the non-refined candidates (0) and the outcome counters: ctr[3] fail_prep, [4] fail_pre,
@@ -3509,11 +3433,7 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
   FCHK(hipStreamSynchronize(st));
   const int na = hv[0], nlive = hv[1];
   int nseg = 0;
-  // PMVS_COMMIT_TAIL=n: the rounds with at most n undecided candidates run in cm_tail_kernel
-  // (default kTailDefault; 0 = grid-wide rounds only)
-  const char* tail_env = getenv("PMVS_COMMIT_TAIL");
-  const int tail_max = tail_env ? std::max(0, std::min(kTailMax, atoi(tail_env))) : kTailDefault;
-  if (na > 0 && nlive > tail_max) {  // the (cell, k) segments of the grid-wide rounds
+  if (na > 0) {
     if ((size_t)na + 1 > W.cap_a) {
       const size_t c = std::max((size_t)na + 1, 2 * W.cap_a);
       FCHK(cm_grow(W.keys, c)); FCHK(cm_grow(W.keys2, c)); FCHK(cm_grow(W.vals, c)); FCHK(cm_grow(W.vals2, c));
@@ -3539,18 +3459,7 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
   }
   // rounds: every round decides at least the lowest undecided candidate
   int decided = 0;
-
   for (int round = 0; decided < nlive; ) {
-    if (nlive - decided <= tail_max) {  // the remaining rounds in one workgroup (cm_tail_kernel)
-      if (W.cap_seg < X.cap_cnt) {
-        FCHK(cm_grow(W.segmin, X.cap_cnt));
-        FCHK(memset_big(W.segmin, 0x7f, X.cap_cnt * sizeof(int), st));
-        W.cap_seg = X.cap_cnt;
-      }
-      hipLaunchKernelGGL(cm_tail_kernel, dim3(1), dim3(kTailThreads), 0, st, s, nk, W.slot2, X.crec, W.dec, W.stc, W.flag,
-                         X.counts, X.occ, cthr, check ? 1 : 0, W.ctr, W.segmin);
-      break;
-    }
     for (int r = 0; r < 4; ++r, ++round) {
       if (nseg > 0)
         hipLaunchKernelGGL(cm_first_kernel, dim3(nblk(nseg)), dim3(256), 0, st, W.keys2, W.dec, W.seghead, nseg, W.segptr,

@@ -240,17 +240,13 @@ def test_sharded_full_loop_matches_single_rank(gpu_available):
         compare(out, np.ones(len(out), np.int32), {}, ref, np.ones(len(ref), np.int32), {})
 
 
-@pytest.mark.parametrize("depth,tail,softcap", [(1, None, None), (2, None, None), (1, "6144", None), (2, "8", None),
-                                               (1, None, "8"), (2, None, "8")],
-                         ids=["d1", "d2", "d1_tail_rounds", "d2_grid_then_tail", "d1_nb_rewalk", "d2_nb_rewalk"])
-def test_expand_min_candidates_matches_oracle(gpu_available, oracle_mod, monkeypatch, depth, tail, softcap):
+@pytest.mark.parametrize("depth,softcap", [(1, None), (2, None), (1, "8"), (2, "8")],
+                         ids=["d1", "d2", "d1_nb_rewalk", "d2_nb_rewalk"])
+def test_expand_min_candidates_matches_oracle(gpu_available, oracle_mod, monkeypatch, depth, softcap):
     """Waves extended by further parent chunks until they hold min_candidates free directions
-    (the schedule bench.py uses for C3): device and oracle run the same schedule.  The commit's
-    rounds run grid-wide (the default), in one workgroup (cm_tail_kernel, PMVS_COMMIT_TAIL=6144: every
-    wave of this scene) or grid-wide until 8 candidates are left (PMVS_COMMIT_TAIL=8)."""
+    (the schedule bench.py uses for C3): device and oracle run the same schedule.  PMVS_NB_SOFTCAP=8:
+    findEmptyBlocks' and check()'s neighbour walks go through the NB_CAP_BIG re-walk."""
     import pmvs_amd as P
-    if tail is not None:
-        monkeypatch.setenv("PMVS_COMMIT_TAIL", tail)
     if softcap is not None:  # findEmptyBlocks / depth >= 2 check() walks re-walked by the NB_CAP_BIG form
         monkeypatch.setenv("PMVS_NB_SOFTCAP", softcap)
     inp, p = P.synth_scene(6, 480, 360, level=1, supersample=2)
