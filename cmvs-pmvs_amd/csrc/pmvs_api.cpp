@@ -261,8 +261,6 @@ pmvs_status ensure(DBuf<T>& b, size_t n) {
   if (e != hipSuccess) return fail(PMVS_ENOMEM, "hipMalloc(%zu bytes): %s", n * sizeof(T), hipGetErrorString(e));
   return PMVS_OK;
 }
-template <class T>
-pmvs_status ensure_keep_data(pmvs_scene*, DBuf<T>& b, size_t n) { return ensure(b, n); }
 int grow_alive(pmvs_scene* sc, int n) {
   ExpandBuffers& X = sc->xbuf;
   if ((size_t)n <= X.cap_alive && X.alive) return 0;
@@ -1303,14 +1301,31 @@ pmvs_status pmvs_run_loop(pmvs_scene* sc, const pmvs_patch* seeds, int32_t n, fl
     if (hsh.world > 1 && !peers_know) (void)loop_header(hsh, 1);
     return s0;
   };
+  // Compaction targets (fpatches2) are sized by the kept records: the source's capacity (the
+  // expansion's, up to twice its model) would hold two full-size models at once -- at C5 scale
+  // (50 M patches of 1608 B after one expansion) more than the GPU has.  The source buffer is
+  // released after the swap when it is much larger than the model.
+  bool dst_oom = false;
+  auto dst_for = [&](int k, pmvs_patch** d) -> hipError_t {
+    if (sc->fpatches2.n > 2 * (size_t)std::max(k, 1)) sc->fpatches2.release();
+    if (ensure(sc->fpatches2, std::max(k, 1))) {
+      dst_oom = true;
+      return hipErrorOutOfMemory;
+    }
+    *d = sc->fpatches2.p;
+    return hipSuccess;
+  };
+  auto swap_models = [&](int kept) {
+    std::swap(sc->fpatches.p, sc->fpatches2.p);
+    std::swap(sc->fpatches.n, sc->fpatches2.n);
+    if (sc->fpatches2.n > 2 * (size_t)std::max(kept, 1)) sc->fpatches2.release();
+  };
   // the model without foreign patches, compacted through fpatches2
   auto drop = [&](int n, int* kept) -> pmvs_status {
     if (n == 0) { *kept = 0; return PMVS_OK; }
-    if (ensure_keep_data(sc, sc->fpatches2, std::max(sc->fpatches.n, (size_t)n))) return fail(PMVS_ENOMEM, "model");
-    if (drop_foreign(sc->fbuf, sc->fpatches.p, n, sc->fpatches2.p, kept, sc->stream) != hipSuccess)
-      return fail(PMVS_EDEVICE, "foreign patches");
-    std::swap(sc->fpatches.p, sc->fpatches2.p);
-    std::swap(sc->fpatches.n, sc->fpatches2.n);
+    if (drop_foreign(sc->fbuf, sc->fpatches.p, n, dst_for, kept, sc->stream) != hipSuccess)
+      return dst_oom ? fail(PMVS_ENOMEM, "model (%d patches)", *kept) : fail(PMVS_EDEVICE, "foreign patches");
+    swap_models(*kept);
     return PMVS_OK;
   };
   for (int it = 0; it < iterations; ++it) {
@@ -1333,11 +1348,10 @@ pmvs_status pmvs_run_loop(pmvs_scene* sc, const pmvs_patch* seeds, int32_t n, fl
     if ((st = filter_device(sc, nn, &li.filter, &handled))) return fail_loop(st, handled && &hsh == &lsh);
     int kept = 0;
     if (nn > 0) {
-      if ((st = ensure_keep_data(sc, sc->fpatches2, sc->fpatches.n))) return fail_loop(st, false);
-      if (compact_model(sc->fbuf, sc->fpatches.p, nn, sc->fkeep.p, sc->fpatches2.p, &kept, sc->stream) != hipSuccess)
-        return fail_loop(fail(PMVS_EDEVICE, "model compaction"), false);
-      std::swap(sc->fpatches.p, sc->fpatches2.p);
-      std::swap(sc->fpatches.n, sc->fpatches2.n);
+      if (compact_model(sc->fbuf, sc->fpatches.p, nn, sc->fkeep.p, dst_for, &kept, sc->stream) != hipSuccess)
+        return fail_loop(dst_oom ? fail(PMVS_ENOMEM, "model (%d patches)", kept) : fail(PMVS_EDEVICE, "model compaction"),
+                         false);
+      swap_models(kept);
     }
     cur = kept;
     li.patches = kept;

@@ -3931,7 +3931,8 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
         FCHK(grow_keep(X.d_next, X.cap_next, pool_need, X.pool_host, st));
         set_delta();
         if ((size_t)(first + added) > pcap) {  // per-patch arrays the waves write, grown keeping their contents
-          const size_t ncap = std::min<size_t>((size_t)cap, std::max((size_t)(first + added), 2 * pcap));
+          // 1.5x: the old and the new model coexist during the copy (at C5 scale ~50 M records of 1608 B)
+          const size_t ncap = std::min<size_t>((size_t)cap, std::max((size_t)(first + added), pcap + pcap / 2));
           size_t c1 = pcap, c2 = pcap, c3 = pcap, c4 = pcap;
           FCHK(grow_keep(dP, dP_cap, ncap, (size_t)first, st));
           FCHK(grow_keep(B.preg, c1, ncap, (size_t)first, st));
@@ -4044,8 +4045,8 @@ __global__ void fill_int_kernel(int* __restrict__ a, int n, int v) {
 
 // The patches a filter pass kept (keep[k] = 1), in order, into dst (CFindMatch::run keeps the
 // model in the organizer; here the removed records are dropped between passes).
-hipError_t compact_model(FilterBuffers& B, const pmvs_patch* src, int n, const int* keep, pmvs_patch* dst, int* nkept,
-                         hipStream_t st) {
+hipError_t compact_model(FilterBuffers& B, const pmvs_patch* src, int n, const int* keep, const CompactDst& dst_for,
+                         int* nkept, hipStream_t st) {
   *nkept = 0;
   if (n <= 0) return hipSuccess;
   FCHK(B.reserve(n, B.cap_cells, 0, B.cap_grid));
@@ -4054,7 +4055,9 @@ hipError_t compact_model(FilterBuffers& B, const pmvs_patch* src, int n, const i
   size_t tb = B.temp_bytes;
   FCHK(hipcub::DeviceScan::ExclusiveSum(B.temp, tb, B.cnt, B.off, n + 1, st));
   FCHK(read_int(B.off + n, nkept, st));
-  hipLaunchKernelGGL(compact_kernel, dim3(n), dim3(64), 0, st, src, n, keep, B.off, dst);
+  pmvs_patch* dst = nullptr;
+  FCHK(dst_for(*nkept, &dst));  // the target is sized by the kept records, not by the source's capacity
+  if (*nkept > 0) hipLaunchKernelGGL(compact_kernel, dim3(n), dim3(64), 0, st, src, n, keep, B.off, dst);
   return hipGetLastError();
 }
 
@@ -4158,12 +4161,13 @@ static hipError_t scan_count(ClusterBuffers& CB, const int* f, int* pos, int n, 
   return read_int(pos + n, total, st);
 }
 
-hipError_t drop_foreign(FilterBuffers& B, const pmvs_patch* src, int n, pmvs_patch* dst, int* n_out, hipStream_t st) {
+hipError_t drop_foreign(FilterBuffers& B, const pmvs_patch* src, int n, const CompactDst& dst_for, int* n_out,
+                        hipStream_t st) {
   *n_out = 0;
   if (n <= 0) return hipSuccess;
   FCHK(B.reserve(n, B.cap_cells, 0, B.cap_grid));
   hipLaunchKernelGGL(own_flags_kernel, dim3(nblk(n)), dim3(256), 0, st, src, n, B.flags);
-  return compact_model(B, src, n, B.flags, dst, n_out, st);
+  return compact_model(B, src, n, B.flags, dst_for, n_out, st);
 }
 
 hipError_t cluster_exchange(const DScene& s, ClusterBuffers& CB, const ClusterMaps& cm, const pmvs_patch* src, int n,

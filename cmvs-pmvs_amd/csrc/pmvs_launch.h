@@ -193,8 +193,10 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
                        const int* d_alive, int cap, long long ncells, const long long* h_tgoff, int wave, int cthr,
                        int flags, int grid, hipStream_t st, const RefineFn& refine, const Shard& sh, long long stats[8],
                        int* n_out, int min_cands = 0);
-hipError_t compact_model(FilterBuffers& B, const pmvs_patch* src, int n, const int* keep, pmvs_patch* dst, int* nkept,
-                         hipStream_t st);
+// dst_for(kept, &dst) supplies the target once the number of kept records is known
+using CompactDst = std::function<hipError_t(int, pmvs_patch**)>;
+hipError_t compact_model(FilterBuffers& B, const pmvs_patch* src, int n, const int* keep, const CompactDst& dst_for,
+                         int* nkept, hipStream_t st);
 hipError_t fill_int(int* a, int n, int v, hipStream_t st);
 
 // ---- CMVS cluster boundary exchange (pmvs_scene_set_cluster)
@@ -214,7 +216,8 @@ struct ClusterBuffers {
   ~ClusterBuffers();
 };
 // The model without other clusters' boundary patches (fix != PMVS_FIX_FOREIGN), compacted into dst.
-hipError_t drop_foreign(FilterBuffers& B, const pmvs_patch* src, int n, pmvs_patch* dst, int* n_out, hipStream_t st);
+hipError_t drop_foreign(FilterBuffers& B, const pmvs_patch* src, int n, const CompactDst& dst_for, int* n_out,
+                        hipStream_t st);
 // One boundary exchange: src[0, n) is this rank's model without foreign patches.  Its boundary
 // patches (registered in a target image another cluster also has as a target) are all-gathered
 // (header {error, count} first, the "visibility counts"; then the records), and every other rank's
