@@ -3049,11 +3049,12 @@ ExpandBuffers::~ExpandBuffers() {
   delete_commit_work(cm);
 }
 
-// Grows a device array keeping its contents (the delta-chain entry pool).
+// Grows a device array keeping its contents (the delta-chain entry pool, the per-patch arrays).
+// 1.5x: old and new coexist during the copy, and at C5 scale the model alone is ~80 GB.
 template <class T>
 static hipError_t grow_keep(T*& p, size_t& cap, size_t need, size_t used, hipStream_t st) {
   if (need <= cap && p) return hipSuccess;
-  const size_t ncap = std::max(need, cap * 2 + 1024);
+  const size_t ncap = std::max(need, cap + cap / 2 + 1024);
   T* q = nullptr;
   FCHK(hipMalloc((void**)&q, ncap * sizeof(T)));
   poison_alloc(q, ncap * sizeof(T));

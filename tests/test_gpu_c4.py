@@ -1,4 +1,4 @@
-"""BASELINE.json configs[3] (C4) and configs[4] (C5) at their full per-GPU size, on one GPU.
+"""BASELINE.json configs[3] (C4) at its full per-GPU size, on one GPU (C5: tests/test_gpu_c5.py).
 
 C4 -- CMVS clusters of a 4K ring, one per GPU, boundary patches exchanged after every iteration
 (pmvs_scene_set_cluster).  Three overlapping clusters of a 75-view 3840x2160 ring
@@ -11,9 +11,6 @@ run as three threads on this GPU, their exchanges through the in-process all-gat
     in full, against the CPU oracle's expand / filter per cluster with the exchange restated in
     numpy (the semantics tests/test_gpu_cluster.py checks on a small ring) -- record for record.
 
-C5 -- one CMVS cluster of maximage 70 at 8K (70 views, 7680x4320, level 0), the per-GPU unit of the
-1000-view configuration: one full loop iteration (expand + filter) with the model checks, and the
-first expansion waves against the oracle record for record.
 """
 import os
 import sys
@@ -203,38 +200,3 @@ def test_c4_bounded_loop_with_exchange_matches_oracle(c4_setup, oracle_mod):
     for r, ((out, log), ref) in enumerate(zip(res, want)):
         assert [it["boundary"]["sent"] for it in log[:-1]] == [s[r] for s in sent], (r, log)
         assert patch_mismatches(out, ref) == 0, r
-
-
-@pytest.mark.timeout(900)
-def test_c5_cluster_8k_one_iteration(gpu_available, oracle_mod):
-    import bench
-    import pmvs_amd as P
-    inp, sp = P.synth_scene(70, 7680, 4320, level=0, supersample=2, nthreads=16)
-    g = P.Scene(inp)
-    cands = P.synth_candidates(sp, inp.projections, 5000, seed=0x5EED)
-    r, _ = g.refine_batch(cands)
-    seeds = P.patches_from_refined(r)
-    # first waves of the iteration-1 expansion, device vs oracle, record for record
-    ncc, before, depth, cthr = bench.iteration_thresholds(inp.threshold, 0)
-    kw = dict(wave=32768, count_threshold=cthr, after_seeds=True, min_candidates=131072)
-    g.set_thresholds(ncc, before, depth)
-    cap = len(seeds) + 600000
-    g_out, g_alive, g_st = g.expand_run(seeds, cap=cap, max_waves=2, **kw)
-    o = oracle_mod.OracleScene(inp)
-    o.set_thresholds(ncc, before, depth)
-    o_out, o_alive, o_st = o.expand_run(seeds, cap=cap, nthreads=_threads(), max_waves=2, **kw)
-    o.close()
-    print(f"C5 first waves: {o_st}")
-    assert o_st["added"] > 20000
-    assert all(g_st[k] == o_st[k] for k in o_st), (g_st, o_st)
-    assert bench.patch_mismatches(g_out, o_out) == 0 and np.array_equal(g_alive, o_alive)
-    del g_out, o_out
-    # one full loop iteration on the device (the C5 per-GPU unit)
-    g.set_thresholds(*bench.iteration_thresholds(inp.threshold, 0)[:2], 0)
-    model, log = g.run_loop(seeds, inp.threshold, iterations=1, wave=32768, min_candidates=131072)
-    g.close()
-    checks = bench.model_checks(model, inp, ["x"])
-    print(f"C5 one iteration: {log[0]['expand']['added']} added, {len(model)} kept, "
-          f"{log[0]['expand']['wall_ms'] / 1e3:.1f} s expand, {log[0]['filter']['kernel_ms'] / 1e3:.1f} s filter; {checks}")
-    assert checks["ok"] and checks["sphere_residual_p99"] < 0.01, checks
-    assert log[0]["expand"]["added"] > 10_000_000

@@ -223,15 +223,16 @@ def _gap(inp, ref, prod):
     }
 
 
-# The 50-view case (83 s on the GPU, mostly the reference's one-parent-per-wave schedule) runs
-# with PMVS_LONG_TESTS=1 only, so the default GPU suite stays inside the round-end time budget.
+# The 50-view case (83 s on the GPU, mostly the reference's one-parent-per-wave schedule) and the
+# hard-scene case (36 s) run with PMVS_LONG_TESTS=1 only, so the default GPU suite stays inside the
+# round-end time budget.
 _LONG = pytest.mark.skipif(not os.environ.get("PMVS_LONG_TESTS"), reason="PMVS_LONG_TESTS=1 runs it")
 
 
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("views,w,h,nseeds,hard", [(10, 400, 300, 150, False),
                                                    pytest.param(50, 320, 180, 300, False, marks=_LONG),
-                                                   (10, 400, 300, 150, True)],
+                                                   pytest.param(10, 400, 300, 150, True, marks=_LONG)],
                          ids=["10v_400x300", "50v_320x180", "10v_400x300_hard"])
 def test_schedule_gap_vs_single_thread(gpu_available, views, w, h, nseeds, hard):
     import pmvs_amd as P
