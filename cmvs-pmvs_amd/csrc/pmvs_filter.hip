@@ -2389,10 +2389,49 @@ struct Ctx {
   }
 };
 
-static hipError_t read_int(const int* d, int* h, hipStream_t st) {
-  FCHK(hipMemcpyAsync(h, d, sizeof(int), hipMemcpyDeviceToHost, st));
-  return hipStreamSynchronize(st);
+// Device -> host reads of the loop's control values (counts, flags, per-wave status) through a
+// pinned staging buffer of the calling host thread.  Into pageable memory every hipMemcpyAsync is
+// a staged copy with a wait of its own (about 75 us each between the C3 loop's kernels,
+// profiles/r04h_kernel_trace gaps); here the reads of one point share one stream synchronisation.
+// Reads above kStageMax bytes go to their destination directly (bandwidth-bound anyway).
+struct D2H {
+  void* h;
+  const void* d;
+  size_t bytes;
+};
+constexpr size_t kStageMax = 256 << 10;
+static PinnedBuf& stage_buf() {
+  static thread_local PinnedBuf* pb = new PinnedBuf();  // not freed: it lives as long as its thread
+  return *pb;
 }
+static hipError_t d2h_sync(hipStream_t st, std::initializer_list<D2H> reads) {
+  auto staged = [](const D2H& r) { return r.bytes <= kStageMax; };
+  auto pad = [](size_t b) { return (b + 15) & ~(size_t)15; };
+  size_t tot = 0;
+  for (const D2H& r : reads)
+    if (staged(r)) tot += pad(r.bytes);
+  PinnedBuf& pb = stage_buf();
+  if (tot) FCHK(pb.ensure(tot));
+  size_t o = 0;
+  for (const D2H& r : reads) {
+    if (!r.bytes) continue;
+    if (staged(r)) {
+      FCHK(hipMemcpyAsync(pb.as<char>(o), r.d, r.bytes, hipMemcpyDeviceToHost, st));
+      o += pad(r.bytes);
+    } else {
+      FCHK(hipMemcpyAsync(r.h, r.d, r.bytes, hipMemcpyDeviceToHost, st));
+    }
+  }
+  FCHK(hipStreamSynchronize(st));
+  o = 0;
+  for (const D2H& r : reads)
+    if (r.bytes && staged(r)) {
+      std::memcpy(r.h, pb.as<char>(o), r.bytes);
+      o += pad(r.bytes);
+    }
+  return hipSuccess;
+}
+static hipError_t read_int(const int* d, int* h, hipStream_t st) { return d2h_sync(st, {{h, d, sizeof(int)}}); }
 
 // CSR cell lists from the registration masks (vis = 0: pgrids, 1: vpgrids)
 static hipError_t build_lists(Ctx& c, int vis) {
@@ -3400,8 +3439,7 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
     hipLaunchKernelGGL(cm_serial_kernel, dim3(1), dim3(64), 0, st, s, X.status, W.slot2, X.crec, nk, np, X.counts, X.occ,
                        cthr, check ? 1 : 0, first, (int)pool0, X.acc, W.ctr, X.parents, dP, apply_dflag ? 1 : 0);
     int h[9 + 2 * kSerialCommit];
-    FCHK(hipMemcpyAsync(h, W.ctr, sizeof(h), hipMemcpyDeviceToHost, st));
-    FCHK(hipStreamSynchronize(st));
+    FCHK(d2h_sync(st, {{h, W.ctr, sizeof(h)}}));
     if (h[7] != 0) {
       fprintf(stderr, "expand: %d refined records are not valid patches\n", h[7]);
       return hipErrorIllegalState;
@@ -3429,9 +3467,7 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
   tb = W.temp_bytes;
   FCHK(hipcub::DeviceScan::ExclusiveSum(W.temp, tb, W.nacc, W.aoff, nk + 1, st));
   int hv[2] = {0, 0};
-  FCHK(hipMemcpyAsync(&hv[0], W.aoff + nk, sizeof(int), hipMemcpyDeviceToHost, st));
-  FCHK(hipMemcpyAsync(&hv[1], W.ctr + 6, sizeof(int), hipMemcpyDeviceToHost, st));
-  FCHK(hipStreamSynchronize(st));
+  FCHK(d2h_sync(st, {{&hv[0], W.aoff + nk, sizeof(int)}, {&hv[1], W.ctr + 6, sizeof(int)}}));
   const int na = hv[0], nlive = hv[1];
   int nseg = 0;
   if (na > 0) {
@@ -3454,8 +3490,7 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
     hipLaunchKernelGGL(cm_head_kernel, dim3(nblk(na)), dim3(256), 0, st, W.keys2, W.vals2, na, W.head, W.pos);
     tb = W.temp_bytes;
     FCHK(hipcub::DeviceScan::InclusiveSum(W.temp, tb, W.head, W.segid, na, st));
-    FCHK(hipMemcpyAsync(&nseg, W.segid + na - 1, sizeof(int), hipMemcpyDeviceToHost, st));
-    FCHK(hipStreamSynchronize(st));
+    FCHK(read_int(W.segid + na - 1, &nseg, st));
     hipLaunchKernelGGL(cm_seg_kernel, dim3(nblk(na)), dim3(256), 0, st, W.head, W.segid, na, W.seghead, W.segptr);
   }
   // rounds: every round decides at least the lowest undecided candidate
@@ -3468,8 +3503,7 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
       hipLaunchKernelGGL(cm_decide_kernel, dim3(nblk(nk)), dim3(256), 0, st, s, nk, W.slot2, X.crec, W.aoff, W.nacc, W.pos,
                          W.segid, W.segfirst, W.dec, W.stc, W.flag, X.counts, X.occ, cthr, check ? 1 : 0, W.ctr);
     }
-    FCHK(hipMemcpyAsync(&decided, W.ctr, sizeof(int), hipMemcpyDeviceToHost, st));
-    FCHK(hipStreamSynchronize(st));
+    FCHK(read_int(W.ctr, &decided, st));
     if (round > 4 * (nlive + 2)) return hipErrorIllegalState;  // cannot happen (progress every round)
   }
   hipLaunchKernelGGL(cm_noref_kernel, dim3(nblk(nk)), dim3(256), 0, st, W.stc, nk, W.flag, W.ctr);
@@ -3493,11 +3527,8 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
                                           nk + 1, st));
   }
   int tot[3], ctr[8];
-  FCHK(hipMemcpyAsync(&tot[0], qa + nk, sizeof(int), hipMemcpyDeviceToHost, st));
-  FCHK(hipMemcpyAsync(&tot[1], qb + nk, sizeof(int), hipMemcpyDeviceToHost, st));
-  FCHK(hipMemcpyAsync(&tot[2], qc + nk, sizeof(int), hipMemcpyDeviceToHost, st));
-  FCHK(hipMemcpyAsync(ctr, W.ctr, 8 * sizeof(int), hipMemcpyDeviceToHost, st));
-  FCHK(hipStreamSynchronize(st));
+  FCHK(d2h_sync(st, {{&tot[0], qa + nk, sizeof(int)}, {&tot[1], qb + nk, sizeof(int)}, {&tot[2], qc + nk, sizeof(int)},
+                     {ctr, W.ctr, 8 * sizeof(int)}}));
   if (ctr[2] != 0) {
     fprintf(stderr, "expand: %d refined records are not valid patches\n", ctr[2]);
     return hipErrorIllegalState;
@@ -3511,16 +3542,11 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
                        (int)pool0, first, X.acc, W.push);
   }
   out.push.resize(tot[1]);
-  if (tot[1] > 0)
-    FCHK(hipMemcpyAsync(out.push.data(), W.push, (size_t)tot[1] * sizeof(int2), hipMemcpyDeviceToHost, st));
   hipLaunchKernelGGL(cm_bits_kernel, dim3(nblk(np)), dim3(256), 0, st, W.stc, np, W.pbits);
   out.pbits = 0;
-  if (apply_dflag) {
-    hipLaunchKernelGGL(cm_dflag_kernel, dim3(nblk(np)), dim3(256), 0, st, dP, X.parents, W.pbits, np);
-  } else {
-    FCHK(hipMemcpyAsync(&out.pbits, W.pbits, sizeof(int), hipMemcpyDeviceToHost, st));
-  }
-  FCHK(hipStreamSynchronize(st));
+  if (apply_dflag) hipLaunchKernelGGL(cm_dflag_kernel, dim3(nblk(np)), dim3(256), 0, st, dP, X.parents, W.pbits, np);
+  FCHK(d2h_sync(st, {{out.push.data(), W.push, (size_t)tot[1] * sizeof(int2)},
+                     {&out.pbits, W.pbits, apply_dflag ? 0 : sizeof(int)}}));
   return hipGetLastError();
 }
 
@@ -3785,9 +3811,8 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
     int nok = 0;
     {
       int last_ok = 0, last_idx = 0;
-      FCHK(hipMemcpyAsync(&last_ok, X.cand_ok + (size_t)np * 6 - 1, sizeof(int), hipMemcpyDeviceToHost, st));
-      FCHK(hipMemcpyAsync(&last_idx, X.cidx + (size_t)np * 6 - 1, sizeof(int), hipMemcpyDeviceToHost, st));
-      FCHK(hipStreamSynchronize(st));
+      FCHK(d2h_sync(st, {{&last_ok, X.cand_ok + (size_t)np * 6 - 1, sizeof(int)},
+                         {&last_idx, X.cidx + (size_t)np * 6 - 1, sizeof(int)}}));
       nok = last_idx + (last_ok != 0);
     }
     FCHK(grow(X.cand, X.cap_cand, (size_t)std::max(nok, 1)));
@@ -3798,8 +3823,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
     std::vector<int> batches{-1};
     if (W == 1) {
       std::vector<int> ok(6);
-      FCHK(hipMemcpyAsync(ok.data(), X.cand_ok, 6 * sizeof(int), hipMemcpyDeviceToHost, st));
-      FCHK(hipStreamSynchronize(st));
+      FCHK(d2h_sync(st, {{ok.data(), X.cand_ok, 6 * sizeof(int)}}));
       batches.clear();
       for (int k = 0; k < 6; ++k)
         if (ok[k]) batches.push_back(k);
@@ -3811,8 +3835,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
                          np, X.cand_coord, X.cand_ok, X.cand, X.prep, X.status, cthr, only, X.cidx);
       FCHK(hipPeekAtLastError());
       std::vector<int> status((size_t)np * 6);
-      FCHK(hipMemcpyAsync(status.data(), X.status, (size_t)np * 6 * sizeof(int), hipMemcpyDeviceToHost, st));
-      FCHK(hipStreamSynchronize(st));
+      FCHK(d2h_sync(st, {{status.data(), X.status, (size_t)np * 6 * sizeof(int)}}));
       T.mark(3);
       std::vector<int> slots, slot2surv((size_t)np * 6, -1);
       for (int k = 0; k < np * 6; ++k) {
