@@ -74,11 +74,17 @@ def _make(path):
     """Build in-tree, unless the built artefacts are already newer than every source (the GPU box
     receives the prebuilt libraries without the object files: rebuilding there is not needed)."""
     if os.path.basename(path) == "cmvs-pmvs_amd":
-        outs = [os.path.join(path, f) for f in ("libpmvs_amd.so", "pmvs2", "genOption")]
-        srcs = [os.path.join(path, "csrc", f) for f in os.listdir(os.path.join(path, "csrc"))]
-        srcs += [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
-        srcs.append(os.path.join(path, "Makefile"))
-        if all(os.path.exists(o) for o in outs) and min(os.path.getmtime(o) for o in outs) >= _newest(srcs):
+        # each artefact against its own inputs: make only rebuilds what is stale, but the object
+        # files do not travel, so any make call on the box would recompile the whole library
+        csrc = os.path.join(path, "csrc")
+        inc = [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
+        mk = [os.path.join(path, "Makefile")]
+        lib_srcs = [os.path.join(csrc, f) for f in os.listdir(csrc) if f not in ("pmvs2_main.cpp", "genoption_main.cpp")]
+        deps = {"libpmvs_amd.so": lib_srcs + inc + mk,
+                "pmvs2": [os.path.join(csrc, "pmvs2_main.cpp")] + inc,
+                "genOption": [os.path.join(csrc, "genoption_main.cpp")]}
+        if all(os.path.exists(os.path.join(path, o)) and os.path.getmtime(os.path.join(path, o)) >= _newest(d)
+               for o, d in deps.items()):
             return
     subprocess.run(["make", "-C", path, "-s"], check=True)
 
