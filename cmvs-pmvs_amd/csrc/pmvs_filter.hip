@@ -3276,18 +3276,33 @@ __device__ __forceinline__ void cm_apply(const DScene& s, int k, const int* r, u
   atomicAdd(&ctr[0], 1);
 }
 
-// Decides every undecided candidate that is the first undecided one in all of its cells.
+// each access's segment (segid[pos[e]]), once per commit instead of once per round
+__global__ void cm_segof_kernel(const int* __restrict__ pos, const int* __restrict__ segid, int na, int* __restrict__ segof) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < na) segof[e] = segid[pos[e]];
+}
+
+// Decides every undecided candidate that is the first undecided one in all of its cells (its
+// accesses' segments, four loads in flight at a time).
 // ctr: [0] decided this call, [1] fail_commit, [2] invalid.
 __global__ void cm_decide_kernel(DScene s, int nk, const int* __restrict__ slot2, const int* __restrict__ rec,
-                                 const int* __restrict__ aoff, const int* __restrict__ nacc, const int* __restrict__ pos,
-                                 const int* __restrict__ segid, const int* __restrict__ segfirst,
-                                 unsigned char* __restrict__ dec, int* __restrict__ stc, int* __restrict__ flag,
-                                 unsigned char* __restrict__ counts, unsigned char* __restrict__ occ, int cthr, int check,
-                                 int* __restrict__ ctr) {
+                                 const int* __restrict__ aoff, const int* __restrict__ nacc, const int* __restrict__ segof,
+                                 const int* __restrict__ segfirst, unsigned char* __restrict__ dec, int* __restrict__ stc,
+                                 int* __restrict__ flag, unsigned char* __restrict__ counts, unsigned char* __restrict__ occ,
+                                 int cthr, int check, int* __restrict__ ctr) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nk || dec[k]) return;
-  for (int e = aoff[k], ee = aoff[k] + nacc[k]; e < ee; ++e)
-    if (segfirst[segid[pos[e]]] != k) return;
+  const int e0 = aoff[k], ee = e0 + nacc[k];
+  for (int e = e0; e < ee; e += 4) {
+    int sg[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) sg[u] = (e + u < ee) ? segof[e + u] : -1;
+    bool first = true;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (sg[u] >= 0 && segfirst[sg[u]] != k) first = false;
+    if (!first) return;
+  }
   cm_apply(s, k, rec + (size_t)slot2[k] * kRecInts, dec, stc, flag, counts, occ, cthr, check, ctr);
 }
 
@@ -3514,6 +3529,8 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
     FCHK(hipcub::DeviceScan::InclusiveSum(W.temp, tb, W.head, W.segid, na, st));
     FCHK(read_int(W.segid + na - 1, &nseg, st));
     hipLaunchKernelGGL(cm_seg_kernel, dim3(nblk(na)), dim3(256), 0, st, W.head, W.segid, na, W.seghead, W.segptr);
+    // W.vals (the sort's input values) is free from here: each access's segment
+    hipLaunchKernelGGL(cm_segof_kernel, dim3(nblk(na)), dim3(256), 0, st, W.pos, W.segid, na, W.vals);
   }
   // rounds: every round decides at least the lowest undecided candidate
   int decided = 0;
@@ -3522,8 +3539,8 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
       if (nseg > 0)
         hipLaunchKernelGGL(cm_first_kernel, dim3(nblk(nseg)), dim3(256), 0, st, W.keys2, W.dec, W.seghead, nseg, W.segptr,
                            W.segfirst);
-      hipLaunchKernelGGL(cm_decide_kernel, dim3(nblk(nk)), dim3(256), 0, st, s, nk, W.slot2, X.crec, W.aoff, W.nacc, W.pos,
-                         W.segid, W.segfirst, W.dec, W.stc, W.flag, X.counts, X.occ, cthr, check ? 1 : 0, W.ctr);
+      hipLaunchKernelGGL(cm_decide_kernel, dim3(nblk(nk)), dim3(256), 0, st, s, nk, W.slot2, X.crec, W.aoff, W.nacc, W.vals,
+                         W.segfirst, W.dec, W.stc, W.flag, X.counts, X.occ, cthr, check ? 1 : 0, W.ctr);
     }
     FCHK(read_int(W.ctr, &decided, st));
     if (round > 4 * (nlive + 2)) return hipErrorIllegalState;  // cannot happen (progress every round)
