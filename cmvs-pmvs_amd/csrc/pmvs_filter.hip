@@ -3728,7 +3728,6 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   std::vector<QItem> wave_run, sort_tmp;
   long long seq = c.nalive;
   auto q_empty = [&]() { return queue.empty(); };
-  auto q_pop = [&]() -> int { return queue.pop(); };
   int rank_next = c.nalive;
   int nmodel = n0;
   const int G = std::max(1, sh.world), R = std::min(std::max(0, sh.rank), G - 1);
@@ -3746,7 +3745,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
     c.n = nmodel;
     do {
       const int off = (int)parents.size();
-      while (!q_empty() && (int)parents.size() - off < W) parents.push_back(q_pop());
+      queue.pop_many(parents, (size_t)W);
       const int nc = (int)parents.size() - off;
       T.mark(1);
       FCHK(grow_keep(X.parents, X.cap_par, parents.size(), (size_t)off, st));

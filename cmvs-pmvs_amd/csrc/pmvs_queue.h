@@ -57,6 +57,33 @@ class RunQueue {
     }
     return p;
   }
+  // up to k pops appended to out, the same sequence as k pop() calls: the top run gives items while
+  // its head stays above every other run's head (one heap step per stretch instead of per item)
+  size_t pop_many(std::vector<int>& out, size_t k) {
+    size_t got = 0;
+    while (got < k && !heads_.empty()) {
+      std::pop_heap(heads_.begin(), heads_.end());
+      const int id = heads_.back().second;
+      heads_.pop_back();
+      const bool others = !heads_.empty();
+      const unsigned long long next = others ? heads_.front().first : 0ull;
+      std::vector<QItem>& r = runs_[id];
+      size_t i = pos_[id];
+      do {
+        out.push_back(r[i].p);
+        ++i;
+        ++got;
+      } while (got < k && i < r.size() && (!others || r[i].key > next));
+      pos_[id] = i;
+      if (i < r.size()) {
+        heads_.push_back({r[i].key, id});
+        std::push_heap(heads_.begin(), heads_.end());
+      } else {
+        std::vector<QItem>().swap(r);
+      }
+    }
+    return got;
+  }
   // a wave's pushes, in push order (seq ascending = low key bits descending): a stable LSD radix sort
   // on the high 32 key bits (the _tmp order bits), descending, gives the run's key order
   static void sort_run(std::vector<QItem>& v, std::vector<QItem>& tmp) {

@@ -1,6 +1,6 @@
 // CPU test of pmvs_queue.h (tests/test_run_queue.py): the sorted-run queue pops the same sequence as
 // one binary heap (std::priority_queue under QCmp) over the same keys, for random waves of pushes
-// with many equal _tmp values, interleaved with batch pops.
+// with many equal _tmp values, interleaved with batch pops (single pops and pop_many).
 #include <cstdio>
 #include <queue>
 #include <random>
@@ -25,13 +25,27 @@ extern "C" int run_queue_check(unsigned seed, int nwaves, int initial, long long
   *npops = 0;
   for (int w = 0; w < nwaves; ++w) {
     const int np = popn(rng);
-    for (int k = 0; k < np && !heap.empty(); ++k) {
-      if (rq.empty()) return 1;
-      const int a = heap.top().p;
-      heap.pop();
-      const int b = rq.pop();
-      if (a != b) return 2;
-      ++*npops;
+    if (w & 1) {  // odd waves: one pop_many call (the expansion's), the same sequence as np pops
+      std::vector<int> got;
+      const size_t n = rq.pop_many(got, (size_t)np);
+      if (n != got.size()) return 5;
+      for (size_t k = 0; k < n; ++k) {
+        if (heap.empty()) return 6;
+        const int a = heap.top().p;
+        heap.pop();
+        if (a != got[k]) return 2;
+        ++*npops;
+      }
+      if (n < (size_t)np && !heap.empty()) return 7;
+    } else {
+      for (int k = 0; k < np && !heap.empty(); ++k) {
+        if (rq.empty()) return 1;
+        const int a = heap.top().p;
+        heap.pop();
+        const int b = rq.pop();
+        if (a != b) return 2;
+        ++*npops;
+      }
     }
     run.clear();
     const int ns = wsz(rng);
