@@ -3982,10 +3982,6 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
       const int added = co.nacc;
       if (added > 0 && nmodel + added > cap) { trace_error(hipErrorOutOfMemory, __LINE__); return hipErrorOutOfMemory; }
       stats[6] += added;
-      wave_run.clear();
-      for (const int2& u : co.push) wave_run.push_back({qkey(__int_as_float_h(u.x), seq++), u.y});
-      RunQueue::sort_run(wave_run, sort_tmp);
-      queue.add_run(std::vector<QItem>(wave_run));
       T.mark(7);
       if (added > 0) {
         pool_need = X.pool_host + (size_t)co.entries;
@@ -4016,6 +4012,12 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
         X.pool_host = pool_need;
         rank_next += added;
       }
+      // the wave's pushes as a sorted run of the queue, on the host while the GPU appends and
+      // registers the wave's patches (the next pops come after this)
+      wave_run.clear();
+      for (const int2& u : co.push) wave_run.push_back({qkey(__int_as_float_h(u.x), seq++), u.y});
+      RunQueue::sort_run(wave_run, sort_tmp);
+      queue.add_run(std::vector<QItem>(wave_run));
       T.mark(8);
     }
     if (W == 1 && pbits) {
