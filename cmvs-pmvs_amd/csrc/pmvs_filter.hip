@@ -58,7 +58,7 @@ inline void poison_alloc(void* p, size_t bytes) {
 // with more unique neighbours are walked again by the NB_CAP_BIG form (NbLdsT<16384>, about 130 KB
 // of LDS, one workgroup per CU); only beyond NB_CAP_BIG is the run an error.
 constexpr int NB_CAP = 1024;
-constexpr int NB_CAP_BIG = 16384;
+constexpr int NB_CAP_BIG = PMVS_MAX_NEIGHBOURS;
 // Global scratch per persistent workgroup of the neighbour walks (doubles): the lls rows M
 // (5 CAP), its right-hand side r (CAP), then the filterQuad coordinates fx, fy, fz as floats
 // (1.5 CAP).  Kept out of LDS so NbLds stays ~8 KB (occupancy of the latency-bound walks).

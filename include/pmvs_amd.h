@@ -32,6 +32,10 @@ extern "C" {
 #define PMVS_MAX_TARGETS 256 /* target images (timages) per scene: a C5 cluster is maximage 70 plus overlap */
 #define PMVS_MAX_TAU 16    /* max textures in the objective: tau = min(2*minImageNum, num) */
 #define PMVS_MAX_LEVEL 4   /* reference MyPow2 table limits level to <= 4 (optim.cpp:808-811) */
+/* Unique neighbours one findNeighbors walk may hold (filterNeighbor, findEmptyBlocks, the depth >= 2
+ * check; reference: unbounded std::vector).  Walks past 1024 are redone with a 16384-entry form;
+ * beyond this the call fails with PMVS_EUNSUPPORTED. */
+#define PMVS_MAX_NEIGHBOURS 16384
 
 typedef enum pmvs_status {
   PMVS_OK = 0,
