@@ -2404,26 +2404,62 @@ static PinnedBuf& stage_buf() {
   static thread_local PinnedBuf* pb = new PinnedBuf();  // not freed: it lives as long as its thread
   return *pb;
 }
+// Several small reads are first gathered on the device into one buffer by one kernel, so they cost
+// one copy: each further hipMemcpyAsync was a blit of its own, about 64 us apart (r04m trace).
+constexpr int kGatherMax = 8;
+constexpr size_t kGatherBytes = 1024;  // per item (whole 4-byte words)
+struct GatherArgs {
+  const unsigned* src[kGatherMax];
+  int words[kGatherMax], off[kGatherMax];
+  int n;
+};
+__global__ void gather_words_kernel(GatherArgs a, unsigned* __restrict__ dst) {
+  for (int i = 0; i < a.n; ++i)
+    for (int w = threadIdx.x; w < a.words[i]; w += blockDim.x) dst[a.off[i] + w] = a.src[i][w];
+}
 static hipError_t d2h_sync(hipStream_t st, std::initializer_list<D2H> reads) {
   auto staged = [](const D2H& r) { return r.bytes <= kStageMax; };
   auto pad = [](size_t b) { return (b + 15) & ~(size_t)15; };
   size_t tot = 0;
-  for (const D2H& r : reads)
-    if (staged(r)) tot += pad(r.bytes);
-  PinnedBuf& pb = stage_buf();
-  if (tot) FCHK(pb.ensure(tot));
-  size_t o = 0;
+  int small = 0;
+  bool gatherable = true;
   for (const D2H& r : reads) {
     if (!r.bytes) continue;
-    if (staged(r)) {
-      FCHK(hipMemcpyAsync(pb.as<char>(o), r.d, r.bytes, hipMemcpyDeviceToHost, st));
+    if (staged(r)) tot += pad(r.bytes);
+    if (r.bytes <= kGatherBytes && r.bytes % 4 == 0) ++small;
+    else gatherable = false;
+  }
+  PinnedBuf& pb = stage_buf();
+  if (tot) FCHK(pb.ensure(tot));
+  if (gatherable && small > 1 && small <= kGatherMax) {  // every read small: one kernel, one copy
+    static thread_local unsigned* dstage = nullptr;  // not freed: it lives as long as its thread
+    if (!dstage) FCHK(hipMalloc((void**)&dstage, kGatherMax * kGatherBytes));
+    GatherArgs a{};
+    size_t o = 0;
+    for (const D2H& r : reads) {
+      if (!r.bytes) continue;
+      a.src[a.n] = static_cast<const unsigned*>(r.d);
+      a.words[a.n] = (int)(r.bytes / 4);
+      a.off[a.n] = (int)(o / 4);
+      ++a.n;
       o += pad(r.bytes);
-    } else {
-      FCHK(hipMemcpyAsync(r.h, r.d, r.bytes, hipMemcpyDeviceToHost, st));
+    }
+    hipLaunchKernelGGL(gather_words_kernel, dim3(1), dim3(256), 0, st, a, dstage);
+    FCHK(hipMemcpyAsync(pb.p, dstage, o, hipMemcpyDeviceToHost, st));
+  } else {
+    size_t o = 0;
+    for (const D2H& r : reads) {
+      if (!r.bytes) continue;
+      if (staged(r)) {
+        FCHK(hipMemcpyAsync(pb.as<char>(o), r.d, r.bytes, hipMemcpyDeviceToHost, st));
+        o += pad(r.bytes);
+      } else {
+        FCHK(hipMemcpyAsync(r.h, r.d, r.bytes, hipMemcpyDeviceToHost, st));
+      }
     }
   }
   FCHK(hipStreamSynchronize(st));
-  o = 0;
+  size_t o = 0;
   for (const D2H& r : reads)
     if (r.bytes && staged(r)) {
       std::memcpy(r.h, pb.as<char>(o), r.bytes);
