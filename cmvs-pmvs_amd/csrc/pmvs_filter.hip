@@ -2468,26 +2468,20 @@ static hipError_t d2h_sync(hipStream_t st, std::initializer_list<D2H> reads) {
   return hipSuccess;
 }
 static hipError_t read_int(const int* d, int* h, hipStream_t st) { return d2h_sync(st, {{h, d, sizeof(int)}}); }
-// Host -> device copies of the per-wave index lists (parents, survivor slots, commit slots) through a
-// second pinned buffer of the calling thread: asynchronous for real, where a pageable source is
-// staged by the runtime first.  The buffer is rewritten only after the previous copy from it has
-// completed (an event; in the loop several stream synchronisations lie between two such copies).
-static hipError_t h2d_async(void* d, const void* h, size_t bytes, hipStream_t st) {
+// Host -> device copies of the per-wave index lists (parents, survivor slots, commit slots) through
+// the scene's pinned staging buffer (ExpandBuffers::h2d): asynchronous for real, where a pageable
+// source is staged by the runtime first.  The buffer is rewritten only after the previous copy from
+// it has completed (its event; in the loop several stream synchronisations lie between two copies).
+static hipError_t h2d_async(H2DStage& sg, void* d, const void* h, size_t bytes, hipStream_t st) {
   if (!bytes) return hipSuccess;
   if (bytes > kStageMax) return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st);
-  struct Stage {
-    PinnedBuf pin;
-    hipEvent_t done = nullptr;
-    bool pending = false;
-  };
-  static thread_local Stage* sg = new Stage();  // not freed: it lives as long as its thread
-  if (!sg->done) FCHK(hipEventCreateWithFlags(&sg->done, hipEventDisableTiming));
-  if (sg->pending) FCHK(hipEventSynchronize(sg->done));
-  FCHK(sg->pin.ensure(bytes));
-  std::memcpy(sg->pin.p, h, bytes);
-  FCHK(hipMemcpyAsync(d, sg->pin.p, bytes, hipMemcpyHostToDevice, st));
-  FCHK(hipEventRecord(sg->done, st));
-  sg->pending = true;
+  if (!sg.done) FCHK(hipEventCreateWithFlags(&sg.done, hipEventDisableTiming));
+  if (sg.pending) FCHK(hipEventSynchronize(sg.done));
+  FCHK(sg.pin.ensure(bytes));
+  std::memcpy(sg.pin.p, h, bytes);
+  FCHK(hipMemcpyAsync(d, sg.pin.p, bytes, hipMemcpyHostToDevice, st));
+  FCHK(hipEventRecord(sg.done, st));
+  sg.pending = true;
   return hipSuccess;
 }
 
@@ -3506,7 +3500,7 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
     W.cap_k = c;
   }
   if (!W.ctr) FCHK(cm_grow(W.ctr, 9 + 2 * kSerialCommit));
-  FCHK(h2d_async(W.slot2, slot2h.data(), (size_t)nk * sizeof(int), st));
+  FCHK(h2d_async(X.h2d, W.slot2, slot2h.data(), (size_t)nk * sizeof(int), st));
   if (nk <= kSerialCommit) {
     FCHK(grow(X.acc, X.cap_acc, 2 * (size_t)nk));
     hipLaunchKernelGGL(cm_serial_kernel, dim3(1), dim3(64), 0, st, s, X.status, W.slot2, X.crec, nk, np, X.counts, X.occ,
@@ -3787,7 +3781,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
       FCHK(grow_keep(X.parents, X.cap_par, parents.size(), (size_t)off, st));
       FCHK(grow_keep(X.cand_coord, X.cap_coord, parents.size() * 24, (size_t)off * 24, st));
       FCHK(grow_keep(X.cand_ok, X.cap_ok, parents.size() * 6, (size_t)off * 6, st));
-      FCHK(h2d_async(X.parents + off, parents.data() + off, nc * sizeof(int), st));
+      FCHK(h2d_async(X.h2d, X.parents + off, parents.data() + off, nc * sizeof(int), st));
       FCHK(hipMemsetAsync(B.counters + 3, 0, 5 * sizeof(int), st));
       // Sharded (G > 1): findEmptyBlocks of a contiguous share of the chunk's parents per rank, the
       // candidates (24 floats + 6 flags per parent) all-gathered, so every rank holds the chunk's.
@@ -3932,7 +3926,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
           FCHK(grow(X.res, X.cap_res, (size_t)m));
           FCHK(grow(X.outp, X.cap_outp, (size_t)m));
           FCHK(grow(X.ostatus, X.cap_ost, (size_t)m));
-          FCHK(h2d_async(X.slots, slots.data(), m * sizeof(int), st));
+          FCHK(h2d_async(X.h2d, X.slots, slots.data(), m * sizeof(int), st));
           hipLaunchKernelGGL(gather_slots_kernel, dim3(nblk(m)), dim3(256), 0, st, X.slots, m, X.cand, X.prep, X.cand2, X.prep2,
                              X.cidx);
           if (mine > 0) {

@@ -137,9 +137,20 @@ hipError_t launch_apply_refpos(const DScene& s, pmvs_patch* P, const int* list, 
 // ---- expansion run (pmvs_filter.hip)
 constexpr int kMaxWave = 65536;  // parents per expansion wave (device slot arrays are sized by it)
 struct CommitWork;  // device commit scratch (pmvs_filter.hip)
+// Pinned staging of the per-wave host -> device index lists, with the event of its last copy
+// (recorded on the scene's stream; owned by the scene, so never waited on after that stream is gone)
+struct H2DStage {
+  PinnedBuf pin;
+  hipEvent_t done = nullptr;
+  bool pending = false;
+  ~H2DStage() {
+    if (done) (void)hipEventDestroy(done);
+  }
+};
 struct ExpandBuffers {
   CommitWork* cm = nullptr;
   PinnedBuf pin;  // host staging of the initial queue (order, sorted keys and ranks)
+  H2DStage h2d;
   unsigned char* occ = nullptr;  // per target cell: pgrids holds a patch (device commit)
   size_t cap_occ = 0;
   int *parents = nullptr, *cand_ok = nullptr, *status = nullptr, *slots = nullptr, *ostatus = nullptr, *alive = nullptr;
