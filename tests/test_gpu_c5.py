@@ -2,7 +2,7 @@
 
 C5 -- one CMVS cluster of maximage 70 at 8K (70 views, 7680x4320, level 0), the per-GPU unit of the
 1000-view configuration: one full loop iteration (expand + filter) with the model checks, and the
-first expansion waves against the oracle record for record.  Its own module, so that no other
+first expansion wave against the oracle record for record.  Its own module, so that no other
 test's scenes hold device memory while it runs (the model reaches ~50 M patches of 1608 B).
 """
 import os
@@ -33,18 +33,18 @@ def test_c5_cluster_8k_one_iteration(gpu_available, oracle_mod):
     cands = P.synth_candidates(sp, inp.projections, 5000, seed=0x5EED)
     r, _ = g.refine_batch(cands)
     seeds = P.patches_from_refined(r)
-    # first waves of the iteration-1 expansion, device vs oracle, record for record
+    # the first wave of the iteration-1 expansion (~30 k candidates), device vs oracle, record for record
     ncc, before, depth, cthr = bench.iteration_thresholds(inp.threshold, 0)
     kw = dict(wave=32768, count_threshold=cthr, after_seeds=True, min_candidates=131072)
     g.set_thresholds(ncc, before, depth)
     cap = len(seeds) + 600000
-    g_out, g_alive, g_st = g.expand_run(seeds, cap=cap, max_waves=2, **kw)
+    g_out, g_alive, g_st = g.expand_run(seeds, cap=cap, max_waves=1, **kw)
     o = oracle_mod.OracleScene(inp)
     o.set_thresholds(ncc, before, depth)
-    o_out, o_alive, o_st = o.expand_run(seeds, cap=cap, nthreads=_threads(), max_waves=2, **kw)
+    o_out, o_alive, o_st = o.expand_run(seeds, cap=cap, nthreads=_threads(), max_waves=1, **kw)
     o.close()
     print(f"C5 first waves: {o_st}")
-    assert o_st["added"] > 20000
+    assert o_st["added"] > 10000
     assert all(g_st[k] == o_st[k] for k in o_st), (g_st, o_st)
     assert bench.patch_mismatches(g_out, o_out) == 0 and np.array_equal(g_alive, o_alive)
     del g_out, o_out
