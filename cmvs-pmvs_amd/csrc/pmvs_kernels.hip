@@ -135,19 +135,59 @@ __device__ void grab_batch(const DScene& s, WaveLds<WS>& L, int cnt, const int* 
   __syncthreads();
   // --- bilinear samples: one lane per (texture, sample); positions by the reference's
   // incremental float sums (left += dy per row, vftmp += dx per column, optim.cpp:846-859).
-  for (int t = lane; t < cnt * S; t += WAVE) {
-    const int j = t / S, k = t - j * S;
-    const int slot = slot0 + j;
-    if (!L.valid[slot]) continue;
-    const int yy = k / WS, xx = k - yy * WS;
-    float lx = L.jrow[slot][yy][0], ly = L.jrow[slot][yy][1];
-    const float dxx = L.jdx[slot][0], dxy = L.jdx[slot][1];
-    for (int c = 0; c < xx; ++c) { lx = lx + dxx; ly = ly + dxy; }
-    float rgb[3];
-    get_color(s, s.views[L.jview[slot]], lx, ly, L.jlevel[slot], rgb);
-    L.tex[slot][k][0] = rgb[0];
-    L.tex[slot][k][1] = rgb[1];
-    L.tex[slot][k][2] = rgb[2];
+  // NB samples per lane at a time with all 4 * NB texel loads issued before use (get_color's
+  // arithmetic per sample, as tex_gather does for the refine kernel)
+  constexpr int NB = 4;
+  const int total = cnt * S;
+  for (int u0 = 0; u0 < total; u0 += WAVE * NB) {
+    uint32_t a0[NB], a1[NB], b0[NB], b1[NB];
+    float fx[NB], fy[NB];
+    int lxs[NB], lys[NB];
+    bool live[NB];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int t = u0 + q * WAVE + lane;
+      const int j = t / S, k = t - j * S;
+      const int slot = slot0 + (t < total ? j : 0);
+      live[q] = t < total && L.valid[slot];
+      const uint32_t* p = s.pyr;
+      int W = 0;
+      float lx = 0.0f, ly = 0.0f;
+      if (live[q]) {
+        const int yy = k / WS, xx = k - yy * WS;
+        lx = L.jrow[slot][yy][0];
+        ly = L.jrow[slot][yy][1];
+        const float dxx = L.jdx[slot][0], dxy = L.jdx[slot][1];
+        for (int c = 0; c < xx; ++c) { lx = lx + dxx; ly = ly + dxy; }
+        const DView& v = s.views[L.jview[slot]];
+        const int level = L.jlevel[slot];
+        W = v.w[level];
+        p = s.pyr + v.pyr_off[level] + (long long)(int)ly * W + (int)lx;
+      }
+      fx[q] = lx; fy[q] = ly;
+      lxs[q] = (int)lx; lys[q] = (int)ly;
+      a0[q] = p[0]; a1[q] = p[1]; b0[q] = p[W]; b1[q] = p[W + 1];
+    }
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      if (!live[q]) continue;
+      const int t = u0 + q * WAVE + lane;
+      const int j = t / S, k = t - j * S;
+      const int slot = slot0 + j;
+      const float dx1 = fx[q] - (float)lxs[q], dx0 = 1.0f - dx1;
+      const float dy1 = fy[q] - (float)lys[q], dy0 = 1.0f - dy1;
+      const float f00 = dx0 * dy0, f01 = dx0 * dy1, f10 = dx1 * dy0, f11 = dx1 * dy1;
+      float r = 0.0f, g = 0.0f, b = 0.0f;
+      r += (float)(a0[q] & 0xff) * f00 + (float)(b0[q] & 0xff) * f01;
+      g += (float)((a0[q] >> 8) & 0xff) * f00 + (float)((b0[q] >> 8) & 0xff) * f01;
+      b += (float)((a0[q] >> 16) & 0xff) * f00 + (float)((b0[q] >> 16) & 0xff) * f01;
+      r += (float)(a1[q] & 0xff) * f10 + (float)(b1[q] & 0xff) * f11;
+      g += (float)((a1[q] >> 8) & 0xff) * f10 + (float)((b1[q] >> 8) & 0xff) * f11;
+      b += (float)((a1[q] >> 16) & 0xff) * f10 + (float)((b1[q] >> 16) & 0xff) * f11;
+      L.tex[slot][k][0] = r;
+      L.tex[slot][k][1] = g;
+      L.tex[slot][k][2] = b;
+    }
   }
   __syncthreads();
   // --- normalize, optim.cpp:1031-1067: sequential channel sums, one lane per texture
