@@ -11,6 +11,11 @@
 #                                           refine launch tails (PMVS_REFINE_TAIL=1) of one C3 step,
 #                                           and the bench line
 #   bash tools/gpu_round.sh kt <tag>        rocprofv3 kernel-trace stats of one C3 step only
+#   bash tools/gpu_round.sh suite <tag>     the whole GPU suite with durations, then smoke() (round 4)
+#   bash tools/gpu_round.sh check <tag>     expansion / filter / parity / seed / golden GPU tests, the
+#                                           default bench line and a kernel trace of one C3 step
+#   bash tools/gpu_round.sh c5 <tag>        the C5 test alone, allocation failures traced
+#                                           (PMVS_TRACE_ERRORS)
 set -o pipefail
 WHAT=${1:-test}; TAG=${2:-r01}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -36,6 +41,20 @@ elif [ "$WHAT" = loop ]; then
   PMVS_EXPAND_PROFILE=1 timeout -k 10 300 python3 -u $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-c2 > $O/phase.json 2> $O/phase.err && \
   PMVS_REFINE_TAIL=1 timeout -k 10 300 python3 -u $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-c2 > $O/tail.json 2> $O/tail.err && \
   timeout -k 10 500 python3 -u $R/bench.py --steps 2 --warmup 1 > $O/bench.json 2> $O/bench.err
+elif [ "$WHAT" = suite ]; then
+  timeout -k 10 1000 python3 -u -m pytest $R/tests -m gpu -v --timeout 600 --timeout-method thread --durations=0 > $O/pytest_all.log 2>&1
+  rc=$?
+  [ $rc -le 1 ] && timeout -k 10 200 python3 -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+  [ $rc -eq 0 ]
+elif [ "$WHAT" = check ]; then
+  T=""; for t in test_gpu_expand.py test_gpu_filter.py test_gpu_parity.py test_gpu_parity_matrix.py test_gpu_seed.py test_gpu_golden.py; do T="$T $R/tests/$t"; done
+  timeout -k 10 420 python3 -u -m pytest $T -m gpu -v --timeout 250 --timeout-method thread --durations=0 > $O/pytest.log 2>&1
+  rc=$?
+  [ $rc -le 1 ] && timeout -k 10 500 python3 -u $R/bench.py > $O/bench.json 2> $O/bench.err && \
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-c2 > $O/kt.log 2>&1 && \
+  [ $rc -eq 0 ]
+elif [ "$WHAT" = c5 ]; then
+  PMVS_TRACE_ERRORS=1 timeout -k 10 420 python3 -u -m pytest $R/tests/test_gpu_c5.py -m gpu -v --timeout 400 --timeout-method thread -s > $O/pytest_c5.log 2>&1
 elif [ "$WHAT" = kt ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-c2 > $O/kt.log 2>&1
 else
