@@ -16,6 +16,8 @@
 #                                           default bench line and a kernel trace of one C3 step
 #   bash tools/gpu_round.sh c5 <tag>        the C5 test alone, allocation failures traced
 #                                           (PMVS_TRACE_ERRORS)
+#   bash tools/gpu_round.sh sq <tag>        two SQ counter passes (issue, waits, instruction mix) over one
+#                                           C3 iteration, kernel-trace only, one rocprofv3 run each
 set -o pipefail
 WHAT=${1:-test}; TAG=${2:-r01}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -55,6 +57,13 @@ elif [ "$WHAT" = check ]; then
   [ $rc -eq 0 ]
 elif [ "$WHAT" = c5 ]; then
   PMVS_TRACE_ERRORS=1 timeout -k 10 420 python3 -u -m pytest $R/tests/test_gpu_c5.py -m gpu -v --timeout 400 --timeout-method thread -s > $O/pytest_c5.log 2>&1
+elif [ "$WHAT" = sq ]; then
+  B="$R/bench.py --steps 1 --warmup 0 --iterations 1 --no-cpu-baseline --no-c2"
+  timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY \
+    --output-format csv -d $O/sq_a -o run -- python3 $B > $O/sq_a.log 2>&1 && \
+  timeout -s KILL 240 rocprofv3 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE \
+    --output-format csv -d $O/sq_b -o run -- python3 $B > $O/sq_b.log 2>&1 && \
+  python3 $R/tools/pmc_summary.py $O/sq_a > $O/sq_a.json && python3 $R/tools/pmc_summary.py $O/sq_b > $O/sq_b.json
 elif [ "$WHAT" = kt ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-c2 > $O/kt.log 2>&1
 else
