@@ -57,7 +57,12 @@ inline void poison_alloc(void* p, size_t bytes) {
 // Neighbours per patch the walks hold in LDS.  The NB_CAP form runs every walk; the few patches
 // with more unique neighbours are walked again by the NB_CAP_BIG form (NbLdsT<16384>, about 130 KB
 // of LDS, one workgroup per CU); only beyond NB_CAP_BIG is the run an error.
-constexpr int NB_CAP = 1024;
+// PMVS_NB_CAP / PMVS_NB_GRID_MULT / PMVS_NB_WAVES_PER_EU: experiment variants only (tools/sweep_walks.sh,
+// `make variant VARTU=pmvs_filter`); the product builds the defaults.
+#ifndef PMVS_NB_CAP
+#define PMVS_NB_CAP 1024
+#endif
+constexpr int NB_CAP = PMVS_NB_CAP;
 constexpr int NB_CAP_BIG = PMVS_MAX_NEIGHBOURS;
 // Global scratch per persistent workgroup of the neighbour walks (doubles): the lls rows M
 // (5 CAP), its right-hand side r (CAP), then the filterQuad coordinates fx, fy, fz as floats
@@ -69,7 +74,15 @@ constexpr int NB_SK = 2;
 constexpr int NB_NE = 2;
 // Persistent workgroups per CU-grid unit for the NbLds kernels (neighbor_kernel, depth_post_kernel,
 // empty_blocks_kernel): twice the organizer grid, since ~8 KB of LDS and <= 107 VGPRs leave room.
-constexpr int NB_GRID_MULT = 2;
+#ifndef PMVS_NB_GRID_MULT
+#define PMVS_NB_GRID_MULT 2
+#endif
+constexpr int NB_GRID_MULT = PMVS_NB_GRID_MULT;
+#ifdef PMVS_NB_WAVES_PER_EU
+#define NB_WALK_ATTR __attribute__((amdgpu_waves_per_eu(PMVS_NB_WAVES_PER_EU)))
+#else
+#define NB_WALK_ATTR
+#endif
 __device__ __forceinline__ int lane_id_w() { return threadIdx.x & 63; }
 // Wave-uniform copies (SGPR) of values that are uniform by construction but loaded from memory:
 // every branch or loop around a barrier is driven by one of these, never by a VGPR value.
@@ -1291,7 +1304,7 @@ struct NbOverflow {
   const int* only_n = nullptr;
 };
 template <int CAP>
-__global__ __launch_bounds__(64) void neighbor_kernel(DScene s, FilterDev F, double* __restrict__ scratch,
+__global__ __launch_bounds__(64) NB_WALK_ATTR void neighbor_kernel(DScene s, FilterDev F, double* __restrict__ scratch,
                                                       int* __restrict__ reject, int* __restrict__ overflow,
                                                       int* __restrict__ queue, int* __restrict__ dbg_counts, int rank,
                                                       int world, QuadJobs qj, NbOverflow ov) {
@@ -1863,7 +1876,7 @@ __global__ void group_edges_kernel(DScene s, FilterDev F, int pass, const int* _
 // bins around the patch that hold no neighbour (findNeighbors(patch, ., 1, 4.0f), margin 1,
 // vimages included) and were not tried before (_dflag) get a candidate at `radius`.
 template <int CAP>
-__global__ __launch_bounds__(64) void empty_blocks_kernel(DScene s, FilterDev F, const int* __restrict__ parents, int np,
+__global__ __launch_bounds__(64) NB_WALK_ATTR void empty_blocks_kernel(DScene s, FilterDev F, const int* __restrict__ parents, int np,
                                                           float* __restrict__ cand_coord, int* __restrict__ cand_ok,
                                                           int* __restrict__ queue, int* __restrict__ overflow, NbOverflow ov) {
   __shared__ NbLdsT<CAP> L;
@@ -2016,7 +2029,7 @@ __global__ void prepare_kernel(DScene s, FilterDev F, const unsigned char* __res
 // computeGain + findNeighbors(patch, ., 1, 4, 2) + filterQuad.  out_status: 0 accepted,
 // 2 preProcess failed, 3 postProcess failed.
 template <int CAP>
-__global__ __launch_bounds__(64) void depth_post_kernel(DScene s, FilterDev F, const pmvs_refined* __restrict__ res,
+__global__ __launch_bounds__(64) NB_WALK_ATTR void depth_post_kernel(DScene s, FilterDev F, const pmvs_refined* __restrict__ res,
                                                         int m, pmvs_patch* __restrict__ outp, int* __restrict__ out_status,
                                                         double* __restrict__ scratch, int* __restrict__ queue,
                                                         int* __restrict__ overflow, NbOverflow ov) {
