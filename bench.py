@@ -16,24 +16,28 @@ roofline: the loop's dominant kernel, refine_v2_kernel (the refine batches of >=
 algorithmic bytes = 588 B x valid textures per my_f evaluation over its HIP-event
 time, against 8 TB/s HBM; the smaller batches' workgroup-form kernel in roofline.small_batches.
 refine_c2: the refine kernel alone on configs[1] (8-view 1920x1080, level 1, 100k candidates).
-cpu_baseline: the same metric on the host CPU -- the oracle (CPU restatement) runs the first
-expansion of the same rank-0 C3 scene from the same seeds with the same wave schedule
-(findEmptyBlocks, preparation and the refinements of a wave on a std::thread pool over every CPU
-this process may use, commit serial as in the product), bounded to its first --cpu-waves waves;
-value = patches committed / wall time of those waves.  A refine-only rate over synthetic seed
-candidates is reported beside it (refine_only).
+cpu_baseline: the same metric on the host CPU -- the oracle (CPU restatement) runs the expansions
+of the same rank-0 C3 scene from the same models with the same wave schedule (findEmptyBlocks,
+preparation and the refinements of a wave on a std::thread pool over every CPU this process may
+use, commit serial as in the product): the first --cpu-waves waves of iteration 1 and the whole
+expansions of iterations 2 and 3; value = the GPU step's patches over the CPU time the
+per-iteration rates extrapolate for them.  A refine-only rate over synthetic seed candidates is
+reported beside it (refine_only).
 checks: size-independent properties of the C3 model (identical model from every repetition,
 finite geometry, unit normals, image-list invariants, the synthetic sphere's surface residual).
 
 Multi-GPU (`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`), one
 process per GPU:
-  --mode cluster (default, weak scaling): each rank owns one CMVS-style cluster -- its own
+  --mode shard (default for N > 1, strong scaling): all ranks run ONE 50-view scene, the metric's
+    "50-view 4K ring at 1/2/4/8 GPUs by target-image sharding" (BASELINE.md); every expansion
+    wave's refinements and findEmptyBlocks are split over the ranks, the filter's per-target stages
+    run on the target's owner, and the records are all-gathered over RCCL
+    (pmvs_scene_set_shard_rccl: a C++ RCCL communicator, device-to-device records).  The model is
+    bit-identical to one GPU's.
+  --mode cluster (opt-in, weak scaling): each rank owns one CMVS-style cluster -- its own
     50-view scene (rank-seeded texture) -- and runs the loop on it independently, as the
     reference runs one pmvs2 per cluster option file (genOption.cpp:73-108); no data-path
     collective, only barriers and the SUM / MAX reductions of the counters and the time.
-  --mode shard (strong scaling): all ranks run ONE scene; every expansion wave's refinements are
-    split over the ranks and all-gathered over RCCL (pmvs_scene_set_shard_rccl: a C++ RCCL
-    communicator, device-to-device records).
   --mode c4 (BASELINE.json configs[3] at 8 GPUs): one ring of --c4-views-per-cluster x N views split
     into N CMVS-style clusters (consecutive targets, each sharing --c4-overlap views with each
     neighbour, as CMVS's ske.dat clusters overlap), one per GPU; the loop exchanges the clusters'
@@ -72,7 +76,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--mode", choices=("cluster", "shard", "c4"), default="cluster")
+    ap.add_argument("--mode", choices=("cluster", "shard", "c4"), default=None,
+                    help="multi-GPU mode; default shard (ONE 50-view ring over all GPUs, the metric's "
+                         "target-image sharding, BASELINE.md); cluster = independent replicas")
     ap.add_argument("--c4-views-per-cluster", type=int, default=25)
     ap.add_argument("--c4-overlap", type=int, default=2)
     ap.add_argument("--views", type=int, default=50)
@@ -90,7 +96,11 @@ def parse():
     ap.add_argument("--no-c2", action="store_true", help="skip the configs[1] refine-kernel side measurement")
     ap.add_argument("--only-c2", action="store_true", help="only the configs[1] refine-kernel measurement (profiling)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="refine-only CPU sample time budget")
-    ap.add_argument("--cpu-waves", type=int, default=2, help="expansion waves per iteration in the CPU loop sample")
+    ap.add_argument("--cpu-waves", type=int, default=6,
+                    help="expansion waves of loop iteration 1 in the CPU loop sample (iteration 1 holds ~99%% of a "
+                         "C3 step's patches; its rate is extrapolated from these waves)")
+    ap.add_argument("--cpu-waves-late", type=int, default=0,
+                    help="expansion waves of loop iterations 2.. in the CPU loop sample (0 = the whole expansion)")
     ap.add_argument("--cpu-iterations", type=int, default=3,
                     help="loop iterations sampled by the CPU baseline / full-size parity check (1..iterations)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
@@ -177,23 +187,24 @@ def iteration_thresholds(threshold, t):
     return float(ncc), float(before), t + 1, 4 if t == 0 else 2
 
 
-def loop_samples(P, scene, inp, seeds, args):
+def loop_samples(P, scene, inp, seeds, args, gpu_added):
     """Full-size parity and the loop-level CPU baseline on the rank-0 C3 scene.
 
     For each sampled loop iteration t the model at the start of t (the seeds, or the device loop's
-    model after t iterations) is expanded for --cpu-waves waves with the production schedule, once on
-    the device (pmvs_expand_run with PMVS_EXPAND_MAX_WAVES) and once by the CPU oracle (the same wave
-    schedule; findEmptyBlocks, preparation and refinement on a std::thread pool over every CPU this
-    process may use, commit serial).  parity: the two results record for record.  cpu_baseline:
-    patches the oracle committed per second of its waves, over all sampled iterations."""
+    model after t iterations) is expanded with the production schedule, once on the device
+    (pmvs_expand_run with PMVS_EXPAND_MAX_WAVES) and once by the CPU oracle (the same wave schedule;
+    findEmptyBlocks, preparation and refinement on a std::thread pool over every CPU this process may
+    use, commit serial): the first --cpu-waves waves of iteration 1 (it holds ~99 % of a C3 step's
+    patches) and --cpu-waves-late waves (0: the whole expansion) of iterations 2... parity: the two
+    results record for record.  cpu_baseline: each iteration's CPU rate (patches committed per second
+    of its waves, the iteration's model setup included) applied to the patches the GPU step commits
+    in that iteration (gpu_added[t]): value = sum_t added_t / sum_t (added_t / rate_t)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
     cpus = host_cpus()
     threads = args.cpu_threads or cpus["usable"]
     o = O.OracleScene(inp)
     parity, per_iter = [], []
-    added = 0
-    wave_s = 0.0
     for t in range(max(1, min(args.cpu_iterations, args.iterations))):
         log(f"parity / CPU sample: iteration {t + 1}")
         if t == 0:
@@ -203,21 +214,27 @@ def loop_samples(P, scene, inp, seeds, args):
                                       min_candidates=args.min_candidates)
         ncc, before, depth, cthr = iteration_thresholds(inp.threshold, t)
         kw = dict(wave=args.wave, count_threshold=cthr, after_seeds=(t == 0), min_candidates=args.min_candidates)
-        cap = len(model) + 16 * args.wave * args.cpu_waves + max(args.min_candidates, 1024) * args.cpu_waves * 6
+        waves = args.cpu_waves if t == 0 else args.cpu_waves_late
+        if waves > 0:
+            cap = len(model) + 16 * args.wave * waves + max(args.min_candidates, 1024) * waves * 6
+        else:
+            cap = len(model) + max(1 << 20, len(model) // 4)
         scene.set_thresholds(ncc, before, depth)
-        g_out, g_alive, g_st = scene.expand_run(model, cap=cap, max_waves=args.cpu_waves, **kw)
+        g_out, g_alive, g_st = scene.expand_run(model, cap=cap, max_waves=waves, **kw)
         o.set_thresholds(ncc, before, depth)
-        o_out, o_alive, o_st = o.expand_run(model, cap=cap, nthreads=threads, max_waves=args.cpu_waves, **kw)
+        o_out, o_alive, o_st = o.expand_run(model, cap=cap, nthreads=threads, max_waves=waves, **kw)
         mism = patch_mismatches(g_out, o_out)
         same_stats = all(g_st[k] == o_st[k] for k in o_st)
         ok = mism == 0 and same_stats and bool(np.array_equal(g_alive, o_alive))
         parity.append({"iteration": t + 1, "model_in": int(len(model)), "waves": int(o_st["waves"]),
-                       "candidates": int(o_st["candidates"]), "added": int(o_st["added"]),
-                       "records": int(len(o_out)), "mismatched_records": mism, "stats_equal": same_stats, "ok": ok})
-        per_iter.append({"iteration": t + 1, "added": int(o_st["added"]), "wave_s": round(o.last_wave_s, 3),
-                         "value": round(o_st["added"] / max(o.last_wave_s, 1e-9), 1)})
-        added += o_st["added"]
-        wave_s += o.last_wave_s
+                       "whole_expansion": waves <= 0, "candidates": int(o_st["candidates"]),
+                       "added": int(o_st["added"]), "records": int(len(o_out)), "mismatched_records": mism,
+                       "stats_equal": same_stats, "ok": ok})
+        rate = o_st["added"] / max(o.last_wave_s, 1e-9)
+        ga = int(gpu_added[t]) if t < len(gpu_added) else 0
+        per_iter.append({"iteration": t + 1, "waves": int(o_st["waves"]), "whole_expansion": waves <= 0,
+                         "added": int(o_st["added"]), "wave_s": round(o.last_wave_s, 3), "value": round(rate, 1),
+                         "gpu_added": ga, "cpu_s_extrapolated": round(ga / max(rate, 1e-9), 2)})
         del g_out, o_out, model
     scene.set_thresholds(*iteration_thresholds(inp.threshold, 0)[:2], 0)
     # refine-only side figure: preProcess -> refinePatch -> postProcess on seed-path candidates
@@ -232,17 +249,26 @@ def loop_samples(P, scene, inp, seeds, args):
         acc += rs["accepted"]
     tr = time.perf_counter() - t0
     o.close()
+    tot_added = sum(p["gpu_added"] for p in per_iter)
+    tot_s = sum(p["cpu_s_extrapolated"] for p in per_iter)
+    sampled_added = sum(p["added"] for p in per_iter)
+    sampled_s = sum(p["wave_s"] for p in per_iter)
     first = per_iter[0]
-    cpu = {"value": round(added / max(wave_s, 1e-9), 1), "unit": "refined patches/s", "cores": threads, "kind": "port",
-           "sample": f"first {args.cpu_waves} expansion waves (wave {args.wave}, min_candidates {args.min_candidates}) "
-                     f"of each of loop iterations 1..{len(per_iter)} on the rank-0 C3 scene (iteration t starts from "
-                     f"the device loop's model after t-1 iterations; the same waves run on the device and match record "
-                     f"for record, parity_c3_first_waves): {added} patches committed in {wave_s:.2f} s; "
-                     f"oracle/liboracle.so (CPU restatement), {threads} threads",
+    cpu = {"value": round(tot_added / max(tot_s, 1e-9), 1), "unit": "refined patches/s", "cores": threads,
+           "kind": "port",
+           "sample": f"per-iteration CPU rates weighted by the GPU step's own patches (extrapolated): iteration 1 "
+                     f"from its first {first['waves']} expansion waves ({first['added']} patches in {first['wave_s']} s), "
+                     f"iterations 2..{len(per_iter)} from "
+                     + ("their whole expansions" if args.cpu_waves_late <= 0 else f"their first {args.cpu_waves_late} waves")
+                     + f" (wave {args.wave}, min_candidates {args.min_candidates}; each iteration starts from the "
+                     f"device loop's model, and the same waves run on the device and match record for record, "
+                     f"parity_c3_first_waves); value = sum_t gpu_added_t / sum_t (gpu_added_t / cpu_rate_t) = "
+                     f"{tot_added} patches in {tot_s:.1f} s extrapolated; expansion only (the filter passes are not "
+                     f"timed on the CPU, so this overstates the CPU); oracle/liboracle.so (CPU restatement), "
+                     f"{threads} threads",
            "per_iteration": per_iter,
-           "first_waves_iteration1": {"value": first["value"], "unit": "refined patches/s",
-                                      "sample": f"first {args.cpu_waves} waves of iteration 1 only: {first['added']} "
-                                                f"patches in {first['wave_s']} s"},
+           "sampled": {"value": round(sampled_added / max(sampled_s, 1e-9), 1), "unit": "refined patches/s",
+                       "sample": f"the sampled waves pooled, unweighted: {sampled_added} patches in {sampled_s:.2f} s"},
            "host": cpus,
            "refine_only": {"value": round(acc / tr, 1), "unit": "refined patches/s",
                            "sample": f"{done} seed-path candidates, preProcess->refinePatch->postProcess, {tr:.1f} s"}}
@@ -376,6 +402,8 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
     dev = torch.device("cuda", local)
+    if args.mode is None:
+        args.mode = "shard" if world > 1 else "cluster"
     shard = args.mode == "shard" and world > 1
     c4 = args.mode == "c4"
     if args.only_c2:
@@ -487,9 +515,9 @@ def main():
         checks = model_checks(last, inp, hashes)
         del last
         cpu = parity = None
-        if not args.no_cpu_baseline and not shard and not c4:
-            cpu, parity = loop_samples(P, scene, inp, seeds, args)
         first = logs[0][1]
+        if not args.no_cpu_baseline and not shard and not c4:
+            cpu, parity = loop_samples(P, scene, inp, seeds, args, [it["expand"]["added"] for it in first])
         result = {
             "metric": METRIC,
             "value": round(added_all / elapsed_max, 1),

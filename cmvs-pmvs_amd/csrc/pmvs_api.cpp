@@ -249,6 +249,7 @@ struct pmvs_scene {
     if (ev1) (void)hipEventDestroy(ev1);
     for (hipEvent_t e : kev)
       if (e) (void)hipEventDestroy(e);
+    if (stream) d2h_stage_release(stream);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };

@@ -31,6 +31,8 @@
 #include <sys/mman.h>
 #include <deque>
 #include <functional>
+#include <mutex>
+#include <unordered_map>
 #include <queue>
 #include <vector>
 
@@ -2051,7 +2053,9 @@ __global__ __launch_bounds__(64) NB_WALK_ATTR void depth_post_kernel(DScene s, F
     // are not guaranteed to reconverge with lane 0 before the next ticket is broadcast.
     const int rstatus = uni(rr.status);
     int st = (rstatus == PMVS_FAIL_POST) ? 3 : 2;
-    if (rstatus == PMVS_FAIL_OVERFLOW && lane == 0) atomicAdd(overflow, 1);  // an error for the run, never a reject
+    // an error for the run, never a reject.  The re-walk pass (ov.only: candidates whose neighbour list
+    // overflowed NB_CAP) runs the whole body again, so the overflow counts are taken in the first pass only
+    if (rstatus == PMVS_FAIL_OVERFLOW && lane == 0 && !ov.only) atomicAdd(overflow, 1);
     if (rstatus == PMVS_ACCEPTED) {
     st = 0;
     if (lane == 0) {
@@ -2098,7 +2102,7 @@ __global__ __launch_bounds__(64) NB_WALK_ATTR void depth_post_kernel(DScene s, F
         }
         __syncthreads();
         // more than PMVS_MAX_IMAGES visible targets: counted as an overflow (the run fails), never clamped silently
-        if (lane == 0 && nv + __popcll(mask) > PMVS_MAX_IMAGES) atomicAdd(overflow, 1);
+        if (lane == 0 && !ov.only && nv + __popcll(mask) > PMVS_MAX_IMAGES) atomicAdd(overflow, 1);
         if (lane == 0) q.num_vimages = imin(PMVS_MAX_IMAGES, nv + __popcll(mask));
         __syncthreads();
       }
@@ -2403,24 +2407,51 @@ struct Ctx {
 };
 
 // Device -> host reads of the loop's control values (counts, flags, per-wave status) through a
-// pinned staging buffer of the calling host thread.  Into pageable memory every hipMemcpyAsync is
-// a staged copy with a wait of its own (about 75 us each between the C3 loop's kernels,
-// profiles/r04h_kernel_trace gaps); here the reads of one point share one stream synchronisation.
-// Reads above kStageMax bytes go to their destination directly (bandwidth-bound anyway).
+// pinned staging buffer.  Into pageable memory every hipMemcpyAsync is a staged copy with a wait of
+// its own (about 75 us each between the C3 loop's kernels, profiles/r04h_kernel_trace gaps); here the
+// reads of one point share one stream synchronisation.  Reads above kStageMax bytes go to their
+// destination directly (bandwidth-bound anyway).
 struct D2H {
   void* h;
   const void* d;
   size_t bytes;
 };
 constexpr size_t kStageMax = 256 << 10;
-static PinnedBuf& stage_buf() {
-  static thread_local PinnedBuf* pb = new PinnedBuf();  // not freed: it lives as long as its thread
-  return *pb;
-}
 // Several small reads are first gathered on the device into one buffer by one kernel, so they cost
 // one copy: each further hipMemcpyAsync was a blit of its own, about 64 us apart (r04m trace).
 constexpr int kGatherMax = 8;
 constexpr size_t kGatherBytes = 1024;  // per item (whole 4-byte words)
+// The staging buffers belong to the stream they are used on, i.e. to one scene on one device (the
+// gather buffer is device memory of the stream's device).  They are created on the stream's first
+// read and freed by d2h_stage_release when the scene is destroyed (pmvs_scene_destroy), so a thread
+// that drives scenes on two GPUs never gathers into another device's memory, and exiting threads
+// leave nothing behind.
+struct D2HStage {
+  PinnedBuf pin;
+  unsigned* dgather = nullptr;
+};
+static std::mutex g_stage_mu;
+static std::unordered_map<hipStream_t, D2HStage*> g_stages;
+static D2HStage& stage_for(hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_stage_mu);
+  D2HStage*& p = g_stages[st];
+  if (!p) p = new D2HStage();
+  return *p;
+}
+}  // namespace
+void d2h_stage_release(hipStream_t st) {
+  D2HStage* p = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    auto it = g_stages.find(st);
+    if (it == g_stages.end()) return;
+    p = it->second;
+    g_stages.erase(it);
+  }
+  if (p->dgather) (void)hipFree(p->dgather);
+  delete p;  // PinnedBuf frees the pinned buffer
+}
+namespace {
 struct GatherArgs {
   const unsigned* src[kGatherMax];
   int words[kGatherMax], off[kGatherMax];
@@ -2442,11 +2473,12 @@ static hipError_t d2h_sync(hipStream_t st, std::initializer_list<D2H> reads) {
     if (r.bytes <= kGatherBytes && r.bytes % 4 == 0) ++small;
     else gatherable = false;
   }
-  PinnedBuf& pb = stage_buf();
+  D2HStage& sg = stage_for(st);
+  PinnedBuf& pb = sg.pin;
   if (tot) FCHK(pb.ensure(tot));
   if (gatherable && small > 1 && small <= kGatherMax) {  // every read small: one kernel, one copy
-    static thread_local unsigned* dstage = nullptr;  // not freed: it lives as long as its thread
-    if (!dstage) FCHK(hipMalloc((void**)&dstage, kGatherMax * kGatherBytes));
+    if (!sg.dgather) FCHK(hipMalloc((void**)&sg.dgather, kGatherMax * kGatherBytes));
+    unsigned* const dstage = sg.dgather;
     GatherArgs a{};
     size_t o = 0;
     for (const D2H& r : reads) {

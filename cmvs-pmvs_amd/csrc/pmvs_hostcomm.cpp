@@ -9,7 +9,7 @@
 //   * with PMVS_EXCHANGE=tcp the boundary records themselves go through it -- several ranks on ONE
 //     GPU (RCCL refuses two ranks per device), e.g. the two-process test of tests/test_gpu_pmvs2.py.
 // One all-gather: every rank sends {bytes, data} to rank 0, which checks that the sizes agree and
-// returns {status, world x data} to each.  A peer that dies closes its socket, so its partners'
+// returns {status, world x data, commit} to each (commit 0: every peer was served).  A peer that dies closes its socket, so its partners'
 // reads fail and the exchange returns -1 instead of blocking (the loop's error protocol then ends
 // every rank).  Blocking reads without a time limit: an exchange waits for the slowest rank's
 // expansion, which may take minutes.
@@ -56,6 +56,27 @@ bool write_all(int fd, const void* p, size_t n) {
 bool read_all(int fd, void* p, size_t n) {
   char* c = static_cast<char*>(p);
   while (n) {
+    const ssize_t k = ::recv(fd, c, n, 0);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) return false;
+    c += k;
+    n -= (size_t)k;
+  }
+  return true;
+}
+
+// read_all with a time limit (the join handshake: a client that connects and sends nothing must not
+// hold rank 0 past the job's start-up deadline)
+bool read_all_within(int fd, void* p, size_t n, int ms) {
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(ms);
+  char* c = static_cast<char*>(p);
+  while (n) {
+    const long long left =
+        std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now()).count();
+    pollfd pf{fd, POLLIN, 0};
+    const int pr = ::poll(&pf, 1, (int)std::max<long long>(0, left));
+    if (pr < 0 && errno == EINTR) continue;
+    if (pr <= 0) return false;
     const ssize_t k = ::recv(fd, c, n, 0);
     if (k < 0 && errno == EINTR) continue;
     if (k <= 0) return false;
@@ -139,7 +160,7 @@ pmvs_status pmvs_tcp_create(int32_t rank, int32_t world, const char* addr, int32
       const int fd = ::accept(ls, nullptr, nullptr);
       if (fd < 0) continue;
       uint32_t hello[3] = {0, 0, 0};  // magic, rank, world
-      if (!read_all(fd, hello, sizeof(hello)) || hello[0] != kMagic || hello[2] != (uint32_t)world || hello[1] == 0 ||
+      if (!read_all_within(fd, hello, sizeof(hello), left_ms()) || hello[0] != kMagic || hello[2] != (uint32_t)world || hello[1] == 0 ||
           hello[1] >= (uint32_t)world || c->peers[hello[1]] >= 0) {
         ::close(fd);
         continue;
@@ -192,8 +213,13 @@ int pmvs_tcp_allgather(void* ctx, const void* send, int64_t bytes, void* recv) {
     const int64_t h = bytes;
     if (!write_all(c->hub, &h, sizeof(h)) || (b && !write_all(c->hub, send, b))) return -1;
     int32_t status = -1;
-    if (!read_all(c->hub, &status, sizeof(status)) || status != 0) return -1;
-    return (b == 0 || read_all(c->hub, recv, b * (size_t)c->world)) ? 0 : -1;
+    if (!read_all(c->hub, &status, sizeof(status))) return -1;
+    if (status == 0 && b && !read_all(c->hub, recv, b * (size_t)c->world)) return -1;
+    // the commit word, sent after every exchange (so a failed one leaves the stream in step): 0 only
+    // if rank 0 delivered the payload to every peer
+    int32_t commit = -1;
+    if (!read_all(c->hub, &commit, sizeof(commit))) return -1;
+    return (status == 0 && commit == 0) ? 0 : -1;
   }
   // rank 0: collect, check, broadcast.  A peer that is gone (or sends a different size) fails the
   // exchange for everyone: the live peers still get the failure status, so none of them blocks.
@@ -220,11 +246,27 @@ int pmvs_tcp_allgather(void* ctx, const void* send, int64_t bytes, void* recv) {
       status = -1;
     }
   }
+  // status to every peer first, then the payload, then a commit word: a peer returns success only
+  // if every peer was served, so the ranks never disagree on the outcome of one exchange.  A peer
+  // whose write fails is closed, which fails its next read.
   for (int p = 1; p < c->world; ++p) {
-    const int fd = c->peers[p];
+    int& fd = c->peers[p];
     if (fd < 0) continue;
-    if (!write_all(fd, &status, sizeof(status)) || (status == 0 && b && !write_all(fd, r, b * (size_t)c->world)))
-      status = -1;
+    if (!write_all(fd, &status, sizeof(status))) { ::close(fd); fd = -1; status = -1; }
+  }
+  if (status == 0 && b)
+    for (int p = 1; p < c->world; ++p) {
+      int& fd = c->peers[p];
+      if (fd < 0) continue;
+      if (!write_all(fd, r, b * (size_t)c->world)) { ::close(fd); fd = -1; status = -1; }
+    }
+  if (status == 0)
+    for (int p = 1; p < c->world; ++p)
+      if (c->peers[p] < 0) status = -1;
+  for (int p = 1; p < c->world; ++p) {
+    int& fd = c->peers[p];
+    if (fd < 0) continue;
+    if (!write_all(fd, &status, sizeof(status))) { ::close(fd); fd = -1; status = -1; }
   }
   return status == 0 ? 0 : -1;
 }

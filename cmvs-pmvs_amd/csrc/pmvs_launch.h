@@ -209,6 +209,8 @@ using CompactDst = std::function<hipError_t(int, pmvs_patch**)>;
 hipError_t compact_model(FilterBuffers& B, const pmvs_patch* src, int n, const int* keep, const CompactDst& dst_for,
                          int* nkept, hipStream_t st);
 hipError_t fill_int(int* a, int n, int v, hipStream_t st);
+// frees the device-to-host staging buffers of a scene's stream (pmvs_scene_destroy)
+void d2h_stage_release(hipStream_t st);
 
 // ---- CMVS cluster boundary exchange (pmvs_scene_set_cluster)
 struct ClusterMaps {              // device tables of one cluster scene

@@ -33,5 +33,7 @@ for cfg in cfgs:
         acc = int((r["status"] == P.ACCEPTED).sum())
         print(json.dumps({"lib": lib, "cfg": cfg, "n": n, "refine_ms": round(best, 3), "accepted": acc,
                           "patches_per_s": round(acc / best * 1e3, 1), "evals": st["evals"],
+                          "opt_cycles": st["opt_cycles"], "objective_cycles": st["objective_cycles"],
+                          "rounds": st["rounds"], "chunks": st["chunks"], "prof": st["prof"],
                           "sha1": hashlib.sha1(r.tobytes()).hexdigest()[:12]}), flush=True)
     g.close()
