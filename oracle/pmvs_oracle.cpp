@@ -1178,6 +1178,25 @@ int oracle_bobyqa_test(int kind, const double* x0, int maxeval, double* xout, do
 // independent of it.
 void oracle_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
 
+// CFindMatch::isNeighbor(lhs, rhs, hunit, thr) and isNeighborRadius (findMatch.cpp:125-185) as
+// restated in filter_oracle.h (is_neighbor_h), on records of 21 floats (lhs coord[4] normal[4] dscale,
+// rhs coord[4] normal[4] dscale, hunit, threshold, radius): out[2i] / out[2i + 1].  Pinned against
+// the reference's own findMatch.cpp by tests/test_isneighbor_pinning.py.
+void oracle_is_neighbor(const float* in, int n, int* out) {
+  for (int i = 0; i < n; ++i) {
+    const float* r = in + (size_t)i * 21;
+    FPatch l, q;
+    for (int k = 0; k < 4; ++k) {
+      l.coord[k] = r[k]; l.normal[k] = r[4 + k];
+      q.coord[k] = r[9 + k]; q.normal[k] = r[13 + k];
+    }
+    l.dscale = r[8];
+    q.dscale = r[17];
+    out[2 * i] = is_neighbor_h(l, q, r[18], r[19], 0.0f, false);
+    out[2 * i + 1] = is_neighbor_h(l, q, r[18], r[19], r[20], true);
+  }
+}
+
 void oracle_filter_run(void* h, pmvs_patch* patches, int n, int* keep, int* counts) {
   const OScene& s = *static_cast<const OScene*>(h);
   std::vector<FPatch> P(n);

@@ -36,6 +36,7 @@ def lib():
         L.oracle_scene_create.restype = C.c_void_p
         L.oracle_scene_create.argtypes = [C.POINTER(P.SceneDesc)]
         L.oracle_scene_destroy.argtypes = [C.c_void_p]
+        L.oracle_is_neighbor.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
         L.oracle_set_thresholds.argtypes = [C.c_void_p, C.c_float, C.c_float, C.c_int]
         L.oracle_get_level.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.oracle_camera.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
@@ -109,6 +110,27 @@ def ref_detect_features(rgb, mask=None, edge=None, fcsize=16):
         if n <= cap:
             return out[:n]
         cap = n
+
+
+def is_neighbor(records):
+    """oracle_is_neighbor: the restated isNeighbor / isNeighborRadius on (n, 21) float32 records."""
+    r = np.ascontiguousarray(records, np.float32)
+    out = np.zeros((len(r), 2), np.int32)
+    lib().oracle_is_neighbor(r.ctypes.data, len(r), out.ctypes.data)
+    return out
+
+
+def ref_is_neighbor(records):
+    """The reference's own CFindMatch::isNeighbor / isNeighborRadius (oracle/_ref/isneighbor, built
+    from findMatch.cpp unmodified) on (n, 21) float32 records; None when _ref is absent."""
+    import struct
+    import subprocess
+    exe = os.path.join(HERE, "_ref", "isneighbor")
+    if not os.path.exists(exe):
+        return None
+    r = np.ascontiguousarray(records, np.float32)
+    p = subprocess.run([exe], input=struct.pack("i", len(r)) + r.tobytes(), capture_output=True, check=True)
+    return np.frombuffer(p.stdout, np.int32).reshape(len(r), 2).copy()
 
 
 def _p(a):

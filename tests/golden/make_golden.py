@@ -136,6 +136,86 @@ def make_expand_dirs():
     print(f"{path}: {os.path.getsize(path)} B")
 
 
+def isneighbor_records(rng, n):
+    """Patch pairs for CFindMatch::isNeighbor / isNeighborRadius (findMatch.cpp:125-185): (n, 21) float32
+    records (lhs coord, normal, dscale, rhs coord, normal, dscale, hunit, threshold, radius) with
+    random geometry at the scales of a patch model (dscale and hunit ~1e-2 around a unit sphere)."""
+    c0 = rng.normal(0, 1, (n, 3))
+    n0 = rng.normal(0, 1, (n, 3))
+    n0 /= np.linalg.norm(n0, axis=1, keepdims=True)
+    tang = rng.normal(0, 1, (n, 3))
+    tang -= (tang * n0).sum(1, keepdims=True) * n0
+    tang /= np.linalg.norm(tang, axis=1, keepdims=True)
+    ds0 = np.exp(rng.uniform(np.log(2e-3), np.log(2e-2), n))
+    ds1 = ds0 * np.exp(rng.uniform(-0.3, 0.3, n))
+    hunit = ds0 * np.exp(rng.uniform(-1, 1, n))
+    along = rng.uniform(0, 6, n) * hunit
+    off = rng.normal(0, 1, n) * ds0 * rng.choice([0.3, 1, 3], n)
+    c1 = c0 + along[:, None] * tang + off[:, None] * n0
+    ang = rng.uniform(0, np.pi, n) * rng.choice([0.05, 0.3, 1.0], n)
+    axis = np.cross(n0, tang)
+    n1 = n0 * np.cos(ang)[:, None] + axis * np.sin(ang)[:, None]
+    thr = rng.choice([0.5, 1.0, 2.0, 4.0], n)
+    radius = hunit * rng.uniform(0.5, 6, n)
+    r = np.zeros((n, 21), np.float32)
+    r[:, 0:3], r[:, 3] = c0, 1
+    r[:, 4:7] = n0
+    r[:, 8] = ds0
+    r[:, 9:12], r[:, 12] = c1, 1
+    r[:, 13:16] = n1
+    r[:, 17], r[:, 18], r[:, 19], r[:, 20] = ds1, hunit, thr, radius
+    return r
+
+
+def isneighbor_boundary(rng, n, col, lo, hi, steps=40):
+    """Records on the decision boundary of the REFERENCE's isNeighbor (or isNeighborRadius, col 1):
+    per record one scalar (the normal offset of rhs, scaled) is bisected between lo and hi until the
+    reference's answer flips between adjacent float32 values; both sides are kept."""
+    base = isneighbor_records(rng, n)
+    d = base[:, 9:12] - base[:, 0:3]
+    a = np.full(n, lo, np.float64)
+    b = np.full(n, hi, np.float64)
+
+    def at(t):
+        r = base.copy()
+        r[:, 9:12] = (base[:, 0:3] + d * t[:, None]).astype(np.float32)
+        return r
+    fa = O.ref_is_neighbor(at(a))[:, col]
+    fb = O.ref_is_neighbor(at(b))[:, col]
+    keep = fa != fb
+    for _ in range(steps):
+        m = 0.5 * (a + b)
+        fm = O.ref_is_neighbor(at(m))[:, col]
+        same = fm == fa
+        a = np.where(same, m, a)
+        b = np.where(same, b, m)
+    return np.concatenate([at(a)[keep], at(b)[keep]])
+
+
+def make_isneighbor():
+    """CFindMatch::isNeighbor / isNeighborRadius of the reference's own findMatch.cpp (compiled
+    unmodified in oracle/_ref/isneighbor) on random patch pairs and on pairs bisected onto the
+    reference's decision boundaries (threshold, radius, and the 120-degree normal test)."""
+    rng = np.random.default_rng(125)
+    recs = [isneighbor_records(rng, 3000), isneighbor_boundary(rng, 1000, 0, 0.0, 4.0),
+            isneighbor_boundary(rng, 1000, 1, 0.0, 4.0)]
+    # normals near 120 degrees apart: lhs . rhs against cos(120 deg) (findMatch.cpp:135)
+    r = isneighbor_records(rng, 500)
+    r[:, 9:12] = r[:, 0:3]
+    n0 = r[:, 4:7].astype(np.float64)
+    perp = np.cross(n0, rng.normal(0, 1, (len(r), 3)))
+    perp /= np.linalg.norm(perp, axis=1, keepdims=True)
+    ang = 2 * np.pi / 3 + rng.normal(0, 1e-6, len(r))
+    r[:, 13:16] = (n0 * np.cos(ang)[:, None] + perp * np.sin(ang)[:, None]).astype(np.float32)
+    recs.append(r)
+    records = np.concatenate(recs).astype(np.float32)
+    ref = O.ref_is_neighbor(records)
+    path = os.path.join(HERE, "isneighbor.npz")
+    np.savez_compressed(path, records=records, ref=ref)
+    print(f"{path}: {os.path.getsize(path)} B, {len(records)} pairs, isNeighbor true {int(ref[:, 0].sum())}, "
+          f"isNeighborRadius true {int(ref[:, 1].sum())}")
+
+
 def make_features():
     """CDetectFeatures' two detectors (harris.cpp / dog.cpp compiled unmodified in oracle/_ref) on
     every view of the scene goldens at their option level: REFERENCE outputs (features.npz)."""
@@ -253,6 +333,7 @@ def make(name, views, width, height, level, csize, ntex, neval, nref):
 
 if __name__ == "__main__":
     O.build()
+    make_isneighbor()
     make_expand_dirs()
     make_features()
     make_seeds()
