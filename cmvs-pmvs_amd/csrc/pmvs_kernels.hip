@@ -26,10 +26,10 @@
 
 #include "bobyqa_dev.h"
 #include "pmvs_device.h"
+#include "pmvs_refine.h"
 
 namespace pmvsdev {
 
-constexpr int WAVE = 64;
 #ifndef REFINE_TSLOTS
 #define REFINE_TSLOTS 48
 #endif
@@ -53,8 +53,6 @@ struct WaveLds {
   int cand;
   int overflow;
 };
-
-__device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
 
 // Order-preserving compaction across the wave: returns the position of this lane's kept element
 // among kept elements of lanes < lane, and writes the number kept to *count.
@@ -238,29 +236,6 @@ __device__ __forceinline__ float tex_dot(const WaveLds<WS>& L, int a, int b) {
     ans += p.z * q.z;
   }
   return __fdiv_rn(ans, (float)(3 * S));
-}
-
-// ---------------------------------------------------------------- encode / decode
-struct RefineSetup {
-  float center[4], ray[4];
-  float dscale, ascale;
-  int ref;  // _indexesT[id][0]
-};
-
-// COptim::decode, optim.cpp:690-707.
-__device__ __forceinline__ void decode(const DScene& s, const RefineSetup& R, const double* vect, float* coord,
-                                       float* normal) {
-  const double sc = (double)R.dscale * vect[0];
-  for (int i = 0; i < 4; ++i) coord[i] = R.center[i] + (float)((double)R.ray[i] * sc);
-  const DView& v = s.views[R.ref];
-  const float angle1 = (float)(vect[1] * (double)R.ascale);
-  const float angle2 = (float)(vect[2] * (double)R.ascale);
-  const double ca2 = cos((double)angle2);
-  const float fx = (float)(sin((double)angle1) * ca2);
-  const float fy = (float)sin((double)angle2);
-  const float fz = (float)(-cos((double)angle1) * ca2);
-  for (int i = 0; i < 3; ++i) normal[i] = (v.xaxis[i] * fx + v.yaxis[i] * fy) + v.zaxis[i] * fz;
-  normal[3] = 0.0f;
 }
 
 // COptim::encode, optim.cpp:660-688, up to its transcendental functions: vect[0] and the normal's
@@ -909,16 +884,6 @@ struct RefLds {
   int rsize[NC], rfirst[NC];
 };
 
-__device__ __forceinline__ int wave_excl_scan(int v) {
-  const int lane = lane_id();
-  int incl = v;
-  for (int d = 1; d < WAVE; d <<= 1) {
-    const int t = __shfl_up(incl, d);
-    if (lane >= d) incl += t;
-  }
-  return incl - v;
-}
-
 // Phase timers of the refine kernel (pmvs_stats.prof / cyc_opt / cyc_eval): diagnostic builds
 // only (-DBQ_PROFILE, libpmvs_amd_prof.so); the product build keeps the counters' registers free.
 #if defined(BQ_PROFILE)
@@ -939,63 +904,23 @@ __device__ __forceinline__ int wave_excl_scan(int v) {
 // Per-texture steps of the cooperative objective evaluation, shared by the wavefront form
 // (refine_v2_kernel) and the workgroup form (refine_wg_kernel).  L is the kernel's LDS layout
 // (jreq / jidx / views / geo name the slot's request, tex / ave / j* hold the slot).
-// setup, one thread per texture: grabTex optim.cpp:818-846 + grabSafe :783-805
+// setup, one thread per texture: tex_geom (pmvs_refine.h) computes the frame, tex_setup stores it.
 template <int WS, class L>
 __device__ __forceinline__ void tex_setup(const DScene& s, L& C, int t) {
   const int r = C.jreq[t];
-  const int index = C.views[r][C.jidx[t]];
-  const float* g = C.geo[r];
-  const float coord[4] = {g[0], g[1], g[2], g[3]}, pz[4] = {g[4], g[5], g[6], g[7]};
-  const float px[4] = {g[8], g[9], g[10], g[11]}, py[4] = {g[12], g[13], g[14], g[15]};
-  const DView& v = s.views[index];
-  int ok = 1;
-  float ray[4] = {v.center[0] - coord[0], v.center[1] - coord[1], v.center[2] - coord[2], v.center[3] - coord[3]};
-  unitize4(ray);
-  const float weight = smax(0.0f, dot4(ray, pz));
-  if ((double)weight < s.cosAngle1) ok = 0;
-  float center[3], c1[3], c2[3], tt[4];
-  project(v, coord, s.level, center);
-  for (int i = 0; i < 4; ++i) tt[i] = coord[i] + px[i];
-  project(v, tt, s.level, c1);
-  for (int i = 0; i < 4; ++i) tt[i] = coord[i] + py[i];
-  project(v, tt, s.level, c2);
-  float dx[3] = {c1[0] - center[0], c1[1] - center[1], c1[2] - center[2]};
-  float dy[3] = {c2[0] - center[0], c2[1] - center[1], c2[2] - center[2]};
-  const float ratio = __fdiv_rn(norm3(dx) + norm3(dy), 2.0f);
-  int leveldif = cvt_int_x86(floor(log((double)ratio) / (double)s.log2f + (double)0.5f));
-  leveldif = imax(-s.level, imin(2, leveldif));
-  const float scale = (leveldif >= 0) ? (float)(1 << leveldif) : __fdiv_rn(1.0f, (float)(1 << (-leveldif)));
-  const int newlevel = s.level + leveldif;
-  for (int i = 0; i < 3; ++i) {
-    center[i] = __fdiv_rn(center[i], scale);
-    dx[i] = __fdiv_rn(dx[i], scale);
-    dy[i] = __fdiv_rn(dy[i], scale);
-  }
-  const float fm = (float)(WS / 2);
-  const float dxm[2] = {dx[0] * fm, dx[1] * fm}, dym[2] = {dy[0] * fm, dy[1] * fm};
-  const float tl0 = (center[0] - dxm[0]) - dym[0], tl1 = (center[1] - dxm[1]) - dym[1];
-  const float tr0 = (center[0] + dxm[0]) - dym[0], tr1 = (center[1] + dxm[1]) - dym[1];
-  const float bl0 = (center[0] - dxm[0]) + dym[0], bl1 = (center[1] - dxm[1]) + dym[1];
-  const float br0 = (center[0] + dxm[0]) + dym[0], br1 = (center[1] + dxm[1]) + dym[1];
-  const float minx = smin(tl0, smin(tr0, smin(bl0, br0)));
-  const float maxx = smax(tl0, smax(tr0, smax(bl0, br0)));
-  const float miny = smin(tl1, smin(tr1, smin(bl1, br1)));
-  const float maxy = smax(tl1, smax(tr1, smax(bl1, br1)));
-  if (ok && (minx < 3.0f || (float)(v.w[newlevel] - 1 - 3) <= maxx || miny < 3.0f ||
-             (float)(v.h[newlevel] - 1 - 3) <= maxy))
-    ok = 0;
-  C.jvalid[t] = ok;
-  C.jW[t] = v.w[newlevel];
-  C.jbase[t] = v.pyr_off[newlevel];
+  const TexGeom T = tex_geom<WS>(s, C.geo[r], C.views[r][C.jidx[t]]);
+  C.jvalid[t] = T.ok;
+  C.jW[t] = T.W;
+  C.jbase[t] = T.base;
   // each row's start, by the reference's recurrence `left += dy` (optim.cpp:850-860), once per texture
   // instead of once per sample in the gather
-  float lx = tl0, ly = tl1;
+  float lx = T.tl0, ly = T.tl1;
   for (int r = 0; r < WS; ++r) {
     C.jrow[t][r][0] = lx; C.jrow[t][r][1] = ly;
-    lx = lx + dy[0]; ly = ly + dy[1];
+    lx = lx + T.dy0; ly = ly + T.dy1;
   }
-  C.jdx[t][0] = dx[0]; C.jdx[t][1] = dx[1];
-  C.jdy[t][0] = dy[0]; C.jdy[t][1] = dy[1];
+  C.jdx[t][0] = T.dx0; C.jdx[t][1] = T.dx1;
+  C.jdy[t][0] = T.dy0; C.jdy[t][1] = T.dy1;
 }
 
 // gather: thread `tid` of `NT` takes samples tid, tid + NT, ...; NB samples per thread at a time,
@@ -1133,49 +1058,6 @@ __device__ __forceinline__ void tex_dot(L& C, int t) {
   C.jres[t] = r;
 }
 
-// The objective value of one request from its slots [off, off + sz): COptim::my_f
-// (optim.cpp:527-577, need 1) or the robust weighted computeINCC (optim.cpp:875-938, need 2).
-template <class L>
-__device__ __forceinline__ double request_value(const DScene& s, const L& C, int off, int sz, int need,
-                                                const RefineJob& J, unsigned long long& tex_valid) {
-  const int ref = off;
-  int nv = 0;
-  for (int i = 0; i < sz; ++i) nv += C.jvalid[off + i];
-  double f;
-  if (need == 1) {
-    const int mininum = imin(s.minImageNum, sz);
-    tex_valid += nv;
-    if (!C.jvalid[ref]) {
-      f = 2.0;
-    } else {
-      double ans = 0.0f;
-      int denom = 0;
-      for (int i = 1; i < sz; ++i) {
-        if (!C.jvalid[off + i]) continue;
-        ans += (double)C.jres[off + i];
-        denom++;
-      }
-      f = (denom < mininum - 1) ? 2.0f : ans / denom;
-    }
-  } else {
-    if (!C.jvalid[ref]) {
-      f = 2.0;
-    } else {
-      double score = 0.0;
-      float totalweight = 0.0f;
-      for (int i = 1; i < sz; ++i) {
-        if (C.jvalid[off + i]) {
-          const float w = J.weights[i];
-          totalweight += w;
-          score += (double)(C.jres[off + i] * w);
-        }
-      }
-      f = (totalweight == 0.0f) ? 2.0 : score / (double)totalweight;
-    }
-  }
-  return f;
-}
-
 template <int WS, int TSLOTS, int NC>
 __device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS, NC>& C, int njobs, unsigned long long* prof,
                            unsigned long long& tprev) {
@@ -1196,19 +1078,6 @@ __device__ void eval_chunk(const DScene& s, RefLds<WS, TSLOTS, NC>& C, int njobs
   PROF_MARK(6);
 }
 
-// Wavefronts per SIMD the refine kernel's register budget is sized for: 2 (<= 256 VGPR+AGPR).  The
-// out-of-line BOBYQA routines get the budget of their most permissive caller, so the self-test
-// kernels that call them use the same value.  Measured on C2 (tools/sweep_variants.sh,
-// profiles/r02g_sweeps.txt): 2 waves of 4 chains with 12 texture slots (19 KB LDS, 8 per CU)
-// beat 1 wave of 8 chains with the 512-register inlined optimizer by 17 %; 3 or 4 waves per SIMD
-// (168 / 128 registers) spill and lose 40-50 %.  With the compacted BqState (1736 B) and 12-byte
-// texture samples, 6 chains x 12 slots fit the same 20 KB (default 1206, +6 %).
-#ifndef REFINE_WPE
-#define REFINE_WPE(NC) 2
-#endif
-#ifndef BQ_CALLER_WPE
-#define BQ_CALLER_WPE 2
-#endif
 template <int WS, int TSLOTS, int NC>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(REFINE_WPE(NC)))) void refine_v2_kernel(
     DScene s, RefineJob* __restrict__ jobs, int n, DevStats* st) {
@@ -1882,6 +1751,7 @@ bool refine_config_supported(int tslots) {
   switch (tslots) {
     case 804: case 807: case 808: case 1201: case 1202: case 1203: case 1204: case 1206: case 1608: case 2408: return true;
     case 164011: case 164021: case 164041: case 148041: case 132022: case 132042: case 116042: return true;
+    case 202032: case 202040: case 203024: case 204016: return refine_split_supported(tslots);
 #if defined(BQ_PRIVATE)
     case 1264: case 2464: case 1232: case 2432: case 1216: case 2448: case 3232: case 3248: case 3264: case 4832:
     case 4864: return true;
@@ -1927,6 +1797,15 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
   }
   const int nc = tslots % 100;
   const int rg = refine_grid < (n + nc - 1) / nc ? refine_grid : (n + nc - 1) / nc;
+  if (tslots >= 200000 && WS > 7) tslots = 1206;  // split form: a texture's 3 * 81 samples exceed its registers
+  if (tslots >= 200000) {  // split form (pmvs_refine_split.hip)
+    if ((e = launch_refine_split(tslots, s, d_jobs, n, d_st, stream)) != hipSuccess) return e;
+    if (refine_tail_on()) hipLaunchKernelGGL(refine_tail_kernel, dim3(1), dim3(64), 0, stream, d_st, 0);
+    (void)hipEventRecord(ev[2], stream);
+    hipLaunchKernelGGL((post_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_jobs, d_out, n, d_st);
+    (void)hipEventRecord(ev[3], stream);
+    return hipGetLastError();
+  }
   if (tslots >= 100000) {  // workgroup form: 100000 + chains * 1000 + optimizer wavefronts * 10 + workgroups per CU
     const int ncw = (tslots / 1000) % 100, wgpc = tslots % 10;
     int dev = 0, cus = 0;
@@ -2231,6 +2110,10 @@ __device__ __forceinline__ double bq_test_f(int kind, const double* v) {
     const double a = 1 - v[0], b = v[1] - v[0] * v[0], c = v[2] - v[1] * v[1];
     return a * a + 100 * b * b + 100 * c * c;
   }
+  if (kind == 3) {  // timing proxy of the refine objective: bounded, a basin plus a ripple
+    const double q = 0.3 * (v[0] - 0.2) * (v[0] - 0.2) + 0.01 * (v[1] - 3) * (v[1] - 3) + 0.02 * (v[2] + 2) * (v[2] + 2);
+    return 1.0 - exp(-q) + 0.02 * sin(3.0 * v[1]) * cos(2.0 * v[2]);
+  }
   return (v[0] - 1) * (v[0] - 1) + (v[1] - 40) * (v[1] - 40) + (v[2] + 50) * (v[2] + 50);
 }
 
@@ -2316,6 +2199,10 @@ hipError_t launch_bobyqa_selftest(int mode, int kind, const double* d_x0, int n,
     hipLaunchKernelGGL((bobyqa_lds_kernel<16>), dim3((n + 15) / 16), dim3(64), 0, stream, kind, d_x0, n, maxeval, d_out);
   else if (mode == 3)
     hipLaunchKernelGGL((bobyqa_lds_kernel<32>), dim3((n + 31) / 32), dim3(64), 0, stream, kind, d_x0, n, maxeval, d_out);
+  else if (mode == 5)  // the wavefront form's chains per wave (timing)
+    hipLaunchKernelGGL((bobyqa_lds_kernel<6>), dim3((n + 5) / 6), dim3(64), 0, stream, kind, d_x0, n, maxeval, d_out);
+  else if (mode == 6)
+    hipLaunchKernelGGL((bobyqa_lds_kernel<48>), dim3((n + 47) / 48), dim3(64), 0, stream, kind, d_x0, n, maxeval, d_out);
   else
     hipLaunchKernelGGL((bobyqa_lds_kernel<64>), dim3((n + 63) / 64), dim3(64), 0, stream, kind, d_x0, n, maxeval, d_out);
   return hipGetLastError();

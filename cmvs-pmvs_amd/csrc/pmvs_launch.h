@@ -40,6 +40,10 @@ struct RefineHost {
 hipError_t launch_refine(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out, int n,
                          DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream, hipEvent_t* ev,
                          RefineHost& rh);
+// split-form refine kernel alone (pmvs_refine_split.hip), config 200000 + optimizer wavefronts * 1000 +
+// chains per optimizer wavefront, wsize 5 or 7
+bool refine_split_supported(int config);
+hipError_t launch_refine_split(int config, const DScene& s, RefineJob* d_jobs, int n, DevStats* d_st, hipStream_t stream);
 hipError_t launch_incc_eval(const DScene& s, const pmvs_eval_query* d_q, int n, double* d_out, DevStats* d_st,
                             hipStream_t stream);
 hipError_t launch_grab_tex(const DScene& s, const pmvs_tex_query* d_q, int n, float* d_out, int* d_valid,

@@ -1,0 +1,412 @@
+// pmvs_refine_split.hip -- refinePatchBFGS (optim.cpp:580-658), split form: optimizer and evaluator
+// wavefronts of one workgroup per CU.  A translation unit of its own
+// because it is compiled without SLP vectorisation (Makefile): packing the evaluator's per-texture
+// float arithmetic into pairs made its 147 sample registers spill (1.6 KB per lane against 0.4 KB).
+#include <hip/hip_runtime.h>
+
+#include "bobyqa_dev.h"
+#include "pmvs_device.h"
+#include "pmvs_launch.h"
+#include "pmvs_refine.h"
+
+namespace pmvsdev {
+
+// ---------------------------------------------------------------- refinePatchBFGS, split form
+// One 512-thread workgroup per CU, its wavefronts in two roles that run concurrently:
+//   * G optimizer wavefronts: wavefront g steps CG chains, one lane each (BqState in LDS), so one
+//     instruction stream of the divergent f64 BOBYQA step serves up to CG chains (the wavefront
+//     form: 6).  After a step the wavefront publishes its chains' objective requests, packed in
+//     chain order into chunks of <= 64 textures, and sleeps until they are evaluated.
+//   * 8 - G evaluator wavefronts: each claims a whole chunk and evaluates it with one LANE PER
+//     TEXTURE, everything in registers: setup, the 49 samples of the texture gathered in sample
+//     order (the channel sums ride along), the second moment, the element-wise normalisation, and
+//     the robust INCC against the request's reference texture, whose normalised samples are read
+//     from the reference's lane (ds_bpermute); the reference's lane then reduces its request as
+//     request_value does.  Every sum keeps the reference's order: results, optimizer
+//     trajectories and counters equal the wavefront form's.
+// While one group's requests are evaluated, the other groups step: the optimizer and the texture
+// work of a CU overlap instead of alternating within each wavefront.  Handshake through LDS: per
+// group, `avail` (chunks not yet claimed: set by the group's atomic exchange after its tables are
+// written, taken by the evaluators' atomic decrements; a stale decrement only drives it below 0) and
+// `done` (chunks evaluated).  No workgroup barrier after the start.
+constexpr int SPLIT_THREADS = 512;
+constexpr int SPLIT_TS = 64;  // texture slots per chunk: one per evaluator lane
+
+template <int WS, int G, int CG>
+struct RefSplitLds {
+  static constexpr int NCH = G * CG;
+  static constexpr int SLOTS = CG * PMVS_MAX_TAU;  // a group's slots per round (<= 16 textures per request)
+  BqState bq[NCH];
+  float geo[NCH][16];                       // requesting chain: coord, normal, pxaxis, pyaxis
+  double fv[NCH];                           // the chain's objective value, written by its evaluator
+  int cand[NCH];                            // the chain's candidate (need 2 reads its weights)
+  unsigned short views[NCH][PMVS_MAX_TAU];  // chain: first size images
+  unsigned char need[NCH], size[NCH];
+  unsigned char sreq[G][SLOTS], sidx[G][SLOTS];  // slot -> chain within the group, texture index
+  short choff[G][CG + 1];                   // chunk k of group g: slots [choff[g][k], choff[g][k + 1])
+  int nchunk[G];
+  int avail[G], done[G];
+  int live;                                 // optimizer wavefronts still running
+  int ejvalid[8][SPLIT_TS];                 // evaluator wavefront's per-slot results for the reduction
+  float ejres[8][SPLIT_TS];
+};
+
+#define SPLIT_AS __attribute__((address_space(3)))
+__device__ __forceinline__ int lds_load_acq(SPLIT_AS int* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// The two roles as separate functions, so that each gets its own register allocation (inlined
+// into one body, the evaluator's 147 sample registers and the optimizer's call sites spilled).
+template <int WS, int G, int CG>
+__device__ __noinline__ void split_optimizer(const DScene& s, SPLIT_AS RefSplitLds<WS, G, CG>& C, RefineJob* __restrict__ jobs,
+                                             int n, int nc_active, DevStats* st) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & (WAVE - 1);
+  const int g = wave;
+  const bool owner = lane < CG && lane < nc_active;
+  const int c = g * CG + (lane < CG ? lane : 0);
+  BQ_AS BqState& bq = *(BQ_AS BqState*)&C.bq[c];
+  RefineSetup R;
+  int cand = -1, need = 0, evals = 0, size = 0, nimg = 0, rc = 0;
+  bool exhausted = !owner;
+  double fv = 0.0;
+  float fcoord[4], fnormal[4];
+  unsigned long long nevals = 0, rounds = 0;
+  const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999};
+  const double ub[3] = {HUGE_VAL, 23.99999, 23.99999};
+  for (;;) {
+    // (a) refill an idle chain from the queue (skipping candidates that failed preProcess)
+    while (cand < 0 && !exhausted) {
+      const unsigned long long q = atomicAdd(&st->queue2, 1ull);
+      if (q >= (unsigned long long)n) {
+        exhausted = true;
+        atomicMax(&st->t_drain_inv, ~__builtin_amdgcn_s_memrealtime());
+        break;
+      }
+      const RefineJob& J = jobs[q];
+      if (J.status != PMVS_ACCEPTED) continue;
+      cand = (int)q;
+      for (int i = 0; i < 4; ++i) { R.center[i] = J.center[i]; R.ray[i] = J.ray[i]; }
+      R.dscale = J.dscale;
+      R.ascale = s.ascale;
+      R.ref = J.images[0];
+      nimg = J.nimg;
+      size = imin(s.tau, nimg);
+      for (int i = 0; i < size; ++i) C.views[c][i] = (unsigned short)J.images[i];
+      C.cand[c] = cand;
+      evals = 0;
+      const double x0[3] = {J.x0[0], J.x0[1], J.x0[2]};
+      bq_begin(bq, x0, lb, ub, 1.e-7, 1000);
+      fv = 0.0;
+      need = 0;
+    }
+    // (b) advance BOBYQA when the chain holds an objective value (or just started)
+    if (cand >= 0 && need == 0) {
+      const int r = (bq.resume < 0) ? BQ_DONE : bq_step(bq, fv);
+      if (r == BQ_NEED_F) {
+        need = 1;
+        const double xe[3] = {bq.xeval[0], bq.xeval[1], bq.xeval[2]};
+        decode(s, R, xe, fcoord, fnormal);
+      } else {
+        rc = bq.rc;
+        const bool success = (rc == BQR_SUCCESS || rc == 2 || rc == 3 || rc == BQR_XTOL);
+        RefineJob& J = jobs[cand];
+        J.refine_code = rc;
+        J.evals = evals;
+        if (success) {
+          const double xo[3] = {bq.xout[0], bq.xout[1], bq.xout[2]};
+          decode(s, R, xo, fcoord, fnormal);
+          if (nimg < 2) {  // computeINCC returns 2.0 without grabbing (optim.cpp:866)
+            J.ncc = (float)(1.0 - (double)unrobustincc(2.0f));
+            for (int i = 0; i < 4; ++i) { J.rcoord[i] = fcoord[i]; J.rnormal[i] = fnormal[i]; }
+            cand = -1;
+          } else {
+            need = 2;  // final computeINCC (robust, weighted) at the refined geometry
+          }
+        } else {
+          cand = -1;  // geometry and _ncc stay unrefined (optim.cpp:649-655)
+        }
+      }
+    }
+    // (c) publish the requests: geometry, then the chunk tables, then `avail`
+    const bool req = (cand >= 0 && need != 0);
+    if (req) {
+      float px[4], py[4];
+      get_paxes(s, s.views[R.ref], fcoord, fnormal, px, py);
+      for (int i = 0; i < 4; ++i) {
+        C.geo[c][i] = fcoord[i]; C.geo[c][4 + i] = fnormal[i];
+        C.geo[c][8 + i] = px[i]; C.geo[c][12 + i] = py[i];
+      }
+      C.need[c] = (unsigned char)need;
+      C.size[c] = (unsigned char)size;
+    }
+    bool pending = req;
+    int k = 0, base = 0;
+    while (__ballot(pending) != 0ull) {
+      const int sz = pending ? size : 0;
+      const int off = wave_excl_scan(sz);
+      const bool in = pending && (off + sz <= SPLIT_TS);
+      const int nj = __shfl(off + sz, 63 - __clzll(__ballot(in)));
+      if (in) {
+        for (int i = 0; i < sz; ++i) {
+          C.sreq[g][base + off + i] = (unsigned char)lane;
+          C.sidx[g][base + off + i] = (unsigned char)i;
+        }
+      }
+      if (lane == 0) C.choff[g][k] = (short)base;
+      base += nj;
+      pending = pending && !in;
+      ++k;
+    }
+    rounds++;
+    if (k == 0) {
+      if (__ballot(cand >= 0 || !exhausted) == 0ull) break;
+      continue;
+    }
+    if (lane == 0) {
+      C.choff[g][k] = (short)base;
+      C.nchunk[g] = k;
+      C.done[g] = 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_exchange(&C.avail[g], k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // (d) wait for the evaluators
+    while (lds_load_acq(&C.done[g]) < k) __builtin_amdgcn_s_sleep(2);
+    // (e) consume the results
+    if (req) {
+      fv = C.fv[c];
+      if (need == 1) {
+        evals++;
+        nevals++;
+        need = 0;
+      } else {
+        RefineJob& J = jobs[cand];
+        J.ncc = (float)(1.0 - (double)unrobustincc((float)fv));
+        for (int i = 0; i < 4; ++i) { J.rcoord[i] = fcoord[i]; J.rnormal[i] = fnormal[i]; }
+        cand = -1;
+        need = 0;
+      }
+    }
+  }
+  if (lane == 0) __hip_atomic_fetch_add(&C.live, -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  for (int d = 32; d >= 1; d >>= 1) nevals += __shfl_xor(nevals, d);
+  if (lane == 0) {
+    atomicAdd(&st->evals, nevals);
+    atomicAdd(&st->rounds, rounds);
+    atomicMax(&st->t_last, __builtin_amdgcn_s_memrealtime());
+  }
+}
+
+template <int WS, int G, int CG>
+__device__ __noinline__ void split_evaluator(const DScene& s, SPLIT_AS RefSplitLds<WS, G, CG>& C, RefineJob* __restrict__ jobs,
+                                             DevStats* st) {
+  constexpr int S = WS * WS;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & (WAVE - 1);
+  const int ew = wave - G;
+  unsigned long long tex_valid = 0, grabs = 0, chunks = 0;
+  SPLIT_AS int* ejvalid = C.ejvalid[wave];
+  SPLIT_AS float* ejres = C.ejres[wave];
+  for (int it = 0;; ++it) {
+    // claim a chunk: groups scanned from a per-wavefront start so the evaluators spread
+    int g = -1, k = -1;
+    for (int i = 0; i < G && g < 0; ++i) {
+      const int gg = (ew + it + i) % G;
+      int got = -1;
+      if (lane == 0 && lds_load_acq(&C.avail[gg]) > 0) {
+        const int old = __hip_atomic_fetch_add(&C.avail[gg], -1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (old > 0) got = C.nchunk[gg] - old;
+      }
+      got = __shfl(got, 0);
+      if (got >= 0) {
+        g = gg;
+        k = got;
+      }
+    }
+    if (g < 0) {
+      if (lds_load_acq(&C.live) == 0) break;
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    const int o0 = C.choff[g][k], nj = C.choff[g][k + 1] - o0;
+    const bool mine = lane < nj;
+    const int chain = mine ? (int)C.sreq[g][o0 + lane] : 0;
+    const int idx = mine ? (int)C.sidx[g][o0 + lane] : 0;
+    const int cc = g * CG + chain;
+    const int rl = lane - idx;  // the slot of the request's reference texture (index 0)
+    // setup
+    TexGeom T;
+    T.ok = 0;
+    if (mine) T = tex_geom<WS>(s, (const float*)C.geo[cc], C.views[cc][idx]);
+    // gather: the texture's samples in sample order, rows by the `left += dy` recurrence, columns by
+    // `+= dx` (optim.cpp:850-860); the channel sums of normalize's first pass ride along
+    float X[S], Y[S], Z[S];
+    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+    if (T.ok) {
+      const uint32_t* pyr = s.pyr + T.base;
+      float rx = T.tl0, ry = T.tl1;
+#pragma unroll
+      for (int yy = 0; yy < WS; ++yy) {
+        uint32_t q00[WS], q01[WS], q10[WS], q11[WS];
+        float fx[WS], fy[WS];
+        float lx = rx, ly = ry;
+#pragma unroll
+        for (int xx = 0; xx < WS; ++xx) {
+          fx[xx] = lx; fy[xx] = ly;
+          const int ix = (int)lx, iy = (int)ly;
+          const uint32_t* p = pyr + (iy * T.W + ix);  // within one level: < 2^31 texels
+          q00[xx] = p[0]; q10[xx] = p[1]; q01[xx] = p[T.W]; q11[xx] = p[T.W + 1];
+          lx = lx + T.dx0; ly = ly + T.dx1;
+        }
+#pragma unroll
+        for (int xx = 0; xx < WS; ++xx) {
+          const float dx1 = fx[xx] - (float)(int)fx[xx], dx0 = 1.0f - dx1;
+          const float dy1 = fy[xx] - (float)(int)fy[xx], dy0 = 1.0f - dy1;
+          const float f00 = dx0 * dy0, f01 = dx0 * dy1, f10 = dx1 * dy0, f11 = dx1 * dy1;
+          float r = 0.0f, gg = 0.0f, b = 0.0f;
+          r += (float)(q00[xx] & 0xff) * f00 + (float)(q01[xx] & 0xff) * f01;
+          gg += (float)((q00[xx] >> 8) & 0xff) * f00 + (float)((q01[xx] >> 8) & 0xff) * f01;
+          b += (float)((q00[xx] >> 16) & 0xff) * f00 + (float)((q01[xx] >> 16) & 0xff) * f01;
+          r += (float)(q10[xx] & 0xff) * f10 + (float)(q11[xx] & 0xff) * f11;
+          gg += (float)((q10[xx] >> 8) & 0xff) * f10 + (float)((q11[xx] >> 8) & 0xff) * f11;
+          b += (float)((q10[xx] >> 16) & 0xff) * f10 + (float)((q11[xx] >> 16) & 0xff) * f11;
+          X[yy * WS + xx] = r; Y[yy * WS + xx] = gg; Z[yy * WS + xx] = b;
+          a0 += r; a1 += gg; a2 += b;
+        }
+        rx = rx + T.dy0; ry = ry + T.dy1;
+        __builtin_amdgcn_sched_barrier(0);  // one row's loads in flight at a time: bounded registers
+      }
+      // normalize (optim.cpp:1031-1067): means, second moment, element-wise scaling
+      const float fs3 = (float)S;
+      a0 = __fdiv_rn(a0, fs3); a1 = __fdiv_rn(a1, fs3); a2 = __fdiv_rn(a2, fs3);
+      float ave2 = 0.0f;
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        const float f0 = a0 - X[i], f1 = a1 - Y[i], f2 = a2 - Z[i];
+        ave2 += f0 * f0 + f1 * f1 + f2 * f2;
+      }
+      ave2 = fsqrt_rn(__fdiv_rn(ave2, (float)(3 * S)));
+      if (ave2 == 0.0f) ave2 = 1.0f;
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        X[i] = __fdiv_rn(X[i] - a0, ave2);
+        Y[i] = __fdiv_rn(Y[i] - a1, ave2);
+        Z[i] = __fdiv_rn(Z[i] - a2, ave2);
+        if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < S; ++i) { X[i] = 0.0f; Y[i] = 0.0f; Z[i] = 0.0f; }
+    }
+    // robust INCC against the reference texture (optim.cpp:561-567, 919-929): its normalised samples
+    // from its lane, the products summed in sample order (R, G, B per sample)
+    const int src = mine ? rl : lane;
+    const int refok = __shfl(T.ok, src);
+    float ans = 0.0f;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      const float px = __shfl(X[i], src), py = __shfl(Y[i], src), pz = __shfl(Z[i], src);
+      ans += px * X[i];
+      ans += py * Y[i];
+      ans += pz * Z[i];
+      if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    }
+    float jr = 0.0f;
+    if (mine && idx >= 1 && refok && T.ok) jr = robustincc((float)(1.0 - (double)__fdiv_rn(ans, (float)(3 * S))));
+    ejvalid[lane] = T.ok;
+    ejres[lane] = jr;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // the request's value on its reference lane, in request_value's order
+    if (mine && idx == 0) {
+      struct {
+        SPLIT_AS int* jvalid;
+        SPLIT_AS float* jres;
+      } V = {ejvalid, ejres};
+      const int need = C.need[cc];
+      C.fv[cc] = request_value(s, V, lane, C.size[cc], need, jobs[C.cand[cc]], tex_valid);
+    }
+    grabs += nj;
+    chunks++;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_fetch_add(&C.done[g], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  for (int d = 32; d >= 1; d >>= 1) tex_valid += __shfl_xor(tex_valid, d);
+  if (lane == 0) {
+    atomicAdd(&st->tex_valid, tex_valid);
+    atomicAdd(&st->tex_grabs, grabs);
+    atomicAdd(&st->chunks, chunks);
+  }
+}
+
+template <int WS, int G, int CG>
+__global__ __launch_bounds__(SPLIT_THREADS) __attribute__((amdgpu_waves_per_eu(REFINE_WPE(CG)))) void refine_split_kernel(
+    DScene s, RefineJob* __restrict__ jobs, int n, int nc_active, DevStats* st) {
+  using L = RefSplitLds<WS, G, CG>;
+  static_assert(G >= 1 && G < SPLIT_THREADS / WAVE && CG <= WAVE && CG <= 255, "roles");
+  static_assert(sizeof(L) <= 160 * 1024, "LDS");
+  __shared__ L C;
+  const int tid = threadIdx.x, wave = tid >> 6;
+  if (tid < G) {
+    C.avail[tid] = 0;
+    C.done[tid] = 0;
+    C.nchunk[tid] = 0;
+  }
+  if (tid == 0) {
+    C.live = G;
+    atomicMax(&st->t_first_inv, ~__builtin_amdgcn_s_memrealtime());
+  }
+  __syncthreads();
+  if (wave < G)
+    split_optimizer<WS, G, CG>(s, *(SPLIT_AS RefSplitLds<WS, G, CG>*)&C, jobs, n, nc_active, st);
+  else
+    split_evaluator<WS, G, CG>(s, *(SPLIT_AS RefSplitLds<WS, G, CG>*)&C, jobs, st);
+}
+
+
+// config = 200000 + optimizer wavefronts * 1000 + chains per optimizer wavefront (WS <= 7)
+bool refine_split_supported(int config) {
+  switch (config) {
+    case 202032: case 202040: case 203024: case 204016: return true;
+    default: return false;
+  }
+}
+
+template <int WS>
+static hipError_t launch_split_ws(int config, const DScene& s, RefineJob* d_jobs, int n, DevStats* d_st, hipStream_t stream) {
+  const int gw = (config / 1000) % 100, cg = config % 1000;
+  int dev = 0, cus = 0;
+  hipError_t e;
+  if ((e = hipGetDevice(&dev)) != hipSuccess ||
+      (e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
+    return e;
+  cus = cus > 0 ? cus : 1;
+  // one workgroup per CU; a small batch runs fewer chains per optimizer wavefront on every CU
+  const int sgrid = cus < (n + gw - 1) / gw ? cus : (n + gw - 1) / gw;
+  const int per = (n + sgrid * gw - 1) / (sgrid * gw);
+  const int nca = per < cg ? per : cg;
+#define PMVS_SPLIT(Gc, CGc)                                                                                            \
+  case 200000 + Gc * 1000 + CGc:                                                                                        \
+    hipLaunchKernelGGL((refine_split_kernel<WS, Gc, CGc>), dim3(sgrid), dim3(SPLIT_THREADS), 0, stream, s, d_jobs, n, nca, \
+                       d_st);                                                                                           \
+    break;
+  switch (config) {
+    PMVS_SPLIT(2, 32)
+    PMVS_SPLIT(2, 40)
+    PMVS_SPLIT(3, 24)
+    PMVS_SPLIT(4, 16)
+    default: return hipErrorInvalidValue;
+  }
+#undef PMVS_SPLIT
+  return hipGetLastError();
+}
+
+hipError_t launch_refine_split(int config, const DScene& s, RefineJob* d_jobs, int n, DevStats* d_st, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  switch (s.wsize) {
+    case 5: return launch_split_ws<5>(config, s, d_jobs, n, d_st, stream);
+    case 7: return launch_split_ws<7>(config, s, d_jobs, n, d_st, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace pmvsdev
