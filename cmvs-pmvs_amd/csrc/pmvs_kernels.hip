@@ -1751,12 +1751,11 @@ bool refine_config_supported(int tslots) {
   switch (tslots) {
     case 804: case 807: case 808: case 1201: case 1202: case 1203: case 1204: case 1206: case 1608: case 2408: return true;
     case 164011: case 164021: case 164041: case 148041: case 132022: case 132042: case 116042: return true;
-    case 202032: case 202040: case 203024: case 204016: return refine_split_supported(tslots);
 #if defined(BQ_PRIVATE)
     case 1264: case 2464: case 1232: case 2432: case 1216: case 2448: case 3232: case 3248: case 3264: case 4832:
     case 4864: return true;
 #endif
-    default: return false;
+    default: return refine_split_supported(tslots);
   }
 }
 

@@ -11,6 +11,24 @@
 
 namespace pmvsdev {
 
+// Diagnostic build only (-DBQ_PROFILE, libpmvs_amd_prof.so): wave time per role and phase in
+// DevStats::prof -- optimizer: [0] refill, [1] BOBYQA step, [2] publish, [3] waiting for the
+// evaluators; evaluator: [4] setup + gather, [5] normalize, [6] dot + reduction, [7] idle.
+#if defined(BQ_PROFILE)
+#define SP_NOW() __builtin_amdgcn_s_memtime()
+#define SP_MARK(slot)                                      \
+  do {                                                     \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+    prof[slot] += _t - tprev;                              \
+    tprev = _t;                                            \
+  } while (0)
+#else
+#define SP_NOW() 0ull
+#define SP_MARK(slot) \
+  do {                \
+  } while (0)
+#endif
+
 // ---------------------------------------------------------------- refinePatchBFGS, split form
 // One 512-thread workgroup per CU, its wavefronts in two roles that run concurrently:
 //   * G optimizer wavefronts: wavefront g steps CG chains, one lane each (BqState in LDS), so one
@@ -58,7 +76,7 @@ __device__ __forceinline__ int lds_load_acq(SPLIT_AS int* p) {
 
 // The two roles as separate functions, so that each gets its own register allocation (inlined
 // into one body, the evaluator's 147 sample registers and the optimizer's call sites spilled).
-template <int WS, int G, int CG>
+template <int WS, int G, int CG, int TS>
 __device__ __noinline__ void split_optimizer(const DScene& s, SPLIT_AS RefSplitLds<WS, G, CG>& C, RefineJob* __restrict__ jobs,
                                              int n, int nc_active, DevStats* st) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & (WAVE - 1);
@@ -74,6 +92,8 @@ __device__ __noinline__ void split_optimizer(const DScene& s, SPLIT_AS RefSplitL
   unsigned long long nevals = 0, rounds = 0;
   const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999};
   const double ub[3] = {HUGE_VAL, 23.99999, 23.99999};
+  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tprev = SP_NOW();
   for (;;) {
     // (a) refill an idle chain from the queue (skipping candidates that failed preProcess)
     while (cand < 0 && !exhausted) {
@@ -100,6 +120,7 @@ __device__ __noinline__ void split_optimizer(const DScene& s, SPLIT_AS RefSplitL
       fv = 0.0;
       need = 0;
     }
+    SP_MARK(0);
     // (b) advance BOBYQA when the chain holds an objective value (or just started)
     if (cand >= 0 && need == 0) {
       const int r = (bq.resume < 0) ? BQ_DONE : bq_step(bq, fv);
@@ -128,6 +149,7 @@ __device__ __noinline__ void split_optimizer(const DScene& s, SPLIT_AS RefSplitL
         }
       }
     }
+    SP_MARK(1);
     // (c) publish the requests: geometry, then the chunk tables, then `avail`
     const bool req = (cand >= 0 && need != 0);
     if (req) {
@@ -145,7 +167,7 @@ __device__ __noinline__ void split_optimizer(const DScene& s, SPLIT_AS RefSplitL
     while (__ballot(pending) != 0ull) {
       const int sz = pending ? size : 0;
       const int off = wave_excl_scan(sz);
-      const bool in = pending && (off + sz <= SPLIT_TS);
+      const bool in = pending && (off + sz <= TS);
       const int nj = __shfl(off + sz, 63 - __clzll(__ballot(in)));
       if (in) {
         for (int i = 0; i < sz; ++i) {
@@ -170,8 +192,10 @@ __device__ __noinline__ void split_optimizer(const DScene& s, SPLIT_AS RefSplitL
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_exchange(&C.avail[g], k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    SP_MARK(2);
     // (d) wait for the evaluators
     while (lds_load_acq(&C.done[g]) < k) __builtin_amdgcn_s_sleep(2);
+    SP_MARK(3);
     // (e) consume the results
     if (req) {
       fv = C.fv[c];
@@ -191,21 +215,37 @@ __device__ __noinline__ void split_optimizer(const DScene& s, SPLIT_AS RefSplitL
   if (lane == 0) __hip_atomic_fetch_add(&C.live, -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   for (int d = 32; d >= 1; d >>= 1) nevals += __shfl_xor(nevals, d);
   if (lane == 0) {
+#if defined(BQ_PROFILE)
+    for (int i = 0; i < 4; ++i) atomicAdd(&st->prof[i], prof[i]);
+#endif
     atomicAdd(&st->evals, nevals);
     atomicAdd(&st->rounds, rounds);
     atomicMax(&st->t_last, __builtin_amdgcn_s_memrealtime());
   }
 }
 
-template <int WS, int G, int CG>
+// An evaluator wavefront takes chunks of TS = 64 / LP textures, LP lanes per texture: lane `sub` of
+// a texture holds its samples [sub * K, sub * K + K) (K = ceil(S / LP)) in registers.  Gather, the
+// bilinear weights and the element-wise normalisation are per lane.  Each of normalize's and dot's
+// sequential sums runs in LP stages, lane sub continuing the partial sum of lane sub - 1, so every
+// sum is the reference's single left-to-right chain (optim.cpp:1031-1077).  LP > 1 shortens a
+// chunk: its instruction count is what the optimizer wavefront waits for.
+template <int WS, int G, int CG, int LP>
 __device__ __noinline__ void split_evaluator(const DScene& s, SPLIT_AS RefSplitLds<WS, G, CG>& C, RefineJob* __restrict__ jobs,
                                              DevStats* st) {
   constexpr int S = WS * WS;
+  constexpr int K = (S + LP - 1) / LP;
+  constexpr int NB = 7;  // samples whose texel loads are in flight together
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & (WAVE - 1);
   const int ew = wave - G;
+  const int t = lane / LP, sub = lane - t * LP;  // the lane's texture slot and part of it
+  const int k0 = sub * K;
+  const int kn = k0 < S ? (S - k0 < K ? S - k0 : K) : 0;  // samples of this lane
   unsigned long long tex_valid = 0, grabs = 0, chunks = 0;
   SPLIT_AS int* ejvalid = C.ejvalid[wave];
   SPLIT_AS float* ejres = C.ejres[wave];
+  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tprev = SP_NOW();
   for (int it = 0;; ++it) {
     // claim a chunk: groups scanned from a per-wavefront start so the evaluators spread
     int g = -1, k = -1;
@@ -227,118 +267,180 @@ __device__ __noinline__ void split_evaluator(const DScene& s, SPLIT_AS RefSplitL
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
+    SP_MARK(7);
     const int o0 = C.choff[g][k], nj = C.choff[g][k + 1] - o0;
-    const bool mine = lane < nj;
-    const int chain = mine ? (int)C.sreq[g][o0 + lane] : 0;
-    const int idx = mine ? (int)C.sidx[g][o0 + lane] : 0;
+    const bool mine = t < nj;
+    const int chain = mine ? (int)C.sreq[g][o0 + t] : 0;
+    const int idx = mine ? (int)C.sidx[g][o0 + t] : 0;
     const int cc = g * CG + chain;
-    const int rl = lane - idx;  // the slot of the request's reference texture (index 0)
-    // setup
+    // setup (every lane of the texture computes it)
     TexGeom T;
     T.ok = 0;
     if (mine) T = tex_geom<WS>(s, (const float*)C.geo[cc], C.views[cc][idx]);
-    // gather: the texture's samples in sample order, rows by the `left += dy` recurrence, columns by
-    // `+= dx` (optim.cpp:850-860); the channel sums of normalize's first pass ride along
-    float X[S], Y[S], Z[S];
-    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
-    if (T.ok) {
+    // gather: samples in sample order, rows by the `left += dy` recurrence, columns by `+= dx`
+    // (optim.cpp:850-860) -- the lane's first sample reached by the same additions
+    float X[K], Y[K], Z[K];
+#pragma unroll
+    for (int q = 0; q < K; ++q) { X[q] = 0.0f; Y[q] = 0.0f; Z[q] = 0.0f; }
+    if (T.ok && kn > 0) {
       const uint32_t* pyr = s.pyr + T.base;
+      const int yy0 = k0 / WS;
+      int xx = k0 - yy0 * WS;
       float rx = T.tl0, ry = T.tl1;
+      for (int r = 0; r < yy0; ++r) { rx = rx + T.dy0; ry = ry + T.dy1; }
+      float lx = rx, ly = ry;
+      for (int c = 0; c < xx; ++c) { lx = lx + T.dx0; ly = ly + T.dx1; }
 #pragma unroll
-      for (int yy = 0; yy < WS; ++yy) {
-        uint32_t q00[WS], q01[WS], q10[WS], q11[WS];
-        float fx[WS], fy[WS];
-        float lx = rx, ly = ry;
+      for (int b0 = 0; b0 < K; b0 += NB) {
+        uint32_t q00[NB], q01[NB], q10[NB], q11[NB];
+        float fx[NB], fy[NB];
 #pragma unroll
-        for (int xx = 0; xx < WS; ++xx) {
-          fx[xx] = lx; fy[xx] = ly;
-          const int ix = (int)lx, iy = (int)ly;
-          const uint32_t* p = pyr + (iy * T.W + ix);  // within one level: < 2^31 texels
-          q00[xx] = p[0]; q10[xx] = p[1]; q01[xx] = p[T.W]; q11[xx] = p[T.W + 1];
-          lx = lx + T.dx0; ly = ly + T.dx1;
+        for (int u = 0; u < NB; ++u) {
+          const int q = b0 + u;
+          if (q < K && q < kn) {
+            fx[u] = lx; fy[u] = ly;
+            const int ix = (int)lx, iy = (int)ly;
+            const uint32_t* p = pyr + (iy * T.W + ix);  // within one level: < 2^31 texels
+            q00[u] = p[0]; q10[u] = p[1]; q01[u] = p[T.W]; q11[u] = p[T.W + 1];
+            if (++xx == WS) {
+              xx = 0;
+              rx = rx + T.dy0; ry = ry + T.dy1;
+              lx = rx; ly = ry;
+            } else {
+              lx = lx + T.dx0; ly = ly + T.dx1;
+            }
+          }
         }
 #pragma unroll
-        for (int xx = 0; xx < WS; ++xx) {
-          const float dx1 = fx[xx] - (float)(int)fx[xx], dx0 = 1.0f - dx1;
-          const float dy1 = fy[xx] - (float)(int)fy[xx], dy0 = 1.0f - dy1;
-          const float f00 = dx0 * dy0, f01 = dx0 * dy1, f10 = dx1 * dy0, f11 = dx1 * dy1;
-          float r = 0.0f, gg = 0.0f, b = 0.0f;
-          r += (float)(q00[xx] & 0xff) * f00 + (float)(q01[xx] & 0xff) * f01;
-          gg += (float)((q00[xx] >> 8) & 0xff) * f00 + (float)((q01[xx] >> 8) & 0xff) * f01;
-          b += (float)((q00[xx] >> 16) & 0xff) * f00 + (float)((q01[xx] >> 16) & 0xff) * f01;
-          r += (float)(q10[xx] & 0xff) * f10 + (float)(q11[xx] & 0xff) * f11;
-          gg += (float)((q10[xx] >> 8) & 0xff) * f10 + (float)((q11[xx] >> 8) & 0xff) * f11;
-          b += (float)((q10[xx] >> 16) & 0xff) * f10 + (float)((q11[xx] >> 16) & 0xff) * f11;
-          X[yy * WS + xx] = r; Y[yy * WS + xx] = gg; Z[yy * WS + xx] = b;
-          a0 += r; a1 += gg; a2 += b;
+        for (int u = 0; u < NB; ++u) {
+          const int q = b0 + u;
+          if (q < K && q < kn) {
+            const float dx1 = fx[u] - (float)(int)fx[u], dx0 = 1.0f - dx1;
+            const float dy1 = fy[u] - (float)(int)fy[u], dy0 = 1.0f - dy1;
+            const float f00 = dx0 * dy0, f01 = dx0 * dy1, f10 = dx1 * dy0, f11 = dx1 * dy1;
+            float r = 0.0f, gg = 0.0f, bb = 0.0f;
+            r += (float)(q00[u] & 0xff) * f00 + (float)(q01[u] & 0xff) * f01;
+            gg += (float)((q00[u] >> 8) & 0xff) * f00 + (float)((q01[u] >> 8) & 0xff) * f01;
+            bb += (float)((q00[u] >> 16) & 0xff) * f00 + (float)((q01[u] >> 16) & 0xff) * f01;
+            r += (float)(q10[u] & 0xff) * f10 + (float)(q11[u] & 0xff) * f11;
+            gg += (float)((q10[u] >> 8) & 0xff) * f10 + (float)((q11[u] >> 8) & 0xff) * f11;
+            bb += (float)((q10[u] >> 16) & 0xff) * f10 + (float)((q11[u] >> 16) & 0xff) * f11;
+            X[q] = r; Y[q] = gg; Z[q] = bb;
+          }
         }
-        rx = rx + T.dy0; ry = ry + T.dy1;
-        __builtin_amdgcn_sched_barrier(0);  // one row's loads in flight at a time: bounded registers
+        __builtin_amdgcn_sched_barrier(0);  // one batch of loads in flight at a time: bounded registers
       }
-      // normalize (optim.cpp:1031-1067): means, second moment, element-wise scaling
-      const float fs3 = (float)S;
-      a0 = __fdiv_rn(a0, fs3); a1 = __fdiv_rn(a1, fs3); a2 = __fdiv_rn(a2, fs3);
-      float ave2 = 0.0f;
-#pragma unroll
-      for (int i = 0; i < S; ++i) {
-        const float f0 = a0 - X[i], f1 = a1 - Y[i], f2 = a2 - Z[i];
-        ave2 += f0 * f0 + f1 * f1 + f2 * f2;
-      }
-      ave2 = fsqrt_rn(__fdiv_rn(ave2, (float)(3 * S)));
-      if (ave2 == 0.0f) ave2 = 1.0f;
-#pragma unroll
-      for (int i = 0; i < S; ++i) {
-        X[i] = __fdiv_rn(X[i] - a0, ave2);
-        Y[i] = __fdiv_rn(Y[i] - a1, ave2);
-        Z[i] = __fdiv_rn(Z[i] - a2, ave2);
-        if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < S; ++i) { X[i] = 0.0f; Y[i] = 0.0f; Z[i] = 0.0f; }
     }
-    // robust INCC against the reference texture (optim.cpp:561-567, 919-929): its normalised samples
-    // from its lane, the products summed in sample order (R, G, B per sample)
-    const int src = mine ? rl : lane;
+    // normalize (optim.cpp:1031-1067), the channel sums in LP stages
+    const bool ok = T.ok != 0;
+    const int last = t * LP + LP - 1;  // the lane that ends a texture's sums
+    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+#pragma unroll
+    for (int j = 0; j < LP; ++j) {
+      if (ok && sub == j) {
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+          if (q < kn) { a0 += X[q]; a1 += Y[q]; a2 += Z[q]; }
+      }
+      if (j + 1 < LP) {
+        const float u0 = __shfl_up(a0, 1), u1 = __shfl_up(a1, 1), u2 = __shfl_up(a2, 1);
+        if (sub == j + 1) { a0 = u0; a1 = u1; a2 = u2; }
+      }
+    }
+    a0 = __shfl(a0, last); a1 = __shfl(a1, last); a2 = __shfl(a2, last);
+    const float fs3 = (float)S;
+    a0 = __fdiv_rn(a0, fs3); a1 = __fdiv_rn(a1, fs3); a2 = __fdiv_rn(a2, fs3);
+    float ave2 = 0.0f;
+#pragma unroll
+    for (int j = 0; j < LP; ++j) {
+      if (ok && sub == j) {
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+          if (q < kn) {
+            const float f0 = a0 - X[q], f1 = a1 - Y[q], f2 = a2 - Z[q];
+            ave2 += f0 * f0 + f1 * f1 + f2 * f2;
+          }
+      }
+      if (j + 1 < LP) {
+        const float u = __shfl_up(ave2, 1);
+        if (sub == j + 1) ave2 = u;
+      }
+    }
+    ave2 = __shfl(ave2, last);
+    ave2 = fsqrt_rn(__fdiv_rn(ave2, (float)(3 * S)));
+    if (ave2 == 0.0f) ave2 = 1.0f;
+    if (ok) {
+#pragma unroll
+      for (int q = 0; q < K; ++q)
+        if (q < kn) {
+          X[q] = __fdiv_rn(X[q] - a0, ave2);
+          Y[q] = __fdiv_rn(Y[q] - a1, ave2);
+          Z[q] = __fdiv_rn(Z[q] - a2, ave2);
+        }
+    }
+    SP_MARK(4);
+    // robust INCC against the reference texture (optim.cpp:561-567, 919-929): the reference texture's
+    // normalised samples from its lane with the same part, the products summed in sample order
+    // (R, G, B per sample) in LP stages
+    const int rt = mine ? t - idx : t;  // the request's reference texture (index 0)
+    const int src = rt * LP + sub;
     const int refok = __shfl(T.ok, src);
+    float px[K], py[K], pz[K];
+#pragma unroll
+    for (int q = 0; q < K; ++q) { px[q] = __shfl(X[q], src); py[q] = __shfl(Y[q], src); pz[q] = __shfl(Z[q], src); }
     float ans = 0.0f;
 #pragma unroll
-    for (int i = 0; i < S; ++i) {
-      const float px = __shfl(X[i], src), py = __shfl(Y[i], src), pz = __shfl(Z[i], src);
-      ans += px * X[i];
-      ans += py * Y[i];
-      ans += pz * Z[i];
-      if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    for (int j = 0; j < LP; ++j) {
+      if (ok && sub == j) {
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+          if (q < kn) {
+            ans += px[q] * X[q];
+            ans += py[q] * Y[q];
+            ans += pz[q] * Z[q];
+          }
+      }
+      if (j + 1 < LP) {
+        const float u = __shfl_up(ans, 1);
+        if (sub == j + 1) ans = u;
+      }
     }
-    float jr = 0.0f;
-    if (mine && idx >= 1 && refok && T.ok) jr = robustincc((float)(1.0 - (double)__fdiv_rn(ans, (float)(3 * S))));
-    ejvalid[lane] = T.ok;
-    ejres[lane] = jr;
+    if (mine && sub == LP - 1) {
+      float jr = 0.0f;
+      if (idx >= 1 && refok && ok) jr = robustincc((float)(1.0 - (double)__fdiv_rn(ans, (float)(3 * S))));
+      ejvalid[t] = T.ok;
+      ejres[t] = jr;
+    }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // the request's value on its reference lane, in request_value's order
-    if (mine && idx == 0) {
+    // the request's value on its reference texture's last lane, in request_value's order
+    if (mine && idx == 0 && sub == LP - 1) {
       struct {
         SPLIT_AS int* jvalid;
         SPLIT_AS float* jres;
       } V = {ejvalid, ejres};
       const int need = C.need[cc];
-      C.fv[cc] = request_value(s, V, lane, C.size[cc], need, jobs[C.cand[cc]], tex_valid);
+      C.fv[cc] = request_value(s, V, t, C.size[cc], need, jobs[C.cand[cc]], tex_valid);
     }
+    SP_MARK(6);
     grabs += nj;
     chunks++;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_fetch_add(&C.done[g], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
+  SP_MARK(7);
   for (int d = 32; d >= 1; d >>= 1) tex_valid += __shfl_xor(tex_valid, d);
   if (lane == 0) {
+#if defined(BQ_PROFILE)
+    for (int i = 4; i < 8; ++i) atomicAdd(&st->prof[i], prof[i]);
+#endif
     atomicAdd(&st->tex_valid, tex_valid);
     atomicAdd(&st->tex_grabs, grabs);
     atomicAdd(&st->chunks, chunks);
   }
 }
 
-template <int WS, int G, int CG>
+template <int WS, int G, int CG, int LP>
 __global__ __launch_bounds__(SPLIT_THREADS) __attribute__((amdgpu_waves_per_eu(REFINE_WPE(CG)))) void refine_split_kernel(
     DScene s, RefineJob* __restrict__ jobs, int n, int nc_active, DevStats* st) {
   using L = RefSplitLds<WS, G, CG>;
@@ -357,23 +459,29 @@ __global__ __launch_bounds__(SPLIT_THREADS) __attribute__((amdgpu_waves_per_eu(R
   }
   __syncthreads();
   if (wave < G)
-    split_optimizer<WS, G, CG>(s, *(SPLIT_AS RefSplitLds<WS, G, CG>*)&C, jobs, n, nc_active, st);
+    split_optimizer<WS, G, CG, WAVE / LP>(s, *(SPLIT_AS RefSplitLds<WS, G, CG>*)&C, jobs, n, nc_active, st);
   else
-    split_evaluator<WS, G, CG>(s, *(SPLIT_AS RefSplitLds<WS, G, CG>*)&C, jobs, st);
+    split_evaluator<WS, G, CG, LP>(s, *(SPLIT_AS RefSplitLds<WS, G, CG>*)&C, jobs, st);
 }
 
 
-// config = 200000 + optimizer wavefronts * 1000 + chains per optimizer wavefront (WS <= 7)
+// config = 200000 + LP * 10000 + optimizer wavefronts * 1000 + chains per optimizer wavefront, LP =
+// lanes per texture in the evaluators (0 reads as 1); WS <= 7
+#define PMVS_SPLIT_CONFIGS(X) X(0, 2, 32) X(0, 2, 40) X(0, 3, 24) X(0, 4, 16) X(2, 2, 32) X(2, 3, 24) X(2, 4, 16) \
+  X(2, 5, 16) X(2, 6, 12) X(3, 4, 16) X(3, 5, 16) X(4, 4, 16) X(4, 5, 16) X(4, 6, 12)
 bool refine_split_supported(int config) {
+#define PMVS_SPLIT_CASE(LPc, Gc, CGc) case 200000 + LPc * 10000 + Gc * 1000 + CGc:
   switch (config) {
-    case 202032: case 202040: case 203024: case 204016: return true;
+    PMVS_SPLIT_CONFIGS(PMVS_SPLIT_CASE)
+    return true;
     default: return false;
   }
+#undef PMVS_SPLIT_CASE
 }
 
 template <int WS>
 static hipError_t launch_split_ws(int config, const DScene& s, RefineJob* d_jobs, int n, DevStats* d_st, hipStream_t stream) {
-  const int gw = (config / 1000) % 100, cg = config % 1000;
+  const int gw = (config / 1000) % 10, cg = config % 1000;
   int dev = 0, cus = 0;
   hipError_t e;
   if ((e = hipGetDevice(&dev)) != hipSuccess ||
@@ -384,19 +492,16 @@ static hipError_t launch_split_ws(int config, const DScene& s, RefineJob* d_jobs
   const int sgrid = cus < (n + gw - 1) / gw ? cus : (n + gw - 1) / gw;
   const int per = (n + sgrid * gw - 1) / (sgrid * gw);
   const int nca = per < cg ? per : cg;
-#define PMVS_SPLIT(Gc, CGc)                                                                                            \
-  case 200000 + Gc * 1000 + CGc:                                                                                        \
-    hipLaunchKernelGGL((refine_split_kernel<WS, Gc, CGc>), dim3(sgrid), dim3(SPLIT_THREADS), 0, stream, s, d_jobs, n, nca, \
-                       d_st);                                                                                           \
+#define PMVS_SPLIT_LAUNCH(LPc, Gc, CGc)                                                                                   \
+  case 200000 + LPc * 10000 + Gc * 1000 + CGc:                                                                             \
+    hipLaunchKernelGGL((refine_split_kernel<WS, Gc, CGc, (LPc > 0 ? LPc : 1)>), dim3(sgrid), dim3(SPLIT_THREADS), 0, stream, \
+                       s, d_jobs, n, nca, d_st);                                                                           \
     break;
   switch (config) {
-    PMVS_SPLIT(2, 32)
-    PMVS_SPLIT(2, 40)
-    PMVS_SPLIT(3, 24)
-    PMVS_SPLIT(4, 16)
+    PMVS_SPLIT_CONFIGS(PMVS_SPLIT_LAUNCH)
     default: return hipErrorInvalidValue;
   }
-#undef PMVS_SPLIT
+#undef PMVS_SPLIT_LAUNCH
   return hipGetLastError();
 }
 
