@@ -92,6 +92,21 @@ constexpr int BQNH = BQN * BQNP / 2;
 
 BQ_HD double bq_min(double a, double b) { return (a <= b) ? a : b; }  // NLopt MIN2
 BQ_HD double bq_max(double a, double b) { return (a >= b) ? a : b; }  // NLopt MAX2
+// Run-time-indexed access to a small local array through selects over its constant positions, so
+// the array stays in registers: a dynamic index (TRSBOX's xbdi[iact], ALTMOV's hcol[knew]) otherwise
+// puts the whole array in scratch, and its hot loops then read scratch (global-memory latency).
+template <int N>
+BQ_HD double bq_get(const double (&a)[N], int i) {
+  double r = a[0];
+#pragma unroll
+  for (int k = 1; k < N; ++k) r = (i == k) ? a[k] : r;
+  return r;
+}
+template <int N>
+BQ_HD void bq_set(double (&a)[N], int i, double v) {
+#pragma unroll
+  for (int k = 0; k < N; ++k) a[k] = (i == k) ? v : a[k];
+}
 
 struct BqState {
   // Powell's 1-based arrays stored without their unused row/column 0 (2216 -> 1736 bytes: the
@@ -222,8 +237,7 @@ L50:
   }
   if (iact > 0) {
     ++nact;
-    xbdi[iact] = one;
-    if (s[iact] < zero) xbdi[iact] = onemin;
+    bq_set(xbdi, iact, bq_get(s, iact) < zero ? onemin : one);
     delsq -= d[iact] * d[iact];
     if (delsq <= zero) goto L90;
     goto L20;
@@ -386,7 +400,7 @@ L150:
   qred += sdec;
   if (iact > 0 && isav == iu) {
     ++nact;
-    xbdi[iact] = xsav;
+    bq_set(xbdi, iact, xsav);
     goto L100;
   }
   if (sdec > qred * .01) goto L120;
@@ -442,7 +456,7 @@ BQ_NI void bq_altmov(const BQ_AS double (*BQ_RS xpt)[BQN], const BQ_AS double* B
     temp = zmat[knew][j];
     for (int k = 1; k <= BQNPT; ++k) hcol[k] += temp * zmat[k][j];
   }
-  *alpha = hcol[knew];
+  *alpha = bq_get(hcol, knew);
   ha = half * *alpha;
   for (int i = 1; i <= BQN; ++i) glag[i] = bmat[knew][i];
   for (int k = 1; k <= BQNPT; ++k) {

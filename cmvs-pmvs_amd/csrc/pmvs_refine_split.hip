@@ -74,11 +74,190 @@ __device__ __forceinline__ int lds_load_acq(SPLIT_AS int* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// One chunk (group g, chunk k) evaluated by the calling wavefront -- an evaluator, or an optimizer
+// wavefront waiting for its own group -- LP lanes per texture; returns the valid textures its my_f
+// requests counted (request_value) and signals the chunk done.
+template <int WS, int G, int CG, int LP>
+__device__ __noinline__ unsigned long long split_chunk(const DScene& s, SPLIT_AS RefSplitLds<WS, G, CG>& C,
+                                                       RefineJob* __restrict__ jobs, int g, int k, unsigned long long* prof) {
+  constexpr int S = WS * WS;
+  constexpr int K = (S + LP - 1) / LP;
+  constexpr int NB = 7;  // samples whose texel loads are in flight together
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & (WAVE - 1);
+  const int t = lane / LP, sub = lane - t * LP;  // the lane's texture slot and part of it
+  const int k0 = sub * K;
+  const int kn = k0 < S ? (S - k0 < K ? S - k0 : K) : 0;  // samples of this lane
+  SPLIT_AS int* ejvalid = C.ejvalid[wave];
+  SPLIT_AS float* ejres = C.ejres[wave];
+  unsigned long long tex_valid = 0;
+  unsigned long long tprev = SP_NOW();
+  (void)prof;
+  const int o0 = C.choff[g][k], nj = C.choff[g][k + 1] - o0;
+  const bool mine = t < nj;
+  const int chain = mine ? (int)C.sreq[g][o0 + t] : 0;
+  const int idx = mine ? (int)C.sidx[g][o0 + t] : 0;
+  const int cc = g * CG + chain;
+  // setup (every lane of the texture computes it)
+  TexGeom T;
+  T.ok = 0;
+  if (mine) T = tex_geom<WS>(s, (const float*)C.geo[cc], C.views[cc][idx]);
+  // gather: samples in sample order, rows by the `left += dy` recurrence, columns by `+= dx`
+  // (optim.cpp:850-860) -- the lane's first sample reached by the same additions
+  float X[K], Y[K], Z[K];
+#pragma unroll
+  for (int q = 0; q < K; ++q) { X[q] = 0.0f; Y[q] = 0.0f; Z[q] = 0.0f; }
+  if (T.ok && kn > 0) {
+    const uint32_t* pyr = s.pyr + T.base;
+    const int yy0 = k0 / WS;
+    int xx = k0 - yy0 * WS;
+    float rx = T.tl0, ry = T.tl1;
+    for (int r = 0; r < yy0; ++r) { rx = rx + T.dy0; ry = ry + T.dy1; }
+    float lx = rx, ly = ry;
+    for (int c = 0; c < xx; ++c) { lx = lx + T.dx0; ly = ly + T.dx1; }
+#pragma unroll
+    for (int b0 = 0; b0 < K; b0 += NB) {
+      uint32_t q00[NB], q01[NB], q10[NB], q11[NB];
+      float fx[NB], fy[NB];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int q = b0 + u;
+        if (q < K && q < kn) {
+          fx[u] = lx; fy[u] = ly;
+          const int ix = (int)lx, iy = (int)ly;
+          const uint32_t* p = pyr + (iy * T.W + ix);  // within one level: < 2^31 texels
+          q00[u] = p[0]; q10[u] = p[1]; q01[u] = p[T.W]; q11[u] = p[T.W + 1];
+          if (++xx == WS) {
+            xx = 0;
+            rx = rx + T.dy0; ry = ry + T.dy1;
+            lx = rx; ly = ry;
+          } else {
+            lx = lx + T.dx0; ly = ly + T.dx1;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int q = b0 + u;
+        if (q < K && q < kn) {
+          const float dx1 = fx[u] - (float)(int)fx[u], dx0 = 1.0f - dx1;
+          const float dy1 = fy[u] - (float)(int)fy[u], dy0 = 1.0f - dy1;
+          const float f00 = dx0 * dy0, f01 = dx0 * dy1, f10 = dx1 * dy0, f11 = dx1 * dy1;
+          float r = 0.0f, gg = 0.0f, bb = 0.0f;
+          r += (float)(q00[u] & 0xff) * f00 + (float)(q01[u] & 0xff) * f01;
+          gg += (float)((q00[u] >> 8) & 0xff) * f00 + (float)((q01[u] >> 8) & 0xff) * f01;
+          bb += (float)((q00[u] >> 16) & 0xff) * f00 + (float)((q01[u] >> 16) & 0xff) * f01;
+          r += (float)(q10[u] & 0xff) * f10 + (float)(q11[u] & 0xff) * f11;
+          gg += (float)((q10[u] >> 8) & 0xff) * f10 + (float)((q11[u] >> 8) & 0xff) * f11;
+          bb += (float)((q10[u] >> 16) & 0xff) * f10 + (float)((q11[u] >> 16) & 0xff) * f11;
+          X[q] = r; Y[q] = gg; Z[q] = bb;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one batch of loads in flight at a time: bounded registers
+    }
+  }
+  // normalize (optim.cpp:1031-1067), the channel sums in LP stages
+  const bool ok = T.ok != 0;
+  const int last = t * LP + LP - 1;  // the lane that ends a texture's sums
+  float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+#pragma unroll
+  for (int j = 0; j < LP; ++j) {
+    if (ok && sub == j) {
+#pragma unroll
+      for (int q = 0; q < K; ++q)
+        if (q < kn) { a0 += X[q]; a1 += Y[q]; a2 += Z[q]; }
+    }
+    if (j + 1 < LP) {
+      const float u0 = __shfl_up(a0, 1), u1 = __shfl_up(a1, 1), u2 = __shfl_up(a2, 1);
+      if (sub == j + 1) { a0 = u0; a1 = u1; a2 = u2; }
+    }
+  }
+  a0 = __shfl(a0, last); a1 = __shfl(a1, last); a2 = __shfl(a2, last);
+  const float fs3 = (float)S;
+  a0 = __fdiv_rn(a0, fs3); a1 = __fdiv_rn(a1, fs3); a2 = __fdiv_rn(a2, fs3);
+  float ave2 = 0.0f;
+#pragma unroll
+  for (int j = 0; j < LP; ++j) {
+    if (ok && sub == j) {
+#pragma unroll
+      for (int q = 0; q < K; ++q)
+        if (q < kn) {
+          const float f0 = a0 - X[q], f1 = a1 - Y[q], f2 = a2 - Z[q];
+          ave2 += f0 * f0 + f1 * f1 + f2 * f2;
+        }
+    }
+    if (j + 1 < LP) {
+      const float u = __shfl_up(ave2, 1);
+      if (sub == j + 1) ave2 = u;
+    }
+  }
+  ave2 = __shfl(ave2, last);
+  ave2 = fsqrt_rn(__fdiv_rn(ave2, (float)(3 * S)));
+  if (ave2 == 0.0f) ave2 = 1.0f;
+  if (ok) {
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+      if (q < kn) {
+        X[q] = __fdiv_rn(X[q] - a0, ave2);
+        Y[q] = __fdiv_rn(Y[q] - a1, ave2);
+        Z[q] = __fdiv_rn(Z[q] - a2, ave2);
+      }
+  }
+  SP_MARK(4);
+  // robust INCC against the reference texture (optim.cpp:561-567, 919-929): the reference texture's
+  // normalised samples from its lane with the same part, the products summed in sample order
+  // (R, G, B per sample) in LP stages
+  const int rt = mine ? t - idx : t;  // the request's reference texture (index 0)
+  const int src = rt * LP + sub;
+  const int refok = __shfl(T.ok, src);
+  float px[K], py[K], pz[K];
+#pragma unroll
+  for (int q = 0; q < K; ++q) { px[q] = __shfl(X[q], src); py[q] = __shfl(Y[q], src); pz[q] = __shfl(Z[q], src); }
+  float ans = 0.0f;
+#pragma unroll
+  for (int j = 0; j < LP; ++j) {
+    if (ok && sub == j) {
+#pragma unroll
+      for (int q = 0; q < K; ++q)
+        if (q < kn) {
+          ans += px[q] * X[q];
+          ans += py[q] * Y[q];
+          ans += pz[q] * Z[q];
+        }
+    }
+    if (j + 1 < LP) {
+      const float u = __shfl_up(ans, 1);
+      if (sub == j + 1) ans = u;
+    }
+  }
+  if (mine && sub == LP - 1) {
+    float jr = 0.0f;
+    if (idx >= 1 && refok && ok) jr = robustincc((float)(1.0 - (double)__fdiv_rn(ans, (float)(3 * S))));
+    ejvalid[t] = T.ok;
+    ejres[t] = jr;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  // the request's value on its reference texture's last lane, in request_value's order
+  if (mine && idx == 0 && sub == LP - 1) {
+    struct {
+      SPLIT_AS int* jvalid;
+      SPLIT_AS float* jres;
+    } V = {ejvalid, ejres};
+    const int need = C.need[cc];
+    C.fv[cc] = request_value(s, V, t, C.size[cc], need, jobs[C.cand[cc]], tex_valid);
+  }
+  SP_MARK(6);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane == 0) __hip_atomic_fetch_add(&C.done[g], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return tex_valid;
+}
+
 // The two roles as separate functions, so that each gets its own register allocation (inlined
 // into one body, the evaluator's 147 sample registers and the optimizer's call sites spilled).
-template <int WS, int G, int CG, int TS>
+template <int WS, int G, int CG, int LP>
 __device__ __noinline__ void split_optimizer(const DScene& s, SPLIT_AS RefSplitLds<WS, G, CG>& C, RefineJob* __restrict__ jobs,
                                              int n, int nc_active, DevStats* st) {
+  constexpr int TS = WAVE / LP;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & (WAVE - 1);
   const int g = wave;
   const bool owner = lane < CG && lane < nc_active;
@@ -89,7 +268,7 @@ __device__ __noinline__ void split_optimizer(const DScene& s, SPLIT_AS RefSplitL
   bool exhausted = !owner;
   double fv = 0.0;
   float fcoord[4], fnormal[4];
-  unsigned long long nevals = 0, rounds = 0;
+  unsigned long long nevals = 0, rounds = 0, tex_valid = 0, grabs = 0, chunks = 0;
   const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999};
   const double ub[3] = {HUGE_VAL, 23.99999, 23.99999};
   unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -193,8 +372,24 @@ __device__ __noinline__ void split_optimizer(const DScene& s, SPLIT_AS RefSplitL
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) __hip_atomic_exchange(&C.avail[g], k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     SP_MARK(2);
-    // (d) wait for the evaluators
-    while (lds_load_acq(&C.done[g]) < k) __builtin_amdgcn_s_sleep(2);
+    // (d) wait for the evaluators, evaluating this group's unclaimed chunks meanwhile
+    while (lds_load_acq(&C.done[g]) < k) {
+      int got = -1;
+      if (lane == 0 && lds_load_acq(&C.avail[g]) > 0) {
+        const int old = __hip_atomic_fetch_add(&C.avail[g], -1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (old > 0) got = C.nchunk[g] - old;
+      }
+      got = __shfl(got, 0);
+      if (got >= 0) {
+        SP_MARK(3);
+        tex_valid += split_chunk<WS, G, CG, LP>(s, C, jobs, g, got, prof);
+        tprev = SP_NOW();
+        grabs += C.choff[g][got + 1] - C.choff[g][got];
+        chunks++;
+      } else {
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
     SP_MARK(3);
     // (e) consume the results
     if (req) {
@@ -213,12 +408,18 @@ __device__ __noinline__ void split_optimizer(const DScene& s, SPLIT_AS RefSplitL
     }
   }
   if (lane == 0) __hip_atomic_fetch_add(&C.live, -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  for (int d = 32; d >= 1; d >>= 1) nevals += __shfl_xor(nevals, d);
+  for (int d = 32; d >= 1; d >>= 1) {
+    nevals += __shfl_xor(nevals, d);
+    tex_valid += __shfl_xor(tex_valid, d);
+  }
   if (lane == 0) {
 #if defined(BQ_PROFILE)
     for (int i = 0; i < 4; ++i) atomicAdd(&st->prof[i], prof[i]);
 #endif
     atomicAdd(&st->evals, nevals);
+    atomicAdd(&st->tex_valid, tex_valid);
+    atomicAdd(&st->tex_grabs, grabs);
+    atomicAdd(&st->chunks, chunks);
     atomicAdd(&st->rounds, rounds);
     atomicMax(&st->t_last, __builtin_amdgcn_s_memrealtime());
   }
@@ -233,17 +434,9 @@ __device__ __noinline__ void split_optimizer(const DScene& s, SPLIT_AS RefSplitL
 template <int WS, int G, int CG, int LP>
 __device__ __noinline__ void split_evaluator(const DScene& s, SPLIT_AS RefSplitLds<WS, G, CG>& C, RefineJob* __restrict__ jobs,
                                              DevStats* st) {
-  constexpr int S = WS * WS;
-  constexpr int K = (S + LP - 1) / LP;
-  constexpr int NB = 7;  // samples whose texel loads are in flight together
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & (WAVE - 1);
   const int ew = wave - G;
-  const int t = lane / LP, sub = lane - t * LP;  // the lane's texture slot and part of it
-  const int k0 = sub * K;
-  const int kn = k0 < S ? (S - k0 < K ? S - k0 : K) : 0;  // samples of this lane
   unsigned long long tex_valid = 0, grabs = 0, chunks = 0;
-  SPLIT_AS int* ejvalid = C.ejvalid[wave];
-  SPLIT_AS float* ejres = C.ejres[wave];
   unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long tprev = SP_NOW();
   for (int it = 0;; ++it) {
@@ -268,165 +461,10 @@ __device__ __noinline__ void split_evaluator(const DScene& s, SPLIT_AS RefSplitL
       continue;
     }
     SP_MARK(7);
-    const int o0 = C.choff[g][k], nj = C.choff[g][k + 1] - o0;
-    const bool mine = t < nj;
-    const int chain = mine ? (int)C.sreq[g][o0 + t] : 0;
-    const int idx = mine ? (int)C.sidx[g][o0 + t] : 0;
-    const int cc = g * CG + chain;
-    // setup (every lane of the texture computes it)
-    TexGeom T;
-    T.ok = 0;
-    if (mine) T = tex_geom<WS>(s, (const float*)C.geo[cc], C.views[cc][idx]);
-    // gather: samples in sample order, rows by the `left += dy` recurrence, columns by `+= dx`
-    // (optim.cpp:850-860) -- the lane's first sample reached by the same additions
-    float X[K], Y[K], Z[K];
-#pragma unroll
-    for (int q = 0; q < K; ++q) { X[q] = 0.0f; Y[q] = 0.0f; Z[q] = 0.0f; }
-    if (T.ok && kn > 0) {
-      const uint32_t* pyr = s.pyr + T.base;
-      const int yy0 = k0 / WS;
-      int xx = k0 - yy0 * WS;
-      float rx = T.tl0, ry = T.tl1;
-      for (int r = 0; r < yy0; ++r) { rx = rx + T.dy0; ry = ry + T.dy1; }
-      float lx = rx, ly = ry;
-      for (int c = 0; c < xx; ++c) { lx = lx + T.dx0; ly = ly + T.dx1; }
-#pragma unroll
-      for (int b0 = 0; b0 < K; b0 += NB) {
-        uint32_t q00[NB], q01[NB], q10[NB], q11[NB];
-        float fx[NB], fy[NB];
-#pragma unroll
-        for (int u = 0; u < NB; ++u) {
-          const int q = b0 + u;
-          if (q < K && q < kn) {
-            fx[u] = lx; fy[u] = ly;
-            const int ix = (int)lx, iy = (int)ly;
-            const uint32_t* p = pyr + (iy * T.W + ix);  // within one level: < 2^31 texels
-            q00[u] = p[0]; q10[u] = p[1]; q01[u] = p[T.W]; q11[u] = p[T.W + 1];
-            if (++xx == WS) {
-              xx = 0;
-              rx = rx + T.dy0; ry = ry + T.dy1;
-              lx = rx; ly = ry;
-            } else {
-              lx = lx + T.dx0; ly = ly + T.dx1;
-            }
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < NB; ++u) {
-          const int q = b0 + u;
-          if (q < K && q < kn) {
-            const float dx1 = fx[u] - (float)(int)fx[u], dx0 = 1.0f - dx1;
-            const float dy1 = fy[u] - (float)(int)fy[u], dy0 = 1.0f - dy1;
-            const float f00 = dx0 * dy0, f01 = dx0 * dy1, f10 = dx1 * dy0, f11 = dx1 * dy1;
-            float r = 0.0f, gg = 0.0f, bb = 0.0f;
-            r += (float)(q00[u] & 0xff) * f00 + (float)(q01[u] & 0xff) * f01;
-            gg += (float)((q00[u] >> 8) & 0xff) * f00 + (float)((q01[u] >> 8) & 0xff) * f01;
-            bb += (float)((q00[u] >> 16) & 0xff) * f00 + (float)((q01[u] >> 16) & 0xff) * f01;
-            r += (float)(q10[u] & 0xff) * f10 + (float)(q11[u] & 0xff) * f11;
-            gg += (float)((q10[u] >> 8) & 0xff) * f10 + (float)((q11[u] >> 8) & 0xff) * f11;
-            bb += (float)((q10[u] >> 16) & 0xff) * f10 + (float)((q11[u] >> 16) & 0xff) * f11;
-            X[q] = r; Y[q] = gg; Z[q] = bb;
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);  // one batch of loads in flight at a time: bounded registers
-      }
-    }
-    // normalize (optim.cpp:1031-1067), the channel sums in LP stages
-    const bool ok = T.ok != 0;
-    const int last = t * LP + LP - 1;  // the lane that ends a texture's sums
-    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
-#pragma unroll
-    for (int j = 0; j < LP; ++j) {
-      if (ok && sub == j) {
-#pragma unroll
-        for (int q = 0; q < K; ++q)
-          if (q < kn) { a0 += X[q]; a1 += Y[q]; a2 += Z[q]; }
-      }
-      if (j + 1 < LP) {
-        const float u0 = __shfl_up(a0, 1), u1 = __shfl_up(a1, 1), u2 = __shfl_up(a2, 1);
-        if (sub == j + 1) { a0 = u0; a1 = u1; a2 = u2; }
-      }
-    }
-    a0 = __shfl(a0, last); a1 = __shfl(a1, last); a2 = __shfl(a2, last);
-    const float fs3 = (float)S;
-    a0 = __fdiv_rn(a0, fs3); a1 = __fdiv_rn(a1, fs3); a2 = __fdiv_rn(a2, fs3);
-    float ave2 = 0.0f;
-#pragma unroll
-    for (int j = 0; j < LP; ++j) {
-      if (ok && sub == j) {
-#pragma unroll
-        for (int q = 0; q < K; ++q)
-          if (q < kn) {
-            const float f0 = a0 - X[q], f1 = a1 - Y[q], f2 = a2 - Z[q];
-            ave2 += f0 * f0 + f1 * f1 + f2 * f2;
-          }
-      }
-      if (j + 1 < LP) {
-        const float u = __shfl_up(ave2, 1);
-        if (sub == j + 1) ave2 = u;
-      }
-    }
-    ave2 = __shfl(ave2, last);
-    ave2 = fsqrt_rn(__fdiv_rn(ave2, (float)(3 * S)));
-    if (ave2 == 0.0f) ave2 = 1.0f;
-    if (ok) {
-#pragma unroll
-      for (int q = 0; q < K; ++q)
-        if (q < kn) {
-          X[q] = __fdiv_rn(X[q] - a0, ave2);
-          Y[q] = __fdiv_rn(Y[q] - a1, ave2);
-          Z[q] = __fdiv_rn(Z[q] - a2, ave2);
-        }
-    }
-    SP_MARK(4);
-    // robust INCC against the reference texture (optim.cpp:561-567, 919-929): the reference texture's
-    // normalised samples from its lane with the same part, the products summed in sample order
-    // (R, G, B per sample) in LP stages
-    const int rt = mine ? t - idx : t;  // the request's reference texture (index 0)
-    const int src = rt * LP + sub;
-    const int refok = __shfl(T.ok, src);
-    float px[K], py[K], pz[K];
-#pragma unroll
-    for (int q = 0; q < K; ++q) { px[q] = __shfl(X[q], src); py[q] = __shfl(Y[q], src); pz[q] = __shfl(Z[q], src); }
-    float ans = 0.0f;
-#pragma unroll
-    for (int j = 0; j < LP; ++j) {
-      if (ok && sub == j) {
-#pragma unroll
-        for (int q = 0; q < K; ++q)
-          if (q < kn) {
-            ans += px[q] * X[q];
-            ans += py[q] * Y[q];
-            ans += pz[q] * Z[q];
-          }
-      }
-      if (j + 1 < LP) {
-        const float u = __shfl_up(ans, 1);
-        if (sub == j + 1) ans = u;
-      }
-    }
-    if (mine && sub == LP - 1) {
-      float jr = 0.0f;
-      if (idx >= 1 && refok && ok) jr = robustincc((float)(1.0 - (double)__fdiv_rn(ans, (float)(3 * S))));
-      ejvalid[t] = T.ok;
-      ejres[t] = jr;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // the request's value on its reference texture's last lane, in request_value's order
-    if (mine && idx == 0 && sub == LP - 1) {
-      struct {
-        SPLIT_AS int* jvalid;
-        SPLIT_AS float* jres;
-      } V = {ejvalid, ejres};
-      const int need = C.need[cc];
-      C.fv[cc] = request_value(s, V, t, C.size[cc], need, jobs[C.cand[cc]], tex_valid);
-    }
-    SP_MARK(6);
-    grabs += nj;
+    tex_valid += split_chunk<WS, G, CG, LP>(s, C, jobs, g, k, prof);
+    tprev = SP_NOW();
+    grabs += C.choff[g][k + 1] - C.choff[g][k];
     chunks++;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) __hip_atomic_fetch_add(&C.done[g], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   SP_MARK(7);
   for (int d = 32; d >= 1; d >>= 1) tex_valid += __shfl_xor(tex_valid, d);
@@ -444,7 +482,7 @@ template <int WS, int G, int CG, int LP>
 __global__ __launch_bounds__(SPLIT_THREADS) __attribute__((amdgpu_waves_per_eu(REFINE_WPE(CG)))) void refine_split_kernel(
     DScene s, RefineJob* __restrict__ jobs, int n, int nc_active, DevStats* st) {
   using L = RefSplitLds<WS, G, CG>;
-  static_assert(G >= 1 && G < SPLIT_THREADS / WAVE && CG <= WAVE && CG <= 255, "roles");
+  static_assert(G >= 1 && G <= SPLIT_THREADS / WAVE && CG <= WAVE && CG <= 255, "roles");
   static_assert(sizeof(L) <= 160 * 1024, "LDS");
   __shared__ L C;
   const int tid = threadIdx.x, wave = tid >> 6;
@@ -459,7 +497,7 @@ __global__ __launch_bounds__(SPLIT_THREADS) __attribute__((amdgpu_waves_per_eu(R
   }
   __syncthreads();
   if (wave < G)
-    split_optimizer<WS, G, CG, WAVE / LP>(s, *(SPLIT_AS RefSplitLds<WS, G, CG>*)&C, jobs, n, nc_active, st);
+    split_optimizer<WS, G, CG, LP>(s, *(SPLIT_AS RefSplitLds<WS, G, CG>*)&C, jobs, n, nc_active, st);
   else
     split_evaluator<WS, G, CG, LP>(s, *(SPLIT_AS RefSplitLds<WS, G, CG>*)&C, jobs, st);
 }
@@ -467,8 +505,8 @@ __global__ __launch_bounds__(SPLIT_THREADS) __attribute__((amdgpu_waves_per_eu(R
 
 // config = 200000 + LP * 10000 + optimizer wavefronts * 1000 + chains per optimizer wavefront, LP =
 // lanes per texture in the evaluators (0 reads as 1); WS <= 7
-#define PMVS_SPLIT_CONFIGS(X) X(0, 2, 32) X(0, 2, 40) X(0, 3, 24) X(0, 4, 16) X(2, 2, 32) X(2, 3, 24) X(2, 4, 16) \
-  X(2, 5, 16) X(2, 6, 12) X(3, 4, 16) X(3, 5, 16) X(4, 4, 16) X(4, 5, 16) X(4, 6, 12)
+#define PMVS_SPLIT_CONFIGS(X) X(0, 2, 32) X(0, 4, 16) X(2, 4, 16) X(2, 5, 16) X(2, 6, 12) X(2, 6, 14) X(2, 7, 12) \
+  X(2, 8, 10) X(3, 6, 14) X(4, 5, 16) X(4, 6, 14) X(4, 7, 12) X(4, 8, 10)
 bool refine_split_supported(int config) {
 #define PMVS_SPLIT_CASE(LPc, Gc, CGc) case 200000 + LPc * 10000 + Gc * 1000 + CGc:
   switch (config) {
