@@ -12,7 +12,7 @@ CFilter::run, updateThreshold) through pmvs_run_loop, with the model resident in
 value = refined patches/s: patches the expansion refined and committed to the model
 (preProcess -> refinePatch -> postProcess passed, expand.cpp:238) over all ranks / step time.
 Also: NCC evals/s (my_f + computeINCC evaluations), refined candidates/s.
-roofline: the loop's dominant kernel, refine_v2_kernel (the refine batches of >= 10000 candidates):
+roofline: the loop's dominant kernel, refine_split_kernel (the refine batches of >= 10000 candidates):
 algorithmic bytes = 588 B x valid textures per my_f evaluation over its HIP-event
 time, against 8 TB/s HBM; the smaller batches' workgroup-form kernel in roofline.small_batches.
 refine_c2: the refine kernel alone on configs[1] (8-view 1920x1080, level 1, 100k candidates).
@@ -58,9 +58,21 @@ sys.path.insert(0, os.path.join(ROOT, "cmvs-pmvs_amd"))
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 BYTES_PER_TEXTURE = 49 * 4 * 3  # wsize^2 samples x 4 texels x 3 B
-_RCFG = int(os.environ.get("PMVS_REFINE_CONFIG", "1206"))  # texture slots * 100 + chains per wavefront
-REFINE_KERNEL = f"refine_v2_kernel<7,{_RCFG // 100},{_RCFG % 100}>"
-SMALL_KERNEL = "refine_wg_kernel<7,32,31,4>"  # batches below 10000 candidates (pmvs_api.cpp refine_cfg)
+
+
+def refine_kernel_name(cfg):
+    """The refine kernel a PMVS_REFINE_CONFIG value launches (pmvs_kernels.hip launch_refine_ws)."""
+    if cfg >= 200000:  # split form: 200000 + LP * 10000 + optimizer wavefronts * 1000 + chains per wavefront
+        return f"refine_split_kernel<7,{(cfg // 1000) % 10},{cfg % 1000},{max(1, (cfg // 10000) % 10)}>"
+    if cfg >= 100000:  # workgroup form: 100000 + chains * 1000 + optimizer wavefronts * 10 + workgroups per CU
+        return f"refine_wg_kernel<7,{(cfg // 1000) % 100},...,{(cfg // 10) % 10}>"
+    return f"refine_v2_kernel<7,{cfg // 100},{cfg % 100}>"  # texture slots * 100 + chains per wavefront
+
+
+# the refine layouts of the batches >= 10000 candidates and below (pmvs_api.cpp Scene::refine_cfg)
+_RCFG = int(os.environ.get("PMVS_REFINE_LARGE_CONFIG", os.environ.get("PMVS_REFINE_CONFIG", "226014")))
+REFINE_KERNEL = refine_kernel_name(_RCFG)
+SMALL_KERNEL = refine_kernel_name(int(os.environ.get("PMVS_REFINE_CONFIG", "132042")))
 
 
 _T0 = time.time()
@@ -118,7 +130,8 @@ def pmc_traffic(workload):
         if d.get("workload") != workload:
             continue
         for k, v in d.get("kernels", {}).items():
-            if k.startswith("pmvsdev::refine_v2_kernel") or k.startswith("refine_v2_kernel"):
+            base = REFINE_KERNEL.split("<")[0]
+            if k.startswith("pmvsdev::" + base) or k.startswith(base):
                 return int(v["hbm_bytes_per_launch"]), int(v.get("launches", 0)), os.path.relpath(f, ROOT)
     return None, None, None
 
@@ -497,7 +510,7 @@ def main():
                                                                          dev)
     launches = tot("refine_launches")
     traffic, traffic_launches, traffic_src = pmc_traffic("c3")
-    # the dominant kernel: the wavefront form, which runs the waves of >= 10k candidates; the
+    # the dominant kernel: the split form, which runs the waves of >= 10k candidates; the
     # workgroup form's small batches (iterations 2-3) are reported beside it
     tv_s, ms_s, l_s = tot("tex_valid_small"), tot("refine_ms_small"), tot("refine_launches_small")
     roof = refine_roofline(tex_valid - tv_s, refine_ms - ms_s, launches - l_s, traffic, traffic_launches, traffic_src)

@@ -202,7 +202,7 @@ struct pmvs_scene {
   ExpandBuffers xbuf;
   DBuf<pmvs_patch> fpatches;
   DBuf<int> fkeep;
-  int grid = 0, refine_grid = 0, tslots = 1206;
+  int grid = 0, refine_grid = 0, tslots = 226014;
   // batches below small_n candidates run the workgroup form spread over every CU (tslots_small):
   // their length is one chain's latency, not the chip's throughput
   int tslots_small = 132042, small_n = 10000;
