@@ -47,7 +47,15 @@ namespace pmvsdev {
 // group, `avail` (chunks not yet claimed: set by the group's atomic exchange after its tables are
 // written, taken by the evaluators' atomic decrements; a stale decrement only drives it below 0) and
 // `done` (chunks evaluated).  No workgroup barrier after the start.
-constexpr int SPLIT_THREADS = 512;
+// Wavefronts per SIMD (register budget) and workgroup size: 2 and 512 (8 wavefronts, 256 VGPRs); an
+// experiment build (SPLIT_WPE=1, SPLIT_THREADS=256) gives 4 wavefronts 512 registers each.
+#ifndef SPLIT_WPE
+#define SPLIT_WPE 2
+#endif
+#ifndef SPLIT_THREADS_
+#define SPLIT_THREADS_ 512
+#endif
+constexpr int SPLIT_THREADS = SPLIT_THREADS_;
 constexpr int SPLIT_TS = 64;  // texture slots per chunk: one per evaluator lane
 
 template <int WS, int G, int CG>
@@ -479,7 +487,7 @@ __device__ __noinline__ void split_evaluator(const DScene& s, SPLIT_AS RefSplitL
 }
 
 template <int WS, int G, int CG, int LP>
-__global__ __launch_bounds__(SPLIT_THREADS) __attribute__((amdgpu_waves_per_eu(REFINE_WPE(CG)))) void refine_split_kernel(
+__global__ __launch_bounds__(SPLIT_THREADS) __attribute__((amdgpu_waves_per_eu(SPLIT_WPE))) void refine_split_kernel(
     DScene s, RefineJob* __restrict__ jobs, int n, int nc_active, DevStats* st) {
   using L = RefSplitLds<WS, G, CG>;
   static_assert(G >= 1 && G <= SPLIT_THREADS / WAVE && CG <= WAVE && CG <= 255, "roles");
@@ -505,8 +513,12 @@ __global__ __launch_bounds__(SPLIT_THREADS) __attribute__((amdgpu_waves_per_eu(R
 
 // config = 200000 + LP * 10000 + optimizer wavefronts * 1000 + chains per optimizer wavefront, LP =
 // lanes per texture in the evaluators (0 reads as 1); WS <= 7
+#if SPLIT_THREADS_ == 512
 #define PMVS_SPLIT_CONFIGS(X) X(0, 2, 32) X(0, 4, 16) X(2, 4, 16) X(2, 5, 16) X(2, 6, 12) X(2, 6, 14) X(2, 7, 12) \
-  X(2, 8, 10) X(3, 6, 14) X(4, 5, 16) X(4, 6, 14) X(4, 7, 12) X(4, 8, 10)
+  X(2, 8, 10) X(3, 6, 14) X(4, 5, 16) X(4, 6, 14) X(4, 7, 12) X(4, 8, 10) X(8, 8, 10)
+#else
+#define PMVS_SPLIT_CONFIGS(X) X(2, 4, 20) X(4, 4, 20) X(8, 4, 20) X(2, 2, 40) X(4, 3, 24)
+#endif
 bool refine_split_supported(int config) {
 #define PMVS_SPLIT_CASE(LPc, Gc, CGc) case 200000 + LPc * 10000 + Gc * 1000 + CGc:
   switch (config) {
