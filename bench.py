@@ -72,7 +72,8 @@ def refine_kernel_name(cfg):
 # the refine layouts of the batches >= 10000 candidates and below (pmvs_api.cpp Scene::refine_cfg)
 _RCFG = int(os.environ.get("PMVS_REFINE_LARGE_CONFIG", os.environ.get("PMVS_REFINE_CONFIG", "226014")))
 REFINE_KERNEL = refine_kernel_name(_RCFG)
-SMALL_KERNEL = refine_kernel_name(int(os.environ.get("PMVS_REFINE_CONFIG", "132042")))
+SMALL_KERNEL = refine_kernel_name(int(os.environ.get("PMVS_REFINE_SMALL_CONFIG", os.environ.get("PMVS_REFINE_CONFIG",
+                                                                                                   "132042"))))
 
 
 _T0 = time.time()

@@ -146,11 +146,30 @@ struct BqState {
   BQ_A2(xpt, BQN); BQ_A2(bmat, BQN); BQ_A2(zmat, BQNPTM); BQ_A2(ptsaux, BQN)
 
 // ---------------------------------------------------------------- TRSBOX
-BQ_NI void bq_trsbox(const BQ_AS double (*BQ_RST xpt)[BQN], const BQ_AS double* BQ_RST xopt, const BQ_AS double* BQ_RST gopt,
-                     const BQ_AS double* BQ_RST hq, const BQ_AS double* BQ_RST pq, const BQ_AS double* BQ_RST sl, const BQ_AS double* BQ_RST su,
-                     double delta, BQ_AS double* BQ_RST xnew, BQ_AS double* BQ_RST d, BQ_AS double* BQ_RST gnew, BQ_AS double* BQ_RST dsq_out,
-                     BQ_AS double* BQ_RST crvmin_out) {
+// The small state arrays TRSBOX reads are copied into registers at entry (xopt, hq, pq, sl, su; xpt
+// stays in LDS: with it the routine exceeds 256 registers) and d / gnew are kept there until the
+// exit, so its loops run on registers instead of chains of dependent LDS round trips; the
+// arithmetic is unchanged.
+BQ_NI void bq_trsbox(const BQ_AS double (*BQ_RST xpt)[BQN], const BQ_AS double* BQ_RST xopt_m, const BQ_AS double* BQ_RST gopt,
+                     const BQ_AS double* BQ_RST hq_m, const BQ_AS double* BQ_RST pq_m, const BQ_AS double* BQ_RST sl_m,
+                     const BQ_AS double* BQ_RST su_m, double delta, BQ_AS double* BQ_RST xnew, BQ_AS double* BQ_RST d_m,
+                     BQ_AS double* BQ_RST gnew_m, BQ_AS double* BQ_RST dsq_out, BQ_AS double* BQ_RST crvmin_out) {
   const double half = 0.5, one = 1.0, onemin = -1.0, zero = 0.0;
+#if !defined(BQ_TRSBOX_LDS)
+  double xopt[BQN + 1], hq[BQNH + 1], pq[BQNPT + 1], sl[BQN + 1], su[BQN + 1], d[BQN + 1], gnew[BQN + 1];
+  for (int k = 1; k <= BQNPT; ++k) pq[k] = pq_m[k];
+  for (int i = 1; i <= BQNH; ++i) hq[i] = hq_m[i];
+  for (int i = 1; i <= BQN; ++i) {
+    xopt[i] = xopt_m[i];
+    sl[i] = sl_m[i];
+    su[i] = su_m[i];
+  }
+#define BQ_D_AT(i) bq_get(d, i)
+#else  // (experiment builds) every array in LDS
+  const BQ_AS double *const xopt = xopt_m, *const hq = hq_m, *const pq = pq_m, *const sl = sl_m, *const su = su_m;
+  BQ_AS double *const d = d_m, *const gnew = gnew_m;
+#define BQ_D_AT(i) d[i]
+#endif
   double xbdi[BQN + 1], s[BQN + 1], hs[BQN + 1], hred[BQN + 1];
   int iterc = 0, nact = 0, itermax = 0, itcsav = 0, iact = 0, isav = 0, iu = 0;
   double delsq, qred, crvmin, beta = 0, stepsq = 0, gredsq = 0, resid, ds, shs = 0, temp, blen = 0,
@@ -238,7 +257,10 @@ L50:
   if (iact > 0) {
     ++nact;
     bq_set(xbdi, iact, bq_get(s, iact) < zero ? onemin : one);
-    delsq -= d[iact] * d[iact];
+    {
+      const double di = BQ_D_AT(iact);
+      delsq -= di * di;
+    }
     if (delsq <= zero) goto L90;
     goto L20;
   }
@@ -404,18 +426,30 @@ L150:
     goto L100;
   }
   if (sdec > qred * .01) goto L120;
-L190:
-  *dsq_out = zero;
-  for (int i = 1; i <= BQN; ++i) {
-    xnew[i] = bq_max(bq_min(xopt[i] + d[i], su[i]), sl[i]);
-    if (xbdi[i] == onemin) xnew[i] = sl[i];
-    if (xbdi[i] == one) xnew[i] = su[i];
-    d[i] = xnew[i] - xopt[i];
-    *dsq_out += d[i] * d[i];
+L190: {
+    double dsq = zero;
+    for (int i = 1; i <= BQN; ++i) {
+      double xn = bq_max(bq_min(xopt[i] + d[i], su[i]), sl[i]);
+      if (xbdi[i] == onemin) xn = sl[i];
+      if (xbdi[i] == one) xn = su[i];
+      xnew[i] = xn;
+      d[i] = xn - xopt[i];
+      dsq += d[i] * d[i];
+    }
+    for (int i = 1; i <= BQN; ++i) {
+      d_m[i] = d[i];
+      gnew_m[i] = gnew[i];
+    }
+    *dsq_out = dsq;
+    *crvmin_out = crvmin;
+    return;
   }
-  *crvmin_out = crvmin;
-  return;
 L210: {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(BQ_TRSBOX_LDS)
+    // xpt is read here only: re-read it per product instead of letting the compiler hoist its 21
+    // loads out of the iterations (with them in registers the routine spills)
+    __asm__ volatile("" ::: "memory");
+#endif
     int ih = 0;
     for (int j = 1; j <= BQN; ++j) {
       hs[j] = zero;
@@ -439,6 +473,8 @@ L210: {
     goto L120;
   }
 }
+
+#undef BQ_D_AT
 
 // ---------------------------------------------------------------- ALTMOV
 BQ_NI void bq_altmov(const BQ_AS double (*BQ_RS xpt)[BQN], const BQ_AS double* BQ_RS xopt, const BQ_AS double (*BQ_RS bmat)[BQN],

@@ -498,6 +498,10 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
     const int v = atoi(e);
     if (refine_config_supported(v)) sc->tslots = v;
   }
+  if (const char* e = getenv("PMVS_REFINE_SMALL_CONFIG")) {  // the layout of the batches < small_n only
+    const int v = atoi(e);
+    if (refine_config_supported(v)) sc->tslots_small = v;
+  }
   if (const char* e = getenv("PMVS_REFINE_SMALL_N")) sc->small_n = std::max(0, atoi(e));
   sc->refine_grid = std::max(1, prop.multiProcessorCount) * wpc;
   if (sc->scratch.alloc((size_t)sc->grid * PMVS_MAX_IMAGES * PMVS_MAX_IMAGES) != hipSuccess)
@@ -1133,7 +1137,7 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
     ++launches;
     pending = true;
     const int cfg = sc->refine_cfg(m);
-    pending_small = cfg >= 100000 && cfg < 200000;  // the workgroup form
+    pending_small = m < sc->small_n;  // the small batches (refine_cfg: tslots_small)
     launches_small += pending_small ? 1 : 0;
     return launch_refine(sc->ds, d_in, sc->jobs.p, d_out, m, sc->stats.p, sc->grid, sc->refine_grid, cfg, sc->stream,
                          sc->kev, sc->rhost);

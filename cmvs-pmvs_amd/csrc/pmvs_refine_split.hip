@@ -12,8 +12,9 @@
 namespace pmvsdev {
 
 // Diagnostic build only (-DBQ_PROFILE, libpmvs_amd_prof.so): wave time per role and phase in
-// DevStats::prof -- optimizer: [0] refill, [1] BOBYQA step, [2] publish, [3] waiting for the
-// evaluators; evaluator: [4] setup + gather, [5] normalize, [6] dot + reduction, [7] idle.
+// DevStats::prof -- optimizer: [0] refill, [1] BOBYQA step, [2] publish, [3] waiting for its
+// chunks (its own chunk evaluations excluded); evaluator: [4] setup + gather + normalize, [6] dot +
+// reduction, [7] idle.
 #if defined(BQ_PROFILE)
 #define SP_NOW() __builtin_amdgcn_s_memtime()
 #define SP_MARK(slot)                                      \
@@ -30,23 +31,24 @@ namespace pmvsdev {
 #endif
 
 // ---------------------------------------------------------------- refinePatchBFGS, split form
-// One 512-thread workgroup per CU, its wavefronts in two roles that run concurrently:
-//   * G optimizer wavefronts: wavefront g steps CG chains, one lane each (BqState in LDS), so one
-//     instruction stream of the divergent f64 BOBYQA step serves up to CG chains (the wavefront
-//     form: 6).  After a step the wavefront publishes its chains' objective requests, packed in
-//     chain order into chunks of <= 64 textures, and sleeps until they are evaluated.
-//   * 8 - G evaluator wavefronts: each claims a whole chunk and evaluates it with one LANE PER
-//     TEXTURE, everything in registers: setup, the 49 samples of the texture gathered in sample
-//     order (the channel sums ride along), the second moment, the element-wise normalisation, and
-//     the robust INCC against the request's reference texture, whose normalised samples are read
-//     from the reference's lane (ds_bpermute); the reference's lane then reduces its request as
-//     request_value does.  Every sum keeps the reference's order: results, optimizer
-//     trajectories and counters equal the wavefront form's.
-// While one group's requests are evaluated, the other groups step: the optimizer and the texture
-// work of a CU overlap instead of alternating within each wavefront.  Handshake through LDS: per
-// group, `avail` (chunks not yet claimed: set by the group's atomic exchange after its tables are
-// written, taken by the evaluators' atomic decrements; a stale decrement only drives it below 0) and
-// `done` (chunks evaluated).  No workgroup barrier after the start.
+// One 512-thread workgroup per CU (8 wavefronts, 2 per SIMD), persistent, pulling candidates from
+// the launch's queue.  Its wavefronts have two roles:
+//   * G optimizer wavefronts: wavefront g steps CG chains, one lane each, their BqStates in LDS, so
+//     one instruction stream of the divergent f64 BOBYQA step serves up to CG chains (the wavefront
+//     form serves 6).  After a step it publishes its chains' objective requests, packed in chain
+//     order into chunks of at most 64 / LP textures, then evaluates unclaimed chunks of its own
+//     group until every chunk of the round is done.
+//   * 8 - G evaluator wavefronts: they claim chunks of any group (split_chunk).
+// A chunk is evaluated with LP lanes per texture and everything in registers: the setup, the
+// texture's samples gathered in sample order, normalize's moments and the robust INCC against the
+// request's reference texture (its normalised samples read from the lanes holding them), each
+// sequential sum in the reference's order; the reference texture's lane then reduces the request as
+// request_value does.  Results, optimizer trajectories and counters equal the wavefront form's.
+// While one group's requests are evaluated, the other groups step, so a CU's optimizer and texture
+// work overlap instead of alternating inside each wavefront.  Handshake through LDS: per group,
+// `avail` (chunks not yet claimed: set by the group's atomic exchange after its tables are written,
+// taken by atomic decrements; a stale decrement only drives it below 0) and `done` (chunks
+// evaluated).  No workgroup barrier after the start.  DESIGN.md §5c.
 // Wavefronts per SIMD (register budget) and workgroup size: 2 and 512 (8 wavefronts, 256 VGPRs); an
 // experiment build (SPLIT_WPE=1, SPLIT_THREADS=256) gives 4 wavefronts 512 registers each.
 #ifndef SPLIT_WPE
@@ -56,7 +58,7 @@ namespace pmvsdev {
 #define SPLIT_THREADS_ 512
 #endif
 constexpr int SPLIT_THREADS = SPLIT_THREADS_;
-constexpr int SPLIT_TS = 64;  // texture slots per chunk: one per evaluator lane
+constexpr int SPLIT_TS = 64;  // texture slots per chunk at most (LP = 1)
 
 template <int WS, int G, int CG>
 struct RefSplitLds {
@@ -73,7 +75,7 @@ struct RefSplitLds {
   int nchunk[G];
   int avail[G], done[G];
   int live;                                 // optimizer wavefronts still running
-  int ejvalid[8][SPLIT_TS];                 // evaluator wavefront's per-slot results for the reduction
+  int ejvalid[8][SPLIT_TS];                 // per wavefront: its chunk's per-texture results for the reduction
   float ejres[8][SPLIT_TS];
 };
 
@@ -83,11 +85,17 @@ __device__ __forceinline__ int lds_load_acq(SPLIT_AS int* p) {
 }
 
 // One chunk (group g, chunk k) evaluated by the calling wavefront -- an evaluator, or an optimizer
-// wavefront waiting for its own group -- LP lanes per texture; returns the valid textures its my_f
-// requests counted (request_value) and signals the chunk done.
+// wavefront waiting for its own group.  TS = 64 / LP textures, LP lanes per texture: lane `sub` of a
+// texture holds its samples [sub * K, sub * K + K) (K = ceil(S / LP)) in registers.  Gather, bilinear
+// weights and the element-wise normalisation are per lane; each of normalize's and dot's sequential
+// sums runs in LP stages, lane sub continuing the partial sum of lane sub - 1, so every sum is the
+// reference's single left-to-right chain (optim.cpp:1031-1077).  LP > 1 shortens a chunk, whose
+// instruction count is what the optimizer waits for.  Returns the valid textures its my_f requests
+// counted (request_value) and signals the chunk done.
 template <int WS, int G, int CG, int LP>
-__device__ __noinline__ unsigned long long split_chunk(const DScene& s, SPLIT_AS RefSplitLds<WS, G, CG>& C,
-                                                       RefineJob* __restrict__ jobs, int g, int k, unsigned long long* prof) {
+__device__ __forceinline__ unsigned long long split_chunk_body(const DScene& s, SPLIT_AS RefSplitLds<WS, G, CG>& C,
+                                                               RefineJob* __restrict__ jobs, int g, int k,
+                                                               unsigned long long* prof) {
   constexpr int S = WS * WS;
   constexpr int K = (S + LP - 1) / LP;
   constexpr int NB = 7;  // samples whose texel loads are in flight together
@@ -217,10 +225,11 @@ __device__ __noinline__ unsigned long long split_chunk(const DScene& s, SPLIT_AS
   const int rt = mine ? t - idx : t;  // the request's reference texture (index 0)
   const int src = rt * LP + sub;
   const int refok = __shfl(T.ok, src);
+  float ans = 0.0f;
+#if !defined(SPLIT_DOT_STREAM)  // the reference texture's samples pulled at once (A/B r05m: equal)
   float px[K], py[K], pz[K];
 #pragma unroll
   for (int q = 0; q < K; ++q) { px[q] = __shfl(X[q], src); py[q] = __shfl(Y[q], src); pz[q] = __shfl(Z[q], src); }
-  float ans = 0.0f;
 #pragma unroll
   for (int j = 0; j < LP; ++j) {
     if (ok && sub == j) {
@@ -237,6 +246,29 @@ __device__ __noinline__ unsigned long long split_chunk(const DScene& s, SPLIT_AS
       if (sub == j + 1) ans = u;
     }
   }
+#else
+#pragma unroll
+  for (int j = 0; j < LP; ++j) {
+    // stage j: the lanes with sub == j, whose reference lanes (same sub) are active with them, read the
+    // reference samples one at a time (no K-wide copy of them in registers)
+    if (sub == j) {
+#pragma unroll
+      for (int q = 0; q < K; ++q)
+        if (q < kn) {
+          const float px = __shfl(X[q], src), py = __shfl(Y[q], src), pz = __shfl(Z[q], src);
+          if (ok) {
+            ans += px * X[q];
+            ans += py * Y[q];
+            ans += pz * Z[q];
+          }
+        }
+    }
+    if (j + 1 < LP) {
+      const float u = __shfl_up(ans, 1);
+      if (sub == j + 1) ans = u;
+    }
+  }
+#endif
   if (mine && sub == LP - 1) {
     float jr = 0.0f;
     if (idx >= 1 && refok && ok) jr = robustincc((float)(1.0 - (double)__fdiv_rn(ans, (float)(3 * S))));
@@ -259,9 +291,17 @@ __device__ __noinline__ unsigned long long split_chunk(const DScene& s, SPLIT_AS
   if (lane == 0) __hip_atomic_fetch_add(&C.done[g], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   return tex_valid;
 }
+// Out of line for the optimizer wavefronts (inlined there, the chunk's registers and the optimizer's
+// spilled); the call saves and restores the callee-saved registers the chunk uses (78 per lane at
+// LP = 2), so the evaluators inline the body instead.
+template <int WS, int G, int CG, int LP>
+__device__ __noinline__ unsigned long long split_chunk(const DScene& s, SPLIT_AS RefSplitLds<WS, G, CG>& C,
+                                                       RefineJob* __restrict__ jobs, int g, int k, unsigned long long* prof) {
+  return split_chunk_body<WS, G, CG, LP>(s, C, jobs, g, k, prof);
+}
 
-// The two roles as separate functions, so that each gets its own register allocation (inlined
-// into one body, the evaluator's 147 sample registers and the optimizer's call sites spilled).
+// The roles and the chunk as separate functions, so that each gets its own register allocation
+// (inlined into one body, the chunk's sample registers and the optimizer's call sites spilled).
 template <int WS, int G, int CG, int LP>
 __device__ __noinline__ void split_optimizer(const DScene& s, SPLIT_AS RefSplitLds<WS, G, CG>& C, RefineJob* __restrict__ jobs,
                                              int n, int nc_active, DevStats* st) {
@@ -433,12 +473,7 @@ __device__ __noinline__ void split_optimizer(const DScene& s, SPLIT_AS RefSplitL
   }
 }
 
-// An evaluator wavefront takes chunks of TS = 64 / LP textures, LP lanes per texture: lane `sub` of
-// a texture holds its samples [sub * K, sub * K + K) (K = ceil(S / LP)) in registers.  Gather, the
-// bilinear weights and the element-wise normalisation are per lane.  Each of normalize's and dot's
-// sequential sums runs in LP stages, lane sub continuing the partial sum of lane sub - 1, so every
-// sum is the reference's single left-to-right chain (optim.cpp:1031-1077).  LP > 1 shortens a
-// chunk: its instruction count is what the optimizer wavefront waits for.
+// An evaluator wavefront: claims chunks of any group, groups scanned from a per-wavefront start.
 template <int WS, int G, int CG, int LP>
 __device__ __noinline__ void split_evaluator(const DScene& s, SPLIT_AS RefSplitLds<WS, G, CG>& C, RefineJob* __restrict__ jobs,
                                              DevStats* st) {
@@ -469,7 +504,11 @@ __device__ __noinline__ void split_evaluator(const DScene& s, SPLIT_AS RefSplitL
       continue;
     }
     SP_MARK(7);
+#if defined(SPLIT_EVAL_CALL)
     tex_valid += split_chunk<WS, G, CG, LP>(s, C, jobs, g, k, prof);
+#else
+    tex_valid += split_chunk_body<WS, G, CG, LP>(s, C, jobs, g, k, prof);
+#endif
     tprev = SP_NOW();
     grabs += C.choff[g][k + 1] - C.choff[g][k];
     chunks++;

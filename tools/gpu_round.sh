@@ -16,8 +16,8 @@
 #                                           default bench line and a kernel trace of one C3 step
 #   bash tools/gpu_round.sh c5 <tag>        the C5 test alone, allocation failures traced
 #                                           (PMVS_TRACE_ERRORS)
-#   bash tools/gpu_round.sh sq <tag>        two SQ counter passes (issue, waits, instruction mix) over one
-#                                           C3 iteration, kernel-trace only, one rocprofv3 run each
+#   bash tools/gpu_round.sh sq <tag>        three SQ counter passes (issue, waits, instruction mix, active
+#                                           lanes per VALU instruction) over one C3 iteration, one run each
 set -o pipefail
 WHAT=${1:-test}; TAG=${2:-r01}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -63,8 +63,11 @@ elif [ "$WHAT" = sq ]; then
     --output-format csv -d $O/sq_a -o run -- python3 $B > $O/sq_a.log 2>&1 && \
   timeout -s KILL 240 rocprofv3 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE \
     --output-format csv -d $O/sq_b -o run -- python3 $B > $O/sq_b.log 2>&1 && \
+  timeout -s KILL 240 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU SQ_WAVES \
+    --output-format csv -d $O/sq_c -o run -- python3 $B > $O/sq_c.log 2>&1 && \
   python3 $R/tools/pmc_summary.py $O/sq_a > $O/sq_a.json && python3 $R/tools/pmc_summary.py $O/sq_b > $O/sq_b.json && \
-  rm -rf $O/sq_a $O/sq_b  # per-dispatch CSVs: far above what gpurun copies back
+  python3 $R/tools/pmc_summary.py $O/sq_c > $O/sq_c.json && \
+  rm -rf $O/sq_a $O/sq_b $O/sq_c  # per-dispatch CSVs: far above what gpurun copies back
 elif [ "$WHAT" = kt ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-c2 > $O/kt.log 2>&1
 else
