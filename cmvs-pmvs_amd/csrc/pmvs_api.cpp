@@ -202,6 +202,7 @@ struct pmvs_scene {
   ExpandBuffers xbuf;
   DBuf<pmvs_patch> fpatches;
   DBuf<int> fkeep;
+  DBuf<unsigned long long> digest;  // pmvs_loop_hash
   int grid = 0, refine_grid = 0, tslots = 226014;
   // batches below small_n candidates run the workgroup form spread over every CU (tslots_small):
   // their length is one chain's latency, not the chip's throughput
@@ -243,7 +244,7 @@ struct pmvs_scene {
   ~pmvs_scene() {
     cl_shared.release(); cl_ids.release(); cl_id2idx.release();
     fpatches2.release(); views.release(); pyr.release(); masks.release(); edges.release(); vis_off.release(); vis.release();
-    bindexes.release(); scratch.release(); stats.release(); jobs.release(); fpatches.release(); fkeep.release(); cand.release(); res.release(); evq.release();
+    bindexes.release(); scratch.release(); stats.release(); jobs.release(); fpatches.release(); fkeep.release(); digest.release(); cand.release(); res.release(); evq.release();
     evout.release(); tq.release(); tout.release(); tvalid.release();
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -1406,6 +1407,21 @@ pmvs_status pmvs_loop_fetch(pmvs_scene* sc, pmvs_patch* out, int32_t n) {
     HIPCHK(hipMemcpy(out, sc->fpatches.p, (size_t)n * sizeof(pmvs_patch), hipMemcpyDeviceToHost));
   }
   sc->lkept = -1;
+  return PMVS_OK;
+}
+
+pmvs_status pmvs_loop_hash(pmvs_scene* sc, uint64_t* hash) {
+  if (!sc || !hash) return fail(PMVS_EINVAL, "invalid argument");
+  if (sc->lkept < 0) return fail(PMVS_EINVAL, "loop_hash: no loop result on the device");
+  HIPCHK(hipSetDevice(sc->device));
+  if (ensure(sc->digest, 1)) return fail(PMVS_ENOMEM, "digest");
+  HIPCHK(hipMemsetAsync(sc->digest.p, 0, sizeof(unsigned long long), sc->stream));
+  static_assert(sizeof(pmvs_patch) % 4 == 0, "record words");
+  HIPCHK(launch_model_digest(sc->fpatches.p, sc->lkept, (int)sizeof(pmvs_patch), sc->digest.p, sc->stream));
+  unsigned long long h = 0;
+  HIPCHK(hipMemcpyAsync(&h, sc->digest.p, sizeof(h), hipMemcpyDeviceToHost, sc->stream));
+  HIPCHK(hipStreamSynchronize(sc->stream));
+  *hash = h ^ (unsigned long long)sc->lkept;
   return PMVS_OK;
 }
 

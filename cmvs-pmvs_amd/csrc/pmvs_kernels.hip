@@ -2066,6 +2066,44 @@ hipError_t launch_patch_colors(const DScene& s, int n, const float* coords, cons
 }
 }  // namespace pmvsdev
 
+// ==================================================================== model digest
+namespace pmvsdev {
+// pmvs_loop_hash: one wavefront per record at a time (grid-stride), its words read coalesced, each
+// word mixed with its position and the record's index (splitmix64 finaliser); the per-lane sums
+// and then every wavefront's sum are added (u64 addition: exact and order-free, so the digest does
+// not depend on the schedule).
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(64) void model_digest_kernel(const uint32_t* __restrict__ recs, int n, int words,
+                                                          unsigned long long* out) {
+  const int lane = threadIdx.x;
+  unsigned long long acc = 0;
+  for (long long r = blockIdx.x; r < n; r += gridDim.x) {
+    const uint32_t* p = recs + r * words;
+    for (int w = lane; w < words; w += 64)
+      acc += mix64((unsigned long long)p[w] ^ ((unsigned long long)w << 32) ^ ((unsigned long long)r * 0x9e3779b97f4a7c15ull));
+  }
+  for (int d = 32; d >= 1; d >>= 1) acc += __shfl_xor(acc, d);
+  if (lane == 0) atomicAdd(out, acc);
+}
+
+hipError_t launch_model_digest(const void* recs, int n, int record_bytes, unsigned long long* d_out, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  int dev = 0, cus = 0;
+  hipError_t e;
+  if ((e = hipGetDevice(&dev)) != hipSuccess ||
+      (e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
+    return e;
+  const int grid = std::min(n, std::max(1, cus) * 32);
+  hipLaunchKernelGGL(model_digest_kernel, dim3(grid), dim3(64), 0, stream, static_cast<const uint32_t*>(recs), n,
+                     record_bytes / 4, d_out);
+  return hipGetLastError();
+}
+}  // namespace pmvsdev
+
 // ==================================================================== device math self-test
 // Evaluates the device implementations of the libm functions the hot path uses, so tests can
 // measure their agreement with the host libm (glibc) that the reference runs on.

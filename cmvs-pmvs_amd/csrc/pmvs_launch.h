@@ -54,6 +54,7 @@ hipError_t launch_unpack_rgba(const uint32_t* d_in, uint8_t* d_rgb, long long np
 hipError_t launch_math_selftest(int op, const double* d_in, double* d_out, int n, hipStream_t stream);
 hipError_t launch_bobyqa_selftest(int mode, int kind, const double* d_x0, int n, int maxeval, double* d_out,
                                   hipStream_t stream);
+hipError_t launch_model_digest(const void* recs, int n, int record_bytes, unsigned long long* d_out, hipStream_t stream);
 hipError_t launch_patch_colors(const DScene& s, int n, const float* coords, const int* off, const int* images, int* out,
                                hipStream_t stream);
 

@@ -143,7 +143,7 @@ EXPORTS = ["pmvs_last_error", "pmvs_device_count", "pmvs_scene_create", "pmvs_sc
            "pmvs_synth_candidates", "pmvs_selftest_math", "pmvs_selftest_bobyqa", "pmvs_camera_load",
            "pmvs_ppm_load", "pmvs_options_load", "pmvs_options_free", "pmvs_write_patches", "pmvs_write_pset",
            "pmvs_write_ply", "pmvs_patch_colors", "pmvs_filter_run",
-           "pmvs_expand_run", "pmvs_expand_fetch", "pmvs_run_loop", "pmvs_loop_fetch", "pmvs_scene_set_shard", "pmvs_scene_set_shard_rccl", "pmvs_scene_set_cluster",
+           "pmvs_expand_run", "pmvs_expand_fetch", "pmvs_run_loop", "pmvs_loop_fetch", "pmvs_loop_hash", "pmvs_scene_set_shard", "pmvs_scene_set_shard_rccl", "pmvs_scene_set_cluster",
            "pmvs_scene_set_cluster_rccl", "pmvs_rccl_unique_id",
            "pmvs_rccl_create", "pmvs_rccl_destroy", "pmvs_rccl_allgather", "pmvs_rccl_allgather_device",
            "pmvs_tcp_create", "pmvs_tcp_allgather", "pmvs_tcp_destroy", "pmvs_thread_exchange_create",
@@ -208,6 +208,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.pmvs_run_loop.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_float, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                   C.c_int32, C.POINTER(C.c_int32), C.c_void_p]
     lib.pmvs_loop_fetch.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+    lib.pmvs_loop_hash.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     lib.pmvs_scene_set_shard.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
     lib.pmvs_scene_set_cluster.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.pmvs_scene_set_cluster_rccl.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
@@ -475,7 +476,8 @@ class Scene:
         _check(self.lib.pmvs_scene_set_cluster(self.handle, rank, world, _ptr(ids), ptr, ctx))
 
     def run_loop(self, seeds: np.ndarray, threshold: float, iterations: int = 3, wave: int = 4096, cap=None,
-                 after_seeds: bool = True, native: bool = True, min_candidates: int = 0, max_waves: int = 0):
+                 after_seeds: bool = True, native: bool = True, min_candidates: int = 0, max_waves: int = 0,
+                 fetch: bool = True):
         """CFindMatch::run after the seed phase (findMatch.cpp:196-217): depth 1, then `iterations` x
         (CExpand::run, CFilter::run, updateThreshold, ++depth).  Thresholds follow the reference's
         float arithmetic: before = threshold - 0.3f (findMatch.cpp:104), -= 0.05f per iteration and
@@ -483,7 +485,8 @@ class Scene:
         library with the model resident in HBM (pmvs_run_loop); native=False composes expand_run
         and filter_run through host memory (same result).  max_waves > 0 bounds every iteration's
         expansion to that many waves (PMVS_EXPAND_MAX_WAVES: bounded full-size parity samples).
-        Returns (patches, per-iteration stats)."""
+        Returns (patches, per-iteration stats).  fetch=False (native only) leaves the result on the
+        device and returns (its size, stats): loop_hash() / loop_fetch(n) then read it."""
         model = np.ascontiguousarray(seeds, PATCH_DTYPE)
         if native:
             iters = (LoopIter * max(1, iterations))()
@@ -492,9 +495,10 @@ class Scene:
                                           iterations, wave, min_candidates,
                                           (1 if after_seeds else 0) | (int(max_waves) << 8), int(cap or (1 << 30)),
                                           C.byref(n_out), iters))
-            out = np.empty(n_out.value, PATCH_DTYPE)
-            _check(self.lib.pmvs_loop_fetch(self.handle, _ptr(out), n_out.value))
-            return out, [iters[t].as_dict() for t in range(iterations)]
+            log = [iters[t].as_dict() for t in range(iterations)]
+            if not fetch:
+                return n_out.value, log
+            return self.loop_fetch(n_out.value), log
         ncc = np.float32(threshold)
         before = np.float32(ncc - np.float32(0.3))
         cthr, depth = 4, 1
@@ -512,6 +516,18 @@ class Scene:
             cthr = 2
             depth += 1
         return model, log
+
+    def loop_fetch(self, n: int) -> np.ndarray:
+        """pmvs_loop_fetch: the n-patch result of the last run_loop(fetch=False), device to host."""
+        out = np.empty(n, PATCH_DTYPE)
+        _check(self.lib.pmvs_loop_fetch(self.handle, _ptr(out), n))
+        return out
+
+    def loop_hash(self) -> int:
+        """pmvs_loop_hash: 64-bit digest of the last run_loop result still on the device."""
+        h = C.c_uint64(0)
+        _check(self.lib.pmvs_loop_hash(self.handle, C.byref(h)))
+        return int(h.value)
 
     def patch_colors(self, coords: np.ndarray, images) -> np.ndarray:
         """writePLY colour mode 0 for patches (coords [n,4], images: list of view-index lists)."""

@@ -328,6 +328,10 @@ typedef struct pmvs_loop_iter {
 pmvs_status pmvs_run_loop(pmvs_scene* scene, const pmvs_patch* seeds, int32_t n, float threshold, int32_t iterations,
                           int32_t wave, int32_t min_candidates, int32_t flags, int32_t cap, int32_t* n_out, pmvs_loop_iter* iters);
 pmvs_status pmvs_loop_fetch(pmvs_scene* scene, pmvs_patch* out, int32_t n);
+/* (new) A 64-bit digest of pmvs_run_loop's result while it is still on the device (no PCIe
+ * transfer): every record's bytes mixed with its position, so equal models give equal digests
+ * (identical-repetition checks of a device-resident pipeline).  pmvs_loop_fetch still works after it. */
+pmvs_status pmvs_loop_hash(pmvs_scene* scene, uint64_t* hash);
 
 /* The seed phase, PMVS3::CSeed::init + run (seed.cpp:11-107) at CPU 1: target images in the
  * reference's std::shuffle(mt19937(42)) order, cells in raster order, the feature points of every
