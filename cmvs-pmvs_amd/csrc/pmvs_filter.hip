@@ -3055,6 +3055,66 @@ __global__ void collect_flags_kernel(pmvs_patch* __restrict__ P, const int* __re
   foreign[i] = (q.fix == PMVS_FIX_FOREIGN);  // another cluster's boundary patch: never expanded here
 }
 
+// The initial queue run in key order (pmvs_queue.h QItem / qkey), built on the device from the
+// device-sorted _tmp keys: item j of the sorted order is {qkey(tmp, collect rank), patch index},
+// kept unless the patch is another cluster's boundary patch; keep flags first, then the scatter to
+// the kept items' positions (an exclusive scan of the flags).
+struct DQItem {  // pmvs_queue.h QItem's layout
+  unsigned long long key;
+  int p, pad;
+};
+__device__ __forceinline__ unsigned long long dqkey(float tmp, long long seq) {
+  unsigned u = __float_as_uint(tmp == 0.0f ? 0.0f : tmp);
+  u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((unsigned long long)u << 32) | (0xffffffffull - (unsigned long long)seq);
+}
+__global__ void queue_keep_kernel(const int* __restrict__ srank, const int* __restrict__ foreign, int n,
+                                  int* __restrict__ keep) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) keep[j] = foreign[srank[j]] ? 0 : 1;
+}
+__global__ void queue_items_kernel(const float* __restrict__ tmp_sorted, const int* __restrict__ srank,
+                                   const int* __restrict__ order, const int* __restrict__ keep,
+                                   const int* __restrict__ pos, int n, DQItem* __restrict__ items) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n || !keep[j]) return;
+  const int r = srank[j];
+  DQItem q;
+  q.key = dqkey(tmp_sorted[j], r);
+  q.p = order[r];
+  q.pad = 0;
+  items[pos[j]] = q;
+}
+
+// The survivors of a wave's preparation (status 0) in (parent, direction) order, on the device:
+// surv_flags_kernel flags them and counts the prepared candidates (status >= 0, one atomic per
+// block); after an exclusive scan of the flags, surv_scatter_kernel writes slots[pos] = k and
+// slot2[k] = pos (-1 for the others).
+__global__ __launch_bounds__(256) void surv_flags_kernel(const int* __restrict__ status, int nk, int* __restrict__ flag,
+                                                         int* __restrict__ nprep) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  const int v = k < nk ? status[k] : -1;
+  if (k < nk) flag[k] = (v == 0) ? 1 : 0;
+  const unsigned long long b = __ballot(v >= 0);
+  __shared__ int cnt;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&cnt, __popcll(b));
+  __syncthreads();
+  if (threadIdx.x == 0 && cnt) atomicAdd(nprep, cnt);
+}
+__global__ void surv_scatter_kernel(const int* __restrict__ flag, const int* __restrict__ pos, int nk,
+                                    int* __restrict__ slots, int* __restrict__ slot2) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nk) return;
+  if (flag[k]) {
+    slots[pos[k]] = k;
+    slot2[k] = pos[k];
+  } else {
+    slot2[k] = -1;
+  }
+}
+
 // Compact per-candidate record the host commit reads (instead of two full patch records):
 // [status, tmp bits, nprep, nimg, nvis | prep cells[64] | image cells[64] | vimage cells[64]],
 // cells as global target-cell indexes.  prep cells: the in-grid target entries of the prepared
@@ -3179,7 +3239,7 @@ void delete_commit_work(CommitWork* w);  // after CommitWork's definition
 ExpandBuffers::~ExpandBuffers() {
   void* ps[] = {parents, cand_coord, cand_ok, cand, prep, status, slots, cand2, prep2, res, outp, ostatus, counts, alive,
                 pg_head, vp_head, d_item, d_next, pool_used, tcells, tvals, qtmp, crec, acc, dupd, cellinit, occ,
-                qkey, qrank, qrank2, qsort_tmp, xsd, xrd, cidx};
+                qkey, qrank, qrank2, qsort_tmp, xsd, xrd, cidx, qkeep, qpos, qitems, sflag, spos, slot2};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete_commit_work(cm);
@@ -3531,7 +3591,7 @@ struct CommitOut {
 // One wave's commit on the device (see CommitWork).  slot2h[k]: survivor slot of candidate k
 // (status[k] == 0).  Writes X.acc = [slot of accepted q | pool0 + entry offset], applies the
 // failed-direction bits to _dflag (apply_dflag) or returns them (wave = 1: one parent).
-static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t st, int np, const std::vector<int>& slot2h,
+static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t st, int np, const int* d_slot2,
                                 int cthr, bool check, int first, long long pool0, bool apply_dflag, pmvs_patch* dP,
                                 CommitOut& out) {
   if (!X.cm) X.cm = new CommitWork();
@@ -3545,7 +3605,7 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
     W.cap_k = c;
   }
   if (!W.ctr) FCHK(cm_grow(W.ctr, 9 + 2 * kSerialCommit));
-  FCHK(h2d_async(X.h2d, W.slot2, slot2h.data(), (size_t)nk * sizeof(int), st));
+  FCHK(hipMemcpyAsync(W.slot2, d_slot2, (size_t)nk * sizeof(int), hipMemcpyDeviceToDevice, st));
   if (nk <= kSerialCommit) {
     FCHK(grow(X.acc, X.cap_acc, 2 * (size_t)nk));
     hipLaunchKernelGGL(cm_serial_kernel, dim3(1), dim3(64), 0, st, s, X.status, W.slot2, X.crec, nk, np, X.counts, X.occ,
@@ -3755,11 +3815,6 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   // pgrids holds a patch, per target cell; the host keeps only the queue
   // The collected patches enter the queue in collect order (seq = collect rank); their max-_tmp
   // order (QCmp: _tmp descending, ties by seq) is a stable descending radix sort on the device.
-  FCHK(X.pin.ensure(4 * (size_t)std::max(1, c.nalive) * sizeof(int)));
-  int* order = X.pin.as<int>();
-  int* srank = order + c.nalive;
-  float* qtmp = reinterpret_cast<float*>(srank + c.nalive);
-  int* qforeign = reinterpret_cast<int*>(qtmp + c.nalive);  // by collect rank
   const size_t na1 = (size_t)std::max(1, c.nalive);
   FCHK(grow(X.qtmp, X.cap_qtmp, na1));
   FCHK(grow(X.qkey, X.cap_qkey, na1));
@@ -3783,21 +3838,38 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
                                                       st));
   }
   hipLaunchKernelGGL(occ_init_kernel, dim3(nblk(ncells)), dim3(256), 0, st, B.pg_off, ncells, X.occ);
+  // the initial run built on the device (queue_items_kernel) and read as QItems: collectPatches(queue)
+  // without other clusters' boundary patches, in key order
+  int ninit = 0;
   if (c.nalive) {
-    FCHK(hipMemcpyAsync(order, B.order, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
-    FCHK(hipMemcpyAsync(qtmp, X.qkey, c.nalive * sizeof(float), hipMemcpyDeviceToHost, st));
-    FCHK(hipMemcpyAsync(srank, X.qrank2, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
-    FCHK(hipMemcpyAsync(qforeign, B.need, c.nalive * sizeof(int), hipMemcpyDeviceToHost, st));
+    static_assert(sizeof(DQItem) == sizeof(QItem), "QItem layout");
+    FCHK(grow(X.qkeep, X.cap_qkeep, na1 + 1));
+    FCHK(grow(X.qpos, X.cap_qpos, na1 + 1));
+    FCHK(grow(X.qitems, X.cap_qitems, na1 * sizeof(DQItem)));
+    hipLaunchKernelGGL(queue_keep_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, X.qrank2, B.need, c.nalive, X.qkeep);
+    size_t tb = 0;
+    FCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, X.qkeep, X.qpos, c.nalive + 1, st));
+    if (tb > X.cap_qsort) {
+      if (X.qsort_tmp) FCHK(hipFree(X.qsort_tmp));
+      X.qsort_tmp = nullptr;
+      X.cap_qsort = 0;
+      FCHK(hipMalloc(&X.qsort_tmp, tb));
+      X.cap_qsort = tb;
+    }
+    FCHK(hipMemsetAsync(X.qkeep + c.nalive, 0, sizeof(int), st));
+    tb = X.cap_qsort;
+    FCHK(hipcub::DeviceScan::ExclusiveSum(X.qsort_tmp, tb, X.qkeep, X.qpos, c.nalive + 1, st));
+    hipLaunchKernelGGL(queue_items_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, X.qkey, X.qrank2, B.order, X.qkeep,
+                       X.qpos, c.nalive, reinterpret_cast<DQItem*>(X.qitems));
+    FCHK(read_int(X.qpos + c.nalive, &ninit, st));
   }
   FCHK(grow(X.counts, X.cap_cnt, (size_t)ncells));
   FCHK(memset_big(X.counts, 0, ncells, st));
-  FCHK(hipStreamSynchronize(st));
   // The max-_tmp queue (P_compare; ties: earlier push first): the collected patches as a sorted
   // run, the patches pushed during the run in a heap, popped by merging the two.
-  std::vector<QItem> initial;
-  initial.reserve(c.nalive);
-  for (int j = 0; j < c.nalive; ++j)  // collectPatches(queue) without other clusters' boundary patches
-    if (!qforeign[srank[j]]) initial.push_back({qkey(qtmp[j], srank[j]), order[srank[j]]});
+  std::vector<QItem> initial(ninit);
+  if (ninit) FCHK(hipMemcpyAsync(initial.data(), X.qitems, (size_t)ninit * sizeof(QItem), hipMemcpyDeviceToHost, st));
+  FCHK(hipStreamSynchronize(st));
   RunQueue queue;
   queue.add_run(std::move(initial));
   std::vector<QItem> wave_run, sort_tmp;
@@ -3947,31 +4019,44 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
       hipLaunchKernelGGL(prepare_kernel, dim3(nblk((long long)np * 6)), dim3(256), 0, st, s, c.dev(), X.counts, X.parents,
                          np, X.cand_coord, X.cand_ok, X.cand, X.prep, X.status, cthr, only, X.cidx);
       FCHK(hipPeekAtLastError());
-      std::vector<int> status((size_t)np * 6);
-      FCHK(d2h_sync(st, {{status.data(), X.status, (size_t)np * 6 * sizeof(int)}}));
-      T.mark(3);
-      std::vector<int> slots, slot2surv((size_t)np * 6, -1);
-      for (int k = 0; k < np * 6; ++k) {
-        if (status[k] >= 0) stats[1]++;
-        if (status[k] == 0) {
-          slot2surv[k] = (int)slots.size();
-          slots.push_back(k);
+      // the survivors compacted on the device (surv_*_kernel): slots, slot2 (candidate -> survivor)
+      const int nk = np * 6;
+      FCHK(grow(X.sflag, X.cap_sflag, (size_t)nk + 2));  // [nk]: 0 for the scan, [nk + 1]: prepared count
+      FCHK(grow(X.spos, X.cap_spos, (size_t)nk + 1));
+      FCHK(grow(X.slot2, X.cap_slot2, (size_t)nk));
+      FCHK(grow(X.slots, X.cap_slots, (size_t)nk));
+      FCHK(hipMemsetAsync(X.sflag + nk, 0, 2 * sizeof(int), st));
+      hipLaunchKernelGGL(surv_flags_kernel, dim3(nblk(nk)), dim3(256), 0, st, X.status, nk, X.sflag, X.sflag + nk + 1);
+      {
+        size_t tb = 0;
+        FCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, X.sflag, X.spos, nk + 1, st));
+        if (tb > X.cap_qsort) {
+          if (X.qsort_tmp) FCHK(hipFree(X.qsort_tmp));
+          X.qsort_tmp = nullptr;
+          X.cap_qsort = 0;
+          FCHK(hipMalloc(&X.qsort_tmp, tb));
+          X.cap_qsort = tb;
         }
+        tb = X.cap_qsort;
+        FCHK(hipcub::DeviceScan::ExclusiveSum(X.qsort_tmp, tb, X.sflag, X.spos, nk + 1, st));
       }
-      const int m = (int)slots.size();
+      hipLaunchKernelGGL(surv_scatter_kernel, dim3(nblk(nk)), dim3(256), 0, st, X.sflag, X.spos, nk, X.slots, X.slot2);
+      int sv[2] = {0, 0};
+      FCHK(d2h_sync(st, {{&sv[0], X.spos + nk, sizeof(int)}, {&sv[1], X.sflag + nk + 1, sizeof(int)}}));
+      stats[1] += sv[1];
+      T.mark(3);
+      const int m = sv[0];
       // this rank's contiguous share of the survivors
       const int chunk = (m + G - 1) / G;
       const int lo = std::min(m, R * chunk), hi = std::min(m, lo + chunk), mine = hi - lo;
       int ovf = 0;
       auto local = [&]() -> hipError_t {
         if (m > 0) {
-          FCHK(grow(X.slots, X.cap_slots, (size_t)m));
           FCHK(grow(X.cand2, X.cap_cand2, (size_t)m));
           FCHK(grow(X.prep2, X.cap_prep2, (size_t)m));
           FCHK(grow(X.res, X.cap_res, (size_t)m));
           FCHK(grow(X.outp, X.cap_outp, (size_t)m));
           FCHK(grow(X.ostatus, X.cap_ost, (size_t)m));
-          FCHK(h2d_async(X.h2d, X.slots, slots.data(), m * sizeof(int), st));
           hipLaunchKernelGGL(gather_slots_kernel, dim3(nblk(m)), dim3(256), 0, st, X.slots, m, X.cand, X.prep, X.cand2, X.prep2,
                              X.cidx);
           if (mine > 0) {
@@ -4051,7 +4136,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
       T.mark(6);
       // ---- commit in (parent priority, direction) order, on the device (device_commit)
       const int first = nmodel;
-      FCHK(device_commit(s, X, st, np, slot2surv, cthr, only < 0, first, (long long)X.pool_host, W > 1, dP, co));
+      FCHK(device_commit(s, X, st, np, X.slot2, cthr, only < 0, first, (long long)X.pool_host, W > 1, dP, co));
       for (int q = 0; q < 4; ++q) stats[2 + q] += co.fail[q];
       if (W == 1) pbits |= co.pbits;
       const int added = co.nacc;

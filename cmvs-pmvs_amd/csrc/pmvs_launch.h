@@ -154,7 +154,7 @@ struct H2DStage {
 };
 struct ExpandBuffers {
   CommitWork* cm = nullptr;
-  PinnedBuf pin;  // host staging of the initial queue (order, sorted keys and ranks)
+  // (the initial queue run is built on the device: qkeep / qpos / qitems)
   H2DStage h2d;
   unsigned char* occ = nullptr;  // per target cell: pgrids holds a patch (device commit)
   size_t cap_occ = 0;
@@ -171,6 +171,11 @@ struct ExpandBuffers {
   float* qtmp = nullptr;        // _tmp of the collected patches (queue)
   float* qkey = nullptr;        // the initial queue sorted on the device: keys, collect ranks, temp
   int *qrank = nullptr, *qrank2 = nullptr;
+  int *qkeep = nullptr, *qpos = nullptr;  // the initial run built on the device (queue_items_kernel)
+  int *sflag = nullptr, *spos = nullptr, *slot2 = nullptr;  // survivor compaction (surv_*_kernel)
+  size_t cap_sflag = 0, cap_spos = 0, cap_slot2 = 0;
+  char* qitems = nullptr;
+  size_t cap_qkeep = 0, cap_qpos = 0, cap_qitems = 0;
   void* qsort_tmp = nullptr;
   size_t cap_qkey = 0, cap_qrank = 0, cap_qrank2 = 0, cap_qsort = 0;
   char *xsd = nullptr, *xrd = nullptr;  // device payload of the sharded exchange (send, all ranks)
