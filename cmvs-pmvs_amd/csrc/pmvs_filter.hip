@@ -3349,7 +3349,7 @@ __global__ void cm_head_kernel(const unsigned long long* __restrict__ keys, cons
 
 // segid = inclusive scan of head - 1; seghead[segment] = its first position, seghead[nseg] = na
 __global__ void cm_seg_kernel(const int* __restrict__ head, int* __restrict__ segid, int na, int* __restrict__ seghead,
-                              int* __restrict__ segptr) {
+                              int* __restrict__ segptr, int* __restrict__ nseg) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= na) return;
   const int s = segid[p] - 1;
@@ -3358,14 +3358,17 @@ __global__ void cm_seg_kernel(const int* __restrict__ head, int* __restrict__ se
     seghead[s] = p;
     segptr[s] = p;
   }
-  if (p == na - 1) seghead[s + 1] = na;
+  if (p == na - 1) {
+    seghead[s + 1] = na;
+    *nseg = s + 1;
+  }
 }
 
 __global__ void cm_first_kernel(const unsigned long long* __restrict__ keys, const unsigned char* __restrict__ dec,
-                                const int* __restrict__ seghead, int nseg, int* __restrict__ segptr,
+                                const int* __restrict__ seghead, const int* __restrict__ nsegp, int* __restrict__ segptr,
                                 int* __restrict__ segfirst) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nseg) return;
+  if (s >= *nsegp) return;
   int p = segptr[s];
   const int end = seghead[s + 1];
   while (p < end && dec[(int)(keys[p] & 0xffffffffull)]) ++p;
@@ -3473,11 +3476,12 @@ __global__ void cm_accept_scan_kernel(const int* __restrict__ flag, int nk, int*
 
 __global__ void cm_write_kernel(const int* __restrict__ flag, int nk, const int* __restrict__ qa, const int* __restrict__ qb,
                                 const int* __restrict__ qc, const int* __restrict__ slot2, const int* __restrict__ rec,
-                                int nacc, int pool0, int first, int* __restrict__ acc, int2* __restrict__ push) {
+                                int pool0, int first, int* __restrict__ acc, int2* __restrict__ push) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nk) return;
   const int f = flag[k];
   if (!(f & 1)) return;
+  const int nacc = qa[nk];  // accepted candidates: the end of the exclusive scan
   const int q = qa[k];
   acc[q] = slot2[k];
   acc[nacc + q] = pool0 + qc[k];
@@ -3591,7 +3595,8 @@ struct CommitOut {
 // One wave's commit on the device (see CommitWork).  slot2h[k]: survivor slot of candidate k
 // (status[k] == 0).  Writes X.acc = [slot of accepted q | pool0 + entry offset], applies the
 // failed-direction bits to _dflag (apply_dflag) or returns them (wave = 1: one parent).
-static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t st, int np, const int* d_slot2,
+static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t st, int np, const int* d_slot2, int m,
+                                const int* d_ovf, int* ovf,
                                 int cthr, bool check, int first, long long pool0, bool apply_dflag, pmvs_patch* dP,
                                 CommitOut& out) {
   if (!X.cm) X.cm = new CommitWork();
@@ -3599,19 +3604,21 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
   const int nk = np * 6;
   if ((size_t)nk + 1 > W.cap_k) {
     const size_t c = std::max((size_t)nk + 1, 2 * W.cap_k);
-    FCHK(cm_grow(W.stc, c)); FCHK(cm_grow(W.nacc, c)); FCHK(cm_grow(W.aoff, c)); FCHK(cm_grow(W.slot2, c));
+    FCHK(cm_grow(W.stc, c)); FCHK(cm_grow(W.nacc, c)); FCHK(cm_grow(W.aoff, c));
     FCHK(cm_grow(W.flag, c)); FCHK(cm_grow(W.scan, 6 * c)); FCHK(cm_grow(W.dec, c)); FCHK(cm_grow(W.pbits, c));
     FCHK(cm_grow(W.push, c));
     W.cap_k = c;
   }
   if (!W.ctr) FCHK(cm_grow(W.ctr, 9 + 2 * kSerialCommit));
-  FCHK(hipMemcpyAsync(W.slot2, d_slot2, (size_t)nk * sizeof(int), hipMemcpyDeviceToDevice, st));
+  const int* slot2v = d_slot2;  // candidate -> survivor (surv_scatter_kernel)
+  *ovf = 0;
   if (nk <= kSerialCommit) {
     FCHK(grow(X.acc, X.cap_acc, 2 * (size_t)nk));
-    hipLaunchKernelGGL(cm_serial_kernel, dim3(1), dim3(64), 0, st, s, X.status, W.slot2, X.crec, nk, np, X.counts, X.occ,
+    hipLaunchKernelGGL(cm_serial_kernel, dim3(1), dim3(64), 0, st, s, X.status, slot2v, X.crec, nk, np, X.counts, X.occ,
                        cthr, check ? 1 : 0, first, (int)pool0, X.acc, W.ctr, X.parents, dP, apply_dflag ? 1 : 0);
     int h[9 + 2 * kSerialCommit];
-    FCHK(d2h_sync(st, {{h, W.ctr, sizeof(h)}}));
+    FCHK(d2h_sync(st, {{h, W.ctr, sizeof(h)}, {ovf, d_ovf, d_ovf ? sizeof(int) : 0}}));
+    if (*ovf) return hipSuccess;
     if (h[7] != 0) {
       fprintf(stderr, "expand: %d refined records are not valid patches\n", h[7]);
       return hipErrorIllegalState;
@@ -3625,7 +3632,7 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
     return hipGetLastError();
   }
   FCHK(hipMemsetAsync(W.ctr, 0, 8 * sizeof(int), st));
-  hipLaunchKernelGGL(cm_stage_kernel, dim3(nblk(nk)), dim3(256), 0, st, X.status, W.slot2, X.crec, nk, W.stc, W.nacc,
+  hipLaunchKernelGGL(cm_stage_kernel, dim3(nblk(nk)), dim3(256), 0, st, X.status, slot2v, X.crec, nk, W.stc, W.nacc,
                      W.dec, W.ctr + 6);
   FCHK(hipMemsetAsync(W.nacc + nk, 0, sizeof(int), st));
   auto temp_need = [&](size_t bytes) -> hipError_t {
@@ -3639,9 +3646,10 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
   tb = W.temp_bytes;
   FCHK(hipcub::DeviceScan::ExclusiveSum(W.temp, tb, W.nacc, W.aoff, nk + 1, st));
   int hv[2] = {0, 0};
-  FCHK(d2h_sync(st, {{&hv[0], W.aoff + nk, sizeof(int)}, {&hv[1], W.ctr + 6, sizeof(int)}}));
+  FCHK(d2h_sync(st, {{&hv[0], W.aoff + nk, sizeof(int)}, {&hv[1], W.ctr + 6, sizeof(int)},
+                     {ovf, d_ovf, d_ovf ? sizeof(int) : 0}}));
+  if (*ovf) return hipSuccess;  // the caller reports the neighbour overflow of the wave's depth_post
   const int na = hv[0], nlive = hv[1];
-  int nseg = 0;
   if (na > 0) {
     if ((size_t)na + 1 > W.cap_a) {
       const size_t c = std::max((size_t)na + 1, 2 * W.cap_a);
@@ -3650,7 +3658,7 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
       FCHK(cm_grow(W.segptr, c)); FCHK(cm_grow(W.segfirst, c));
       W.cap_a = c;
     }
-    hipLaunchKernelGGL(cm_emit_kernel, dim3(nblk(nk)), dim3(256), 0, st, W.stc, W.slot2, X.crec, W.aoff, nk, W.keys,
+    hipLaunchKernelGGL(cm_emit_kernel, dim3(nblk(nk)), dim3(256), 0, st, W.stc, slot2v, X.crec, W.aoff, nk, W.keys,
                        W.vals);
     tb = 0;
     FCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, W.keys, W.keys2, W.vals, W.vals2, na, 0, 64, st));
@@ -3662,8 +3670,8 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
     hipLaunchKernelGGL(cm_head_kernel, dim3(nblk(na)), dim3(256), 0, st, W.keys2, W.vals2, na, W.head, W.pos);
     tb = W.temp_bytes;
     FCHK(hipcub::DeviceScan::InclusiveSum(W.temp, tb, W.head, W.segid, na, st));
-    FCHK(read_int(W.segid + na - 1, &nseg, st));
-    hipLaunchKernelGGL(cm_seg_kernel, dim3(nblk(na)), dim3(256), 0, st, W.head, W.segid, na, W.seghead, W.segptr);
+    hipLaunchKernelGGL(cm_seg_kernel, dim3(nblk(na)), dim3(256), 0, st, W.head, W.segid, na, W.seghead, W.segptr,
+                       W.ctr + 8);  // the segment count stays on the device (cm_first_kernel reads it)
     // W.vals (the sort's input values) is free from here: each access's segment
     hipLaunchKernelGGL(cm_segof_kernel, dim3(nblk(na)), dim3(256), 0, st, W.pos, W.segid, na, W.vals);
   }
@@ -3671,10 +3679,10 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
   int decided = 0;
   for (int round = 0; decided < nlive; ) {
     for (int r = 0; r < 4; ++r, ++round) {
-      if (nseg > 0)
-        hipLaunchKernelGGL(cm_first_kernel, dim3(nblk(nseg)), dim3(256), 0, st, W.keys2, W.dec, W.seghead, nseg, W.segptr,
+      if (na > 0)  // <= na segments
+        hipLaunchKernelGGL(cm_first_kernel, dim3(nblk(na)), dim3(256), 0, st, W.keys2, W.dec, W.seghead, W.ctr + 8, W.segptr,
                            W.segfirst);
-      hipLaunchKernelGGL(cm_decide_kernel, dim3(nblk(nk)), dim3(256), 0, st, s, nk, W.slot2, X.crec, W.aoff, W.nacc, W.vals,
+      hipLaunchKernelGGL(cm_decide_kernel, dim3(nblk(nk)), dim3(256), 0, st, s, nk, slot2v, X.crec, W.aoff, W.nacc, W.vals,
                          W.segfirst, W.dec, W.stc, W.flag, X.counts, X.occ, cthr, check ? 1 : 0, W.ctr);
     }
     FCHK(read_int(W.ctr, &decided, st));
@@ -3688,7 +3696,7 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
   int* ia = W.scan + 3 * (size_t)(nk + 1);
   int* ib = W.scan + 4 * (size_t)(nk + 1);
   int* ic = W.scan + 5 * (size_t)(nk + 1);
-  hipLaunchKernelGGL(cm_accept_scan_kernel, dim3(nblk(nk)), dim3(256), 0, st, W.flag, nk, ia, ib, ic, W.slot2, X.crec);
+  hipLaunchKernelGGL(cm_accept_scan_kernel, dim3(nblk(nk)), dim3(256), 0, st, W.flag, nk, ia, ib, ic, slot2v, X.crec);
   FCHK(hipMemsetAsync(ia + nk, 0, sizeof(int), st));
   FCHK(hipMemsetAsync(ib + nk, 0, sizeof(int), st));
   FCHK(hipMemsetAsync(ic + nk, 0, sizeof(int), st));
@@ -3700,27 +3708,28 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
     FCHK(hipcub::DeviceScan::ExclusiveSum(W.temp, tb, t == 0 ? ia : t == 1 ? ib : ic, t == 0 ? qa : t == 1 ? qb : qc,
                                           nk + 1, st));
   }
+  // accepted / pushed / entries written in k order (the accepted count read on the device), then ONE
+  // read of the totals, the counters, the pushes (at most the m survivors) and the parents' bits
+  FCHK(grow(X.acc, X.cap_acc, 2 * (size_t)std::max(m, 1)));
+  hipLaunchKernelGGL(cm_write_kernel, dim3(nblk(nk)), dim3(256), 0, st, W.flag, nk, qa, qb, qc, slot2v, X.crec, (int)pool0,
+                     first, X.acc, W.push);
+  hipLaunchKernelGGL(cm_bits_kernel, dim3(nblk(np)), dim3(256), 0, st, W.stc, np, W.pbits);
+  if (apply_dflag) hipLaunchKernelGGL(cm_dflag_kernel, dim3(nblk(np)), dim3(256), 0, st, dP, X.parents, W.pbits, np);
   int tot[3], ctr[8];
+  out.push.resize((size_t)std::max(m, 0));
+  out.pbits = 0;
   FCHK(d2h_sync(st, {{&tot[0], qa + nk, sizeof(int)}, {&tot[1], qb + nk, sizeof(int)}, {&tot[2], qc + nk, sizeof(int)},
-                     {ctr, W.ctr, 8 * sizeof(int)}}));
+                     {ctr, W.ctr, 8 * sizeof(int)}, {out.push.data(), W.push, (size_t)std::max(m, 0) * sizeof(int2)},
+                     {&out.pbits, W.pbits, apply_dflag ? 0 : sizeof(int)}}));
   if (ctr[2] != 0) {
     fprintf(stderr, "expand: %d refined records are not valid patches\n", ctr[2]);
     return hipErrorIllegalState;
   }
+  if (tot[0] > m || tot[1] > m) return hipErrorIllegalState;  // cannot happen: only survivors are accepted
   out.nacc = tot[0];
   out.entries = tot[2];
   out.fail[0] = ctr[3]; out.fail[1] = ctr[4]; out.fail[2] = ctr[5]; out.fail[3] = ctr[1];
-  if (out.nacc > 0) {
-    FCHK(grow(X.acc, X.cap_acc, 2 * (size_t)out.nacc));
-    hipLaunchKernelGGL(cm_write_kernel, dim3(nblk(nk)), dim3(256), 0, st, W.flag, nk, qa, qb, qc, W.slot2, X.crec, out.nacc,
-                       (int)pool0, first, X.acc, W.push);
-  }
   out.push.resize(tot[1]);
-  hipLaunchKernelGGL(cm_bits_kernel, dim3(nblk(np)), dim3(256), 0, st, W.stc, np, W.pbits);
-  out.pbits = 0;
-  if (apply_dflag) hipLaunchKernelGGL(cm_dflag_kernel, dim3(nblk(np)), dim3(256), 0, st, dP, X.parents, W.pbits, np);
-  FCHK(d2h_sync(st, {{out.push.data(), W.push, (size_t)tot[1] * sizeof(int2)},
-                     {&out.pbits, W.pbits, apply_dflag ? 0 : sizeof(int)}}));
   return hipGetLastError();
 }
 
@@ -3994,7 +4003,9 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
       FCHK(hipcub::DeviceScan::ExclusiveSum(X.qsort_tmp, tb, X.cand_ok, X.cidx, np * 6, st));
     }
     int nok = 0;
-    {
+    if (W > 1 && min_cands > 0) {
+      nok = (int)ndirs;  // the chunks' free directions, already counted (count_ok_kernel): no read
+    } else {
       int last_ok = 0, last_idx = 0;
       FCHK(d2h_sync(st, {{&last_ok, X.cand_ok + (size_t)np * 6 - 1, sizeof(int)},
                          {&last_idx, X.cidx + (size_t)np * 6 - 1, sizeof(int)}}));
@@ -4072,7 +4083,8 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
             FCHK(hipPeekAtLastError());
           }
         }
-        return read_int(B.counters + 3, &ovf, st);
+        // one rank: the neighbour-overflow flag is read with the commit's first read (device_commit)
+        return G > 1 ? read_int(B.counters + 3, &ovf, st) : hipPeekAtLastError();
       };
       hipError_t lerr = local();
       T.mark(5);
@@ -4136,7 +4148,10 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
       T.mark(6);
       // ---- commit in (parent priority, direction) order, on the device (device_commit)
       const int first = nmodel;
-      FCHK(device_commit(s, X, st, np, X.slot2, cthr, only < 0, first, (long long)X.pool_host, W > 1, dP, co));
+      int ovf2 = 0;
+      FCHK(device_commit(s, X, st, np, X.slot2, m, G > 1 ? nullptr : B.counters + 3, &ovf2, cthr, only < 0, first,
+                         (long long)X.pool_host, W > 1, dP, co));
+      if (ovf2) { trace_error(hipErrorOutOfMemory, __LINE__); return hipErrorOutOfMemory; }  // more than NB_CAP neighbours
       for (int q = 0; q < 4; ++q) stats[2 + q] += co.fail[q];
       if (W == 1) pbits |= co.pbits;
       const int added = co.nacc;
