@@ -1,0 +1,110 @@
+"""BASELINE.json configs[4] (C5) with its boundary exchange: two overlapping CMVS clusters of an 8K
+ring, 70 views each (66 targets + 2 views shared with each neighbour, as tests/test_gpu_c4.py splits
+its 4K ring), two loop iterations with the boundary patches exchanged after the first through
+ThreadExchange -- the reference's per-cluster pmvs2 runs plus the exchange this framework adds
+between them (the reference runs clusters independently, bundle.cpp:1465-1485
+being where one cluster's patches are written for the next stage).
+
+Opt-in (PMVS_LONG_TESTS=1): the two clusters' iterations take about five minutes on one GPU.
+The clusters run as two threads on this GPU, but their compute phases take turns (a baton passed at
+every all-gather), so that only one 8K model grows at a time: one cluster's first expansion reaches
+~51 M records (82 GB) and the two growing together would not fit in 288 GB.  The exchange itself is
+the native pmvs_thread_allgather, called from the baton wrapper.
+"""
+import ctypes as C
+import os
+import sys
+import threading
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+_LONG = pytest.mark.skipif(not os.environ.get("PMVS_LONG_TESTS"), reason="PMVS_LONG_TESTS=1 runs it")
+
+ALLGATHER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p)
+
+
+@_LONG
+@pytest.mark.timeout(1100)
+def test_c5_two_clusters_two_iterations_exchange(gpu_available):
+    import bench
+    import pmvs_amd as P
+    from test_gpu_c4 import ring_clusters
+    world, vpc, ov = 2, 66, 2
+    clusters = ring_clusters(vpc, world, ov)
+    assert all(len(c) == 70 for c in clusters)
+    full, sp = P.synth_scene(vpc * world, 7680, 4320, level=0, supersample=2, nthreads=16)
+    cands = P.synth_candidates(sp, full.projections, 5000 * world, seed=0x5EED)
+    inps = [P.SceneInputs(images=[full.images[i] for i in ids], projections=full.projections[ids], num_targets=len(ids),
+                          level=0) for ids in clusters]
+    del full
+    scenes = [P.Scene(inp) for inp in inps]
+    try:
+        seeds = []
+        for g, ids in zip(scenes, clusters):
+            loc = {v: k for k, v in enumerate(ids)}
+            keep = [i for i in range(len(cands)) if int(cands["images"][i][0]) in loc and int(cands["images"][i][1]) in loc]
+            cs = cands[keep].copy()
+            cs["images"][:, 0] = [loc[int(v)] for v in cs["images"][:, 0]]
+            cs["images"][:, 1] = [loc[int(v)] for v in cs["images"][:, 1]]
+            r, _ = g.refine_batch(cs)
+            seeds.append(P.patches_from_refined(r))
+
+        ex = P.ThreadExchange(world)
+        native = ALLGATHER(C.cast(ex.lib.pmvs_thread_allgather, C.c_void_p).value)
+        baton = threading.Lock()
+        calls = [0] * world
+
+        def endpoint(r):
+            ctx = ex.endpoint(r)[1]
+
+            def fn(_ctx, send, nbytes, recv):
+                calls[r] += 1
+                baton.release()  # the other cluster computes while this one waits in the all-gather
+                try:
+                    return native(ctx, send, nbytes, recv)
+                finally:
+                    baton.acquire()
+            return ALLGATHER(fn)
+
+        fns = [endpoint(r) for r in range(world)]
+        res, errs = [None] * world, [None] * world
+
+        def work(r):
+            baton.acquire()
+            try:
+                scenes[r].set_cluster(r, world, clusters[r], fns[r], None)
+                res[r] = scenes[r].run_loop(seeds[r], inps[r].threshold, iterations=2, wave=32768,
+                                            min_candidates=131072)
+            except Exception as e:  # noqa: BLE001 -- reported below
+                errs[r] = e
+            finally:
+                baton.release()
+
+        th = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(world)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=1000)
+        assert not any(t.is_alive() for t in th), "cluster exchange deadlock"
+        ex.close()
+        assert not any(errs), errs
+        assert all(c > 0 for c in calls), calls
+        for r, (model, log) in enumerate(res):
+            checks = bench.model_checks(model, inps[r], ["x"])
+            print(f"C5 cluster {r}: seeds {len(seeds[r])}, patches {[it['patches'] for it in log]}, added "
+                  f"{[it['expand']['added'] for it in log]}, expand s {[round(it['expand']['wall_ms'] / 1e3, 1) for it in log]}, "
+                  f"boundary {[(it['boundary']['sent'], it['boundary']['inserted']) for it in log]}, checks {checks}")
+            assert checks["ok"], (r, checks)
+            assert checks["sphere_residual_p99"] < 0.01, checks
+            assert log[0]["expand"]["added"] > 10_000_000
+            assert log[0]["boundary"]["sent"] > 0 and log[0]["boundary"]["inserted"] > 0, log
+            assert model["fix"].max() != P.FIX_FOREIGN  # foreign patches never returned
+    finally:
+        for g in scenes:
+            g.close()
