@@ -577,56 +577,75 @@ __global__ void exact_entries_kernel(DScene s, FilterDev F, long long ncells, Re
 // filterExact (filter.cpp:234-348) per collected, non-fixed patch: new list = safe targets in
 // increasing image order (the reference's image-major scan) with their cells, then the
 // non-target images; _timages = #safe.  need_ref[p] = 1 when setRefImage + setGrids follow.
-__global__ void exact_patch_kernel(DScene s, FilterDev F, const Reg* __restrict__ safe,
-                                   Reg* __restrict__ preg, Reg* __restrict__ vreg,
-                                   int* __restrict__ need_ref, int* __restrict__ removed) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= F.nalive) return;
+// One wavefront per patch (4 per 256-lane block): lane l holds list entries l and l + 64.  A kept
+// target entry goes to the number of kept target entries before it in (image, list position)
+// order -- the reference loops over the targets and looks each up in the list, filter.cpp:305-330
+// -- and a non-target entry to the kept count plus the non-target entries before it in list order.
+// Every lane's entries are in registers before any lane writes, so the list is rewritten in place.
+// (Round 4's thread-per-patch form staged the new list in 1.5 KB of per-thread arrays, which lived
+// in scratch: 87 GB of HBM traffic per C3 launch, profiles/r05j_pmc.json.)
+__global__ __launch_bounds__(256) void exact_patch_kernel(DScene s, FilterDev F, const Reg* __restrict__ safe,
+                                                          Reg* __restrict__ preg, Reg* __restrict__ vreg,
+                                                          int* __restrict__ need_ref, int* __restrict__ removed) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= F.nalive) return;  // wave-uniform; no barriers below
   const int p = F.order[i];
   pmvs_patch& q = F.P[p];
-  need_ref[p] = 0;
-  if (q.fix) return;
+  if (q.fix) {
+    if (lane == 0) need_ref[p] = 0;
+    return;
+  }
   const Reg sm = reg_and(safe[p], preg[p]);
-  int ni = 0;
-  int imgs[PMVS_MAX_IMAGES], grd[PMVS_MAX_IMAGES][2];
-  // the kept target entries in ascending image order (the reference loops over the targets and
-  // looks each up in the list, filter.cpp:305-330): entry k goes to the number of kept target
-  // entries before it in (image, list position) order
   const int n0 = q.num_images;
-  for (int k = 0; k < n0; ++k) {
-    const int t = q.images[k];
-    if (t >= s.tnum || !reg_test(sm, k)) continue;
-    int pos = 0;
-    for (int k2 = 0; k2 < n0; ++k2) {
-      const int t2 = q.images[k2];
-      pos += (t2 < s.tnum && reg_test(sm, k2) && (t2 < t || (t2 == t && k2 < k)));  // ties in list order
+  int t[2], g0[2], g1[2];
+  bool kept[2], other[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int k = lane + 64 * u;
+    t[u] = 0; g0[u] = 0; g1[u] = 0; kept[u] = false; other[u] = false;
+    if (k < n0) {
+      t[u] = q.images[k];
+      g0[u] = q.grids[k][0];
+      g1[u] = q.grids[k][1];
+      kept[u] = t[u] < s.tnum && reg_test(sm, k);
+      other[u] = s.tnum <= t[u];
     }
-    imgs[pos] = t;
-    grd[pos][0] = q.grids[k][0];
-    grd[pos][1] = q.grids[k][1];
-    ni++;
   }
-  q.timages = ni;
-  for (int k = 0; k < q.num_images; ++k)
-    if (s.tnum <= q.images[k]) {
-      imgs[ni] = q.images[k];
-      grd[ni][0] = q.grids[k][0];
-      grd[ni][1] = q.grids[k][1];
-      ni++;
+  int pos[2] = {0, 0};
+  for (int k2 = 0; k2 < n0; ++k2) {  // n0 is wave-uniform: every lane reads entry k2 by a shuffle
+    const int t2 = __shfl(k2 < 64 ? t[0] : t[1], k2 & 63);
+    const int kp2 = __shfl(k2 < 64 ? (int)kept[0] : (int)kept[1], k2 & 63);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      pos[u] += (kp2 && (t2 < t[u] || (t2 == t[u] && k2 < lane + 64 * u)));  // ties in list order
+  }
+  const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const unsigned long long bk0 = __ballot(kept[0]), bk1 = __ballot(kept[1]);
+  const unsigned long long bo0 = __ballot(other[0]), bo1 = __ballot(other[1]);
+  const int nkept = __popcll(bk0) + __popcll(bk1);
+  const int ni = nkept + __popcll(bo0) + __popcll(bo1);
+  const int opos[2] = {nkept + (int)__popcll(bo0 & lt), nkept + (int)__popcll(bo0) + (int)__popcll(bo1 & lt)};
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (!kept[u] && !other[u]) continue;
+    const int d = kept[u] ? pos[u] : opos[u];
+    q.images[d] = (int16_t)t[u];
+    q.grids[d][0] = (int16_t)g0[u];
+    q.grids[d][1] = (int16_t)g1[u];
+  }
+  if (lane == 0) {
+    q.timages = nkept;
+    q.num_images = ni;
+    if (s.minImageNum <= ni) {
+      preg[p] = reg_first(nkept);
+      need_ref[p] = 1;
+    } else {
+      preg[p] = reg_zero();
+      vreg[p] = reg_zero();
+      need_ref[p] = 0;
+      atomicAdd(removed, 1);
     }
-  for (int k = 0; k < ni; ++k) {
-    q.images[k] = imgs[k];
-    q.grids[k][0] = grd[k][0];
-    q.grids[k][1] = grd[k][1];
-  }
-  q.num_images = ni;
-  preg[p] = reg_first(q.timages);
-  if (s.minImageNum <= ni) {
-    need_ref[p] = 1;
-  } else {
-    preg[p] = reg_zero();
-    vreg[p] = reg_zero();
-    atomicAdd(removed, 1);
   }
 }
 
@@ -1891,7 +1910,12 @@ __global__ __launch_bounds__(64) NB_WALK_ATTR void empty_blocks_kernel(DScene s,
     const int k = ov.only ? __builtin_amdgcn_readfirstlane(ov.only[i]) : i;
     const pmvs_patch& q = F.P[parents[k]];
     const float radius = compute_radius_wave(s, L, q);
+#if defined(EBX_SKIP_WALK)  // timing experiment only (tools/eb_breakdown.sh): no neighbour walk
+    const int n = 0;
+    if (lane == 0) L.overflow = 0;
+#else
     const int n = gather_neighbors(s, F, L, q, 4.0f, 1, 0);
+#endif
     // overflowed: this parent's bins are rewritten by the NB_CAP_BIG re-walk
     if (lane == 0 && L.overflow && ov.items) ov.items[atomicAdd(ov.count, 1)] = k;
     if (lane == 0 && L.overflow && !ov.items) atomicAdd(overflow, 1);
@@ -1909,7 +1933,11 @@ __global__ __launch_bounds__(64) NB_WALK_ATTR void empty_blocks_kernel(DScene s,
     // it is > 0 iff some term is > 0 and none is NaN, so the neighbours are scanned lane-parallel
     // and only those two facts per bin are reduced.
     unsigned pos = 0u, nan = 0u;
+#if defined(EBX_SKIP_BIN)  // timing experiment only (tools/eb_breakdown.sh): the neighbours not binned
+    for (int a = lane; a < 0; a += 64) {
+#else
     for (int a = lane; a < n; a += 64) {
+#endif
       float d[4];
       for (int c = 0; c < 4; ++c) d[c] = F.hot[L.nb[a]].coord[c] - q.coord[c];
       float f0 = dot4(d, xdir), f1 = dot4(d, ydir);
@@ -2810,7 +2838,7 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
   }
   FCHK(hipMemsetAsync(B.need, 0, n * sizeof(int), st));
   if (c.nalive)
-    hipLaunchKernelGGL(exact_patch_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, s, c.dev(), B.safe, B.preg, B.vreg,
+    hipLaunchKernelGGL(exact_patch_kernel, dim3((c.nalive + 3) / 4), dim3(256), 0, st, s, c.dev(), B.safe, B.preg, B.vreg,
                        B.need, B.counters + 2);
   {
     // the patches that need setRefImage, in index order: compacted on the device
@@ -3364,16 +3392,21 @@ __global__ void cm_seg_kernel(const int* __restrict__ head, int* __restrict__ se
   }
 }
 
-__global__ void cm_first_kernel(const unsigned long long* __restrict__ keys, const unsigned char* __restrict__ dec,
-                                const int* __restrict__ seghead, const int* __restrict__ nsegp, int* __restrict__ segptr,
-                                int* __restrict__ segfirst) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= *nsegp) return;
+__device__ __forceinline__ void cm_first_at(int s, const unsigned long long* __restrict__ keys,
+                                            const unsigned char* dec, const int* __restrict__ seghead,
+                                            int* __restrict__ segptr, int* __restrict__ segfirst) {
   int p = segptr[s];
   const int end = seghead[s + 1];
   while (p < end && dec[(int)(keys[p] & 0xffffffffull)]) ++p;
   segptr[s] = p;
   segfirst[s] = (p < end) ? (int)(keys[p] & 0xffffffffull) : -1;
+}
+__global__ void cm_first_kernel(const unsigned long long* __restrict__ keys, const unsigned char* __restrict__ dec,
+                                const int* __restrict__ seghead, const int* __restrict__ nsegp, int* __restrict__ segptr,
+                                int* __restrict__ segfirst) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= *nsegp) return;
+  cm_first_at(s, keys, dec, seghead, segptr, segfirst);
 }
 
 // The decision of candidate k (record r) once it is the first undecided candidate in all of its
@@ -3423,13 +3456,13 @@ __global__ void cm_segof_kernel(const int* __restrict__ pos, const int* __restri
 // Decides every undecided candidate that is the first undecided one in all of its cells (its
 // accesses' segments, four loads in flight at a time).
 // ctr: [0] decided this call, [1] fail_commit, [2] invalid.
-__global__ void cm_decide_kernel(DScene s, int nk, const int* __restrict__ slot2, const int* __restrict__ rec,
-                                 const int* __restrict__ aoff, const int* __restrict__ nacc, const int* __restrict__ segof,
-                                 const int* __restrict__ segfirst, unsigned char* __restrict__ dec, int* __restrict__ stc,
-                                 int* __restrict__ flag, unsigned char* __restrict__ counts, unsigned char* __restrict__ occ,
-                                 int cthr, int check, int* __restrict__ ctr) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= nk || dec[k]) return;
+__device__ __forceinline__ void cm_decide_at(const DScene& s, int k, const int* __restrict__ slot2,
+                                             const int* __restrict__ rec, const int* __restrict__ aoff,
+                                             const int* __restrict__ nacc, const int* __restrict__ segof,
+                                             const int* segfirst, unsigned char* dec, int* __restrict__ stc,
+                                             int* __restrict__ flag, unsigned char* counts, unsigned char* occ, int cthr,
+                                             int check, int* ctr) {
+  if (dec[k]) return;
   const int e0 = aoff[k], ee = e0 + nacc[k];
   for (int e = e0; e < ee; e += 4) {
     int sg[4];
@@ -3442,6 +3475,15 @@ __global__ void cm_decide_kernel(DScene s, int nk, const int* __restrict__ slot2
     if (!first) return;
   }
   cm_apply(s, k, rec + (size_t)slot2[k] * kRecInts, dec, stc, flag, counts, occ, cthr, check, ctr);
+}
+__global__ void cm_decide_kernel(DScene s, int nk, const int* __restrict__ slot2, const int* __restrict__ rec,
+                                 const int* __restrict__ aoff, const int* __restrict__ nacc, const int* __restrict__ segof,
+                                 const int* __restrict__ segfirst, unsigned char* __restrict__ dec, int* __restrict__ stc,
+                                 int* __restrict__ flag, unsigned char* __restrict__ counts, unsigned char* __restrict__ occ,
+                                 int cthr, int check, int* __restrict__ ctr) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nk) return;
+  cm_decide_at(s, k, slot2, rec, aoff, nacc, segof, segfirst, dec, stc, flag, counts, occ, cthr, check, ctr);
 }
 
 // flags of the non-refined candidates (0) and the outcome counters: ctr[3] fail_prep, [4] fail_pre,
