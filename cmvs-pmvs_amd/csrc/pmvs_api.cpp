@@ -505,7 +505,9 @@ pmvs_status pmvs_scene_create(const pmvs_scene_desc* d, int32_t device, pmvs_sce
   }
   if (const char* e = getenv("PMVS_REFINE_SMALL_N")) sc->small_n = std::max(0, atoi(e));
   sc->refine_grid = std::max(1, prop.multiProcessorCount) * wpc;
-  if (sc->scratch.alloc((size_t)sc->grid * PMVS_MAX_IMAGES * PMVS_MAX_IMAGES) != hipSuccess)
+  // per-workgroup global scratch: the scene grid, or pre / post's larger grid (prepost_waves)
+  const size_t scratch_blocks = (size_t)sc->grid * std::max(2, prepost_waves()) / 2;
+  if (sc->scratch.alloc(scratch_blocks * PMVS_MAX_IMAGES * PMVS_MAX_IMAGES) != hipSuccess)
     return bail(fail(PMVS_ENOMEM, "scratch"));
 
   DScene& s = sc->ds;

@@ -239,16 +239,43 @@ __device__ int is_visible(const DScene& s, const FilterDev& F, int p, int t, int
 // --------------------------------------------------------------------------- organizer build
 // CPatchOrganizerS::addPatch (patchOrganizerS.cpp:308-324): register every target entry of the
 // input patches (out-of-grid cells, undefined in the reference, are not registered).
+// The list kernels below read a patch's image / cell lists with kLG lanes per patch (entry i on
+// lane i mod kLG): one load instruction covers kLG consecutive entries of one record, so each list
+// line is fetched once.  Thread-per-patch forms re-fetched the lines for every entry (a CU's
+// thousands of in-flight records do not stay in L1 / L2 between one thread's iterations): 10.9 GB
+// of HBM reads per first_cell launch and 6.2 GB per emit_entries launch on C3
+// (profiles/r05j_pmc.json) against ~1.5 GB of list lines.
+constexpr int kLG = 8;
+__device__ __forceinline__ int reg_rank(const Reg& r, int i) {  // set entries below i
+  return (i < 64) ? __popcll(r.w[0] & ((1ull << i) - 1ull)) : __popcll(r.w[0]) + __popcll(r.w[1] & ((1ull << (i - 64)) - 1ull));
+}
+__device__ __forceinline__ int reg_last(const Reg& r) {  // highest set entry, -1 if none
+  return r.w[1] ? 127 - __clzll(r.w[1]) : (r.w[0] ? 63 - __clzll(r.w[0]) : -1);
+}
 __global__ void init_reg_kernel(DScene s, const pmvs_patch* __restrict__ P, int n, Reg* __restrict__ preg,
                                 Reg* __restrict__ vreg) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = (int)(g / kLG), l = (int)(g % kLG);
+  if (p >= n) return;  // whole lane groups
   const pmvs_patch& q = P[p];
-  Reg m = reg_zero();
-  for (int i = 0; i < q.num_images; ++i)
-    if (q.images[i] < s.tnum && in_grid(s, q.images[i], q.grids[i][0], q.grids[i][1])) reg_set(m, i);
-  preg[p] = m;
-  vreg[p] = reg_zero();
+  const int ni = q.num_images;
+  unsigned long long w0 = 0ull, w1 = 0ull;
+  for (int i = l; i < ni; i += kLG)
+    if (q.images[i] < s.tnum && in_grid(s, q.images[i], q.grids[i][0], q.grids[i][1])) {
+      if (i < 64) w0 |= 1ull << i;
+      else w1 |= 1ull << (i - 64);
+    }
+  for (int d = 1; d < kLG; d <<= 1) {
+    w0 |= __shfl_xor(w0, d);
+    w1 |= __shfl_xor(w1, d);
+  }
+  if (l == 0) {
+    Reg m;
+    m.w[0] = w0;
+    m.w[1] = w1;
+    preg[p] = m;
+    vreg[p] = reg_zero();
+  }
 }
 
 __global__ void keep_kernel(int n, const Reg* __restrict__ preg, const int* __restrict__ rank,
@@ -268,17 +295,21 @@ __global__ void count_entries_kernel(const pmvs_patch* __restrict__ P, int n, co
 __global__ void emit_entries_kernel(DScene s, const pmvs_patch* __restrict__ P, int n,
                                     const Reg* __restrict__ reg, int vis, const int* __restrict__ off,
                                     const long long* __restrict__ tgoff, unsigned long long* __restrict__ keys) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = (int)(g / kLG), l = (int)(g % kLG);
   if (p >= n) return;
   const Reg m = reg[p];
-  int o = off[p];
+  const int last = reg_last(m);
+  if (last < 0) return;
+  const int o = off[p];
   const pmvs_patch& q = P[p];
-  for (int i = reg_next(m, -1); i >= 0; i = reg_next(m, i)) {
+  for (int i = l; i <= last; i += kLG) {
+    if (!reg_test(m, i)) continue;
     const int t = vis ? q.vimages[i] : q.images[i];
     const int ix = vis ? q.vgrids[i][0] : q.grids[i][0];
     const int iy = vis ? q.vgrids[i][1] : q.grids[i][1];
     const unsigned long long cell = (unsigned long long)(tgoff[t] + (long long)iy * gwidth(s, t) + ix);
-    keys[o++] = (cell << 32) | (unsigned)p;
+    keys[o + reg_rank(m, i)] = (cell << 32) | (unsigned)p;
   }
 }
 
@@ -295,21 +326,37 @@ __global__ void items_kernel(const unsigned long long* __restrict__ keys, int e,
 }
 
 // first registered pgrids cell of each patch (collectPatches order key)
+// Grid-stride over the patches (kLG lanes each), the collected count summed per wavefront and added
+// with one atomic per wavefront of the grid: an atomic per wavefront of patches (525 k same-address
+// atomics per C3 launch) made the lane-group form 4x slower than the thread-per-patch one.
 __global__ void first_cell_kernel(DScene s, const pmvs_patch* __restrict__ P, int n,
                                   const Reg* __restrict__ preg, const long long* __restrict__ tgoff,
                                   unsigned long long* __restrict__ keys, int* __restrict__ nalive) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  const Reg m = preg[p];
-  unsigned long long best = ~0ull;
-  const pmvs_patch& q = P[p];
-  for (int i = reg_next(m, -1); i >= 0; i = reg_next(m, i)) {
-    const int t = q.images[i];
-    const unsigned long long cell = (unsigned long long)(tgoff[t] + (long long)q.grids[i][1] * gwidth(s, t) + q.grids[i][0]);
-    if (cell < best) best = cell;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  int live = 0;
+  for (long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x; g < (long long)n * kLG; g += stride) {
+    const int p = (int)(g / kLG), l = (int)(g % kLG);  // stride is a multiple of kLG: groups stay whole
+    const Reg m = preg[p];
+    const int last = reg_last(m);
+    unsigned long long best = ~0ull;
+    const pmvs_patch& q = P[p];
+    for (int i = l; i <= last; i += kLG) {
+      if (!reg_test(m, i)) continue;
+      const int t = q.images[i];
+      const unsigned long long cell = (unsigned long long)(tgoff[t] + (long long)q.grids[i][1] * gwidth(s, t) + q.grids[i][0]);
+      if (cell < best) best = cell;
+    }
+    for (int d = 1; d < kLG; d <<= 1) {
+      const unsigned long long o = __shfl_xor(best, d);
+      best = o < best ? o : best;
+    }
+    if (l == 0) {
+      keys[p] = (best == ~0ull) ? ~0ull : ((best << 32) | (unsigned)p);
+      live += (best != ~0ull);
+    }
   }
-  keys[p] = (best == ~0ull) ? ~0ull : ((best << 32) | (unsigned)p);
-  if (best != ~0ull) atomicAdd(nalive, 1);
+  for (int d = 32; d >= 1; d >>= 1) live += __shfl_xor(live, d);
+  if ((threadIdx.x & 63) == 0 && live) atomicAdd(nalive, live);
 }
 
 __global__ void rank_kernel(const unsigned long long* __restrict__ keys, int nalive, int* __restrict__ order,
@@ -364,31 +411,37 @@ __device__ __forceinline__ long long xcd_block() {
 // nearby cells of the same map.
 // Owner-partitioned filter pass (world > 1): only the targets rank owns (t = rank + world j) -- the
 // other targets' maps are never read on this rank (its visibility tests are its own targets').
+// tpt targets per thread (PMVS_DM_TARGETS, default 4): the patch's coordinate is read once for them.
 __global__ void depth_map_kernel(DScene s, FilterDev F, const float4* __restrict__ coordc,
-                                 unsigned long long* __restrict__ dpkey, int rank = 0, int world = 1) {
+                                 unsigned long long* __restrict__ dpkey, int rank = 0, int world = 1, int tpt = 1) {
   const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // hardware order (r03k3: the XCD
   const int nown = (F.tnum - rank + world - 1) / world;                   // order made it 7.9 -> 10.6 ms)
-  if (g >= (long long)F.nalive * nown) return;
-  const int j = (int)(g / F.nalive), i = (int)(g - (long long)j * F.nalive);
-  const int t = rank + world * j;
+  const int ngrp = (nown + tpt - 1) / tpt;
+  if (g >= (long long)F.nalive * ngrp) return;
+  const int jg = (int)(g / F.nalive), i = (int)(g - (long long)jg * F.nalive);
   const float4 c4 = coordc[i];
   const float coord[4] = {c4.x, c4.y, c4.z, c4.w};
-  const DView& v = s.views[t];
-  float ic[3];
-  project(v, coord, s.level, ic);
-  const float fx = __fdiv_rn(ic[0], (float)s.csize), fy = __fdiv_rn(ic[1], (float)s.csize);
-  const int xs[2] = {(int)floor((double)fx), (int)ceil((double)fx)};
-  const int ys[2] = {(int)floor((double)fy), (int)ceil((double)fy)};
-  const unsigned long long key = ((unsigned long long)depth_bits(depth_of(v, coord)) << 32) | (unsigned)i;
-  const int gw = gwidth(s, t), gh = gheight(s, t);
-  for (int j = 0; j < 2; ++j)
-    for (int k = 0; k < 2; ++k) {
-      if (xs[k] < 0 || gw <= xs[k] || ys[j] < 0 || gh <= ys[j]) continue;
-      unsigned long long* cell = &dpkey[F.tgoff[t] + (long long)ys[j] * gw + xs[k]];
-      // the stored minimum only decreases, so a (possibly stale) value <= key means the atomic
-      // could not change the cell: skip it (most updates of a dense model)
-      if (key < *cell) atomicMin(cell, key);
-    }
+  for (int u = 0; u < tpt; ++u) {
+    const int j = jg * tpt + u;
+    if (j >= nown) break;
+    const int t = rank + world * j;
+    const DView& v = s.views[t];
+    float ic[3];
+    project(v, coord, s.level, ic);
+    const float fx = __fdiv_rn(ic[0], (float)s.csize), fy = __fdiv_rn(ic[1], (float)s.csize);
+    const int xs[2] = {(int)floor((double)fx), (int)ceil((double)fx)};
+    const int ys[2] = {(int)floor((double)fy), (int)ceil((double)fy)};
+    const unsigned long long key = ((unsigned long long)depth_bits(depth_of(v, coord)) << 32) | (unsigned)i;
+    const int gw = gwidth(s, t), gh = gheight(s, t);
+    for (int y = 0; y < 2; ++y)
+      for (int x = 0; x < 2; ++x) {
+        if (xs[x] < 0 || gw <= xs[x] || ys[y] < 0 || gh <= ys[y]) continue;
+        unsigned long long* cell = &dpkey[F.tgoff[t] + (long long)ys[y] * gw + xs[x]];
+        // the stored minimum only decreases, so a (possibly stale) value <= key means the atomic
+        // could not change the cell: skip it (most updates of a dense model)
+        if (key < *cell) atomicMin(cell, key);
+      }
+  }
 }
 
 // setVImagesVGrids (patchOrganizerS.cpp:429-459) in two steps, target-major:
@@ -413,40 +466,67 @@ __global__ void used_kernel(DScene s, FilterDev F, int additive, unsigned long l
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= F.nalive) return;
   const pmvs_patch& q = F.P[F.order[i]];
-  unsigned long long u[PMVS_MAX_TARGETS / 64] = {};
+  unsigned long long u0 = 0ull, u1 = 0ull, u2 = 0ull, u3 = 0ull;  // registers (a dynamically indexed array went to scratch)
+  auto add = [&](int t) {
+    const unsigned long long b = 1ull << (t & 63);
+    const int w = t >> 6;
+    u0 |= (w == 0) ? b : 0ull;
+    u1 |= (w == 1) ? b : 0ull;
+    u2 |= (w == 2) ? b : 0ull;
+    u3 |= (w == 3) ? b : 0ull;
+  };
+  static_assert(PMVS_MAX_TARGETS == 256, "four used words per patch");
   for (int k = 0; k < q.num_images; ++k)
-    if (q.images[k] < s.tnum) u[q.images[k] >> 6] |= 1ull << (q.images[k] & 63);
+    if (q.images[k] < s.tnum) add(q.images[k]);
   if (additive)
-    for (int k = 0; k < q.num_vimages; ++k) u[q.vimages[k] >> 6] |= 1ull << (q.vimages[k] & 63);
-  for (int w = 0; w < PMVS_MAX_TARGETS / 64; ++w) used[(size_t)i * (PMVS_MAX_TARGETS / 64) + w] = u[w];
+    for (int k = 0; k < q.num_vimages; ++k) add(q.vimages[k]);
+  // word-major (word w of every patch together): vis_rows_kernel's wavefronts read one word of 64
+  // consecutive patches, contiguously
+  const size_t na = (size_t)F.nalive;
+  used[i] = u0;
+  used[na + i] = u1;
+  used[2 * na + i] = u2;
+  used[3 * na + i] = u3;
 }
 
 struct PCN {  // the fields isVisible reads of the tested patch
   float coord[4], normal[4];
 };
 
+// kVisT targets per thread: the patch's coordinate and normal are read once for them (round 4 read
+// them once per target, 32 B x targets x patches per launch).
+constexpr int kVisT = 4;
 __global__ __launch_bounds__(256) void vis_rows_kernel(DScene s, FilterDev F, const float4* __restrict__ coordc,
                                                        const float4* __restrict__ normalc,
                                                        const unsigned long long* __restrict__ used, int rank, int world,
                                                        int nown, long long row_words, unsigned long long* __restrict__ rows) {
   const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long napad = row_words * 64;
-  if (g >= (long long)nown * napad) return;  // whole wavefronts: napad is a multiple of 64
-  const int j = (int)(g / napad), i = (int)(g - (long long)j * napad);
-  const int t = rank + world * j;
-  bool vis = false;
-  if (i < F.nalive && !((used[(size_t)i * (PMVS_MAX_TARGETS / 64) + (t >> 6)] >> (t & 63)) & 1ull)) {
+  const int ngrp = (nown + kVisT - 1) / kVisT;
+  if (g >= (long long)ngrp * napad) return;  // whole wavefronts: napad is a multiple of 64
+  const int jg = (int)(g / napad), i = (int)(g - (long long)jg * napad);
+  const bool live = i < F.nalive;
+  PCN q{};
+  if (live) {
     const float4 c4 = coordc[i], n4 = normalc[i];
-    const PCN q{{c4.x, c4.y, c4.z, c4.w}, {n4.x, n4.y, n4.z, n4.w}};
-    const DView& v = s.views[t];
-    float ic[3];
-    project(v, q.coord, s.level, ic);
-    const int ix = ((int)floorf(ic[0] + 0.5f)) / s.csize;
-    const int iy = ((int)floorf(ic[1] + 0.5f)) / s.csize;
-    vis = is_visible_q(s, F, q, t, ix, iy, 0.5f) != 0 && get_edge(s, v, q.coord, s.level) != 0;
+    q = PCN{{c4.x, c4.y, c4.z, c4.w}, {n4.x, n4.y, n4.z, n4.w}};
   }
-  const unsigned long long b = __ballot(vis);
-  if ((threadIdx.x & 63) == 0) rows[(long long)j * row_words + i / 64] = b;
+  for (int u = 0; u < kVisT; ++u) {
+    const int j = jg * kVisT + u;
+    if (j >= nown) break;  // wave-uniform
+    const int t = rank + world * j;
+    bool vis = false;
+    if (live && !((used[(size_t)(t >> 6) * F.nalive + i] >> (t & 63)) & 1ull)) {
+      const DView& v = s.views[t];
+      float ic[3];
+      project(v, q.coord, s.level, ic);
+      const int ix = ((int)floorf(ic[0] + 0.5f)) / s.csize;
+      const int iy = ((int)floorf(ic[1] + 0.5f)) / s.csize;
+      vis = is_visible_q(s, F, q, t, ix, iy, 0.5f) != 0 && get_edge(s, v, q.coord, s.level) != 0;
+    }
+    const unsigned long long b = __ballot(vis);
+    if ((threadIdx.x & 63) == 0) rows[(long long)j * row_words + i / 64] = b;
+  }
 }
 
 // rows: world blocks (rank r: nown_max rows of row_words words; row j = target r + world j)
@@ -486,39 +566,49 @@ __global__ void or_bits_kernel(const unsigned* __restrict__ all, int world, size
 // --------------------------------------------------------------------------- filterOutside
 // CFilter::filterOutsideThread (filter.cpp:148-201), neighbourThreshold1 = 1.0.  Owner-partitioned
 // (world > 1): the patches whose reference image this rank owns; the flags are all-gathered.
+// kLG lanes per patch (as the list kernels): entry e of the patch's images-then-vimages sequence on
+// lane e mod kLG computes its cell's max; the gain is then reduced in the reference's entry order by
+// every lane of the group (the maxima come by shuffles), so the float result is the sequential one.
 __global__ void gain_kernel(DScene s, FilterDev F, int* __restrict__ remove, int rank = 0, int world = 1) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= F.nalive) return;
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = (int)(g / kLG), l = (int)(g % kLG);
+  if (i >= F.nalive) return;  // whole lane groups
   const int p = F.order[i];
   const pmvs_patch& q = F.P[p];
-  remove[p] = 0;
-  if (q.fix || q.images[0] % world != rank) return;
+  if (q.fix || q.images[0] % world != rank) {
+    if (l == 0) remove[p] = 0;
+    return;
+  }
   float gain = smax(0.0f, q.ncc - s.nccThreshold) * (float)q.timages;
-  for (int k = 0; k < q.num_images; ++k) {
-    const int t = q.images[k];
-    if (s.tnum <= t) continue;
-    const long long c = F.tgoff[t] + (long long)q.grids[k][1] * gwidth(s, t) + q.grids[k][0];
+  const int ni = q.num_images, ne = ni + q.num_vimages;
+  const int base = (int)(threadIdx.x & 63) & ~(kLG - 1);  // the group's first lane in the wavefront
+  for (int c = 0; c < ne; c += kLG) {
+    const int k = c + l;
     float maxp = 0.0f;
-    for (int e = F.pg_off[c]; e < F.pg_off[c + 1]; ++e) {
-      const int j = F.pg_items[e];
-      if (!is_neighbor(s, F, p, j, 1.0f)) maxp = smax(maxp, F.hot[j].ncc - s.nccThreshold);
+    if (k < ni) {
+      const int t = q.images[k];
+      if (t < s.tnum) {
+        const long long cell = F.tgoff[t] + (long long)q.grids[k][1] * gwidth(s, t) + q.grids[k][0];
+        for (int e = F.pg_off[cell]; e < F.pg_off[cell + 1]; ++e) {
+          const int j = F.pg_items[e];
+          if (!is_neighbor(s, F, p, j, 1.0f)) maxp = smax(maxp, F.hot[j].ncc - s.nccThreshold);
+        }
+      }
+    } else if (k < ne) {
+      const int t = q.vimages[k - ni];
+      if (t < s.tnum) {
+        const float pdepth = depth_of(s.views[t], q.coord);
+        const long long cell = F.tgoff[t] + (long long)q.vgrids[k - ni][1] * gwidth(s, t) + q.vgrids[k - ni][0];
+        for (int e = F.pg_off[cell]; e < F.pg_off[cell + 1]; ++e) {
+          const int j = F.pg_items[e];
+          const float bdepth = depth_of(s.views[t], F.hot[j].coord);
+          if (pdepth < bdepth && !is_neighbor(s, F, p, j, 1.0f)) maxp = smax(maxp, F.hot[j].ncc - s.nccThreshold);
+        }
+      }
     }
-    gain -= maxp;
+    for (int u = 0; u < kLG && c + u < ne; ++u) gain -= __shfl(maxp, base + u);  // gain -= maxp, entry order
   }
-  for (int k = 0; k < q.num_vimages; ++k) {
-    const int t = q.vimages[k];
-    if (s.tnum <= t) continue;
-    const float pdepth = depth_of(s.views[t], q.coord);
-    const long long c = F.tgoff[t] + (long long)q.vgrids[k][1] * gwidth(s, t) + q.vgrids[k][0];
-    float maxp = 0.0f;
-    for (int e = F.pg_off[c]; e < F.pg_off[c + 1]; ++e) {
-      const int j = F.pg_items[e];
-      const float bdepth = depth_of(s.views[t], F.hot[j].coord);
-      if (pdepth < bdepth && !is_neighbor(s, F, p, j, 1.0f)) maxp = smax(maxp, F.hot[j].ncc - s.nccThreshold);
-    }
-    gain -= maxp;
-  }
-  remove[p] = (gain < 0.0) ? 1 : 0;
+  if (l == 0) remove[p] = (gain < 0.0) ? 1 : 0;
 }
 
 __global__ void clear_fixed_kernel(const pmvs_patch* __restrict__ P, int n, int* __restrict__ flags) {
@@ -2281,6 +2371,10 @@ static void trace_error(hipError_t e, int line) {
   } while (0)
 
 static inline unsigned nblk(long long n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+static int dm_tpt() {  // depth_map_kernel's targets per thread (PMVS_DM_TARGETS; 4: r05x, 134 -> 121 ms per C3 step)
+  static const int v = getenv("PMVS_DM_TARGETS") ? std::max(1, std::min(16, atoi(getenv("PMVS_DM_TARGETS")))) : 4;
+  return v;
+}
 // a grid for the XCD-remapped kernels (xcd_block): nblk rounded up to a multiple of the XCD count
 static inline unsigned xcd_grid(long long n, int b = 256) { return (nblk(n, b) + kXcds - 1) / kXcds * kXcds; }
 
@@ -2573,7 +2667,7 @@ static hipError_t build_lists(Ctx& c, int vis) {
   (vis ? c.nvp : c.npg) = e;
   FCHK(B.ensure_entries((size_t)e, vis));
   items = vis ? B.vp_items : B.pg_items;  // (re)allocated by ensure_entries
-  hipLaunchKernelGGL(emit_entries_kernel, dim3(nblk(c.n)), dim3(256), 0, c.st, c.s, c.P, c.n, reg, vis, B.off, B.tgoff,
+  hipLaunchKernelGGL(emit_entries_kernel, dim3(nblk((long long)c.n * kLG)), dim3(256), 0, c.st, c.s, c.P, c.n, reg, vis, B.off, B.tgoff,
                      B.keys);
   tb = B.temp_bytes;
   if (e > 0) FCHK(hipcub::DeviceRadixSort::SortKeys(B.temp, tb, B.keys, B.keys2, e, 0, 64, c.st));
@@ -2665,7 +2759,8 @@ __global__ void lab_flags_kernel(const int* __restrict__ lab, const int* __restr
 static hipError_t collect(Ctx& c) {
   FilterBuffers& B = c.B;
   FCHK(hipMemsetAsync(B.counters, 0, 8 * sizeof(int), c.st));
-  hipLaunchKernelGGL(first_cell_kernel, dim3(nblk(c.n)), dim3(256), 0, c.st, c.s, c.P, c.n, B.preg, B.tgoff, B.keys,
+  hipLaunchKernelGGL(first_cell_kernel, dim3(std::min(nblk((long long)c.n * kLG), 2048u)), dim3(256), 0, c.st, c.s, c.P, c.n,
+                     B.preg, B.tgoff, B.keys,
                      B.counters);
   size_t tb = B.temp_bytes;
   FCHK(hipcub::DeviceRadixSort::SortKeys(B.temp, tb, B.keys, B.keys2, c.n, 0, 64, c.st));
@@ -2690,8 +2785,8 @@ static hipError_t set_dm_vgrids(Ctx& c, int additive) {
   // owner-partitioned: this rank's targets only (t = rank + world j)
   const int nown = (c.s.tnum - c.rank + c.world - 1) / c.world;
   if (c.nalive > 0 && nown > 0)
-    hipLaunchKernelGGL(depth_map_kernel, dim3(nblk((long long)c.nalive * nown)), dim3(256), 0, c.st, c.s, c.dev(), B.coordc,
-                       B.dpkey, c.rank, c.world);
+    hipLaunchKernelGGL(depth_map_kernel, dim3(nblk((long long)c.nalive * ((nown + dm_tpt() - 1) / dm_tpt()))), dim3(256), 0,
+                       c.st, c.s, c.dev(), B.coordc, B.dpkey, c.rank, c.world, dm_tpt());
   dbg(c.st, "  depth");
   FCHK(hipMemsetAsync(B.vreg, 0, c.n * sizeof(Reg), c.st));
   if (c.nalive > 0) {
@@ -2706,7 +2801,8 @@ static hipError_t set_dm_vgrids(Ctx& c, int additive) {
     hipLaunchKernelGGL(normalc_kernel, dim3(nblk(c.nalive)), dim3(256), 0, c.st, c.P, B.order, c.nalive, B.normalc);
     hipLaunchKernelGGL(used_kernel, dim3(nblk(c.nalive)), dim3(256), 0, c.st, c.s, c.dev(), additive, B.used);
     if (nown > 0)
-      hipLaunchKernelGGL(vis_rows_kernel, dim3(nblk((long long)nown * row_words * 64)), dim3(256), 0, c.st, c.s, c.dev(),
+      hipLaunchKernelGGL(vis_rows_kernel, dim3(nblk((long long)((nown + kVisT - 1) / kVisT) * row_words * 64)), dim3(256), 0,
+                         c.st, c.s, c.dev(),
                          B.coordc, B.normalc, B.used, c.rank, c.world, nown, row_words, B.vrows);
     const unsigned long long* rows = B.vrows;
     if (c.world > 1) {
@@ -2815,12 +2911,12 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
   for (int k = 0; k < 4; ++k) counts[k] = 0;
   *overflow = 0;
   FCHK(hipMemsetAsync(B.counters + 8, 0, sizeof(int), st));  // vimages list overflows (vis_lists_kernel)
-  hipLaunchKernelGGL(init_reg_kernel, dim3(nblk(n)), dim3(256), 0, st, s, dP, n, B.preg, B.vreg);
+  hipLaunchKernelGGL(init_reg_kernel, dim3(nblk((long long)n * kLG)), dim3(256), 0, st, s, dP, n, B.preg, B.vreg);
   FCHK(set_dm_vgrids(c, 0));
   dbg(st, "set_dm_vgrids(0)");
   // ---- filterOutside
   FCHK(hipMemsetAsync(B.flags, 0, n * sizeof(int), st));
-  if (c.nalive) hipLaunchKernelGGL(gain_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, s, c.dev(), B.flags, R, G);
+  if (c.nalive) hipLaunchKernelGGL(gain_kernel, dim3(nblk((long long)c.nalive * kLG)), dim3(256), 0, st, s, c.dev(), B.flags, R, G);
   if (part) FCHK(merge_flags(0, nullptr));
   FCHK(apply_flags(c, &counts[0]));
   dbg(st, "outside");
@@ -3839,7 +3935,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   FCHK(hipMemcpyAsync(B.tgoff, h_tgoff, (s.tnum + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
   Ctx c{s, B, dP, n0, ncells, grid, st};
   // ---- model load (the state CFilter::run leaves): registrations, collect order, depth maps, lists
-  hipLaunchKernelGGL(init_reg_kernel, dim3(nblk(n0)), dim3(256), 0, st, s, dP, n0, B.preg, B.vreg);
+  hipLaunchKernelGGL(init_reg_kernel, dim3(nblk((long long)n0 * kLG)), dim3(256), 0, st, s, dP, n0, B.preg, B.vreg);
   hipLaunchKernelGGL(alive_reg_kernel, dim3(nblk(n0)), dim3(256), 0, st, n0, d_alive, B.preg, B.vreg, dP);
   FCHK(build_lists(c, 0));
   FCHK(collect(c));
@@ -3847,8 +3943,8 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   if (c.nalive > 0 && !(flags & 1))  // after the seed phase the depth maps are still empty
   {
     hipLaunchKernelGGL(coordc_kernel, dim3(nblk(c.nalive)), dim3(256), 0, st, dP, B.order, c.nalive, B.coordc);
-    hipLaunchKernelGGL(depth_map_kernel, dim3(nblk((long long)c.nalive * s.tnum)), dim3(256), 0, st, s, c.dev(), B.coordc,
-                       B.dpkey);
+    hipLaunchKernelGGL(depth_map_kernel, dim3(nblk((long long)c.nalive * ((s.tnum + dm_tpt() - 1) / dm_tpt()))), dim3(256), 0,
+                       st, s, c.dev(), B.coordc, B.dpkey, 0, 1, dm_tpt());
   }
   FCHK(build_lists(c, 1));
   // ---- registrations committed by this run: per-cell chains (no per-wave rebuild of the CSR)

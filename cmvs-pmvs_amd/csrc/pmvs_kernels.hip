@@ -193,6 +193,7 @@ __device__ void grab_batch(const DScene& s, WaveLds<WS>& L, int cnt, const int* 
     const int slot = slot0 + lane;
     if (L.valid[slot]) {
       float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+      #pragma unroll 7  // a bounded unroll: the full 49-step one held every texel in registers (pre / post spilled)
       for (int i = 0; i < S; ++i) {
         const float4 q = *reinterpret_cast<const float4*>(L.tex[slot][i]);
         a0 += q.x; a1 += q.y; a2 += q.z;
@@ -200,6 +201,7 @@ __device__ void grab_batch(const DScene& s, WaveLds<WS>& L, int cnt, const int* 
       const float fs3 = (float)S;
       a0 = __fdiv_rn(a0, fs3); a1 = __fdiv_rn(a1, fs3); a2 = __fdiv_rn(a2, fs3);
       float ave2 = 0.0f;
+      #pragma unroll 7
       for (int i = 0; i < S; ++i) {
         const float4 q = *reinterpret_cast<const float4*>(L.tex[slot][i]);
         const float f0 = a0 - q.x, f1 = a1 - q.y, f2 = a2 - q.z;
@@ -228,6 +230,7 @@ template <int WS>
 __device__ __forceinline__ float tex_dot(const WaveLds<WS>& L, int a, int b) {
   constexpr int S = WS * WS;
   float ans = 0.0f;
+  #pragma unroll 7
   for (int i = 0; i < S; ++i) {
     const float4 p = *reinterpret_cast<const float4*>(L.tex[a][i]);
     const float4 q = *reinterpret_cast<const float4*>(L.tex[b][i]);
@@ -1498,8 +1501,16 @@ namespace pmvsdev {
 // Kernel 1: preProcess, one wavefront per candidate, persistent with a device work queue.  Pre and
 // post are latency-bound wave-per-candidate walks: a 256-register budget (2 waves per SIMD, the
 // persistent grid's 8 per CU) instead of the 324 the inlined code would take (1 per SIMD).
+// Round 5: with the texture loops' unroll bounded (grab_batch, tex_dot) they fit 188 / 150
+// registers without spills, and 3 waves per SIMD measured best (r05w: pre 161 -> 144, post 207 ->
+// 200 ms per C3 step against round 4's 2 waves with spills; 4 waves no better).  PMVS_PREPOST_WPE:
+// the waves-per-SIMD target (timing variants).
+#ifndef PMVS_PREPOST_WPE
+#define PMVS_PREPOST_WPE 3
+#endif
+int prepost_waves() { return PMVS_PREPOST_WPE; }
 template <int WS>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void pre_kernel(DScene s, const pmvs_candidate* __restrict__ in,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PMVS_PREPOST_WPE))) void pre_kernel(DScene s, const pmvs_candidate* __restrict__ in,
                                                   RefineJob* __restrict__ jobs, float4* __restrict__ enc, int n,
                                                   DevStats* st) {
   __shared__ WaveLds<WS> L;
@@ -1521,7 +1532,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void pr
 
 // Kernel 3: postProcess, one wavefront per candidate.
 template <int WS>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void post_kernel(DScene s, const RefineJob* __restrict__ jobs,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PMVS_PREPOST_WPE))) void post_kernel(DScene s, const RefineJob* __restrict__ jobs,
                                                    pmvs_refined* __restrict__ out, int n, DevStats* st) {
   __shared__ WaveLds<WS> L;
   unsigned long long acc[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -1768,7 +1779,9 @@ template <int WS>
 static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out,
                                    int n, DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream,
                                    hipEvent_t* ev, RefineHost& rh) {
-  const int g = grid < n ? grid : n;
+  // pre / post: the persistent grid (2 single-wave workgroups per SIMD) scaled to their residency
+  const int gp = grid * PMVS_PREPOST_WPE / 2;
+  const int g = gp < n ? gp : n;
   hipError_t e = rh.ensure((size_t)n);
   if (e != hipSuccess) return e;
   (void)hipEventRecord(ev[0], stream);

@@ -37,6 +37,9 @@ struct RefineHost {
   void release();
   ~RefineHost() { release(); }
 };
+// Waves per SIMD pre_kernel / post_kernel are built for (PMVS_PREPOST_WPE, default 2); their
+// persistent grid is the scene grid x this / 2, and the per-workgroup global scratch is sized for it.
+int prepost_waves();
 hipError_t launch_refine(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out, int n,
                          DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream, hipEvent_t* ev,
                          RefineHost& rh);
