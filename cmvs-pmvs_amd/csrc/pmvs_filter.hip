@@ -2371,6 +2371,15 @@ static void trace_error(hipError_t e, int line) {
   } while (0)
 
 static inline unsigned nblk(long long n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+// The (cell << 32 | index) keys of the list builds, the collect order and the commit are written in
+// index order, and hipcub's radix sort is stable: sorting only the cell bits [32, 32 + cell_bits)
+// gives the full 64-bit order (ties by index = input order) in about half the passes.  2^cell_bits
+// > ncells, so the collect's dead-patch keys (~0) still sort after every cell.
+static int cell_bits(long long ncells) {
+  int b = 1;
+  while (b < 31 && (1ll << b) <= ncells) ++b;
+  return b;
+}
 static int dm_tpt() {  // depth_map_kernel's targets per thread (PMVS_DM_TARGETS; 4: r05x, 134 -> 121 ms per C3 step)
   static const int v = getenv("PMVS_DM_TARGETS") ? std::max(1, std::min(16, atoi(getenv("PMVS_DM_TARGETS")))) : 4;
   return v;
@@ -2670,7 +2679,7 @@ static hipError_t build_lists(Ctx& c, int vis) {
   hipLaunchKernelGGL(emit_entries_kernel, dim3(nblk((long long)c.n * kLG)), dim3(256), 0, c.st, c.s, c.P, c.n, reg, vis, B.off, B.tgoff,
                      B.keys);
   tb = B.temp_bytes;
-  if (e > 0) FCHK(hipcub::DeviceRadixSort::SortKeys(B.temp, tb, B.keys, B.keys2, e, 0, 64, c.st));
+  if (e > 0) FCHK(hipcub::DeviceRadixSort::SortKeys(B.temp, tb, B.keys, B.keys2, e, 32, 32 + cell_bits(c.ncells), c.st));
   FCHK(memset_big(B.cellcnt, 0, (c.ncells + 1) * sizeof(int), c.st));
   if (e > 0) {
     hipLaunchKernelGGL(cell_hist_kernel, dim3(nblk(e)), dim3(256), 0, c.st, B.keys2, e, B.cellcnt);
@@ -2763,7 +2772,7 @@ static hipError_t collect(Ctx& c) {
                      B.preg, B.tgoff, B.keys,
                      B.counters);
   size_t tb = B.temp_bytes;
-  FCHK(hipcub::DeviceRadixSort::SortKeys(B.temp, tb, B.keys, B.keys2, c.n, 0, 64, c.st));
+  FCHK(hipcub::DeviceRadixSort::SortKeys(B.temp, tb, B.keys, B.keys2, c.n, 32, 32 + cell_bits(c.ncells), c.st));
   FCHK(read_int(B.counters, &c.nalive, c.st));
   FCHK(hipMemsetAsync(B.rank, 0xff, c.n * sizeof(int), c.st));
   if (c.nalive > 0)
@@ -3799,12 +3808,13 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
     hipLaunchKernelGGL(cm_emit_kernel, dim3(nblk(nk)), dim3(256), 0, st, W.stc, slot2v, X.crec, W.aoff, nk, W.keys,
                        W.vals);
     tb = 0;
-    FCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, W.keys, W.keys2, W.vals, W.vals2, na, 0, 64, st));
+    const int cb = X.ncells > 0 ? 32 + cell_bits(X.ncells) : 64;
+    FCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, W.keys, W.keys2, W.vals, W.vals2, na, 32, cb, st));
     size_t tb2 = 0;
     FCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb2, W.head, W.segid, na, st));
     FCHK(temp_need(std::max(tb, tb2)));
     tb = W.temp_bytes;
-    FCHK(hipcub::DeviceRadixSort::SortPairs(W.temp, tb, W.keys, W.keys2, W.vals, W.vals2, na, 0, 64, st));
+    FCHK(hipcub::DeviceRadixSort::SortPairs(W.temp, tb, W.keys, W.keys2, W.vals, W.vals2, na, 32, cb, st));
     hipLaunchKernelGGL(cm_head_kernel, dim3(nblk(na)), dim3(256), 0, st, W.keys2, W.vals2, na, W.head, W.pos);
     tb = W.temp_bytes;
     FCHK(hipcub::DeviceScan::InclusiveSum(W.temp, tb, W.head, W.segid, na, st));
@@ -3934,6 +3944,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   FCHK(grow_keep(dP, dP_cap, pcap, (size_t)n0, st));
   FCHK(hipMemcpyAsync(B.tgoff, h_tgoff, (s.tnum + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
   Ctx c{s, B, dP, n0, ncells, grid, st};
+  X.ncells = ncells;
   // ---- model load (the state CFilter::run leaves): registrations, collect order, depth maps, lists
   hipLaunchKernelGGL(init_reg_kernel, dim3(nblk((long long)n0 * kLG)), dim3(256), 0, st, s, dP, n0, B.preg, B.vreg);
   hipLaunchKernelGGL(alive_reg_kernel, dim3(nblk(n0)), dim3(256), 0, st, n0, d_alive, B.preg, B.vreg, dP);

@@ -157,6 +157,7 @@ struct H2DStage {
 };
 struct ExpandBuffers {
   CommitWork* cm = nullptr;
+  long long ncells = 0;  // target cells of the pass (the commit sorts only the cell bits of its keys)
   // (the initial queue run is built on the device: qkeep / qpos / qitems)
   H2DStage h2d;
   unsigned char* occ = nullptr;  // per target cell: pgrids holds a patch (device commit)

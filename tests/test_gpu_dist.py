@@ -31,9 +31,9 @@ import hashlib, json, os, sys
 sys.path[:0] = [sys.argv[1], os.path.join(sys.argv[1], "cmvs-pmvs_amd")]
 import numpy as np
 import pmvs_amd as P
-def scene_and_seeds(views, ids=None):
-    full, p = P.synth_scene(views, 320, 240, level=1, supersample=2, nthreads=8)
-    cands = P.synth_candidates(p, full.projections, 300, seed=7)
+def scene_and_seeds(views, ids=None, w=320, h=240, level=1, ncand=300):
+    full, p = P.synth_scene(views, w, h, level=level, supersample=2, nthreads=8)
+    cands = P.synth_candidates(p, full.projections, ncand, seed=7)
     if ids is None:
         g = P.Scene(full)
         r, _ = g.refine_batch(cands)
@@ -57,14 +57,19 @@ import torch.distributed as dist
 rank, world, mode = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]), sys.argv[2]
 dist.init_process_group("gloo", rank=rank, world_size=world)
 ex = P.DistExchange()
+kw = dict(wave=256, min_candidates=512)
 if mode == "shard":
     inp, g, seeds = scene_and_seeds(6)
     ex.attach(g)
+elif mode == "shard_ring50":  # a 50-view 1280x720 ring at level 0, the bench's C3 schedule
+    inp, g, seeds = scene_and_seeds(50, None, 1280, 720, 0, 2000)
+    ex.attach(g)
+    kw = dict(wave=32768, min_candidates=131072)
 else:
     ids = json.loads(sys.argv[3])[rank]
     inp, g, seeds = scene_and_seeds(8, ids)
     g.set_cluster(rank, world, ids, ex.fn, None)
-out, log = g.run_loop(seeds, inp.threshold, wave=256, min_candidates=512)
+out, log = g.run_loop(seeds, inp.threshold, **kw)
 g.close()
 print("RESULT", json.dumps({"rank": rank, "n": len(out), "digest": digest(out),
                             "sent": [it["boundary"]["sent"] for it in log]}), flush=True)
@@ -144,6 +149,24 @@ def test_two_process_sharded_loop_gloo(gpu_available):
     ref, _ = g.run_loop(P.patches_from_refined(r), full.threshold, wave=256, min_candidates=512)
     g.close()
     res = _run_gloo("shard")
+    digest = hashlib.sha1(ref.tobytes()).hexdigest()
+    assert [x["digest"] for x in res] == [digest, digest], (len(ref), res)
+
+
+@pytest.mark.timeout(600)
+def test_two_process_sharded_ring50_720p_gloo(gpu_available):
+    """The owner-partitioned loop (wave-sharded refine / findEmptyBlocks / postProcess, target-owner
+    filter stages) on a 50-view 1280x720 ring at level 0 with the bench's C3 schedule, two processes
+    over gloo: both ranks' models equal the one-rank model byte for byte."""
+    import pmvs_amd as P
+    full, p = P.synth_scene(50, 1280, 720, level=0, supersample=2, nthreads=8)
+    cands = P.synth_candidates(p, full.projections, 2000, seed=7)
+    g = P.Scene(full)
+    r, _ = g.refine_batch(cands)
+    ref, _ = g.run_loop(P.patches_from_refined(r), full.threshold, wave=32768, min_candidates=131072)
+    g.close()
+    assert len(ref) > 50_000
+    res = _run_gloo("shard_ring50")
     digest = hashlib.sha1(ref.tobytes()).hexdigest()
     assert [x["digest"] for x in res] == [digest, digest], (len(ref), res)
 
