@@ -1152,10 +1152,11 @@ pmvs_status expand_device(pmvs_scene* sc, int n0, int wave, int min_cands, int c
                                    tgoff[sc->ds.tnum], tgoff.data(), wave, cthr, flags, sc->grid, sc->stream, refine, sh,
                                    sv, n_out, min_cands);
   if (handled) *handled = e != hipSuccess;  // expand_pass ends every failure with a header all ranks see
-  if (e == hipErrorOutOfMemory)
+  if (e == kCapacityOverflow)
     return fail(PMVS_EUNSUPPORTED,
                 "expansion: capacity %d exceeded, a patch has more than 16384 neighbours, or a patch's image / "
                 "visible-target list exceeds %d entries", cap, PMVS_MAX_IMAGES);
+  if (e == hipErrorOutOfMemory) return fail(PMVS_ENOMEM, "expansion: device memory");
   if (e == hipErrorUnknown && sh.world > 1) return fail(PMVS_EDEVICE, "expansion: the shard exchange or another rank failed");
   HIPCHK(e);
   if (handled) *handled = false;  // from here on a failure is this rank's alone
@@ -1371,6 +1372,14 @@ pmvs_status pmvs_run_loop(pmvs_scene* sc, const pmvs_patch* seeds, int32_t n, fl
       int own = 0;
       if ((st = drop(cur, &own))) return fail_loop(st, false);
       li.patches = own;
+      // PMVS_LOOP_LEAN=1: the pass buffers go back to the device while this rank waits for its peers
+      // (several 8K clusters sharing one GPU, tests/test_gpu_c5_exchange.py); the next pass reserves
+      // them again
+      if (getenv("PMVS_LOOP_LEAN")) {
+        if (hipStreamSynchronize(sc->stream) != hipSuccess) return fail_loop(fail(PMVS_EDEVICE, "loop synchronisation"), false);
+        sc->fbuf.release();
+        sc->xbuf.release();
+      }
       const ClusterMaps cm{sc->cl_shared.p, sc->cl_ids.p, sc->cl_id2idx.p, sc->cl_maxid};
       long long xs[3] = {0, 0, 0};
       bool agreed = false;

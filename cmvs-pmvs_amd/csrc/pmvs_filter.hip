@@ -22,6 +22,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <new>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -2070,6 +2071,184 @@ __global__ __launch_bounds__(64) NB_WALK_ATTR void empty_blocks_kernel(DScene s,
   }
 }
 
+// findEmptyBlocks' re-walk of the parents whose neighbour set overflowed the NB_CAP walk (round 5:
+// replaces the NB_CAP_BIG form, whose 16 384-entry LDS buffer could overflow in its turn on dense
+// 8K clusters).  fill[] of the reference (expand.cpp:160-176) only needs, per angular bin, whether
+// some term is > 0 and whether one is NaN; neither depends on the order of the neighbour list or on
+// duplicates in it, so this walk bins each neighbour as it meets it: no buffer, no sort, no
+// capacity.  As the only walk it measured 10 % slower (duplicates re-tested, 146 registers, branch
+// exp-stream-walks); as the re-walk of a few parents its speed does not matter.
+__device__ __forceinline__ void eb_bin(const float* hc, const float* qc, const float* xdir, const float* ydir, float rlow,
+                                       float rhigh, unsigned& pos, unsigned& nan) {
+  float d[4];
+  for (int c = 0; c < 4; ++c) d[c] = hc[c] - qc[c];
+  float f0 = dot4(d, xdir), f1 = dot4(d, ydir);
+  const float len = (float)sqrt((double)(f0 * f0 + f1 * f1));
+  if (len < rlow || rhigh < len) return;
+  f0 = __fdiv_rn(f0, len);
+  f1 = __fdiv_rn(f1, len);
+  float angle = (float)atan2((double)f1, (double)f0);
+  if (angle < 0.0) angle = (float)((double)angle + 2 * M_PI);
+  const float findex = (float)((double)angle / (2 * M_PI / 6));
+  const int lindex = (int)floor((double)findex);
+  const int hindex = lindex + 1;
+  const float t0 = (float)hindex - findex, t1 = findex - (float)lindex;
+  const int b0 = ((lindex % 6) + 6) % 6, b1 = ((hindex % 6) + 6) % 6;
+  if (t0 > 0.0f) pos |= 1u << b0;
+  if (t0 != t0) nan |= 1u << b0;
+  if (t1 > 0.0f) pos |= 1u << b1;
+  if (t1 != t1) nan |= 1u << b1;
+}
+
+__global__ __launch_bounds__(64) NB_WALK_ATTR void empty_blocks_stream_kernel(DScene s, FilterDev F, const int* __restrict__ parents,
+                                                                              float* __restrict__ cand_coord, int* __restrict__ cand_ok,
+                                                                              int* __restrict__ queue, NbOverflow ov) {
+  __shared__ NbSmall L;
+  const int lane = threadIdx.x;
+  constexpr int margin = 1;
+  for (;;) {
+    int i = 0;
+    if (lane == 0) i = atomicAdd(queue, 1);
+    i = __builtin_amdgcn_readfirstlane(i);
+    if (i >= *ov.only_n) break;
+    const int pk = __builtin_amdgcn_readfirstlane(ov.only[i]);  // an overflowed parent of the NB_CAP walk
+    const pmvs_patch& q = F.P[parents[pk]];
+    const float radius = compute_radius_wave(s, L, q);
+    float xdir[4] = {0, 0, 0, 0}, ydir[4] = {0, 0, 0, 0};
+    const float* z = q.normal;
+    if (fabs((double)z[0]) > 0.5) { xdir[0] = z[1]; xdir[1] = -z[0]; xdir[2] = 0; }
+    else if (fabs((double)z[1]) > 0.5) { xdir[1] = z[2]; xdir[2] = -z[1]; xdir[0] = 0; }
+    else { xdir[2] = z[0]; xdir[0] = -z[2]; xdir[1] = 0; }
+    unitize4(xdir);
+    ydir[0] = z[1] * xdir[2] - z[2] * xdir[1];
+    ydir[1] = z[2] * xdir[0] - z[0] * xdir[2];
+    ydir[2] = z[0] * xdir[1] - z[1] * xdir[0];
+    const float radiuslow = __fdiv_rn(radius, 6.0f), radiushigh = radius * 2.5f;
+    // findNeighbors(patch, ., 1, 4.0f) (patchOrganizerS.cpp:527-631) as in gather_neighbors: the
+    // cells NB_SK per lane per round, their entries NB_NE per lane at a time
+    const int ni = uni(q.num_images);
+    const float nradius = (float)(1.5 * margin * (double)radius);
+    float unit = 0.0f;
+    for (int k = 0; k < ni; ++k) unit += get_unit(s, s.views[q.images[k]], q.coord);
+    unit = __fdiv_rn(unit, (float)ni);
+    unit *= (float)s.csize;
+    const float thr = 0.5f * 4.0f;
+    const int nlists = ni + uni(q.num_vimages);
+    constexpr int side = 2 * margin + 1, per_list = side * side * 2;
+    const int nslots = nlists * per_list;
+    unsigned pos = 0u, nan = 0u;
+    for (int base = 0; base < nslots; base += 64 * NB_SK) {
+      int bk[NB_SK], ck[NB_SK], hk[NB_SK];
+#pragma unroll
+      for (int k = 0; k < NB_SK; ++k) {
+        const int slot = base + k * 64 + lane;
+        int b = 0, e = 0, lst = 0, head = -1;
+        if (slot < nslots) {
+          const int li = slot / per_list;
+          int r = slot - li * per_list;
+          const int dyi = r / (2 * side);
+          r -= dyi * 2 * side;
+          const int dxi = r >> 1;
+          lst = r & 1;
+          const bool vis = li >= ni;
+          const int t = vis ? q.vimages[li - ni] : q.images[li];
+          if (t < s.tnum) {
+            const int gw = gwidth(s, t), gh = gheight(s, t);
+            const int yt = (vis ? q.vgrids[li - ni][1] : q.grids[li][1]) + dyi - margin;
+            const int xt = (vis ? q.vgrids[li - ni][0] : q.grids[li][0]) + dxi - margin;
+            if (0 <= yt && yt < gh && 0 <= xt && xt < gw) {
+              const long long c = F.tgoff[t] + (long long)yt * gw + xt;
+              const int* off = lst ? F.vp_off : F.pg_off;
+              const int lim = lst ? F.nvp : F.npg;
+              b = off[c];
+              e = off[c + 1];
+              if (b < 0 || e > lim || b > e) {
+                atomicAdd(&F.err[0], 1);
+                atomicExch(&F.err[1], 12 + lst);
+                b = 0;
+                e = 0;
+              }
+              if (F.pg_dhead) head = (lst ? F.vp_dhead : F.pg_dhead)[c];
+            }
+          }
+        }
+        bk[k] = b | (lst << 31);
+        ck[k] = e - b;
+        hk[k] = head;
+      }
+      int mine = 0;
+#pragma unroll
+      for (int k = 0; k < NB_SK; ++k) mine += ck[k];
+      const int offl = wave_excl_scan_w(mine);
+      const int tot = uni(__shfl(offl + mine, 63));
+      {
+        int o = offl;
+#pragma unroll
+        for (int k = 0; k < NB_SK; ++k) {
+          L.sb[lane * NB_SK + k] = bk[k];
+          L.so[lane * NB_SK + k] = o;
+          o += ck[k];
+        }
+      }
+      __syncthreads();
+      for (int ib = 0; ib < tot; ib += 64 * NB_NE) {
+        int jv[NB_NE];
+#pragma unroll
+        for (int u = 0; u < NB_NE; ++u) {
+          const int idx = ib + u * 64 + lane;
+          jv[u] = -1;
+          if (idx < tot) {
+            int sidx = 0;  // the last slot whose offset is <= idx (it holds idx)
+            for (int step = 64 * NB_SK / 2; step >= 1; step >>= 1)
+              if (sidx + step < 64 * NB_SK && L.so[sidx + step] <= idx) sidx += step;
+            const int sb = L.sb[sidx];
+            const int fi = (sb & 0x7fffffff) + idx - L.so[sidx];
+            jv[u] = ((sb < 0) ? F.vp_items : F.pg_items)[fi];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < NB_NE; ++u) {
+          const int j = jv[u];
+          if (ib + u * 64 + lane >= tot) continue;
+          if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 14); continue; }
+          const PHot& h = F.hot[j];
+          if (is_neighbor_h(q, h, unit, thr, nradius, true)) eb_bin(h.coord, q.coord, xdir, ydir, radiuslow, radiushigh, pos, nan);
+        }
+      }
+      // entries committed by earlier expansion waves (short chains, walked per lane)
+#pragma unroll
+      for (int k = 0; k < NB_SK; ++k)
+        for (int ent = hk[k]; ent >= 0; ent = F.d_next[ent]) {
+          const int j = F.d_item[ent];
+          if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 15); continue; }
+          const PHot& h = F.hot[j];
+          if (is_neighbor_h(q, h, unit, thr, nradius, true)) eb_bin(h.coord, q.coord, xdir, ydir, radiuslow, radiushigh, pos, nan);
+        }
+      __syncthreads();
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+      pos |= __shfl_xor(pos, d);
+      nan |= __shfl_xor(nan, d);
+    }
+    if (lane == 0) {
+      for (int b = 0; b < 6; ++b) {
+        int ok = 1;
+        if ((pos >> b & 1u) && !(nan >> b & 1u)) ok = 0;  // 0.0f < fill[b]
+        if (q.dflag & (0x0001 << b)) ok = 0;
+        cand_ok[6 * pk + b] = ok;
+        if (ok) {
+          // expand.cpp:176-177: the angle is stored as float, then cos/sin run in double.
+          const float angle = (float)(2 * M_PI * b / 6);
+          const double cr = cos((double)angle) * (double)radius, sr = sin((double)angle) * (double)radius;
+          for (int c = 0; c < 4; ++c)
+            cand_coord[4 * (6 * pk + b) + c] = (q.coord[c] + (float)((double)xdir[c] * cr)) + (float)((double)ydir[c] * sr);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // CExpand::expandSub up to the refine (expand.cpp:200-226), one thread per candidate slot:
 // setGridsImages from the parent's images, mask / bimages, checkCounts, removeImagesEdge.
 // status: -1 no candidate, 1 rejected, 0 goes to preProcess (pmvs_candidate written).
@@ -2413,6 +2592,11 @@ FilterBuffers::~FilterBuffers() {
     if (p) (void)hipFree(p);
 }
 
+void FilterBuffers::release() {
+  this->~FilterBuffers();
+  new (this) FilterBuffers();
+}
+
 hipError_t FilterBuffers::reserve(int n_, long long ncells_, int tnum_, int grid_) {
   if (n_ <= cap_n && ncells_ <= cap_cells && grid_ <= cap_grid) return hipSuccess;
   // 25 % headroom: the next loop iteration's expansion reserves its model plus a few waves, so an exact
@@ -2690,13 +2874,16 @@ static hipError_t build_lists(Ctx& c, int vis) {
   return hipGetLastError();
 }
 
-__global__ void flag01_kernel(const int* __restrict__ v, int n, int* __restrict__ f) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < n) f[k] = v[k] != 0;
+// flags / scatter over the collect order: out lists the flagged patches in collect order (sorted by
+// their first cell), so concurrent workgroups work on neighbouring patches
+__global__ void flag_order_kernel(const int* __restrict__ v, const int* __restrict__ order, int na, int* __restrict__ f) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < na) f[i] = v[order[i]] != 0;
 }
-__global__ void scatter_index_kernel(const int* __restrict__ f, const int* __restrict__ off, int n, int* __restrict__ out) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < n && f[k]) out[off[k]] = k;
+__global__ void scatter_order_kernel(const int* __restrict__ f, const int* __restrict__ off, const int* __restrict__ order,
+                                     int na, int* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < na && f[i]) out[off[i]] = order[i];
 }
 
 __global__ void pack_bits_kernel(const int* __restrict__ f, int n, unsigned* __restrict__ bits) {
@@ -2727,6 +2914,9 @@ __global__ void lab_relax_kernel(const int* __restrict__ eoff, const int* __rest
                                  int* active, int all, int* changed) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= na) return;
+  // a plain read first: most vertices are inactive in most sweeps, and an atomic per vertex per sweep
+  // cost more than the relaxation (a flag set during this sweep and read stale stays set for the next)
+  if (!all && __builtin_nontemporal_load(&active[i]) == 0) return;
   if (atomicExch(&active[i], 0) == 0 && !all) return;
   const int li = atomicAdd(&lab[i], 0);
   bool any = false;
@@ -2946,14 +3136,20 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
     hipLaunchKernelGGL(exact_patch_kernel, dim3((c.nalive + 3) / 4), dim3(256), 0, st, s, c.dev(), B.safe, B.preg, B.vreg,
                        B.need, B.counters + 2);
   {
-    // the patches that need setRefImage, in index order: compacted on the device
-    hipLaunchKernelGGL(flag01_kernel, dim3(nblk(n)), dim3(256), 0, st, B.need, n, B.cnt);
-    FCHK(hipMemsetAsync(B.cnt + n, 0, sizeof(int), st));
-    size_t tb = B.temp_bytes;
-    FCHK(hipcub::DeviceScan::ExclusiveSum(B.temp, tb, B.cnt, B.off, n + 1, st));
-    hipLaunchKernelGGL(scatter_index_kernel, dim3(nblk(n)), dim3(256), 0, st, B.cnt, B.off, n, B.list);
+    // the patches that need setRefImage (all collected: exact_patch_kernel sets need over the collect
+    // order), compacted on the device in collect order -- sorted by their first cell, so the
+    // persistent grid's concurrent patches are neighbours and share their texels in L2 (index
+    // order, round 4, scattered them: 68 GB of texel reads per C3 launch)
+    const int na = c.nalive;
     int m = 0;
-    FCHK(read_int(B.off + n, &m, st));
+    if (na > 0) {
+      hipLaunchKernelGGL(flag_order_kernel, dim3(nblk(na)), dim3(256), 0, st, B.need, B.order, na, B.cnt);
+      FCHK(hipMemsetAsync(B.cnt + na, 0, sizeof(int), st));
+      size_t tb = B.temp_bytes;
+      FCHK(hipcub::DeviceScan::ExclusiveSum(B.temp, tb, B.cnt, B.off, na + 1, st));
+      hipLaunchKernelGGL(scatter_order_kernel, dim3(nblk(na)), dim3(256), 0, st, B.cnt, B.off, B.order, na, B.list);
+      FCHK(read_int(B.off + na, &m, st));
+    }
     if (part) {  // the owners' setRefImage outcomes (m is the same on every rank)
       FCHK(fgrow(B.refpos, B.cap_refpos, (size_t)std::max(m, 1)));
       FCHK(fgrow(B.xr, B.cap_xr, (size_t)std::max(m, 1) * 4 * G));
@@ -3376,6 +3572,11 @@ ExpandBuffers::~ExpandBuffers() {
   for (void* p : ps)
     if (p) (void)hipFree(p);
   delete_commit_work(cm);
+}
+
+void ExpandBuffers::release() {
+  this->~ExpandBuffers();
+  new (this) ExpandBuffers();
 }
 
 // Grows a device array keeping its contents (the delta-chain entry pool, the per-patch arrays).
@@ -4062,15 +4263,15 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
       // candidates (24 floats + 6 flags per parent) all-gathered, so every rank holds the chunk's.
       const int pch = (nc + G - 1) / G;
       const int plo = (G > 1) ? std::min(nc, R * pch) : 0, phi = (G > 1) ? std::min(nc, plo + pch) : nc;
-      if (phi > plo) {  // the NB_CAP walk, then the NB_CAP_BIG re-walk of the parents it overflowed on
+      if (phi > plo) {  // the NB_CAP walk, then the unbounded re-walk of the parents it overflowed on
         NbOverflow nbw, nbr;
         FCHK(nb_overflow_lists(B, (size_t)(phi - plo), st, nbw, nbr));
         hipLaunchKernelGGL(empty_blocks_kernel<NB_CAP>, dim3(std::min(grid * NB_GRID_MULT, phi - plo)), dim3(64), 0, st, s,
                            c.dev(), X.parents + off + plo, phi - plo, X.cand_coord + (size_t)(off + plo) * 24,
                            X.cand_ok + (size_t)(off + plo) * 6, B.counters + 4, B.counters + 3, nbw);
-        hipLaunchKernelGGL(empty_blocks_kernel<NB_CAP_BIG>, dim3(NB_GRID_BIG), dim3(64), 0, st, s, c.dev(),
-                           X.parents + off + plo, phi - plo, X.cand_coord + (size_t)(off + plo) * 24,
-                           X.cand_ok + (size_t)(off + plo) * 6, B.counters + 11, B.counters + 3, nbr);
+        hipLaunchKernelGGL(empty_blocks_stream_kernel, dim3(NB_GRID_BIG), dim3(64), 0, st, s, c.dev(), X.parents + off + plo,
+                           X.cand_coord + (size_t)(off + plo) * 24, X.cand_ok + (size_t)(off + plo) * 6, B.counters + 11,
+                           nbr);
       }
       if (G > 1) {
         hipError_t lerr = hipPeekAtLastError();
@@ -4107,7 +4308,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
           ovf |= hall[2 * r + 1];
         }
         FCHK(lerr);
-        if (ovf) { trace_error(hipErrorOutOfMemory, __LINE__); return hipErrorOutOfMemory; }  // more than NB_CAP neighbours (reported by the API)
+        if (ovf) { trace_error(kCapacityOverflow, __LINE__); return kCapacityOverflow; }  // more than NB_CAP neighbours (reported by the API)
         if (dev ? sh.exchange_dev(X.xsd, pb, X.xrd, st) != 0 : sh.exchange(xsend.data(), pb, xrecv.data()) != 0)
           return hipErrorUnknown;
         agreed = false;
@@ -4272,7 +4473,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
           ovf |= hall[2 * r + 1];
         }
         FCHK(lerr);
-        if (ovf) { trace_error(hipErrorOutOfMemory, __LINE__); return hipErrorOutOfMemory; }  // more than NB_CAP neighbours (reported by the API)
+        if (ovf) { trace_error(kCapacityOverflow, __LINE__); return kCapacityOverflow; }  // more than NB_CAP neighbours (reported by the API)
         if (dev ? sh.exchange_dev(X.xsd, bytes, X.xrd, st) != 0 : sh.exchange(xsend.data(), bytes, xrecv.data()) != 0)
           return hipErrorUnknown;
         agreed = false;
@@ -4288,7 +4489,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
         if (inject && inj_where == 'a' && stats[7] == inj_wave) return hipErrorOutOfMemory;
       }
       FCHK(lerr);
-      if (ovf) { trace_error(hipErrorOutOfMemory, __LINE__); return hipErrorOutOfMemory; }  // more than NB_CAP neighbours (reported by the API)
+      if (ovf) { trace_error(kCapacityOverflow, __LINE__); return kCapacityOverflow; }  // more than NB_CAP neighbours (reported by the API)
       if (m > 0) {
         FCHK(grow(X.crec, X.cap_crec, (size_t)m * kRecInts));
         hipLaunchKernelGGL(commit_rec_kernel, dim3(nblk(m)), dim3(256), 0, st, s, B.tgoff, X.outp, X.ostatus, X.prep2, m,
@@ -4300,11 +4501,11 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
       int ovf2 = 0;
       FCHK(device_commit(s, X, st, np, X.slot2, m, G > 1 ? nullptr : B.counters + 3, &ovf2, cthr, only < 0, first,
                          (long long)X.pool_host, W > 1, dP, co));
-      if (ovf2) { trace_error(hipErrorOutOfMemory, __LINE__); return hipErrorOutOfMemory; }  // more than NB_CAP neighbours
+      if (ovf2) { trace_error(kCapacityOverflow, __LINE__); return kCapacityOverflow; }  // more than NB_CAP neighbours
       for (int q = 0; q < 4; ++q) stats[2 + q] += co.fail[q];
       if (W == 1) pbits |= co.pbits;
       const int added = co.nacc;
-      if (added > 0 && nmodel + added > cap) { trace_error(hipErrorOutOfMemory, __LINE__); return hipErrorOutOfMemory; }
+      if (added > 0 && nmodel + added > cap) { trace_error(kCapacityOverflow, __LINE__); return kCapacityOverflow; }
       stats[6] += added;
       T.mark(7);
       if (added > 0) {

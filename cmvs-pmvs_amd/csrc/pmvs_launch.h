@@ -132,6 +132,7 @@ struct FilterBuffers {
   size_t cap_e = 0, cap_pi = 0, cap_vi = 0;  // entries of keys/keys2, pg_items, vp_items: grown to the lists' size
   hipError_t reserve(int n, long long ncells, int tnum, int grid);
   hipError_t ensure_entries(size_t e, int vis);
+  void release();  // frees every buffer; the next pass reserves again (PMVS_LOOP_LEAN)
   ~FilterBuffers();
 };
 
@@ -155,6 +156,11 @@ struct H2DStage {
     if (done) (void)hipEventDestroy(done);
   }
 };
+// The expansion's logical capacity overflows (more than NB_CAP_BIG neighbours, a list past
+// PMVS_MAX_IMAGES, the model cap) return this code, so the API tells them from a device allocation
+// that failed (hipErrorOutOfMemory: PMVS_ENOMEM).
+constexpr hipError_t kCapacityOverflow = hipErrorNotSupported;
+
 struct ExpandBuffers {
   CommitWork* cm = nullptr;
   long long ncells = 0;  // target cells of the pass (the commit sorts only the cell bits of its keys)
@@ -195,6 +201,7 @@ struct ExpandBuffers {
          cap_vphead = 0, cap_item = 0, cap_next = 0, cap_pused = 0, cap_tcells = 0, cap_tvals = 0,
          cap_qtmp = 0, cap_crec = 0, cap_acc = 0, cap_dupd = 0, cap_cellinit = 0;
   std::vector<int> gw, gh;  // grid sizes of the target images
+  void release();  // frees every buffer; the next pass grows them again (PMVS_LOOP_LEAN)
   ~ExpandBuffers();
 };
 using RefineFn = std::function<hipError_t(const pmvs_candidate* d_in, int n, pmvs_refined* d_out)>;
