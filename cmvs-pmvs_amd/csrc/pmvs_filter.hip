@@ -462,10 +462,12 @@ __global__ void normalc_kernel(const pmvs_patch* __restrict__ P, const int* __re
   normalc[i] = make_float4(c[0], c[1], c[2], c[3]);
 }
 
-// per collected patch: the targets already in its lists (images; vimages too when additive)
+// per collected patch: the targets already in its lists (images; vimages too when additive), kLG
+// lanes per patch (the lists read as the list kernels read them), OR-reduced over the lane group
 __global__ void used_kernel(DScene s, FilterDev F, int additive, unsigned long long* __restrict__ used) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= F.nalive) return;
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = (int)(g / kLG), l = (int)(g % kLG);
+  if (i >= F.nalive) return;  // whole lane groups
   const pmvs_patch& q = F.P[F.order[i]];
   unsigned long long u0 = 0ull, u1 = 0ull, u2 = 0ull, u3 = 0ull;  // registers (a dynamically indexed array went to scratch)
   auto add = [&](int t) {
@@ -477,17 +479,28 @@ __global__ void used_kernel(DScene s, FilterDev F, int additive, unsigned long l
     u3 |= (w == 3) ? b : 0ull;
   };
   static_assert(PMVS_MAX_TARGETS == 256, "four used words per patch");
-  for (int k = 0; k < q.num_images; ++k)
+  const int ni = q.num_images;
+  for (int k = l; k < ni; k += kLG)
     if (q.images[k] < s.tnum) add(q.images[k]);
-  if (additive)
-    for (int k = 0; k < q.num_vimages; ++k) add(q.vimages[k]);
+  if (additive) {
+    const int nv = q.num_vimages;
+    for (int k = l; k < nv; k += kLG) add(q.vimages[k]);
+  }
+  for (int d = 1; d < kLG; d <<= 1) {
+    u0 |= __shfl_xor(u0, d);
+    u1 |= __shfl_xor(u1, d);
+    u2 |= __shfl_xor(u2, d);
+    u3 |= __shfl_xor(u3, d);
+  }
   // word-major (word w of every patch together): vis_rows_kernel's wavefronts read one word of 64
   // consecutive patches, contiguously
-  const size_t na = (size_t)F.nalive;
-  used[i] = u0;
-  used[na + i] = u1;
-  used[2 * na + i] = u2;
-  used[3 * na + i] = u3;
+  if (l == 0) {
+    const size_t na = (size_t)F.nalive;
+    used[i] = u0;
+    used[na + i] = u1;
+    used[2 * na + i] = u2;
+    used[3 * na + i] = u3;
+  }
 }
 
 struct PCN {  // the fields isVisible reads of the tested patch
@@ -2914,10 +2927,14 @@ __global__ void lab_relax_kernel(const int* __restrict__ eoff, const int* __rest
                                  int* active, int all, int* changed) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= na) return;
-  // a plain read first: most vertices are inactive in most sweeps, and an atomic per vertex per sweep
-  // cost more than the relaxation (a flag set during this sweep and read stale stays set for the next)
-  if (!all && __builtin_nontemporal_load(&active[i]) == 0) return;
-  if (atomicExch(&active[i], 0) == 0 && !all) return;
+  // the pointer jump lab[i] = lab[lab[i]] (reachability is transitive) in every sweep, fused here
+  // (round 4 ran it as its own full pass after every other sweep); a jumped vertex relaxes too
+  const int l0 = lab[i], l1 = lab[l0];
+  const bool jumped = l1 < l0 && atomicMin(&lab[i], l1) > l1;
+  if (jumped) atomicOr(changed, 1);
+  // a plain read first (a flag set during this sweep and read stale stays set for the next)
+  if (!all && !jumped && active[i] == 0) return;
+  if (atomicExch(&active[i], 0) == 0 && !all && !jumped) return;
   const int li = atomicAdd(&lab[i], 0);
   bool any = false;
   for (int e = eoff[i]; e < eoff[i + 1]; ++e) {
@@ -2928,15 +2945,6 @@ __global__ void lab_relax_kernel(const int* __restrict__ eoff, const int* __rest
     }
   }
   if (any) atomicOr(changed, 1);
-}
-__global__ void lab_jump_kernel(int* lab, int na, int* active, int* changed) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= na) return;
-  const int l = lab[i], ll = lab[l];
-  if (ll < l && atomicMin(&lab[i], ll) > ll) {
-    atomicOr(&active[i], 1);
-    atomicOr(changed, 1);
-  }
 }
 // Most patches share a few labels (one big component per surface): the lanes holding the wave's
 // first label add it with one atomic, the others one each (no same-address atomic storm).
@@ -2998,7 +3006,7 @@ static hipError_t set_dm_vgrids(Ctx& c, int additive) {
     FCHK(fgrow(B.used, B.cap_used, (size_t)c.nalive * (PMVS_MAX_TARGETS / 64)));
     FCHK(fgrow(B.vrows, B.cap_vrows, rwords));
     hipLaunchKernelGGL(normalc_kernel, dim3(nblk(c.nalive)), dim3(256), 0, c.st, c.P, B.order, c.nalive, B.normalc);
-    hipLaunchKernelGGL(used_kernel, dim3(nblk(c.nalive)), dim3(256), 0, c.st, c.s, c.dev(), additive, B.used);
+    hipLaunchKernelGGL(used_kernel, dim3(nblk((long long)c.nalive * kLG)), dim3(256), 0, c.st, c.s, c.dev(), additive, B.used);
     if (nown > 0)
       hipLaunchKernelGGL(vis_rows_kernel, dim3(nblk((long long)((nown + kVisT - 1) / kVisT) * row_words * 64)), dim3(256), 0,
                          c.st, c.s, c.dev(),
@@ -3297,7 +3305,6 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
         if (ne)
           hipLaunchKernelGGL(lab_relax_kernel, dim3(nblk(na)), dim3(256), 0, st, B.edge_off, B.edges, na, lab, active,
                              verify ? 1 : 0, changed);
-        if (verify || (r & 1)) hipLaunchKernelGGL(lab_jump_kernel, dim3(nblk(na)), dim3(256), 0, st, lab, na, active, changed);
       }
       int ch = 0;
       FCHK(read_int(changed, &ch, st));
@@ -3792,6 +3799,29 @@ __global__ void cm_decide_kernel(DScene s, int nk, const int* __restrict__ slot2
   cm_decide_at(s, k, slot2, rec, aoff, nacc, segof, segfirst, dec, stc, flag, counts, occ, cthr, check, ctr);
 }
 
+// the undecided candidates of a wave's commit, listed after its first rounds (device_commit)
+__global__ void cm_undecided_kernel(const unsigned char* __restrict__ dec, int nk, int* __restrict__ f) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < nk) f[k] = dec[k] ? 0 : 1;
+}
+__global__ void cm_list_kernel(const int* __restrict__ f, const int* __restrict__ pos, int nk, int* __restrict__ list,
+                               int* __restrict__ cnt) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < nk && f[k]) list[pos[k]] = k;
+  if (k == nk - 1) *cnt = pos[k] + f[k];
+}
+// cm_decide_kernel over the listed candidates (grid-stride over *cnt)
+__global__ void cm_decide_list_kernel(DScene s, const int* __restrict__ list, const int* __restrict__ cnt,
+                                      const int* __restrict__ slot2, const int* __restrict__ rec, const int* __restrict__ aoff,
+                                      const int* __restrict__ nacc, const int* __restrict__ segof,
+                                      const int* __restrict__ segfirst, unsigned char* __restrict__ dec, int* __restrict__ stc,
+                                      int* __restrict__ flag, unsigned char* __restrict__ counts, unsigned char* __restrict__ occ,
+                                      int cthr, int check, int* __restrict__ ctr) {
+  const int n = *cnt;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x)
+    cm_decide_at(s, list[t], slot2, rec, aoff, nacc, segof, segfirst, dec, stc, flag, counts, occ, cthr, check, ctr);
+}
+
 // flags of the non-refined candidates (0) and the outcome counters: ctr[3] fail_prep, [4] fail_pre,
 // [5] fail_post, [2] invalid records
 __global__ void cm_noref_kernel(const int* __restrict__ stc, int nk, int* __restrict__ flag, int* __restrict__ ctr) {
@@ -4024,17 +4054,40 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
     // W.vals (the sort's input values) is free from here: each access's segment
     hipLaunchKernelGGL(cm_segof_kernel, dim3(nblk(na)), dim3(256), 0, st, W.pos, W.segid, na, W.vals);
   }
-  // rounds: every round decides at least the lowest undecided candidate
+  // rounds: every round decides at least the lowest undecided candidate.  The first four rounds
+  // decide most of a wave; the candidates still undecided are then listed once (W.scan is free
+  // until the accept scans below) and the later rounds' decide steps visit only them.
   int decided = 0;
+  bool listed = false;
+  int* uflag = W.scan;
+  int* upos = W.scan + (nk + 1);
+  int* ulist = W.scan + 2 * (size_t)(nk + 1);
+  int* ucnt = W.ctr + 9;  // free in this (non-serial) form
+  const unsigned lgrid = std::min(nblk(nk), 1024u);
   for (int round = 0; decided < nlive; ) {
     for (int r = 0; r < 4; ++r, ++round) {
       if (na > 0)  // <= na segments
         hipLaunchKernelGGL(cm_first_kernel, dim3(nblk(na)), dim3(256), 0, st, W.keys2, W.dec, W.seghead, W.ctr + 8, W.segptr,
                            W.segfirst);
-      hipLaunchKernelGGL(cm_decide_kernel, dim3(nblk(nk)), dim3(256), 0, st, s, nk, slot2v, X.crec, W.aoff, W.nacc, W.vals,
-                         W.segfirst, W.dec, W.stc, W.flag, X.counts, X.occ, cthr, check ? 1 : 0, W.ctr);
+      if (listed)
+        hipLaunchKernelGGL(cm_decide_list_kernel, dim3(lgrid), dim3(256), 0, st, s, ulist, ucnt, slot2v, X.crec, W.aoff, W.nacc,
+                           W.vals, W.segfirst, W.dec, W.stc, W.flag, X.counts, X.occ, cthr, check ? 1 : 0, W.ctr);
+      else
+        hipLaunchKernelGGL(cm_decide_kernel, dim3(nblk(nk)), dim3(256), 0, st, s, nk, slot2v, X.crec, W.aoff, W.nacc, W.vals,
+                           W.segfirst, W.dec, W.stc, W.flag, X.counts, X.occ, cthr, check ? 1 : 0, W.ctr);
     }
     FCHK(read_int(W.ctr, &decided, st));
+    if (decided < nlive && !listed) {
+      hipLaunchKernelGGL(cm_undecided_kernel, dim3(nblk(nk)), dim3(256), 0, st, W.dec, nk, uflag);
+      FCHK(hipMemsetAsync(uflag + nk, 0, sizeof(int), st));
+      size_t ub = 0;
+      FCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, ub, uflag, upos, nk + 1, st));
+      FCHK(temp_need(ub));
+      ub = W.temp_bytes;
+      FCHK(hipcub::DeviceScan::ExclusiveSum(W.temp, ub, uflag, upos, nk + 1, st));
+      hipLaunchKernelGGL(cm_list_kernel, dim3(nblk(nk)), dim3(256), 0, st, uflag, upos, nk, ulist, ucnt);
+      listed = true;
+    }
     if (round > 4 * (nlive + 2)) return hipErrorIllegalState;  // cannot happen (progress every round)
   }
   hipLaunchKernelGGL(cm_noref_kernel, dim3(nblk(nk)), dim3(256), 0, st, W.stc, nk, W.flag, W.ctr);
