@@ -2515,7 +2515,8 @@ __global__ void add_patches_kernel(DScene s, FilterDev F, int first, int count, 
   for (int j = 0; j < 2; ++j)
     for (int i = 0; i < 2; ++i) {
       if (xs[i] < 0 || gw <= xs[i] || ys[j] < 0 || gh <= ys[j]) continue;
-      atomicMin(&dpkey[F.tgoff[t] + (long long)ys[j] * gw + xs[i]], key);
+      unsigned long long* cell = &dpkey[F.tgoff[t] + (long long)ys[j] * gw + xs[i]];
+      if (key < *cell) atomicMin(cell, key);  // as depth_map_kernel: a value <= key cannot change
     }
 }
 
