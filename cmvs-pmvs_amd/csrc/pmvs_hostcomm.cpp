@@ -25,6 +25,8 @@
 #include <cerrno>
 #include <chrono>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -246,27 +248,44 @@ int pmvs_tcp_allgather(void* ctx, const void* send, int64_t bytes, void* recv) {
       status = -1;
     }
   }
-  // status to every peer first, then the payload, then a commit word: a peer returns success only
-  // if every peer was served, so the ranks never disagree on the outcome of one exchange.  A peer
-  // whose write fails is closed, which fails its next read.
+  // status to every peer first, then the payload to every peer that was told 0, then a commit word:
+  // a peer returns success only if every peer was served.  A peer told 0 always gets its payload, even
+  // when a later peer fails, so it never waits for bytes that do not come; the commit word is decided
+  // before any is sent, so every live rank returns the same outcome.  A peer whose write fails is
+  // closed, which fails its own read (and every later exchange).
+  // PMVS_TEST_TCP_FAIL=p:k (tests only): the status write to peer p fails in this rank's k-th exchange.
+  static int inj_peer = -2, inj_call = 0, calls = 0;
+  if (inj_peer == -2) {
+    inj_peer = -1;
+    if (const char* e = getenv("PMVS_TEST_TCP_FAIL")) (void)sscanf(e, "%d:%d", &inj_peer, &inj_call);
+  }
+  ++calls;
+  std::vector<int32_t> told(c->world, -1);
   for (int p = 1; p < c->world; ++p) {
     int& fd = c->peers[p];
     if (fd < 0) continue;
-    if (!write_all(fd, &status, sizeof(status))) { ::close(fd); fd = -1; status = -1; }
+    const bool fail = (p == inj_peer && calls == inj_call);
+    if (fail || !write_all(fd, &status, sizeof(status))) {
+      ::close(fd);
+      fd = -1;
+      status = -1;
+    } else {
+      told[p] = status;
+    }
   }
-  if (status == 0 && b)
+  if (b)
     for (int p = 1; p < c->world; ++p) {
       int& fd = c->peers[p];
-      if (fd < 0) continue;
+      if (fd < 0 || told[p] != 0) continue;
       if (!write_all(fd, r, b * (size_t)c->world)) { ::close(fd); fd = -1; status = -1; }
     }
-  if (status == 0)
-    for (int p = 1; p < c->world; ++p)
-      if (c->peers[p] < 0) status = -1;
+  int32_t commit = status;
+  for (int p = 1; p < c->world; ++p)
+    if (c->peers[p] < 0 || told[p] != 0) commit = -1;
   for (int p = 1; p < c->world; ++p) {
     int& fd = c->peers[p];
     if (fd < 0) continue;
-    if (!write_all(fd, &status, sizeof(status))) { ::close(fd); fd = -1; status = -1; }
+    if (!write_all(fd, &commit, sizeof(commit))) { ::close(fd); fd = -1; }
   }
-  return status == 0 ? 0 : -1;
+  return commit == 0 ? 0 : -1;
 }

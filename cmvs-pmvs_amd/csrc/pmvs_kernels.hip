@@ -1766,7 +1766,7 @@ bool refine_config_supported(int tslots) {
     case 1264: case 2464: case 1232: case 2432: case 1216: case 2448: case 3232: case 3248: case 3264: case 4832:
     case 4864: return true;
 #endif
-    default: return refine_split_supported(tslots);
+    default: return refine_split_supported(tslots) || refine_lane_supported(tslots);
   }
 }
 
@@ -1801,6 +1801,16 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
     if (hipEventElapsedTime(&ms, rh.ev_pre, ev[1]) == hipSuccess) rh.trip_ms += ms;
     ++rh.trips;
   }
+  if (tslots >= 300000) {  // lane form (pmvs_refine_lane.hip)
+    if ((e = launch_refine_lane(tslots, s, d_jobs, n, d_st, stream)) != hipSuccess) return e;
+    if (refine_tail_on()) hipLaunchKernelGGL(refine_tail_kernel, dim3(1), dim3(64), 0, stream, d_st, 1);
+    (void)hipEventRecord(ev[2], stream);
+    hipLaunchKernelGGL((post_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_jobs, d_out, n, d_st);
+    (void)hipEventRecord(ev[3], stream);
+    return hipGetLastError();
+  }
+  // (before the tau check below, which then also applies to the fallback layout)
+  if (tslots >= 200000 && tslots < 300000 && WS > 7) tslots = 1206;  // split form: a texture's 3 * 81 samples exceed its registers
   // a request's textures must fit one chunk (TSLOTS >= tau, tau <= PMVS_MAX_TAU = 16): smaller
   // chunk configs are only valid for small tau, otherwise the default 24-slot kernel runs
   if (tslots / 100 < s.tau) {
@@ -1809,7 +1819,6 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
   }
   const int nc = tslots % 100;
   const int rg = refine_grid < (n + nc - 1) / nc ? refine_grid : (n + nc - 1) / nc;
-  if (tslots >= 200000 && WS > 7) tslots = 1206;  // split form: a texture's 3 * 81 samples exceed its registers
   if (tslots >= 200000) {  // split form (pmvs_refine_split.hip)
     if ((e = launch_refine_split(tslots, s, d_jobs, n, d_st, stream)) != hipSuccess) return e;
     if (refine_tail_on()) hipLaunchKernelGGL(refine_tail_kernel, dim3(1), dim3(64), 0, stream, d_st, 0);

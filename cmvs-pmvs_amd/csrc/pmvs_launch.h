@@ -37,7 +37,7 @@ struct RefineHost {
   void release();
   ~RefineHost() { release(); }
 };
-// Waves per SIMD pre_kernel / post_kernel are built for (PMVS_PREPOST_WPE, default 2); their
+// Waves per SIMD pre_kernel / post_kernel are built for (PMVS_PREPOST_WPE, default 3: pmvs_kernels.hip); their
 // persistent grid is the scene grid x this / 2, and the per-workgroup global scratch is sized for it.
 int prepost_waves();
 hipError_t launch_refine(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out, int n,
@@ -47,6 +47,10 @@ hipError_t launch_refine(const DScene& s, const pmvs_candidate* d_in, RefineJob*
 // chains per optimizer wavefront, wsize 5 or 7
 bool refine_split_supported(int config);
 hipError_t launch_refine_split(int config, const DScene& s, RefineJob* d_jobs, int n, DevStats* d_st, hipStream_t stream);
+// lane-form refine kernel (pmvs_refine_lane.hip): one candidate per wavefront, BOBYQA state spread over
+// the lanes; config 300000 (lanes per texture from tau), 300004, 300008
+bool refine_lane_supported(int config);
+hipError_t launch_refine_lane(int config, const DScene& s, RefineJob* d_jobs, int n, DevStats* d_st, hipStream_t stream);
 hipError_t launch_incc_eval(const DScene& s, const pmvs_eval_query* d_q, int n, double* d_out, DevStats* d_st,
                             hipStream_t stream);
 hipError_t launch_grab_tex(const DScene& s, const pmvs_tex_query* d_q, int n, float* d_out, int* d_valid,

@@ -1,19 +1,13 @@
 // tests/csrc/bq_host.cpp -- host build of the DEVICE reverse-communication BOBYQA
 // (cmvs-pmvs_amd/csrc/bobyqa_dev.h) so its trajectories can be compared with the callback
-// oracle (oracle/bobyqa_oracle.h) on the CPU.  Same objectives as oracle_bobyqa_test.
+// oracle (oracle/bobyqa_oracle.h) on the CPU.  Same objectives as oracle_bobyqa_test (bq_objectives.h).
 #include <math.h>
 #include "bobyqa_dev.h"
+#include "bq_objectives.h"
 
 using namespace pmvsdev;
 
-static double objective(int kind, const double* v) {
-  if (kind == 0) return (v[0] - 1.5) * (v[0] - 1.5) + 2 * (v[1] - 3) * (v[1] - 3) + 0.5 * (v[2] + 2) * (v[2] + 2) + 0.1 * v[0] * v[1];
-  if (kind == 1) {
-    const double a = 1 - v[0], b = v[1] - v[0] * v[0], c = v[2] - v[1] * v[1];
-    return a * a + 100 * b * b + 100 * c * c;
-  }
-  return (v[0] - 1) * (v[0] - 1) + (v[1] - 40) * (v[1] - 40) + (v[2] + 50) * (v[2] + 50);
-}
+static double objective(int kind, const double* v) { return bq_objective(kind, v); }
 
 extern "C" int bq_host_run(int kind, const double* x0, int maxeval, double* xout, double* fout, double* frec,
                            int maxrec, int* nrec) {

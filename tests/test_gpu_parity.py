@@ -108,7 +108,7 @@ def test_refine_batch_bit_exact(scenes):
         assert sg[k] == so[k], k
 
 
-REFINE_CONFIGS = [1206, 2408, 164011, 164021, 164041, 148041, 132022, 132042, 116042, 202032, 224016, 225016, 226014, 227012, 228010, 245016, 246014, 248010]
+REFINE_CONFIGS = [300000, 300004, 300008, 1206, 2408, 164011, 164021, 164041, 148041, 132022, 132042, 116042, 202032, 224016, 225016, 226014, 227012, 228010, 245016, 246014, 248010]
 
 
 @pytest.mark.parametrize("config", REFINE_CONFIGS)

@@ -100,6 +100,47 @@ print("ok", rank)
     assert "ok 0" in outs[0][0] and "ok 2" in outs[2][0]
 
 
+def test_tcp_allgather_status_write_failure(product_lib, tmp_path):
+    """pmvs_tcp's dead-peer path (round-5 advisor): rank 0's status write to rank 2 fails after rank 1
+    was already told success (PMVS_TEST_TCP_FAIL=2:2 on rank 0: its second exchange).  Rank 1 must still get its payload and
+    the failing commit word instead of waiting for bytes that never come; every rank returns -1, and
+    the next exchange fails on every live rank too (rank 2's channel is closed) -- nobody blocks."""
+    import socket
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    prog = f"""
+import ctypes as C, sys
+sys.path.insert(0, {os.path.join(ROOT, 'cmvs-pmvs_amd')!r})
+import pmvs_amd as P
+lib = P.load_library()
+rank, world = int(sys.argv[1]), 3
+h = C.c_void_p()
+assert lib.pmvs_tcp_create(rank, world, b"127.0.0.1", {port}, 20000, C.byref(h)) == 0, lib.pmvs_last_error()
+send = bytes([rank + 1] * 5)
+recv = C.create_string_buffer(15)
+assert lib.pmvs_tcp_allgather(h, send, 5, recv) == 0
+r = lib.pmvs_tcp_allgather(h, send, 5, recv)   # rank 0 fails its status write to rank 2
+assert r == -1, (rank, r)
+if rank != 2:
+    r = lib.pmvs_tcp_allgather(h, send, 5, recv)   # rank 2 is cut off: the next exchange fails as well
+    assert r == -1, (rank, r)
+print("ok", rank)
+"""
+    f = tmp_path / "tcp_fail.py"
+    f.write_text(prog)
+    env = dict(os.environ)
+    env.pop("PMVS_TEST_TCP_FAIL", None)
+    ps = [subprocess.Popen([sys.executable, str(f), str(r)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                           env=dict(env, PMVS_TEST_TCP_FAIL="2:2") if r == 0 else env) for r in range(3)]
+    outs = [p.communicate(timeout=60) for p in ps]
+    for r, (p, (o, e)) in enumerate(zip(ps, outs)):
+        assert p.returncode == 0, (r, o, e)
+        assert f"ok {r}" in o
+
+
 def test_jpeg_matches_libjpeg(product_lib, tmp_path):
     import pmvs_amd as P
     cjpeg, djpeg = shutil.which("cjpeg") or "/opt/conda/bin/cjpeg", shutil.which("djpeg") or "/opt/conda/bin/djpeg"
