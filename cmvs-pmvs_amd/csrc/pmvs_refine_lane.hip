@@ -19,6 +19,8 @@
 // (tests/test_gpu_parity.py::test_refine_configs_bit_exact).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "bobyqa_lane.h"
 #include "pmvs_device.h"
 #include "pmvs_launch.h"
@@ -228,6 +230,11 @@ __global__ __launch_bounds__(LANE_THREADS) __attribute__((amdgpu_waves_per_eu(LA
   const int lane = lane_id();
   const int t = lane / LP;
   unsigned long long nevals = 0, tex_valid = 0, grabs = 0, nreq = 0;
+#if defined(LANE_PROFILE)
+  // diagnostic build (tools: make variant VAR=laneprof VARTU=pmvs_refine_lane VARFLAGS=-DLANE_PROFILE):
+  // shader cycles per wavefront in the optimizer step, the objective evaluations, whole candidates
+  unsigned long long prof_step = 0, prof_eval = 0, prof_cand = 0, prof_mark = 0;
+#endif
   if (threadIdx.x == 0) atomicMax(&st->t_first_inv, ~__builtin_amdgcn_s_memrealtime());
   const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999};
   const double ub[3] = {HUGE_VAL, 23.99999, 23.99999};
@@ -262,14 +269,35 @@ __global__ __launch_bounds__(LANE_THREADS) __attribute__((amdgpu_waves_per_eu(LA
       return lane_request<WS, LP>(s, geo, myview, size, need, J, tex_valid);
     };
     auto fobj = [&](const double* xe) -> double {
+#if defined(LANE_PROFILE)
+      const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
       float fc[4], fn[4];
       decode(s, R, xe, fc, fn);
-      return request(fc, fn, 1);
+      const double fv = request(fc, fn, 1);
+#if defined(LANE_PROFILE)
+      const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+      prof_eval += t1 - t0;
+      prof_step += t0 - prof_mark;
+      prof_mark = t1;
+#endif
+      return fv;
     };
     double xo[3], minf = 0.0;
     int nev = 0;
+#if defined(LANE_PROFILE)
+    prof_mark = __builtin_amdgcn_s_memtime();
+    const unsigned long long tc0 = prof_mark;
+#endif
     const int rc = bql::bobyqa(U, fobj, x0, lb, ub, 1.e-7, 1000, xo, &minf, &nev);
     nevals += (unsigned long long)nev;
+#if defined(LANE_PROFILE)
+    {
+      const unsigned long long tc1 = __builtin_amdgcn_s_memtime();
+      prof_step += tc1 - prof_mark;  // the optimizer's tail after its last evaluation
+      prof_cand += tc1 - tc0;
+    }
+#endif
     const bool success = (rc == BQR_SUCCESS || rc == 2 || rc == 3 || rc == BQR_XTOL);
     float fc[4], fn[4];
     float ncc = 0.0f;
@@ -297,6 +325,11 @@ __global__ __launch_bounds__(LANE_THREADS) __attribute__((amdgpu_waves_per_eu(LA
     atomicAdd(&st->rounds, nreq);
     atomicAdd(&st->chunks, nreq);
     atomicMax(&st->t_last, __builtin_amdgcn_s_memrealtime());
+#if defined(LANE_PROFILE)
+    atomicAdd(&st->prof[0], prof_step);
+    atomicAdd(&st->prof[1], prof_eval);
+    atomicAdd(&st->prof[2], prof_cand);
+#endif
   }
 }
 
@@ -316,8 +349,14 @@ static hipError_t launch_lane_ws(int config, const DScene& s, RefineJob* d_jobs,
       (e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
     return e;
   cus = cus > 0 ? cus : 1;
-  // persistent: LANE_WPE wavefronts per SIMD on every CU, no more than the batch needs
-  const int waves = cus * 4 * LANE_WPE;
+  // persistent: LANE_WPE wavefronts per SIMD on every CU (PMVS_LANE_WPS: fewer, for latency
+  // experiments), no more than the batch needs
+  static const int wps = [] {
+    const char* e = getenv("PMVS_LANE_WPS");
+    const int v = e ? atoi(e) : LANE_WPE;
+    return v >= 1 && v <= LANE_WPE ? v : LANE_WPE;
+  }();
+  const int waves = cus * 4 * wps;
   const int need = (n + 3) / 4;
   const int grid = need < waves / 4 ? need : waves / 4;
   if (lp == 8)

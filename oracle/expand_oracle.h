@@ -179,6 +179,23 @@ struct Cand {
   int status;                    // 0 ok, 1 prep fail, 2 preProcess fail, 3 postProcess fail
 };
 
+// CPatchOrganizerS::setGridsImages (patchOrganizerS.cpp:383-399): c.images / c.grids := the entries of
+// `images` whose cell at c.coord lies in the target's grid.  Pinned to the reference's own
+// patchOrganizerS.cpp (tests/test_organizer_pinning.py).
+static void set_grids_images(const OScene& s, const std::vector<int>& images, FPatch& c) {
+  c.images.clear();
+  c.grids.clear();
+  for (int t : images) {
+    const V3 ic = project(s, t, c.coord, s.level);
+    const int ix = ((int)std::floor(ic[0] + 0.5f)) / s.csize;
+    const int iy = ((int)std::floor(ic[1] + 0.5f)) / s.csize;
+    if (0 <= ix && ix < s.gwidths[t] && 0 <= iy && iy < s.gheights[t]) {
+      c.images.push_back(t);
+      c.grids.push_back({ix, iy});
+    }
+  }
+}
+
 // expandSub up to the refine (expand.cpp:200-226): returns 0 when the candidate goes on.
 static int prepare_candidate(const Model& m, const FPatch& par, const V4& coord, int cthr, int depth, FPatch& c,
                              std::vector<int>& edge_images) {
@@ -188,15 +205,7 @@ static int prepare_candidate(const Model& m, const FPatch& par, const V4& coord,
   c.normal = par.normal;
   c.flag = 1;
   c.ncc = -1.0f; c.dscale = 0.0f; c.ascale = 0.0f; c.tmp = 0.0f; c.timages = 0; c.fix = 0;
-  for (int t : par.images) {  // CPatchOrganizerS::setGridsImages (patchOrganizerS.cpp:383-399)
-    const V3 ic = project(s, t, coord, s.level);
-    const int ix = ((int)std::floor(ic[0] + 0.5f)) / s.csize;
-    const int iy = ((int)std::floor(ic[1] + 0.5f)) / s.csize;
-    if (0 <= ix && ix < s.gwidths[t] && 0 <= iy && iy < s.gheights[t]) {
-      c.images.push_back(t);
-      c.grids.push_back({ix, iy});
-    }
-  }
+  set_grids_images(s, par.images, c);
   if (c.images.empty()) return 1;
   if (get_mask_all(s, coord, s.level) == 0 || inside_bimages(s, coord) == 0) return 1;
   if (check_counts(m, c, cthr, depth)) return 1;

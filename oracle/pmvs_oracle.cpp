@@ -907,6 +907,102 @@ void oracle_set_grids(void* h, pmvs_patch* patches, int n) {
   }
 }
 
+// ---- organizer pieces, pinned to the reference's own patchOrganizerS.cpp / photoSetS.cpp compiled
+// in oracle/_ref/organizer (tests/test_organizer_pinning.py).  Records: coords4[4 * i], image lists
+// images[off[i] .. off[i + 1]).
+
+// set_grids_images (expand_oracle.h) per record: out[i * (3 * PMVS_MAX_IMAGES + 1)] = kept entries,
+// then (image, ix, iy) triples.
+void oracle_set_grids_images(void* h, int n, const float* coords4, const int* off, const int* images, int* out) {
+  const OScene& s = *static_cast<const OScene*>(h);
+  const int stride = 3 * PMVS_MAX_IMAGES + 1;
+  for (int i = 0; i < n; ++i) {
+    FPatch c;
+    for (int k = 0; k < 4; ++k) c.coord[k] = coords4[4 * i + k];
+    set_grids_images(s, std::vector<int>(images + off[i], images + off[i + 1]), c);
+    int* o = out + (size_t)i * stride;
+    o[0] = (int)c.images.size();
+    for (size_t k = 0; k < c.images.size() && k < (size_t)PMVS_MAX_IMAGES; ++k) {
+      o[1 + 3 * k] = c.images[k];
+      o[2 + 3 * k] = c.grids[k].first;
+      o[3 + 3 * k] = c.grids[k].second;
+    }
+  }
+}
+
+// set_grids (CPatchOrganizerS::setGrids, full int cells) per record, out as oracle_set_grids_images.
+void oracle_set_grids_full(void* h, int n, const float* coords4, const int* off, const int* images, int* out) {
+  const OScene& s = *static_cast<const OScene*>(h);
+  const int stride = 3 * PMVS_MAX_IMAGES + 1;
+  for (int i = 0; i < n; ++i) {
+    OPatch p;
+    for (int k = 0; k < 4; ++k) p.coord[k] = coords4[4 * i + k];
+    p.images.assign(images + off[i], images + off[i + 1]);
+    set_grids(s, p);
+    int* o = out + (size_t)i * stride;
+    o[0] = (int)p.images.size();
+    for (size_t k = 0; k < p.images.size() && k < (size_t)PMVS_MAX_IMAGES; ++k) {
+      o[1 + 3 * k] = p.images[k];
+      o[2 + 3 * k] = p.grids[k].first;
+      o[3 + 3 * k] = p.grids[k].second;
+    }
+  }
+}
+
+// update_depth_maps (expand_oracle.h, CPatchOrganizerS::updateDepthMaps) for the n patches added in
+// order to empty depth maps; out: every target's cells, row-major, concatenated (patch or -1).
+void oracle_update_depth_maps(void* h, int n, const float* coords4, int* out) {
+  const OScene& s = *static_cast<const OScene*>(h);
+  Model m(s);
+  std::vector<FPatch> P((size_t)n);
+  for (int i = 0; i < n; ++i) {
+    for (int k = 0; k < 4; ++k) P[i].coord[k] = coords4[4 * i + k];
+    update_depth_maps(m, P, i);
+  }
+  size_t o = 0;
+  for (int t = 0; t < s.tnum; ++t)
+    for (int d : m.o.dpgrids[t]) out[o++] = d;
+}
+
+// isVisible0 at depth 0 as set_vimages_vgrids evaluates it: the patch's cell in image t, and
+// is_visible (filter_oracle.h); out3: visible, ix, iy.
+void oracle_is_visible0(void* h, int n, const float* coords4, const int* images, int* out3) {
+  const OScene& s = *static_cast<const OScene*>(h);
+  const Organizer o(s);
+  const std::vector<FPatch> P;
+  for (int i = 0; i < n; ++i) {
+    FPatch q;
+    for (int k = 0; k < 4; ++k) q.coord[k] = coords4[4 * i + k];
+    const int t = images[i];
+    const V3 ic = project(s, t, q.coord, s.level);
+    const int ix = ((int)std::floor(ic[0] + 0.5f)) / s.csize;
+    const int iy = ((int)std::floor(ic[1] + 0.5f)) / s.csize;
+    out3[3 * i] = is_visible(o, P, q, t, ix, iy, 0.5f);
+    out3[3 * i + 1] = ix;
+    out3[3 * i + 2] = iy;
+  }
+}
+
+// check_angles (CPhotoSetS::checkAngles) per record.
+void oracle_check_angles(void* h, int n, const float* coords4, const int* off, const int* idx, float minA, float maxA,
+                         int* out) {
+  const OScene& s = *static_cast<const OScene*>(h);
+  for (int i = 0; i < n; ++i) {
+    V4 c;
+    for (int k = 0; k < 4; ++k) c[k] = coords4[4 * i + k];
+    out[i] = check_angles(s, c, std::vector<int>(idx + off[i], idx + off[i + 1]), minA, maxA);
+  }
+}
+
+// set_distances (seed_oracle.h, CPhotoSetS::setDistances): num x num.
+void oracle_distances(void* h, float* out) {
+  const OScene& s = *static_cast<const OScene*>(h);
+  std::vector<std::vector<float>> d;
+  set_distances(s, d);
+  for (int i = 0; i < s.num; ++i)
+    for (int j = 0; j < s.num; ++j) out[(size_t)i * s.num + j] = d[i][j];
+}
+
 // 1 when a result list exceeded PMVS_MAX_IMAGES since the last reset (see list_len).
 int oracle_list_overflow(int reset) {
   const int v = g_list_overflow.load();

@@ -64,6 +64,12 @@ def lib():
         L.oracle_lls5.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
         L.oracle_bobyqa_test.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_int, C.POINTER(C.c_int)]
+        L.oracle_set_grids_images.argtypes = [C.c_void_p, C.c_int] + [C.c_void_p] * 4
+        L.oracle_set_grids_full.argtypes = [C.c_void_p, C.c_int] + [C.c_void_p] * 4
+        L.oracle_update_depth_maps.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        L.oracle_is_visible0.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_check_angles.argtypes = [C.c_void_p, C.c_int] + [C.c_void_p] * 3 + [C.c_float, C.c_float, C.c_void_p]
+        L.oracle_distances.argtypes = [C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -137,6 +143,88 @@ def _p(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
 
 
+def _lists(lists):
+    off = np.zeros(len(lists) + 1, np.int32)
+    for i, l in enumerate(lists):
+        off[i + 1] = off[i] + len(l)
+    flat = np.array([int(x) for l in lists for x in l] or [0], np.int32)
+    return off, flat
+
+
+def ref_organizer(projections, widths, heights, num_targets, level, csize, ops):
+    """The reference's own CPatchOrganizerS / CPhotoSetS (oracle/_ref/organizer, built from
+    patchOrganizerS.cpp, photoSetS.cpp, camera.cpp and patch.cpp unmodified) on a scene given by its
+    level-0 projections (CONTOUR camera files) and per-level image sizes [V, L]; `ops` as in
+    OracleScene.organizer_ops.  Returns one result per op, or None when _ref is absent."""
+    import struct
+    import subprocess
+    import tempfile
+    exe = os.path.join(HERE, "_ref", "organizer")
+    if not os.path.exists(exe):
+        return None
+    V, L = np.asarray(widths).shape
+    out = bytearray(struct.pack("5i", V, num_targets, level, csize, L))
+    with tempfile.TemporaryDirectory() as d:
+        for v in range(V):
+            path = os.path.join(d, "%08d.txt" % v)
+            with open(path, "w") as f:
+                f.write("CONTOUR\n")
+                for row in projections[v]:
+                    f.write(" ".join(repr(float(x)) for x in row) + "\n")
+            b = path.encode()
+            out += struct.pack("i", len(b)) + b
+            out += np.asarray(widths[v], np.int32).tobytes() + np.asarray(heights[v], np.int32).tobytes()
+        for op in ops:
+            kind = op[0]
+            if kind in ("grids_images", "grids"):
+                coords, lists = op[1], op[2]
+                out += struct.pack("ii", 1 if kind == "grids_images" else 2, len(coords))
+                for c, l in zip(coords, lists):
+                    out += np.asarray(c, np.float32).tobytes() + struct.pack("i", len(l)) + np.asarray(l, np.int32).tobytes()
+            elif kind == "depth":
+                out += struct.pack("ii", 3, len(op[1])) + np.ascontiguousarray(op[1], np.float32).tobytes()
+            elif kind == "vis0":
+                out += struct.pack("ii", 4, len(op[1]))
+                for c, t in zip(op[1], op[2]):
+                    out += np.asarray(c, np.float32).tobytes() + struct.pack("i", int(t))
+            elif kind == "angles":
+                coords, lists, lo, hi = op[1:]
+                out += struct.pack("iiff", 5, len(coords), lo, hi)
+                for c, l in zip(coords, lists):
+                    out += np.asarray(c, np.float32).tobytes() + struct.pack("i", len(l)) + np.asarray(l, np.int32).tobytes()
+            elif kind == "dist":
+                out += struct.pack("i", 6)
+        r = subprocess.run([exe], input=bytes(out), capture_output=True, check=True).stdout
+    gw = [(int(widths[v][level]) + csize - 1) // csize for v in range(V)]
+    gh = [(int(heights[v][level]) + csize - 1) // csize for v in range(V)]
+    pos, res = 0, []
+
+    def ints(k):
+        nonlocal pos
+        a = np.frombuffer(r, np.int32, k, pos).copy()
+        pos += 4 * k
+        return a
+    for op in ops:
+        kind = op[0]
+        if kind in ("grids_images", "grids"):
+            recs = []
+            for _ in range(len(op[1])):
+                m = int(ints(1)[0])
+                recs.append(ints(3 * m).reshape(m, 3))
+            res.append(recs)
+        elif kind == "depth":
+            res.append(ints(sum(gw[t] * gh[t] for t in range(num_targets))))
+        elif kind == "vis0":
+            res.append(ints(3 * len(op[1])).reshape(-1, 3))
+        elif kind == "angles":
+            res.append(ints(len(op[1])))
+        elif kind == "dist":
+            res.append(np.frombuffer(r, np.float32, V * V, pos).reshape(V, V).copy())
+            pos += 4 * V * V
+    assert pos == len(r), (pos, len(r))
+    return res
+
+
 def _check_lists():
     """The oracle never truncates a list: a result list longer than PMVS_MAX_IMAGES is an error."""
     if lib().oracle_list_overflow(1):
@@ -160,6 +248,68 @@ class OracleScene:
             self.close()
         except Exception:
             pass
+
+    def organizer_ops(self, ops):
+        """The restatement's setGridsImages / setGrids / updateDepthMaps / isVisible0 (depth 0) /
+        checkAngles / setDistances on the same op list as ref_organizer:
+          ("grids_images", coords [n,4], image lists)  -> per record [m, 3] (image, ix, iy)
+          ("grids", coords, image lists)                -> the same, every image kept
+          ("depth", coords)                             -> every target's cells (patch or -1), concatenated
+          ("vis0", coords, images)                      -> [n, 3] (visible, ix, iy)
+          ("angles", coords, index lists, min, max)     -> [n] checkAngles
+          ("dist",)                                     -> [V, V] setDistances"""
+        L = lib()
+        res = []
+        for op in ops:
+            kind = op[0]
+            if kind in ("grids_images", "grids"):
+                coords = np.ascontiguousarray(op[1], np.float32)
+                off, flat = _lists(op[2])
+                stride = 3 * P.MAX_IMAGES + 1
+                out = np.zeros((len(coords), stride), np.int32)
+                fn = L.oracle_set_grids_images if kind == "grids_images" else L.oracle_set_grids_full
+                fn(self.h, len(coords), _p(coords), _p(off), _p(flat), _p(out))
+                res.append([out[i, 1:1 + 3 * out[i, 0]].reshape(-1, 3) for i in range(len(coords))])
+            elif kind == "depth":
+                coords = np.ascontiguousarray(op[1], np.float32)
+                gw, gh = self.grid_sizes()
+                out = np.zeros(int(sum(gw[t] * gh[t] for t in range(self.inputs.num_targets))), np.int32)
+                L.oracle_update_depth_maps(self.h, len(coords), _p(coords), _p(out))
+                res.append(out)
+            elif kind == "vis0":
+                coords = np.ascontiguousarray(op[1], np.float32)
+                imgs = np.ascontiguousarray(op[2], np.int32)
+                out = np.zeros((len(coords), 3), np.int32)
+                L.oracle_is_visible0(self.h, len(coords), _p(coords), _p(imgs), _p(out))
+                res.append(out)
+            elif kind == "angles":
+                coords = np.ascontiguousarray(op[1], np.float32)
+                off, flat = _lists(op[2])
+                out = np.zeros(len(coords), np.int32)
+                L.oracle_check_angles(self.h, len(coords), _p(coords), _p(off), _p(flat), op[3], op[4], _p(out))
+                res.append(out)
+            elif kind == "dist":
+                V = len(self.inputs.images)
+                out = np.zeros((V, V), np.float32)
+                L.oracle_distances(self.h, _p(out))
+                res.append(out)
+        return res
+
+    def level_sizes(self, levels):
+        """Per view, the (width, height) of pyramid levels 0 .. levels-1: [V, L] each."""
+        V = len(self.inputs.images)
+        w = np.zeros((V, levels), np.int32)
+        h = np.zeros((V, levels), np.int32)
+        for v in range(V):
+            for lv in range(levels):
+                a = self.get_level(v, lv)
+                h[v, lv], w[v, lv] = a.shape[:2]
+        return w, h
+
+    def grid_sizes(self):
+        lv, cs = self.inputs.level, self.inputs.csize
+        w, h = self.level_sizes(lv + 1)
+        return (w[:, lv] + cs - 1) // cs, (h[:, lv] + cs - 1) // cs
 
     def set_thresholds(self, ncc, before, depth=0):
         lib().oracle_set_thresholds(self.h, ncc, before, depth)

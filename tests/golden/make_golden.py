@@ -15,7 +15,7 @@ renderer regenerates them bit-for-bit).  Expected outputs come from two sources:
   * oracle/liboracle.so (the CPU restatement, pinned on the pieces above): pyramid CRCs,
     grabTex textures, my_f values, full preProcess->refinePatch->postProcess records and the
     seed phase's seed patches (seeds.npz).
-Run from the repo root in the build container:  python tests/golden/make_golden.py
+Run from the repo root in the build container:  python tests/golden/make_golden.py [name ...]
 """
 import os
 import sys
@@ -290,6 +290,68 @@ def make_seeds():
     print(f"{path}: {os.path.getsize(path)} B")
 
 
+def organizer_cases(o, inp, p, rng, n=600):
+    """Inputs of the organizer / photo-set pins: points on and around the synthetic surface
+    (candidates jittered along their normals, so several compete for a depth-map cell) and far
+    points; image lists of every length; view sets and angle bounds for checkAngles."""
+    V = len(inp.images)
+    c = P.synth_candidates(p, inp.projections, n, seed=int(rng.integers(1 << 30)))
+    coords = c["coord"].astype(np.float32).copy()
+    coords[:, :3] += (c["normal"][:, :3] * rng.normal(0, 0.02, (n, 1))).astype(np.float32)
+    coords[-40:, :3] = rng.normal(0, 5.0, (40, 3)).astype(np.float32)  # far, often outside every grid
+    coords[:, 3] = 1.0
+    lists = [sorted(rng.choice(V, int(rng.integers(1, V + 1)), replace=False).tolist()) for _ in range(n)]
+    lists = [rng.permutation(l).tolist() for l in lists]
+    vis_images = rng.integers(0, inp.num_targets, n).astype(np.int32)
+    ang_lists = [rng.choice(V, int(rng.integers(2, min(V, 7) + 1)), replace=False).tolist() for _ in range(n)]
+    return coords, lists, vis_images, ang_lists
+
+
+def organizer_ops(coords, lists, vis_images, ang_lists, min_angle, max_angle):
+    return [("grids_images", coords, lists), ("grids", coords, lists), ("depth", coords[:300]),
+            ("depth", coords), ("vis0", coords, vis_images), ("angles", coords, ang_lists, min_angle, max_angle),
+            ("angles", coords, ang_lists, 0.05, 0.6), ("dist",)]
+
+
+def make_organizer():
+    """CPatchOrganizerS::setGridsImages / setGrids / updateDepthMaps / isVisible0 and
+    CPhotoSetS::checkAngles / setDistances of the reference's own patchOrganizerS.cpp /
+    photoSetS.cpp (oracle/_ref/organizer) on the ring8 scene."""
+    views, width, height, level, csize = SCENES["ring8"][:5]
+    inp, p = P.synth_scene(views, width, height, level=level, csize=csize, supersample=2)
+    o = O.OracleScene(inp)
+    maxlv = level + 3
+    w, h = o.level_sizes(maxlv)
+    coords, lists, vis_images, ang_lists = organizer_cases(o, inp, p, np.random.default_rng(17))
+    min_angle = float(np.float32(inp.max_angle_rad()))
+    max_angle = float(np.float32(np.float64(np.float32(60.0)) * np.pi / 180.0))
+    ops = organizer_ops(coords, lists, vis_images, ang_lists, min_angle, max_angle)
+    ref = O.ref_organizer(inp.projections, w, h, inp.num_targets, level, csize, ops)
+    if ref is None:
+        raise SystemExit("oracle/_ref/organizer not built (reference absent)")
+    o.close()
+    off = np.zeros(len(lists) + 1, np.int64)
+    off[1:] = np.cumsum([len(l) for l in lists])
+    aoff = np.zeros(len(ang_lists) + 1, np.int64)
+    aoff[1:] = np.cumsum([len(l) for l in ang_lists])
+    g = {"params": np.array([views, width, height, level, csize, inp.num_targets], np.int64),
+         "widths": w, "heights": h, "coords": coords, "list_off": off,
+         "lists": np.array([x for l in lists for x in l], np.int32), "vis_images": vis_images,
+         "ang_off": aoff, "ang_lists": np.array([x for l in ang_lists for x in l], np.int32),
+         "angles": np.array([min_angle, max_angle], np.float32)}
+    for k, (op, r) in enumerate(zip(ops, ref)):
+        if op[0] in ("grids_images", "grids"):
+            g[f"ref{k}_n"] = np.array([len(x) for x in r], np.int32)
+            g[f"ref{k}"] = np.concatenate(r).astype(np.int32)
+        else:
+            g[f"ref{k}"] = r
+    path = os.path.join(HERE, "organizer.npz")
+    np.savez_compressed(path, **g)
+    kept = g["ref0_n"].sum()
+    print(f"{path}: {os.path.getsize(path)} B, setGridsImages kept {kept} of {off[-1]} entries, "
+          f"depth cells set {(g['ref3'] >= 0).sum()}, visible {g['ref4'][:, 0].sum()}/{len(coords)}")
+
+
 def make(name, views, width, height, level, csize, ntex, neval, nref):
     inp, p = P.synth_scene(views, width, height, level=level, csize=csize, supersample=2)
     o = O.OracleScene(inp)
@@ -333,6 +395,11 @@ def make(name, views, width, height, level, csize, ntex, neval, nref):
 
 if __name__ == "__main__":
     O.build()
+    if len(sys.argv) > 1:  # named fixtures only, e.g. `make_golden.py organizer`
+        for name in sys.argv[1:]:
+            globals()["make_" + name]()
+        raise SystemExit(0)
+    make_organizer()
     make_isneighbor()
     make_expand_dirs()
     make_features()
