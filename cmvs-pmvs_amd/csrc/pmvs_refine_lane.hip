@@ -217,6 +217,37 @@ __device__ __forceinline__ double lane_request(const DScene& s, const float* geo
   return f;
 }
 
+// One objective request out of line (LANE_EVAL_CALL): decode, getPAxes and lane_request from the job
+// record, so the evaluation's code exists once instead of once per CALFUN site of the optimizer (4
+// copies inlined), and its registers are allocated apart from the optimizer's.
+#ifndef LANE_EVAL_CALL
+#define LANE_EVAL_CALL 0
+#endif
+struct LaneEval {
+  double f;
+  unsigned nvalid;
+};
+template <int WS, int LP>
+__device__ __noinline__ LaneEval lane_eval(const DScene& s, const RefineJob* __restrict__ J, double x0, double x1,
+                                           double x2, int need, int myview, int size) {
+  RefineSetup R;
+  for (int i = 0; i < 4; ++i) { R.center[i] = J->center[i]; R.ray[i] = J->ray[i]; }
+  R.dscale = J->dscale;
+  R.ascale = s.ascale;
+  R.ref = __builtin_amdgcn_readfirstlane(J->images[0]);
+  const double xe[3] = {x0, x1, x2};
+  float fc[4], fn[4], geo[16], px[4], py[4];
+  decode(s, R, xe, fc, fn);
+  get_paxes(s, s.views[R.ref], fc, fn, px, py);
+  for (int i = 0; i < 4; ++i) {
+    geo[i] = fc[i]; geo[4 + i] = fn[i];
+    geo[8 + i] = px[i]; geo[12 + i] = py[i];
+  }
+  unsigned long long tv = 0;
+  const double f = lane_request<WS, LP>(s, geo, myview, size, need, *J, tv);
+  return {f, (unsigned)tv};
+}
+
 // One wavefront per candidate, persistent: candidates from the launch's queue (DevStats::queue2), the
 // ones preProcess rejected skipped.
 template <int WS, int LP>
@@ -272,9 +303,17 @@ __global__ __launch_bounds__(LANE_THREADS) __attribute__((amdgpu_waves_per_eu(LA
 #if defined(LANE_PROFILE)
       const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
+#if LANE_EVAL_CALL
+      const LaneEval e = lane_eval<WS, LP>(s, &J, xe[0], xe[1], xe[2], 1, myview, size);
+      tex_valid += e.nvalid;
+      grabs += size;
+      ++nreq;
+      const double fv = e.f;
+#else
       float fc[4], fn[4];
       decode(s, R, xe, fc, fn);
       const double fv = request(fc, fn, 1);
+#endif
 #if defined(LANE_PROFILE)
       const unsigned long long t1 = __builtin_amdgcn_s_memtime();
       prof_eval += t1 - t0;
@@ -305,8 +344,16 @@ __global__ __launch_bounds__(LANE_THREADS) __attribute__((amdgpu_waves_per_eu(LA
       decode(s, R, xo, fc, fn);
       if (nimg < 2)  // computeINCC returns 2.0 without grabbing (optim.cpp:866)
         ncc = (float)(1.0 - (double)unrobustincc(2.0f));
-      else  // final computeINCC (robust, weighted) at the refined geometry
+      else {  // final computeINCC (robust, weighted) at the refined geometry
+#if LANE_EVAL_CALL
+        const LaneEval e = lane_eval<WS, LP>(s, &J, xo[0], xo[1], xo[2], 2, myview, size);
+        grabs += size;
+        ++nreq;
+        ncc = (float)(1.0 - (double)unrobustincc((float)e.f));
+#else
         ncc = (float)(1.0 - (double)unrobustincc((float)request(fc, fn, 2)));
+#endif
+      }
     }
     if (lane == 0) {
       J.refine_code = rc;
