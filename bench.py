@@ -14,7 +14,7 @@ value = refined patches/s: patches the expansion refined and committed to the mo
 Also: NCC evals/s (my_f + computeINCC evaluations), refined candidates/s.
 roofline: the loop's dominant kernel, refine_split_kernel (the refine batches of >= 10000 candidates):
 algorithmic bytes = 588 B x valid textures per my_f evaluation over its HIP-event
-time, against 8 TB/s HBM; the smaller batches' workgroup-form kernel in roofline.small_batches.
+time, against 8 TB/s HBM; the smaller batches' lane-form kernel (below 7000 candidates) in roofline.small_batches.
 refine_c2: the refine kernel alone on configs[1] (8-view 1920x1080, level 1, 100k candidates).
 cpu_baseline: the same metric on the host CPU -- the oracle (CPU restatement) runs the expansions
 of the same rank-0 C3 scene from the same models with the same wave schedule (findEmptyBlocks,
@@ -62,6 +62,8 @@ BYTES_PER_TEXTURE = 49 * 4 * 3  # wsize^2 samples x 4 texels x 3 B (SURVEY.md §
 
 def refine_kernel_name(cfg):
     """The refine kernel a PMVS_REFINE_CONFIG value launches (pmvs_kernels.hip launch_refine_ws)."""
+    if cfg >= 300000:  # lane form: 300000 + lanes per texture (0: from tau; 8 at C3's tau 6)
+        return f"refine_lane_kernel<7,{cfg % 100 or 8}>"
     if cfg >= 200000:  # split form: 200000 + LP * 10000 + optimizer wavefronts * 1000 + chains per wavefront
         return f"refine_split_kernel<7,{(cfg // 1000) % 10},{cfg % 1000},{max(1, (cfg // 10000) % 10)}>"
     if cfg >= 100000:  # workgroup form: 100000 + chains * 1000 + optimizer wavefronts * 10 + workgroups per CU
@@ -73,7 +75,7 @@ def refine_kernel_name(cfg):
 _RCFG = int(os.environ.get("PMVS_REFINE_LARGE_CONFIG", os.environ.get("PMVS_REFINE_CONFIG", "226014")))
 REFINE_KERNEL = refine_kernel_name(_RCFG)
 SMALL_KERNEL = refine_kernel_name(int(os.environ.get("PMVS_REFINE_SMALL_CONFIG", os.environ.get("PMVS_REFINE_CONFIG",
-                                                                                                   "132042"))))
+                                                                                                   "300000"))))
 
 
 _T0 = time.time()

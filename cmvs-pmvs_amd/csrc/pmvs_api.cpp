@@ -204,9 +204,11 @@ struct pmvs_scene {
   DBuf<int> fkeep;
   DBuf<unsigned long long> digest;  // pmvs_loop_hash
   int grid = 0, refine_grid = 0, tslots = 226014;
-  // batches below small_n candidates run the workgroup form spread over every CU (tslots_small):
-  // their length is one chain's latency, not the chip's throughput
-  int tslots_small = 132042, small_n = 10000;
+  // batches below small_n candidates run the lane form, one candidate per wavefront with its BOBYQA
+  // state over the lanes (tslots_small, pmvs_refine_lane.hip): their length is one chain's latency,
+  // not the chip's throughput (the C3 loop, gpurun r06d: small launches 1029 -> 687 ms
+  // per step against the workgroup form 132042, split point 7000 against 5000 / 10000)
+  int tslots_small = 300000, small_n = 7000;
   int refine_cfg(int n) const { return n < small_n ? tslots_small : tslots; }
   // expansion sharding (pmvs_scene_set_shard) and the kept result of pmvs_expand_run(out = NULL)
   int shard_rank = 0, shard_world = 1;

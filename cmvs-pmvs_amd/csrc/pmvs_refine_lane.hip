@@ -36,6 +36,18 @@ constexpr int LANE_THREADS = 256;  // four independent wavefronts per workgroup
 __device__ __forceinline__ float readlane_f(float v, int k) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
 }
+// Lane l - 1's value (row_shr:1 DPP; a texture's LP <= 8 lanes never straddle a 16-lane row), for the
+// LP-stage hand-off of an ordered sum: no LDS round trip (ds_bpermute) on the sum's chain.
+__device__ __forceinline__ float shr1_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, false));
+}
+// The last lane of each LP-lane group's value, to every lane of the group (ds_swizzle bit mode:
+// lane (i & ~(LP-1)) | (LP-1) within each 32-lane half).
+template <int LP>
+__device__ __forceinline__ float group_last_f(float v) {
+  constexpr int pattern = (0x1f & ~(LP - 1)) | ((LP - 1) << 5);
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), pattern));
+}
 
 // One request of the wavefront's candidate: the objective at the geometry geo (coord, normal, pxaxis,
 // pyaxis), over its first `size` textures; need 1 = my_f, need 2 = the final computeINCC.  Every lane
@@ -107,7 +119,6 @@ __device__ __forceinline__ double lane_request(const DScene& s, const float* geo
   }
   // normalize (optim.cpp:1031-1067), the channel sums in LP stages
   const bool ok = T.ok != 0;
-  const int last = t * LP + LP - 1;  // the lane that ends a texture's sums
   float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
 #pragma unroll
   for (int j = 0; j < LP; ++j) {
@@ -117,11 +128,11 @@ __device__ __forceinline__ double lane_request(const DScene& s, const float* geo
         if (q < kn) { a0 += X[q]; a1 += Y[q]; a2 += Z[q]; }
     }
     if (j + 1 < LP) {
-      const float u0 = __shfl_up(a0, 1), u1 = __shfl_up(a1, 1), u2 = __shfl_up(a2, 1);
+      const float u0 = shr1_f(a0), u1 = shr1_f(a1), u2 = shr1_f(a2);
       if (sub == j + 1) { a0 = u0; a1 = u1; a2 = u2; }
     }
   }
-  a0 = __shfl(a0, last); a1 = __shfl(a1, last); a2 = __shfl(a2, last);
+  a0 = group_last_f<LP>(a0); a1 = group_last_f<LP>(a1); a2 = group_last_f<LP>(a2);
   const float fs3 = (float)S;
   a0 = __fdiv_rn(a0, fs3); a1 = __fdiv_rn(a1, fs3); a2 = __fdiv_rn(a2, fs3);
   float ave2 = 0.0f;
@@ -136,11 +147,11 @@ __device__ __forceinline__ double lane_request(const DScene& s, const float* geo
         }
     }
     if (j + 1 < LP) {
-      const float u = __shfl_up(ave2, 1);
+      const float u = shr1_f(ave2);
       if (sub == j + 1) ave2 = u;
     }
   }
-  ave2 = __shfl(ave2, last);
+  ave2 = group_last_f<LP>(ave2);
   ave2 = fsqrt_rn(__fdiv_rn(ave2, (float)(3 * S)));
   if (ave2 == 0.0f) ave2 = 1.0f;
   if (ok) {
@@ -155,15 +166,16 @@ __device__ __forceinline__ double lane_request(const DScene& s, const float* geo
   // robust INCC against the reference texture (texture 0, optim.cpp:561-567, 919-929): its normalised
   // samples read one at a time from its lane with the same part, the products summed in sample order
   // (R, G, B per sample) in LP stages
-  const int src = sub;
+  // (stage j: the reference texture's part j is lane j's registers, read by readlane -- wave-uniform)
   float ans = 0.0f;
 #pragma unroll
   for (int j = 0; j < LP; ++j) {
     if (sub == j) {
+      const int knj = j * K < S ? (S - j * K < K ? S - j * K : K) : 0;  // samples of part j
 #pragma unroll
       for (int q = 0; q < K; ++q)
-        if (q < kn) {
-          const float px = __shfl(X[q], src), py = __shfl(Y[q], src), pz = __shfl(Z[q], src);
+        if (q < knj) {
+          const float px = readlane_f(X[q], j), py = readlane_f(Y[q], j), pz = readlane_f(Z[q], j);
           if (ok) {
             ans += px * X[q];
             ans += py * Y[q];
@@ -172,7 +184,7 @@ __device__ __forceinline__ double lane_request(const DScene& s, const float* geo
         }
     }
     if (j + 1 < LP) {
-      const float u = __shfl_up(ans, 1);
+      const float u = shr1_f(ans);
       if (sub == j + 1) ans = u;
     }
   }
