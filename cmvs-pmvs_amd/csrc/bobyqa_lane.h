@@ -25,6 +25,19 @@
 namespace pmvsdev {
 namespace bql {
 
+// Diagnostic builds (-DLANE_PROFILE): shader cycles per optimizer phase, accumulated in registers of
+// the caller's BqlProf: [0] TRSBOX, [1] ALTMOV, [2] UPDATE.
+struct BqlProf {
+  unsigned long long t[4] = {0, 0, 0, 0};
+};
+#if defined(LANE_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
+#define BQL_T0(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define BQL_T1(slot, v) prof.t[slot] += __builtin_amdgcn_s_memtime() - v
+#else
+#define BQL_T0(v)
+#define BQL_T1(slot, v)
+#endif
+
 // Host tests only (-DBQL_COUNT): how often each rare branch ran, so the tests can show they covered them.
 #if defined(BQL_COUNT) && !defined(__HIPCC__)
 extern long long bql_hits[16];
@@ -879,7 +892,8 @@ BQL_HD void update(V (&BM)[N], V (&ZM)[NPTM], V& VL, double beta, double denom, 
 // (unscaled) and *minf as bq_step leaves st.xout / st.minf; *nevals the evaluations made.
 template <class F>
 BQL_HD int bobyqa(BQL_AS BqlU& U, F&& fobj, const double* x0, const double* lb, const double* ub, double xtol_rel,
-                  int maxeval, double* xout, double* minf_out, int* nevals_out) {
+                  int maxeval, double* xout, double* minf_out, int* nevals_out, BqlProf& prof) {
+  (void)prof;
   const double half = 0.5, one = 1.0, ten = 10.0, tenth = 0.1, two = 2.0, zero = 0.0;
   // ---- bq_begin
   BQL_AS double* const sc = U.sc;
@@ -1118,7 +1132,11 @@ L20:
   }
 L60:
   BQL_FENCE();
-  trsbox(XP, PQ, xopt, gopt, hq, sl, su, delta, xnew, d, gnew, &dsq, &crvmin);
+  {
+    BQL_T0(t0);
+    trsbox(XP, PQ, xopt, gopt, hq, sl, su, delta, xnew, d, gnew, &dsq, &crvmin);
+    BQL_T1(0, t0);
+  }
   BQL_FENCE();
   dnorm = bq_min(delta, sqrt(dsq));
   if (dnorm < half * rho) {
@@ -1615,7 +1633,11 @@ R350:
   if (ntrits > 0) goto L60;
 L210:
   BQL_FENCE();
-  altmov(XP, xopt, BM, ZM, sl, su, kopt, knew, adelt, xnew, xalt, &alpha, &cauchy);
+  {
+    BQL_T0(t0);
+    altmov(XP, xopt, BM, ZM, sl, su, kopt, knew, adelt, xnew, xalt, &alpha, &cauchy);
+    BQL_T1(1, t0);
+  }
   BQL_FENCE();
 #pragma unroll
   for (int i = 1; i <= N; ++i) d[i] = xnew[i] - xopt[i];
@@ -1833,7 +1855,11 @@ L360:
     }
   }
   BQL_FENCE();
-  update(BM, ZM, VL, beta, denom, knew, W1, W2);
+  {
+    BQL_T0(t0);
+    update(BM, ZM, VL, beta, denom, knew, W1, W2);
+    BQL_T1(2, t0);
+  }
   BQL_FENCE();
   ih = 0;
   pqold = bc(PQ, knew - 1);

@@ -278,6 +278,7 @@ __global__ __launch_bounds__(LANE_THREADS) __attribute__((amdgpu_waves_per_eu(LA
   // shader cycles per wavefront in the optimizer step, the objective evaluations, whole candidates
   unsigned long long prof_step = 0, prof_eval = 0, prof_cand = 0, prof_mark = 0;
 #endif
+  bql::BqlProf bprof;
   if (threadIdx.x == 0) atomicMax(&st->t_first_inv, ~__builtin_amdgcn_s_memrealtime());
   const double lb[3] = {-HUGE_VAL, -23.99999, -23.99999};
   const double ub[3] = {HUGE_VAL, 23.99999, 23.99999};
@@ -340,7 +341,7 @@ __global__ __launch_bounds__(LANE_THREADS) __attribute__((amdgpu_waves_per_eu(LA
     prof_mark = __builtin_amdgcn_s_memtime();
     const unsigned long long tc0 = prof_mark;
 #endif
-    const int rc = bql::bobyqa(U, fobj, x0, lb, ub, 1.e-7, 1000, xo, &minf, &nev);
+    const int rc = bql::bobyqa(U, fobj, x0, lb, ub, 1.e-7, 1000, xo, &minf, &nev, bprof);
     nevals += (unsigned long long)nev;
 #if defined(LANE_PROFILE)
     {
@@ -388,6 +389,9 @@ __global__ __launch_bounds__(LANE_THREADS) __attribute__((amdgpu_waves_per_eu(LA
     atomicAdd(&st->prof[0], prof_step);
     atomicAdd(&st->prof[1], prof_eval);
     atomicAdd(&st->prof[2], prof_cand);
+    atomicAdd(&st->prof[3], bprof.t[0]);
+    atomicAdd(&st->prof[4], bprof.t[1]);
+    atomicAdd(&st->prof[5], bprof.t[2]);
 #endif
   }
 }

@@ -24,7 +24,8 @@ extern "C" int bql_host_run(int kind, const double* x0, int maxeval, double* xou
   };
   int nev = 0;
   bql::BqlU U;
-  const int rc = bql::bobyqa(U, f, x0, lb, ub, 1e-7, maxeval, xout, fout, &nev);
+  bql::BqlProf prof;
+  const int rc = bql::bobyqa(U, f, x0, lb, ub, 1e-7, maxeval, xout, fout, &nev, prof);
   *nrec = cnt;
   return rc;
 }
