@@ -4065,6 +4065,23 @@ static hipError_t device_commit(const DScene& s, ExpandBuffers& X, hipStream_t s
   int* ulist = W.scan + 2 * (size_t)(nk + 1);
   int* ucnt = W.ctr + 9;  // free in this (non-serial) form
   const unsigned lgrid = std::min(nblk(nk), 1024u);
+  static const bool trace = getenv("PMVS_COMMIT_TRACE") != nullptr;
+  if (trace) {
+    // diagnostic: decided count after every round (one read per round), to stderr
+    fprintf(stderr, "[commit] nk=%d nlive=%d na=%d:", nk, nlive, na);
+    int d = 0;
+    for (int round = 0; d < nlive && round < 4 * (nlive + 2); ++round) {
+      if (na > 0)
+        hipLaunchKernelGGL(cm_first_kernel, dim3(nblk(na)), dim3(256), 0, st, W.keys2, W.dec, W.seghead, W.ctr + 8, W.segptr,
+                           W.segfirst);
+      hipLaunchKernelGGL(cm_decide_kernel, dim3(nblk(nk)), dim3(256), 0, st, s, nk, slot2v, X.crec, W.aoff, W.nacc, W.vals,
+                         W.segfirst, W.dec, W.stc, W.flag, X.counts, X.occ, cthr, check ? 1 : 0, W.ctr);
+      FCHK(read_int(W.ctr, &d, st));
+      fprintf(stderr, " %d", nlive - d);
+    }
+    fprintf(stderr, "\n");
+    decided = d;
+  }
   for (int round = 0; decided < nlive; ) {
     for (int r = 0; r < 4; ++r, ++round) {
       if (na > 0)  // <= na segments
