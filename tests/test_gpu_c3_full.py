@@ -47,7 +47,7 @@ def test_c3_full_size_step_and_first_waves_match_oracle(c3):
     del model
     # iteration 1 here (every bench.py run samples all three iterations: parity_c3_first_waves)
     args = argparse.Namespace(iterations=3, cpu_iterations=1, cpu_waves=2, cpu_waves_late=0, cpu_seconds=1.0,
-                              cpu_threads=0, wave=32768, min_candidates=131072)
+                              cpu_threads=0, cpu_filter_every=0, wave=32768, min_candidates=131072)
     _, parity = bench.loop_samples(P, scene, inp, seeds, args, [it["expand"]["added"] for it in log])
     print(f"first waves: {parity}")
     assert all(p["ok"] for p in parity), parity

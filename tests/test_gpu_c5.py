@@ -7,6 +7,7 @@ test's scenes hold device memory while it runs (the model reaches ~50 M patches 
 """
 import os
 import sys
+import time
 
 import numpy as np
 import pytest
@@ -28,7 +29,10 @@ def _threads():
 def test_c5_cluster_8k_one_iteration(gpu_available, oracle_mod):
     import bench
     import pmvs_amd as P
+    t0 = time.perf_counter()
+    lap = lambda what: print(f"[c5 {time.perf_counter() - t0:6.1f} s] {what}", flush=True)  # noqa: E731
     inp, sp = P.synth_scene(70, 7680, 4320, level=0, supersample=2, nthreads=16)
+    lap("scene rendered")
     g = P.Scene(inp)
     cands = P.synth_candidates(sp, inp.projections, 5000, seed=0x5EED)
     r, _ = g.refine_batch(cands)
@@ -39,10 +43,12 @@ def test_c5_cluster_8k_one_iteration(gpu_available, oracle_mod):
     g.set_thresholds(ncc, before, depth)
     cap = len(seeds) + 600000
     g_out, g_alive, g_st = g.expand_run(seeds, cap=cap, max_waves=1, **kw)
+    lap("device: scene, seeds, first wave")
     o = oracle_mod.OracleScene(inp)
     o.set_thresholds(ncc, before, depth)
     o_out, o_alive, o_st = o.expand_run(seeds, cap=cap, nthreads=_threads(), max_waves=1, **kw)
     o.close()
+    lap("oracle first wave")
     print(f"C5 first waves: {o_st}")
     assert o_st["added"] > 10000
     assert all(g_st[k] == o_st[k] for k in o_st), (g_st, o_st)
@@ -52,7 +58,9 @@ def test_c5_cluster_8k_one_iteration(gpu_available, oracle_mod):
     g.set_thresholds(*bench.iteration_thresholds(inp.threshold, 0)[:2], 0)
     model, log = g.run_loop(seeds, inp.threshold, iterations=1, wave=32768, min_candidates=131072)
     g.close()
+    lap("device iteration + model fetch")
     checks = bench.model_checks(model, inp, ["x"])
+    lap("model checks")
     print(f"C5 one iteration: {log[0]['expand']['added']} added, {len(model)} kept, "
           f"{log[0]['expand']['wall_ms'] / 1e3:.1f} s expand, {log[0]['filter']['kernel_ms'] / 1e3:.1f} s filter; {checks}")
     assert checks["ok"] and checks["sphere_residual_p99"] < 0.01, checks

@@ -11,9 +11,9 @@ import pytest
 from pmvs_cases import bits
 
 pytestmark = pytest.mark.gpu
-# scene goldens (c1, ring8); expand_dirs / features / seeds / isneighbor.npz hold other reference vectors
+# scene goldens (c1, ring8); expand_dirs / features / seeds / isneighbor / organizer.npz hold other reference vectors
 GOLDEN = sorted(p for p in glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz"))
-                if not os.path.basename(p).startswith(("expand_dirs", "features", "seeds", "isneighbor")))
+                if not os.path.basename(p).startswith(("expand_dirs", "features", "seeds", "isneighbor", "organizer")))
 
 
 @pytest.fixture(scope="module", params=GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
