@@ -5,7 +5,8 @@ ThreadExchange -- the reference's per-cluster pmvs2 runs plus the exchange this 
 between them (the reference runs clusters independently, bundle.cpp:1465-1485
 being where one cluster's patches are written for the next stage).
 
-Opt-in (PMVS_LONG_TESTS=1): the two clusters' iterations take about five minutes on one GPU.
+Opt-in (PMVS_LONG_TESTS=1): the two clusters' iterations take about five minutes on one GPU.  The
+same two clusters at 1920x1080 (matched at 960x540) run in the default GPU suite.
 The clusters run as two threads on this GPU, but their compute phases take turns (a baton passed at
 every all-gather), so that only one 8K model grows at a time: one cluster's first expansion reaches
 ~51 M records (82 GB) and the two growing together would not fit in 288 GB.  The waiting cluster
@@ -39,6 +40,17 @@ LEVEL = 1
 @_LONG
 @pytest.mark.timeout(1100)
 def test_c5_two_clusters_two_iterations_exchange(gpu_available, monkeypatch):
+    _two_clusters(monkeypatch, 7680, 4320, LEVEL, 2, min_added=1_000_000)
+
+
+@pytest.mark.timeout(300)
+def test_c5_shaped_two_clusters_exchange_small(gpu_available, monkeypatch):
+    """The same two 70-view clusters, baton and exchange at 1920x1080 matched at level 1 (960x540): the
+    C5 cluster shape in the default GPU suite (the 8K case above is opt-in)."""
+    _two_clusters(monkeypatch, 1920, 1080, 1, 1, min_added=20_000)
+
+
+def _two_clusters(monkeypatch, width, height, level, supersample, min_added):
     import bench
     import pmvs_amd as P
     from test_gpu_c4 import ring_clusters
@@ -48,10 +60,10 @@ def test_c5_two_clusters_two_iterations_exchange(gpu_available, monkeypatch):
     world, vpc, ov = 2, 66, 2
     clusters = ring_clusters(vpc, world, ov)
     assert all(len(c) == 70 for c in clusters)
-    full, sp = P.synth_scene(vpc * world, 7680, 4320, level=LEVEL, supersample=2, nthreads=16)
+    full, sp = P.synth_scene(vpc * world, width, height, level=level, supersample=supersample, nthreads=16)
     cands = P.synth_candidates(sp, full.projections, 5000 * world, seed=0x5EED)
     inps = [P.SceneInputs(images=[full.images[i] for i in ids], projections=full.projections[ids], num_targets=len(ids),
-                          level=LEVEL) for ids in clusters]
+                          level=level) for ids in clusters]
     del full
     scenes = [P.Scene(inp) for inp in inps]
     try:
@@ -112,7 +124,7 @@ def test_c5_two_clusters_two_iterations_exchange(gpu_available, monkeypatch):
                   f"boundary {[(it['boundary']['sent'], it['boundary']['inserted']) for it in log]}, checks {checks}")
             assert checks["ok"], (r, checks)
             assert checks["sphere_residual_p99"] < 0.01, checks
-            assert log[0]["expand"]["added"] > 1_000_000
+            assert log[0]["expand"]["added"] > min_added
             assert log[0]["boundary"]["sent"] > 0 and log[0]["boundary"]["inserted"] > 0, log
             assert model["fix"].max() != P.FIX_FOREIGN  # foreign patches never returned
     finally:
