@@ -75,6 +75,13 @@ constexpr int NB_GRID_BIG = 32;  // workgroups of the NB_CAP_BIG re-walks
 // gather_neighbors: cell slots per lane per round, entries per lane per test round
 constexpr int NB_SK = 2;
 constexpr int NB_NE = 2;
+// gather_neighbors' slots (round 6): 1 = one slot per ROW of a list's (2 margin + 1)^2 window -- the
+// row's cells are consecutive in the CSR cell order, so their entries are the one range
+// [off[c0], off[c0 + nx]) -- against 0 = one slot per cell (rounds 2-5).  The neighbour set is the
+// same; a filterNeighbor walk loads 10 list bounds per image instead of 50.
+#ifndef PMVS_NB_ROWS
+#define PMVS_NB_ROWS 1
+#endif
 // Persistent workgroups per CU-grid unit for the NbLds kernels (neighbor_kernel, depth_post_kernel,
 // empty_blocks_kernel): twice the organizer grid, since ~8 KB of LDS and <= 107 VGPRs leave room.
 #ifndef PMVS_NB_GRID_MULT
@@ -1204,49 +1211,73 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLdsT<CAP>
   __syncthreads();
   const int nlists = skipvis ? ni : ni + uni(q.num_vimages);
   const int side = 2 * margin + 1;
-  const int per_list = side * side * 2;
+#if PMVS_NB_ROWS
+  const int per_list = side * 2;  // (row, pgrids / vpgrids)
+#else
+  const int per_list = side * side * 2;  // (row, column, pgrids / vpgrids)
+#endif
+  const bool chains = F.pg_dhead != nullptr;
   const int nslots = nlists * per_list;
-  // NB_SK cells per lane per round (their list bounds load together), then the round's entries
+  // NB_SK slots per lane per round (their list bounds load together), then the round's entries
   // NB_NE per lane at a time (their item and patch loads in flight together): fewer dependent
-  // global-memory round trips per patch than one cell / one entry per lane.
+  // global-memory round trips per patch than one slot / one entry per lane.
   for (int base = 0; base < nslots; base += 64 * NB_SK) {
+    // per slot: list start (bit 31: vpgrids) and length; for the expansion's chains its first cell
+    // and the cells (bit dx) whose chain is not empty
     int bk[NB_SK], ck[NB_SK], hk[NB_SK];
+    long long ck0[NB_SK];
 #pragma unroll
     for (int k = 0; k < NB_SK; ++k) {
       const int slot = base + k * 64 + lane;
-      int b = 0, e = 0, lst = 0, head = -1;
+      int b = 0, e = 0, lst = 0, hm = 0;
+      long long c0 = 0;
       if (slot < nslots) {
         const int li = slot / per_list;
         int r = slot - li * per_list;
+#if PMVS_NB_ROWS
+        const int dyi = r >> 1;
+        lst = r & 1;
+#else
         const int dyi = r / (2 * side);
         r -= dyi * 2 * side;
         const int dxi = r >> 1;
         lst = r & 1;
+#endif
         const bool vis = li >= ni;
         const int t = vis ? q.vimages[li - ni] : q.images[li];
         if (t < s.tnum) {
           const int gw = gwidth(s, t), gh = gheight(s, t);
           const int yt = (vis ? q.vgrids[li - ni][1] : q.grids[li][1]) + dyi - margin;
-          const int xt = (vis ? q.vgrids[li - ni][0] : q.grids[li][0]) + dxi - margin;
-          if (0 <= yt && yt < gh && 0 <= xt && xt < gw) {
-            const long long c = F.tgoff[t] + (long long)yt * gw + xt;
+          const int gx = vis ? q.vgrids[li - ni][0] : q.grids[li][0];
+#if PMVS_NB_ROWS
+          const int x0 = imax(gx - margin, 0), x1 = imin(gx + margin, gw - 1);
+#else
+          const int x0 = gx + dxi - margin, x1 = x0;
+#endif
+          if (0 <= yt && yt < gh && 0 <= x0 && x0 <= x1 && x1 < gw) {
+            c0 = F.tgoff[t] + (long long)yt * gw + x0;
+            const int nx = x1 - x0 + 1;
             const int* off = lst ? F.vp_off : F.pg_off;
             const int lim = lst ? F.nvp : F.npg;
-            b = off[c];
-            e = off[c + 1];
+            b = off[c0];
+            e = off[c0 + nx];
             if (b < 0 || e > lim || b > e) {
               atomicAdd(&F.err[0], 1);
               atomicExch(&F.err[1], 12 + lst);
               b = 0;
               e = 0;
             }
-            if (F.pg_dhead) head = (lst ? F.vp_dhead : F.pg_dhead)[c];
+            if (chains) {
+              const int* dh = lst ? F.vp_dhead : F.pg_dhead;
+              for (int dx = 0; dx < nx; ++dx) hm |= (dh[c0 + dx] >= 0 ? 1 : 0) << dx;
+            }
           }
         }
       }
       bk[k] = b | (lst << 31);  // list start, list kind in bit 31
       ck[k] = e - b;
-      hk[k] = head;
+      hk[k] = hm;
+      ck0[k] = c0;
     }
     // the round's CSR entries, flattened in (lane, k) order
     int mine = 0;
@@ -1293,11 +1324,15 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLdsT<CAP>
       for (int u = 0; u < NB_NE; ++u)
         if (ib + u * 64 < tot) nb_append(L, hv[u], jv[u] < 0 ? 0 : jv[u], cap);
     }
-    // entries committed by earlier expansion waves (short chains, walked per lane)
+    // entries committed by earlier expansion waves (short chains, walked per lane), cell by cell of
+    // the slot's row
 #pragma unroll
     for (int k = 0; k < NB_SK; ++k) {
-      const int head = hk[k];
-      if (F.pg_dhead && __ballot(head >= 0) != 0ull) {
+      if (!chains || __ballot(hk[k] != 0) == 0ull) continue;
+      for (int dx = 0; dx < side; ++dx) {
+        const int* dh = (bk[k] < 0) ? F.vp_dhead : F.pg_dhead;
+        const int head = ((hk[k] >> dx) & 1) ? dh[ck0[k] + dx] : -1;
+        if (__ballot(head >= 0) == 0ull) continue;
         if (uni(L.cnt) > cap / 2 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(uni(L.cnt), cap), &L.cnt);
         for (int ent = head; ent >= 0; ent = F.d_next[ent]) {
           const int j = F.d_item[ent];
