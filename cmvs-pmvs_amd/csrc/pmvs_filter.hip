@@ -82,6 +82,36 @@ constexpr int NB_NE = 2;
 #ifndef PMVS_NB_ROWS
 #define PMVS_NB_ROWS 1
 #endif
+// Diagnostic build only (-DNB_PROFILE, tools/r06w.sh): shader cycles per phase of the neighbour walks,
+// summed over wavefronts, per kernel (0 neighbor_kernel, 1 empty_blocks_kernel, 2 depth_post_kernel):
+// [0] setup (radius, units, seen-set clear), [1] slot bounds, [2] entries (items, tests, appends),
+// [3] delta chains, [4] final sort + unique, [5] the kernel's work after the walk, [6] queue / other.
+// Printed to stderr after every filter pass and expansion (pmvs_filter.hip, nb_prof_dump).
+#if defined(NB_PROFILE)
+__device__ unsigned long long g_nb_prof[3][8];
+#define NBP_NOW() __builtin_amdgcn_s_memtime()
+#define NBP(ph)                                   \
+  do {                                            \
+    if (prof) {                                   \
+      const unsigned long long _t = NBP_NOW();    \
+      prof[ph] += _t - nbp_t;                     \
+      nbp_t = _t;                                 \
+    }                                             \
+  } while (0)
+#define NBP_FLUSH(kid)                                                    \
+  do {                                                                    \
+    if (threadIdx.x == 0)                                                 \
+      for (int _i = 0; _i < 8; ++_i) atomicAdd(&g_nb_prof[kid][_i], prof[_i]); \
+  } while (0)
+#else
+#define NBP_NOW() 0ull
+#define NBP(ph) \
+  do {          \
+  } while (0)
+#define NBP_FLUSH(kid) \
+  do {                 \
+  } while (0)
+#endif
 // Persistent workgroups per CU-grid unit for the NbLds kernels (neighbor_kernel, depth_post_kernel,
 // empty_blocks_kernel): twice the organizer grid, since ~8 KB of LDS and <= 107 VGPRs leave room.
 #ifndef PMVS_NB_GRID_MULT
@@ -1106,18 +1136,33 @@ __device__ int sort_unique_lds(int* a, int n, int* cnt_slot) {
 // (patchOrganizerS.cpp:527-631) + filterQuad (filter.cpp:387-446), one wavefront per patch.
 // CExpand::computeRadius (expand.cpp:182-198): second smallest of COptim::computeUnits
 // (optim.cpp:446-471) times csize.  All lanes call; result in every lane.
-__device__ float compute_radius_wave(const DScene& s, NbSmall& L, const pmvs_patch& q) {
+// With the radius, findNeighbors' unit (patchOrganizerS.cpp:541-545) before its division: the images'
+// getUnit summed in image order.  Lane k computes image k's getUnit once for both; the sum then reads
+// them from LDS (the walks' setup had summed them in one lane-serial loop of dependent global loads).
+struct RadUnit {
+  float radius;  // computeRadius, csize included; < 0: not computed
+  float usum;    // sum of getUnit(images[k], coord) over the images, in order
+};
+static_assert(PMVS_MAX_IMAGES <= 128, "compute_radius_unit: two images per lane");
+__device__ RadUnit compute_radius_unit(const DScene& s, NbSmall& L, const pmvs_patch& q, bool want_usum) {
   const int lane = lane_id_w();
   const int ni = uni(q.num_images);
   __syncthreads();
-  for (int k = lane; k < ni; k += 64) {
-    const DView& v = s.views[q.images[k]];
-    float u = get_unit(s, v, q.coord);
-    float ray[4] = {v.center[0] - q.coord[0], v.center[1] - q.coord[1], v.center[2] - q.coord[2], v.center[3] - q.coord[3]};
-    unitize4(ray);
-    const float den = dot4(ray, q.normal);
-    u = (0.0f < den) ? __fdiv_rn(u, den) : 1073741824.0f;
-    L.units[k] = u;
+  float raw0 = 0.0f, raw1 = 0.0f;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int k = lane + 64 * r;
+    if (k < ni) {
+      const DView& v = s.views[q.images[k]];
+      float u = get_unit(s, v, q.coord);
+      if (r == 0) raw0 = u;
+      else raw1 = u;
+      float ray[4] = {v.center[0] - q.coord[0], v.center[1] - q.coord[1], v.center[2] - q.coord[2], v.center[3] - q.coord[3]};
+      unitize4(ray);
+      const float den = dot4(ray, q.normal);
+      u = (0.0f < den) ? __fdiv_rn(u, den) : 1073741824.0f;
+      L.units[k] = u;
+    }
   }
   __syncthreads();
   float m1 = 3.0e38f, m2 = 3.0e38f;  // two smallest (nth_element(begin, begin + 1, end))
@@ -1126,7 +1171,20 @@ __device__ float compute_radius_wave(const DScene& s, NbSmall& L, const pmvs_pat
     if (u < m1) { m2 = m1; m1 = u; }
     else if (u < m2) m2 = u;
   }
-  return m2 * (float)s.csize;
+  RadUnit ru{m2 * (float)s.csize, 0.0f};
+  if (want_usum) {
+    __syncthreads();
+    if (lane < ni) L.units[lane] = raw0;
+    if (lane + 64 < ni) L.units[lane + 64] = raw1;
+    __syncthreads();
+    float us = 0.0f;
+    for (int k = 0; k < ni; ++k) us += L.units[k];
+    ru.usum = us;
+  }
+  return ru;
+}
+__device__ float compute_radius_wave(const DScene& s, NbSmall& L, const pmvs_patch& q) {
+  return compute_radius_unit(s, L, q, false).radius;
 }
 
 // CPatchOrganizerS::findNeighbors(patch, neighbors, lock, scale, margin, skipvis)
@@ -1195,15 +1253,17 @@ __device__ __forceinline__ void nb_append(NbLdsT<CAP>& L, bool hit, int j, int c
 // reference's; the visiting order only matters for the buffer's compaction points.
 template <int CAP>
 __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLdsT<CAP>& L, const pmvs_patch& q, float scale,
-                                int margin, int skipvis) {
+                                int margin, int skipvis, unsigned long long* prof = nullptr, RadUnit pre = {-1.0f, 0.0f}) {
   const int lane = lane_id_w();
+  unsigned long long nbp_t = NBP_NOW();
+  (void)nbp_t;
+  (void)prof;
   // the capacity in use: CAP (a test soft cap, F.nb_softcap, applies to the NB_CAP form only)
   const int cap = (CAP == NB_CAP && F.nb_softcap > 0) ? imin(CAP, F.nb_softcap) : CAP;
   const int ni = uni(q.num_images);
-  const float radius = (float)(1.5 * margin * (double)compute_radius_wave(s, L, q));
-  float unit = 0.0f;
-  for (int k = 0; k < ni; ++k) unit += get_unit(s, s.views[q.images[k]], q.coord);
-  unit = __fdiv_rn(unit, (float)ni);
+  const RadUnit ru = (pre.radius >= 0.0f) ? pre : compute_radius_unit(s, L, q, true);
+  const float radius = (float)(1.5 * margin * (double)ru.radius);
+  float unit = __fdiv_rn(ru.usum, (float)ni);
   unit *= (float)s.csize;
   const float thr = 0.5f * scale;
   if (lane == 0) { L.cnt = 0; L.overflow = 0; }
@@ -1227,6 +1287,7 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLdsT<CAP>
     int bk[NB_SK], ck[NB_SK], hk[NB_SK];
     long long ck0[NB_SK];
 #pragma unroll
+    NBP(base == 0 ? 0 : 2);
     for (int k = 0; k < NB_SK; ++k) {
       const int slot = base + k * 64 + lane;
       int b = 0, e = 0, lst = 0, hm = 0;
@@ -1295,6 +1356,7 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLdsT<CAP>
       }
     }
     __syncthreads();
+    NBP(1);
     for (int ib = 0; ib < tot; ib += 64 * NB_NE) {
       int jv[NB_NE];
       bool hv[NB_NE];
@@ -1324,6 +1386,7 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLdsT<CAP>
       for (int u = 0; u < NB_NE; ++u)
         if (ib + u * 64 < tot) nb_append(L, hv[u], jv[u] < 0 ? 0 : jv[u], cap);
     }
+    NBP(2);
     // entries committed by earlier expansion waves (short chains, walked per lane), cell by cell of
     // the slot's row
 #pragma unroll
@@ -1351,12 +1414,15 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLdsT<CAP>
       }
     }
     __syncthreads();
+    NBP(3);
   }
   const int n = imin(uni(L.cnt), cap);
 #if defined(NBX_SKIP_SORT)  // timing experiment only (tools): the final sort skipped
   return n;
 #else
-  return sort_unique_lds(L.nb, n, &L.cnt);
+  const int nu = sort_unique_lds(L.nb, n, &L.cnt);
+  NBP(4);
+  return nu;
 #endif
 }
 
@@ -1472,7 +1538,13 @@ __global__ __launch_bounds__(64) NB_WALK_ATTR void neighbor_kernel(DScene s, Fil
   const int lane = threadIdx.x;
   double* M = scratch + (size_t)blockIdx.x * (CAP * 8);
   double* r = M + (size_t)CAP * 5;
+#if defined(NB_PROFILE)
+  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nbp_t = NBP_NOW();
+#else
+  unsigned long long* prof = nullptr;
+#endif
   for (;;) {
+    NBP(6);
     int i = 0;
     if (lane == 0) i = atomicAdd(queue, 1);
     i = __builtin_amdgcn_readfirstlane(i);  // work-queue index, wave-uniform (SGPR)
@@ -1482,7 +1554,11 @@ __global__ __launch_bounds__(64) NB_WALK_ATTR void neighbor_kernel(DScene s, Fil
     int rej = 0;  // _fix patches are kept; no early `continue` (see depth_post_kernel)
     const bool mine = world <= 1 || uni(q.images[0]) % world == rank;
     if (mine && !uni(q.fix)) {
-      const int n = gather_neighbors(s, F, L, q, 4.0f, 2, 1);
+      NBP(6);
+      const int n = gather_neighbors(s, F, L, q, 4.0f, 2, 1, prof);
+#if defined(NB_PROFILE)
+      nbp_t = NBP_NOW();
+#endif
       const bool rewalk = ov.items && uni(L.overflow);
       if (lane == 0 && rewalk) ov.items[atomicAdd(ov.count, 1)] = p;
       if (lane == 0 && L.overflow && !ov.items) atomicAdd(overflow, 1);
@@ -1511,7 +1587,9 @@ __global__ __launch_bounds__(64) NB_WALK_ATTR void neighbor_kernel(DScene s, Fil
     }
     if (lane == 0) reject[p] = rej;
     __syncthreads();
+    NBP(5);
   }
+  NBP_FLUSH(0);
 }
 
 // filterQuad's fit and residual test for the patches neighbor_kernel deferred, one lane per patch:
@@ -2041,19 +2119,30 @@ __global__ __launch_bounds__(64) NB_WALK_ATTR void empty_blocks_kernel(DScene s,
                                                           int* __restrict__ queue, int* __restrict__ overflow, NbOverflow ov) {
   __shared__ NbLdsT<CAP> L;
   const int lane = threadIdx.x;
+#if defined(NB_PROFILE)
+  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nbp_t = NBP_NOW();
+#else
+  unsigned long long* prof = nullptr;
+#endif
   for (;;) {
+    NBP(5);
     int i = 0;
     if (lane == 0) i = atomicAdd(queue, 1);
     i = __builtin_amdgcn_readfirstlane(i);
     if (i >= (ov.only ? *ov.only_n : np)) break;
     const int k = ov.only ? __builtin_amdgcn_readfirstlane(ov.only[i]) : i;
     const pmvs_patch& q = F.P[parents[k]];
-    const float radius = compute_radius_wave(s, L, q);
+    const RadUnit ru = compute_radius_unit(s, L, q, true);
+    const float radius = ru.radius;
+    NBP(6);
 #if defined(EBX_SKIP_WALK)  // timing experiment only (tools/eb_breakdown.sh): no neighbour walk
     const int n = 0;
     if (lane == 0) L.overflow = 0;
 #else
-    const int n = gather_neighbors(s, F, L, q, 4.0f, 1, 0);
+    const int n = gather_neighbors(s, F, L, q, 4.0f, 1, 0, prof, ru);  // the radius and units computed once
+#endif
+#if defined(NB_PROFILE)
+    nbp_t = NBP_NOW();
 #endif
     // overflowed: this parent's bins are rewritten by the NB_CAP_BIG re-walk
     if (lane == 0 && L.overflow && ov.items) ov.items[atomicAdd(ov.count, 1)] = k;
@@ -2117,6 +2206,7 @@ __global__ __launch_bounds__(64) NB_WALK_ATTR void empty_blocks_kernel(DScene s,
     }
     __syncthreads();
   }
+  NBP_FLUSH(1);
 }
 
 // findEmptyBlocks' re-walk of the parents whose neighbour set overflowed the NB_CAP walk (round 5:
@@ -3371,11 +3461,31 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
 
 // Owner-partitioned (world > 1): a rank that fails outside an exchange sends one 8-byte error header
 // here (see filter_pass_impl), so its peers fail at their next header instead of blocking.
+// NB_PROFILE builds: the walk-phase cycle sums since the last dump, one JSON line on stderr, then cleared
+static void nb_prof_dump(const char* what) {
+#if defined(NB_PROFILE)
+  unsigned long long h[3][8];
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(h, HIP_SYMBOL(g_nb_prof), sizeof(h)) != hipSuccess) return;
+  fprintf(stderr, "{\"nb_prof\": \"%s\"", what);
+  for (int k = 0; k < 3; ++k) {
+    fprintf(stderr, ", \"k%d\": [", k);
+    for (int i = 0; i < 8; ++i) fprintf(stderr, "%s%llu", i ? ", " : "", h[k][i]);
+    fprintf(stderr, "]");
+  }
+  fprintf(stderr, "}\n");
+  std::memset(h, 0, sizeof(h));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_nb_prof), h, sizeof(h));
+#else
+  (void)what;
+#endif
+}
+
 hipError_t filter_pass(const DScene& s, FilterBuffers& B, pmvs_patch* dP, int n, long long ncells, const long long* h_tgoff,
                        int grid, hipStream_t st, int counts[4], int* overflow, int* keep_dev, const Shard* sh,
                        bool* handled) {
   bool agreed = false;
   hipError_t e = filter_pass_impl(s, B, dP, n, ncells, h_tgoff, grid, st, counts, overflow, keep_dev, sh, agreed);
+  nb_prof_dump("filter");
   if (handled) *handled = true;
   if (e != hipSuccess && sh && sh->world > 1 && n > 0 && !agreed) {
     int h[2] = {1, 0};
@@ -4670,6 +4780,7 @@ hipError_t expand_pass(const DScene& s, FilterBuffers& B, ExpandBuffers& X, pmvs
   bool agreed = false;
   hipError_t e = expand_pass_impl(s, B, X, dP, dP_cap, n0, d_alive, cap, ncells, h_tgoff, wave, cthr, flags, grid, st,
                                   refine, sh, stats, n_out, min_cands, agreed);
+  nb_prof_dump("expand");
   if (sh.world > 1 && !agreed) {  // terminal header: a local failure reaches the peers, or theirs reach us
     const int G = sh.world;
     int hdr[2] = {(int)e, 0};
