@@ -223,7 +223,7 @@ __device__ __forceinline__ int gheight(const DScene& s, int t) { return (s.views
 
 // CFindMatch::isNeighbor / isNeighborRadius (findMatch.cpp:125-185).
 template <class PL, class PR>
-__device__ int is_neighbor_h(const PL& l, const PR& r, float hunit, float thr, float radius, bool use_radius) {
+__device__ __forceinline__ int is_neighbor_h(const PL& l, const PR& r, float hunit, float thr, float radius, bool use_radius) {
   if ((double)dot4(l.normal, r.normal) < cos(120.0 * M_PI / 180.0)) return 0;
   float diff[4];
   for (int k = 0; k < 4; ++k) diff[k] = r.coord[k] - l.coord[k];
@@ -246,7 +246,7 @@ __device__ int is_neighbor(const DScene& s, const FilterDev& F, int a, int b, fl
 
 // CPatchOrganizerS::isVisible (patchOrganizerS.cpp:500-525).
 template <class PQ>
-__device__ int is_visible_q(const DScene& s, const FilterDev& F, const PQ& q, int t, int ix, int iy, float strict) {
+__device__ __forceinline__ int is_visible_q(const DScene& s, const FilterDev& F, const PQ& q, int t, int ix, int iy, float strict) {
   if (!in_grid(s, t, ix, iy)) return 0;
   if (s.depth == 0) return 1;
   const unsigned long long key = F.dpkey[F.tgoff[t] + (long long)iy * gwidth(s, t) + ix];
@@ -1251,8 +1251,10 @@ __device__ __forceinline__ void nb_append(NbLdsT<CAP>& L, bool hit, int j, int c
 // list bounds load in parallel); the cells' entries are then flattened and tested 64 per round.
 // Expansion-time chain entries (FilterDev delta) are walked per lane.  The neighbour SET is the
 // reference's; the visiting order only matters for the buffer's compaction points.
-template <int CAP>
-__device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLdsT<CAP>& L, const pmvs_patch& q, float scale,
+// CHM: the largest margin whose expansion-time chains the caller walks (0: the filter pass, which has
+// none -- F.pg_dhead is nullptr there; chains met anyway are an error, code 16).
+template <int CAP, int CHM>
+__device__ __forceinline__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLdsT<CAP>& L, const pmvs_patch& q, float scale,
                                 int margin, int skipvis, unsigned long long* prof = nullptr, RadUnit pre = {-1.0f, 0.0f}) {
   const int lane = lane_id_w();
   unsigned long long nbp_t = NBP_NOW();
@@ -1387,28 +1389,60 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLdsT<CAP>
         if (ib + u * 64 < tot) nb_append(L, hv[u], jv[u] < 0 ? 0 : jv[u], cap);
     }
     NBP(2);
-    // entries committed by earlier expansion waves (short chains, walked per lane), cell by cell of
-    // the slot's row
+    // entries committed by earlier expansion waves (per-cell chains, FilterDev delta): slot by slot,
+    // every lane walks the chains of all the slot's row cells at once -- one cursor per cell, their
+    // item / next loads in flight together -- so a round costs one dependent load per chain step, not
+    // one per chain step of every cell in turn (round 6: iteration 1 of the C3 loop, where the whole
+    // growing model is in chains, spent 69 % of findEmptyBlocks' cycles here cell by cell, r06w)
+    int hany = 0;
 #pragma unroll
-    for (int k = 0; k < NB_SK; ++k) {
-      if (!chains || __ballot(hk[k] != 0) == 0ull) continue;
-      for (int dx = 0; dx < side; ++dx) {
-        const int* dh = (bk[k] < 0) ? F.vp_dhead : F.pg_dhead;
-        const int head = ((hk[k] >> dx) & 1) ? dh[ck0[k] + dx] : -1;
-        if (__ballot(head >= 0) == 0ull) continue;
-        if (uni(L.cnt) > cap / 2 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(uni(L.cnt), cap), &L.cnt);
-        for (int ent = head; ent >= 0; ent = F.d_next[ent]) {
-          const int j = F.d_item[ent];
-          if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 15); continue; }
-          if (nb_first_visit(L, j) && is_neighbor_h(q, F.hot[j], unit, thr, radius, true)) {
-            const int pos = atomicAdd(&L.cnt, 1);
-            if (pos < cap) L.nb[pos] = j;
-            else L.overflow = 1;
-          }
+    for (int k = 0; k < NB_SK; ++k) hany |= hk[k];
+    if (chains && __ballot(hany != 0) != 0ull) {
+      if (CHM == 0 || margin > CHM) {
+        if (lane == 0) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 16); }
+      } else {
+        constexpr int MC = 2 * CHM + 1;
+#pragma unroll
+        for (int k = 0; k < NB_SK; ++k) {
+        if (__ballot(hk[k] != 0) == 0ull) continue;
+        int cur[MC];
+#pragma unroll
+        for (int dx = 0; dx < MC; ++dx) {
+          const int* dh = (bk[k] < 0) ? F.vp_dhead : F.pg_dhead;
+          cur[dx] = (dx < side && ((hk[k] >> dx) & 1)) ? dh[ck0[k] + dx] : -1;
         }
-        __syncthreads();
-        if (lane == 0 && L.cnt > cap) L.cnt = cap;
-        __syncthreads();
+        for (;;) {
+          int adds = 0;  // the round's appends at most: its live cursors over the wavefront
+#pragma unroll
+          for (int m = 0; m < MC; ++m) adds += __popcll(__ballot(cur[m] >= 0));
+          if (adds == 0) break;
+          const int cnt0 = uni(L.cnt);
+          if (cnt0 + adds > cap && !uni(L.overflow)) sort_unique_lds(L.nb, imin(cnt0, cap), &L.cnt);
+          int jm[MC];
+#pragma unroll
+          for (int m = 0; m < MC; ++m) {
+            jm[m] = -2;
+            if (cur[m] >= 0) {
+              jm[m] = F.d_item[cur[m]];
+              cur[m] = F.d_next[cur[m]];
+            }
+          }
+#pragma unroll
+          for (int m = 0; m < MC; ++m) {
+            const int j = jm[m];
+            if (j == -2) continue;
+            if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 15); continue; }
+            if (nb_first_visit(L, j) && is_neighbor_h(q, F.hot[j], unit, thr, radius, true)) {
+              const int pos = atomicAdd(&L.cnt, 1);
+              if (pos < cap) L.nb[pos] = j;
+              else L.overflow = 1;
+            }
+          }
+          __syncthreads();
+          if (lane == 0 && L.cnt > cap) L.cnt = cap;
+          __syncthreads();
+        }
+        }
         const int cnt = uni(L.cnt);
         if (cnt > cap - 64 && !uni(L.overflow)) sort_unique_lds(L.nb, imin(cnt, cap), &L.cnt);
       }
@@ -1430,7 +1464,7 @@ __device__ int gather_neighbors(const DScene& s, const FilterDev& F, NbLdsT<CAP>
 // fout != nullptr: the rows' fx[n], fy[n], fz[n] go there and the fit is left to quad_lane_kernel
 // (returns -1).
 template <int CAP>
-__device__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLdsT<CAP>& L, double* M, double* r,
+__device__ __forceinline__ int filter_quad_wave(const DScene& s, const FilterDev& F, NbLdsT<CAP>& L, double* M, double* r,
                                 const pmvs_patch& q, int n, float* fout = nullptr) {
   const int lane = lane_id_w();
   n = uni(n);
@@ -1555,7 +1589,7 @@ __global__ __launch_bounds__(64) NB_WALK_ATTR void neighbor_kernel(DScene s, Fil
     const bool mine = world <= 1 || uni(q.images[0]) % world == rank;
     if (mine && !uni(q.fix)) {
       NBP(6);
-      const int n = gather_neighbors(s, F, L, q, 4.0f, 2, 1, prof);
+      const int n = gather_neighbors<CAP, 0>(s, F, L, q, 4.0f, 2, 1, prof);
 #if defined(NB_PROFILE)
       nbp_t = NBP_NOW();
 #endif
@@ -2139,7 +2173,7 @@ __global__ __launch_bounds__(64) NB_WALK_ATTR void empty_blocks_kernel(DScene s,
     const int n = 0;
     if (lane == 0) L.overflow = 0;
 #else
-    const int n = gather_neighbors(s, F, L, q, 4.0f, 1, 0, prof, ru);  // the radius and units computed once
+    const int n = gather_neighbors<CAP, 1>(s, F, L, q, 4.0f, 1, 0, prof, ru);  // the radius and units computed once
 #endif
 #if defined(NB_PROFILE)
     nbp_t = NBP_NOW();
@@ -2584,7 +2618,7 @@ __global__ __launch_bounds__(64) NB_WALK_ATTR void depth_post_kernel(DScene s, F
           st = 3;
         } else {
           // ... findNeighbors(patch, neighbors, 1, 4, 2) + filterQuad when more than 6 neighbours
-          const int n = gather_neighbors(s, F, L, q, 4.0f, 2, 0);
+          const int n = gather_neighbors<CAP, 2>(s, F, L, q, 4.0f, 2, 0);
           // overflowed: candidate k is rewritten by the NB_CAP_BIG re-walk
           if (lane == 0 && L.overflow && ov.items) ov.items[atomicAdd(ov.count, 1)] = k;
           if (lane == 0 && L.overflow && !ov.items) atomicAdd(overflow, 1);
