@@ -3072,6 +3072,10 @@ __global__ void unpack_bits_kernel(const unsigned* __restrict__ bits, int n, int
 }
 
 // filterSmallGroups labels on the device (filter_pass): see the comment at the call.
+static int lab_jump() {  // PMVS_LAB_JUMP: sweeps per all-vertex pointer jump (A/B knob)
+  static const int v = getenv("PMVS_LAB_JUMP") ? std::max(1, atoi(getenv("PMVS_LAB_JUMP"))) : 1;
+  return v;
+}
 __global__ void lab_init_kernel(int* __restrict__ lab, int* __restrict__ active, int na) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < na) {
@@ -3083,12 +3087,15 @@ __global__ void lab_init_kernel(int* __restrict__ lab, int* __restrict__ active,
 // (active[i] != 0), or over every vertex (all = 1: the verifying sweep).  A lowered target is
 // re-activated; the sweep's reads of other vertices' labels may already see this sweep's updates
 // (labels only decrease, so any interleaving converges to the same fixpoint).
+// jump: whether every vertex tries the pointer jump in this sweep (else only the active ones do: an
+// inactive vertex then costs one coalesced flag read, not the jump's dependent gather).
 __global__ void lab_relax_kernel(const int* __restrict__ eoff, const int* __restrict__ edges, int na, int* lab,
-                                 int* active, int all, int* changed) {
+                                 int* active, int all, int* changed, int jump) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= na) return;
-  // the pointer jump lab[i] = lab[lab[i]] (reachability is transitive) in every sweep, fused here
-  // (round 4 ran it as its own full pass after every other sweep); a jumped vertex relaxes too
+  if (!all && !jump && active[i] == 0) return;
+  // the pointer jump lab[i] = lab[lab[i]] (reachability is transitive), fused here (round 4 ran it as
+  // its own full pass after every other sweep); a jumped vertex relaxes too
   const int l0 = lab[i], l1 = lab[l0];
   const bool jumped = l1 < l0 && atomicMin(&lab[i], l1) > l1;
   if (jumped) atomicOr(changed, 1);
@@ -3458,13 +3465,15 @@ static hipError_t filter_pass_impl(const DScene& s, FilterBuffers& B, pmvs_patch
     // loop ends after a sweep over EVERY vertex changes nothing, i.e. at the fixpoint itself.
     int* active = B.list;  // csize's buffer, free until the counting below
     hipLaunchKernelGGL(lab_init_kernel, dim3(nblk(na)), dim3(256), 0, st, lab, active, na);
+    // every lab_jump()-th active sweep jumps every vertex's pointer (1: every sweep, rounds 4-5)
+    int sweep = 0;
     for (int it = 0;; ++it) {
       const bool verify = (it % 9) == 8;  // a full sweep after each 8 rounds of active sweeps that changed something
       FCHK(hipMemsetAsync(changed, 0, sizeof(int), st));
       for (int r = 0; r < (verify ? 1 : 8); ++r) {
         if (ne)
           hipLaunchKernelGGL(lab_relax_kernel, dim3(nblk(na)), dim3(256), 0, st, B.edge_off, B.edges, na, lab, active,
-                             verify ? 1 : 0, changed);
+                             verify ? 1 : 0, changed, (sweep++ % lab_jump()) == 0 ? 1 : 0);
       }
       int ch = 0;
       FCHK(read_int(changed, &ch, st));
