@@ -1775,6 +1775,31 @@ static bool refine_tail_on() {
   return on;
 }
 
+// Diagnostics only (PMVS_DUMP_JOBS=<file>, tools/r06ad.sh): after the first four refine batches of at
+// least 50 000 candidates, every refined job's preProcess outputs and its evaluation count are
+// appended to <file> as float32 rows [batch, nimg, evals, refine_code, dscale, ascale, x0[0..2],
+// weights[0..5], ncc] -- the data for a chain-length predictor.
+static void dump_jobs(const RefineJob* d_jobs, int n, hipStream_t stream) {
+  static const char* path = getenv("PMVS_DUMP_JOBS");
+  static int batches = 0;
+  if (!path || n < 50000 || batches >= 4) return;
+  std::vector<RefineJob> h((size_t)n);
+  if (hipStreamSynchronize(stream) != hipSuccess ||
+      hipMemcpy(h.data(), d_jobs, (size_t)n * sizeof(RefineJob), hipMemcpyDeviceToHost) != hipSuccess)
+    return;
+  FILE* f = fopen(path, "ab");
+  if (!f) return;
+  for (const RefineJob& J : h) {
+    if (J.status != PMVS_ACCEPTED) continue;
+    float r[16] = {(float)batches, (float)J.nimg, (float)J.evals, (float)J.refine_code, J.dscale, J.ascale,
+                   (float)J.x0[0], (float)J.x0[1], (float)J.x0[2], 0, 0, 0, 0, 0, 0, J.ncc};
+    for (int i = 0; i < 6 && i < PMVS_MAX_TAU; ++i) r[9 + i] = J.weights[i];
+    fwrite(r, sizeof(r), 1, f);
+  }
+  fclose(f);
+  ++batches;
+}
+
 template <int WS>
 static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, RefineJob* d_jobs, pmvs_refined* d_out,
                                    int n, DevStats* d_st, int grid, int refine_grid, int tslots, hipStream_t stream,
@@ -1825,6 +1850,7 @@ static hipError_t launch_refine_ws(const DScene& s, const pmvs_candidate* d_in, 
     (void)hipEventRecord(ev[2], stream);
     hipLaunchKernelGGL((post_kernel<WS>), dim3(g), dim3(64), 0, stream, s, d_jobs, d_out, n, d_st);
     (void)hipEventRecord(ev[3], stream);
+    dump_jobs(d_jobs, n, stream);
     return hipGetLastError();
   }
   if (tslots >= 100000) {  // workgroup form: 100000 + chains * 1000 + optimizer wavefronts * 10 + workgroups per CU
