@@ -73,8 +73,14 @@ constexpr int NB_CAP_BIG = PMVS_MAX_NEIGHBOURS;
 constexpr int NB_SCR = NB_CAP * 8;
 constexpr int NB_GRID_BIG = 32;  // workgroups of the NB_CAP_BIG re-walks
 // gather_neighbors: cell slots per lane per round, entries per lane per test round
-constexpr int NB_SK = 2;
-constexpr int NB_NE = 2;
+#ifndef PMVS_NB_SK  // experiment variants only (tools/sweep_walks.sh)
+#define PMVS_NB_SK 2
+#endif
+#ifndef PMVS_NB_NE
+#define PMVS_NB_NE 2
+#endif
+constexpr int NB_SK = PMVS_NB_SK;
+constexpr int NB_NE = PMVS_NB_NE;
 // gather_neighbors' slots (round 6): 1 = one slot per ROW of a list's (2 margin + 1)^2 window -- the
 // row's cells are consecutive in the CSR cell order, so their entries are the one range
 // [off[c0], off[c0 + nx]) -- against 0 = one slot per cell (rounds 2-5).  The neighbour set is the
