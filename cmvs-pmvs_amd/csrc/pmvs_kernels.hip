@@ -820,12 +820,19 @@ __device__ void post_candidate(const DScene& s, WaveLds<WS>& L, const RefineJob&
       filter_images_by_angle<WS>(s, L, coord, normal);
       if (L.nimg < s.minImageNum) pfail = 1;
     }
+    int ref_before = -1;
     if (!pfail) {
+      ref_before = L.images[0];
       set_ref_image<WS>(s, L, coord, normal, mat, &acc[2]);
       if (L.nimg == 0) pfail = 1;
     }
     if (!pfail) {
-      constraint_images<WS>(s, L, coord, normal, s.nccThreshold, &acc[2]);
+      // optim.cpp:165.  With the reference image unchanged by setRefImage, this second pass is the
+      // identity: every image it tests passed the first pass (optim.cpp:157) against the same reference
+      // texture, with the same geometry and the same frame (getPAxes of images[0]), and nothing
+      // between the passes re-admits an image.  Only its grabTex count is charged then.
+      if (L.images[0] != ref_before) constraint_images<WS>(s, L, coord, normal, s.nccThreshold, &acc[2]);
+      else if (lane == 0) acc[2] += (unsigned long long)L.nimg;
       if (L.nimg < s.minImageNum) pfail = 1;
     }
     if (!pfail) {
