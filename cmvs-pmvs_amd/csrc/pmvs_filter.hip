@@ -195,7 +195,7 @@ struct FilterDev {
   // takes a max per cell, checkCounts tests occupancy), so chains need no insertion order.
   // nullptr in the filter pass.
   const int* pg_dhead; const int* vp_dhead;
-  const int* d_item; const int* d_next;
+  const int2* d_ent;  // {item, next} per pool entry
   // Filter pass only: the collected patches' coordinates in collect order (the dpkey payload),
   // so depth tests read 16 B instead of a patch record; nullptr in the expansion.
   const float4* coordc;
@@ -1429,8 +1429,9 @@ __device__ __forceinline__ int gather_neighbors(const DScene& s, const FilterDev
           for (int m = 0; m < MC; ++m) {
             jm[m] = -2;
             if (cur[m] >= 0) {
-              jm[m] = F.d_item[cur[m]];
-              cur[m] = F.d_next[cur[m]];
+              const int2 en = F.d_ent[cur[m]];
+              jm[m] = en.x;
+              cur[m] = en.y;
             }
           }
 #pragma unroll
@@ -2396,8 +2397,10 @@ __global__ __launch_bounds__(64) NB_WALK_ATTR void empty_blocks_stream_kernel(DS
       // entries committed by earlier expansion waves (short chains, walked per lane)
 #pragma unroll
       for (int k = 0; k < NB_SK; ++k)
-        for (int ent = hk[k]; ent >= 0; ent = F.d_next[ent]) {
-          const int j = F.d_item[ent];
+        for (int ent = hk[k]; ent >= 0;) {
+          const int2 en = F.d_ent[ent];
+          ent = en.y;
+          const int j = en.x;
           if (j < 0 || j >= F.n) { atomicAdd(&F.err[0], 1); atomicExch(&F.err[1], 15); continue; }
           const PHot& h = F.hot[j];
           if (is_neighbor_h(q, h, unit, thr, nradius, true)) eb_bin(h.coord, q.coord, xdir, ydir, radiuslow, radiushigh, pos, nan);
@@ -2601,7 +2604,7 @@ __global__ __launch_bounds__(64) NB_WALK_ATTR void depth_post_kernel(DScene s, F
               for (int e = eb, ent = F.pg_dhead ? F.pg_dhead[c] : -1; e < ee || ent >= 0;) {
                 int j;
                 if (e < ee) j = F.pg_items[e++];
-                else { j = F.d_item[ent]; ent = F.d_next[ent]; }
+                else { const int2 en = F.d_ent[ent]; j = en.x; ent = en.y; }
                 const PHot& hj = F.hot[j];
                 if (vis && !(pdepth < depth_of(s.views[t], hj.coord))) continue;
                 const float hunit = (float)((double)(u0 + hj.unit0) / 2.0 * s.csize);
@@ -2647,8 +2650,7 @@ __global__ __launch_bounds__(64) NB_WALK_ATTR void depth_post_kernel(DScene s, F
 struct DeltaLists {  // the per-cell chains of FilterDev (expansion), writable
   int* pg_head;
   int* vp_head;
-  int* item;
-  int* next;
+  int2* ent;  // {item, next}
 };
 
 __global__ void add_patches_kernel(DScene s, FilterDev F, int first, int count, int rank0, Reg* __restrict__ preg,
@@ -2698,8 +2700,8 @@ __global__ __launch_bounds__(64) void register_kernel(DeltaLists D, const int* _
     const int e = eoff[k] + i;
     const bool vis = i >= ni;
     const int cell = vis ? r[5 + 2 * PMVS_MAX_IMAGES + (i - ni)] : r[5 + PMVS_MAX_IMAGES + i];
-    D.item[e] = first + k;
-    D.next[e] = atomicExch(&(vis ? D.vp_head : D.pg_head)[cell], e);
+    const int nx = atomicExch(&(vis ? D.vp_head : D.pg_head)[cell], e);  // readers are later kernels
+    D.ent[e] = make_int2(first + k, nx);
   }
 }
 
@@ -2884,7 +2886,8 @@ struct Ctx {
   int rank = 0, world = 1;  // owner partition of the target images (world > 1: xchg is set)
   FilterXchg xchg;
   int nalive = 0, npg = 0, nvp = 0;
-  const int *pg_dhead = nullptr, *vp_dhead = nullptr, *d_item = nullptr, *d_next = nullptr;
+  const int *pg_dhead = nullptr, *vp_dhead = nullptr;
+  const int2* d_ent = nullptr;
   const float4* coordc = nullptr;
   FilterDev dev() const {
     FilterDev F{};
@@ -2892,7 +2895,7 @@ struct Ctx {
     F.pg_off = B.pg_off; F.pg_items = B.pg_items; F.vp_off = B.vp_off; F.vp_items = B.vp_items;
     F.dpkey = B.dpkey; F.order = B.order; F.rank = B.rank; F.nalive = nalive; F.hot = B.hot;
     F.ncells = ncells; F.npg = npg; F.nvp = nvp; F.err = B.counters + 6; F.lovf = B.counters + 8;
-    F.pg_dhead = pg_dhead; F.vp_dhead = vp_dhead; F.d_item = d_item; F.d_next = d_next;
+    F.pg_dhead = pg_dhead; F.vp_dhead = vp_dhead; F.d_ent = d_ent;
     F.coordc = coordc;
     const char* sc = getenv("PMVS_NB_SOFTCAP");
     F.nb_softcap = sc ? atoi(sc) : 0;
@@ -3769,7 +3772,7 @@ static hipError_t grow(T*& p, size_t& cap, size_t need) {
 void delete_commit_work(CommitWork* w);  // after CommitWork's definition
 ExpandBuffers::~ExpandBuffers() {
   void* ps[] = {parents, cand_coord, cand_ok, cand, prep, status, slots, cand2, prep2, res, outp, ostatus, counts, alive,
-                pg_head, vp_head, d_item, d_next, pool_used, tcells, tvals, qtmp, crec, acc, dupd, cellinit, occ,
+                pg_head, vp_head, d_ent, pool_used, tcells, tvals, qtmp, crec, acc, dupd, cellinit, occ,
                 qkey, qrank, qrank2, qsort_tmp, xsd, xrd, cidx, qkeep, qpos, qitems, sflag, spos, slot2};
   for (void* p : ps)
     if (p) (void)hipFree(p);
@@ -4432,7 +4435,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
   size_t pool_need = 0;
   X.pool_host = 0;
   auto set_delta = [&]() {
-    c.pg_dhead = X.pg_head; c.vp_dhead = X.vp_head; c.d_item = X.d_item; c.d_next = X.d_next;
+    c.pg_dhead = X.pg_head; c.vp_dhead = X.vp_head; c.d_ent = X.d_ent;
   };
   set_delta();
   // ---- device state of the commit: CExpand's _counts (unsigned char, clearCounts) and whether
@@ -4775,8 +4778,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
       T.mark(7);
       if (added > 0) {
         pool_need = X.pool_host + (size_t)co.entries;
-        FCHK(grow_keep(X.d_item, X.cap_item, pool_need, X.pool_host, st));
-        FCHK(grow_keep(X.d_next, X.cap_next, pool_need, X.pool_host, st));
+        FCHK(grow_keep(X.d_ent, X.cap_ent, pool_need, X.pool_host, st));
         set_delta();
         if ((size_t)(first + added) > pcap) {  // per-patch arrays the waves write, grown keeping their contents
           // 1.5x: the old and the new model coexist during the copy (at C5 scale ~50 M records of 1608 B)
@@ -4794,7 +4796,7 @@ static hipError_t expand_pass_impl(const DScene& s, FilterBuffers& B, ExpandBuff
         hipLaunchKernelGGL(append_kernel, dim3(added), dim3(64), 0, st, dP, first, X.acc, added, X.outp);
         nmodel += added;
         c.n = nmodel;
-        DeltaLists D{X.pg_head, X.vp_head, X.d_item, X.d_next};
+        DeltaLists D{X.pg_head, X.vp_head, X.d_ent};
         hipLaunchKernelGGL(register_kernel, dim3(added), dim3(64), 0, st, D, X.acc, X.acc + added, added, first, X.crec,
                            kRecInts);
         hipLaunchKernelGGL(add_patches_kernel, dim3(nblk((long long)added * s.tnum)), dim3(256), 0, st, s, c.dev(), first,

@@ -179,7 +179,10 @@ struct ExpandBuffers {
   pmvs_refined* res = nullptr;
   unsigned char* counts = nullptr;
   // registrations committed during the run: per-cell chain heads + entry pool (FilterDev delta)
-  int *pg_head = nullptr, *vp_head = nullptr, *d_item = nullptr, *d_next = nullptr, *pool_used = nullptr;
+  // d_ent: the pool, {item, next} per entry (one 8-B load per chain step; round 6, separate item / next
+  // arrays made every step touch two cache lines)
+  int *pg_head = nullptr, *vp_head = nullptr, *pool_used = nullptr;
+  int2* d_ent = nullptr;
   int* tcells = nullptr;        // cells whose counts a commit changed, and their values
   unsigned short* cellinit = nullptr;  // per-cell {count, occupied} staged for the host mirror
   float* qtmp = nullptr;        // _tmp of the collected patches (queue)
@@ -202,7 +205,7 @@ struct ExpandBuffers {
   size_t pool_host = 0;
   size_t cap_coord = 0, cap_ok = 0, cap_cand = 0, cap_prep = 0, cap_slots = 0, cap_prep2 = 0, cap_res = 0, cap_outp = 0,
          cap_ost = 0, cap_par = 0, cap_status = 0, cap_cand2 = 0, cap_alive = 0, cap_cnt = 0, cap_pghead = 0,
-         cap_vphead = 0, cap_item = 0, cap_next = 0, cap_pused = 0, cap_tcells = 0, cap_tvals = 0,
+         cap_vphead = 0, cap_ent = 0, cap_pused = 0, cap_tcells = 0, cap_tvals = 0,
          cap_qtmp = 0, cap_crec = 0, cap_acc = 0, cap_dupd = 0, cap_cellinit = 0;
   std::vector<int> gw, gh;  // grid sizes of the target images
   void release();  // frees every buffer; the next pass grows them again (PMVS_LOOP_LEAN)
